@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""DeepVCP registration hot path benchmark (BASELINE.json metric, config C3 / C4).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    torchrun --nproc-per-node N bench.py --gpus N ...        (one rank per GPU, RCCL)
+
+One step = DeepVCP.forward + deepVCP_loss (the two-pass pose solve) over one batch of
+synthetic KITTI-like pairs (B pairs per GPU, N=16384 points, K=64 key points, candidate grid
+r=2.0 / s=0.4 -> C=1331), inputs resident in HBM, eval mode, random-init weights
+(torch.manual_seed(0)).  Pairs are independent, so ranks shard the pairs with no data-path
+collective ("weak" scaling); the per-pair (R, t) are all-gathered over RCCL once at the end of
+the timed region.  Rank 0 prints one JSON line.  At N=1 the CPU oracle (REF-R restated in
+torch CPU ops) is timed on one of the same pairs with the same weights and FPS starts, and
+its R, t are compared with the GPU's.
+"""
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "deepvcp-pointcloud-registration_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
+PEAK_FP32_TFLOPS = 157.3   # fp32 vector = fp32 MFMA dense rate
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--batch", type=int, default=8, help="pairs per GPU")
+    p.add_argument("--npoints", type=int, default=16384)
+    p.add_argument("--K", type=int, default=64)
+    p.add_argument("--r", type=float, default=2.0)
+    p.add_argument("--s", type=float, default=0.4)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--stage-report", action="store_true", help="print the per-kernel table to stderr")
+    return p.parse_args()
+
+
+# ---------------------------------------------------------------------------------------------
+# Algorithmic work per launch, by entry point (DESIGN.md "Roofline accounting").  Flops count
+# the reference op graph's arithmetic for the work one launch performs.
+def algorithmic_flops(name, cfg):
+    B, N, K, S, C = cfg["B"], cfg["N"], cfg["K"], cfg["S"], cfg["C"]
+    if name == "dvcp_fps":          # per launch: npoint x N point updates (3 sub, 3 mul, 2 add, 1 min)
+        return None  # per-launch N differs (16384 for sa1, 10000 for sa2/sa3): handled below
+    if name == "dvcp_knn":          # Q x M distance evaluations, 8 flops each
+        return B * K * C * S * 8.0
+    if name == "dvcp_dfe_tgt":      # rows x (35*32 + 32*32 + 32*32) MACs
+        return B * K * C * 32 * 2.0 * (35 * 32 + 32 * 32 + 32 * 32)
+    if name == "dvcp_cpg":          # per key point: C x (32*16 + 16*4 + 4*1) x 27 MACs
+        return B * K * C * 2.0 * 27 * (32 * 16 + 16 * 4 + 4)
+    return None
+
+
+def fps_flops(n, npoint, B):
+    return B * float(npoint) * n * 9.0
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import dvcp
+    from dvcp import _lib
+    from dvcp.synthetic import make_pairs
+
+    B, N, K, r, s = args.batch, args.npoints, args.K, args.r, args.s
+    torch.manual_seed(0)
+    model = dvcp.DeepVCP(use_normal=False, K=K, r=r, s=s).eval().to(dev)
+    src, tgt, R_gt, t_gt = make_pairs(B, N, seed=1234 + 7919 * rank)
+    src, tgt, R_gt, t_gt = src.to(dev), tgt.to(dev), R_gt.to(dev), t_gt.to(dev)
+    t_init = torch.zeros(1, 3)
+    torch.manual_seed(1 + rank)
+
+    def step(starts=None):
+        with torch.no_grad():
+            kp, vcp = model(src, tgt, R_gt, t_init, starts=starts)
+            loss, Rp, tp = dvcp.deepVCP_loss(kp, vcp, R_gt, t_gt, 0.5)
+        return Rp, tp, loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+
+    _lib.EVENT_LOG = []
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    outs = [step() for _ in range(args.steps)]
+    res = torch.cat([torch.cat([o[0].reshape(B, 9), o[1].reshape(B, 3)], 1) for o in outs])  # (steps*B, 12)
+    if world > 1:
+        gathered = [torch.empty_like(res) for _ in range(world)]
+        dist.all_gather(gathered, res)
+        res = torch.cat(gathered)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    log, _lib.EVENT_LOG = _lib.EVENT_LOG, None
+    if world > 1:
+        dist.barrier()
+        tmax = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        elapsed = float(tmax.item())
+
+    # per-kernel live HIP-event timing over the timed region
+    S = model.FE1.sa1.npoint
+    C = int((2 * r) / s + 1) ** 3
+    cfg = dict(B=B, N=N, K=K, S=S, C=C)
+    per = {}
+    for name, e0, e1 in log:
+        per.setdefault(name, []).append(e0.elapsed_time(e1))
+    tot = {k: sum(v) for k, v in per.items()}
+    dom = max(tot, key=tot.get)
+    if dom == "dvcp_fps":
+        # launches alternate sa1 (N -> S), sa2 (S -> S), sa3 (S -> S) per cloud
+        works = [fps_flops(N if (i % 3) == 0 else S, S, B) for i in range(len(per[dom]))]
+        achieved = sum(works) / (sum(per[dom]) * 1e-3) / 1e12
+    else:
+        achieved = algorithmic_flops(dom, cfg) / (sum(per[dom]) / len(per[dom]) * 1e-3) / 1e12
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 4), "peak": PEAK_FP32_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 6), "traffic": traffic,
+                "avg_launch_ms": round(tot[dom] / len(per[dom]), 4),
+                "note": "fp32 arithmetic (VALU/MFMA share one 157.3 TF peak); FPS is a serial chain of "
+                        "npoint dependent argmax steps per cloud (latency-bound)"}
+    stages = {k: {"launches": len(v), "total_ms_per_step": round(sum(v) / args.steps, 3),
+                  "avg_ms": round(sum(v) / len(v), 4)} for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1]))}
+
+    pairs = B * world * args.steps
+    value = pairs / elapsed
+    out = {
+        "metric": "pairs/sec (full DeepVCP forward) at N=16384, K=64; rot/trans error vs ref",
+        "value": round(value, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "C3: KITTI-like synthetic pairs, DeepVCP.forward + deepVCP_loss (eval)",
+                   "pairs_per_gpu": B, "global_batch": B * world, "n_points": N, "K": K, "r": r, "s": s,
+                   "candidates": C, "fe_npoint": S, "parallelism": f"pairs sharded x{world}, all_gather(R,t)"},
+        "roofline": roofline,
+        "stages": stages,
+    }
+    # HBM fraction of the whole step (north_star asks for it; the path is compute/latency bound)
+    out["hbm_fraction_step"] = round(177e6 * B / (elapsed / args.steps) / (PEAK_HBM_GBS * 1e9), 6)
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"], out["parity"] = cpu_baseline(model, src, tgt, R_gt, t_gt, dev)
+    if rank == 0:
+        if args.stage_report:
+            for k, v in stages.items():
+                print(f"{k:28s} {v}", file=sys.stderr)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(model, src, tgt, R_gt, t_gt, dev):
+    """Time the CPU oracle (REF-R in torch CPU ops) on pair 0, same weights and FPS starts."""
+    import oracle as O
+    import dvcp
+    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = max(1, min(threads, 16))
+    torch.set_num_threads(threads)
+    ref = O.DeepVCP(use_normal=False, K=model.K, r=model.r, s=model.s).eval()
+    ref.load_state_dict({k: v.cpu() for k, v in model.state_dict().items()})
+    N = src.shape[2]
+    starts = model.draw_starts(1, N, N)
+    with torch.no_grad():
+        kp, vcp = model(src[:1], tgt[:1], R_gt[:1], torch.zeros(1, 3), starts=starts)
+        _, Rg, tg = dvcp.deepVCP_loss(kp, vcp, R_gt[:1], t_gt[:1], 0.5)
+    s0, g0, R0, t0 = src[:1].cpu(), tgt[:1].cpu(), R_gt[:1].cpu(), t_gt[:1].cpu()
+    t_start = time.perf_counter()
+    with torch.no_grad(), O.fps_starts(list(starts)):
+        kpo, vcpo = ref(s0, g0, R0, torch.zeros(1, 3))
+        _, Ro, to = O.deepVCP_loss(kpo, vcpo, R0, t0, 0.5)
+    secs = time.perf_counter() - t_start
+    cpu_model = platform.processor() or ""
+    try:
+        for line in subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout.splitlines():
+            if line.startswith("Model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    base = {"value": round(1.0 / secs, 5), "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"1 C3 pair (N=16384, K=64, r=2.0), oracle/ref_r.py torch CPU ops, {secs:.1f} s",
+            "cpu_model": cpu_model, "os_cpu_count": os.cpu_count()}
+    parity = {"R_maxabs_vs_ref": float((Rg.cpu() - Ro).abs().max()), "t_maxabs_vs_ref": float((tg.cpu() - to).abs().max()),
+              "vcp_maxabs_vs_ref": float((vcp.cpu() - vcpo).abs().max()),
+              "keypts_equal": bool(torch.equal(kp.cpu(), kpo))}
+    return base, parity
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,145 @@
+// head_topk.hip -- FE output projection + weighting layer + key-point top-k.
+//   dvcp_fe_head: deep_feat_extraction.py:15 `fc` (64 -> 32, applied per REF-R R1) and
+//                 weighting_layer.py:26-30 (Linear 32-16-8-1, ReLU, ReLU, Softplus).
+//   dvcp_topk:    weighting_layer.py:31 torch.topk(X, K, dim=1) (sorted, descending).
+#include "common.h"
+
+namespace dvcp {
+
+__device__ __forceinline__ float relu(float v) { return v > 0.0f ? v : 0.0f; }
+
+// torch.nn.Softplus(beta=1, threshold=20)
+__device__ __forceinline__ float softplus(float v) { return v > 20.0f ? v : log1pf(expf(v)); }
+
+__global__ __launch_bounds__(256) void fe_head_kernel(const float* __restrict__ x, int P, const float* __restrict__ params,
+                                                      float* __restrict__ feat, float* __restrict__ score) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  float in[64];
+  const float4* src = reinterpret_cast<const float4*>(x + static_cast<int64_t>(i) * 64);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const float4 v = src[q];
+    in[4 * q] = v.x;
+    in[4 * q + 1] = v.y;
+    in[4 * q + 2] = v.z;
+    in[4 * q + 3] = v.w;
+  }
+  float f[32];
+  linear_sgpr<64, 32>(in, f, params);
+  float4* dst = reinterpret_cast<float4*>(feat + static_cast<int64_t>(i) * 32);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dst[q] = make_float4(f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]);
+  if (!score) return;
+  const float* w1 = params + 64 * 32 + 32;
+  const float* w2 = w1 + 32 * 16 + 16;
+  const float* w3 = w2 + 16 * 8 + 8;
+  float h1[16], h2[8], h3[1];
+  linear_sgpr<32, 16>(f, h1, w1);
+#pragma unroll
+  for (int c = 0; c < 16; ++c) h1[c] = relu(h1[c]);
+  linear_sgpr<16, 8>(h1, h2, w2);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) h2[c] = relu(h2[c]);
+  linear_sgpr<8, 1>(h2, h3, w3);
+  score[i] = softplus(h3[0]);
+}
+
+// weighting_layer.py:27-30 alone on (P, 32) features.
+__global__ __launch_bounds__(256) void weighting_kernel(const float* __restrict__ x, int P, const float* __restrict__ params,
+                                                        float* __restrict__ score) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  float f[32];
+  const float4* src = reinterpret_cast<const float4*>(x + static_cast<int64_t>(i) * 32);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float4 v = src[q];
+    f[4 * q] = v.x;
+    f[4 * q + 1] = v.y;
+    f[4 * q + 2] = v.z;
+    f[4 * q + 3] = v.w;
+  }
+  const float* w2 = params + 32 * 16 + 16;
+  const float* w3 = w2 + 16 * 8 + 8;
+  float h1[16], h2[8], h3[1];
+  linear_sgpr<32, 16>(f, h1, params);
+#pragma unroll
+  for (int c = 0; c < 16; ++c) h1[c] = relu(h1[c]);
+  linear_sgpr<16, 8>(h1, h2, w2);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) h2[c] = relu(h2[c]);
+  linear_sgpr<8, 1>(h2, h3, w3);
+  score[i] = softplus(h3[0]);
+}
+
+// Top-K of one row per workgroup: K rounds of a block argmax over the remaining elements
+// (value descending, ties -> lower index), one barrier per round (double-buffered slots).
+template <int PPT>
+__global__ __launch_bounds__(1024) void topk_kernel(const float* __restrict__ score, int S, int K, int64_t* __restrict__ out) {
+  constexpr int NT = 1024;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ uint64_t slots[2][NT / kWave];
+  uint64_t key[PPT];
+#pragma unroll
+  for (int p = 0; p < PPT; ++p) {
+    const int n = tid + p * NT;
+    key[p] = n < S ? ((static_cast<uint64_t>(float_order(score[static_cast<int64_t>(b) * S + n])) << 32) |
+                      static_cast<uint64_t>(0xFFFFFFFFu - static_cast<uint32_t>(n)))
+                   : 0ull;
+  }
+  for (int k = 0; k < K; ++k) {
+    uint64_t best = 0;
+#pragma unroll
+    for (int p = 0; p < PPT; ++p) best = key[p] > best ? key[p] : best;
+    const uint64_t w = wave_max_u64(best);
+    if (lane == 0) slots[k & 1][wave] = w;
+    __syncthreads();
+    uint64_t m = slots[k & 1][0];
+#pragma unroll
+    for (int q = 1; q < NT / kWave; ++q) m = slots[k & 1][q] > m ? slots[k & 1][q] : m;
+    const uint32_t win = key_index(m);
+    if (tid == 0) out[static_cast<int64_t>(b) * K + k] = win;
+#pragma unroll
+    for (int p = 0; p < PPT; ++p)
+      if (key[p] == m) key[p] = 0ull;
+  }
+}
+
+}  // namespace dvcp
+
+extern "C" int dvcp_fe_head(const float* x, int P, const float* params, float* feat, float* score, void* stream) {
+  DVCP_REQUIRE(x && params && feat, "dvcp_fe_head: null pointer");
+  if (P <= 0) return DVCP_OK;
+  hipLaunchKernelGGL(dvcp::fe_head_kernel, dim3(dvcp::ceil_div(P, 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     x, P, params, feat, score);
+  return dvcp::launch_status("dvcp_fe_head");
+}
+
+extern "C" int dvcp_weighting(const float* feat, int P, const float* params, float* score, void* stream) {
+  DVCP_REQUIRE(feat && params && score, "dvcp_weighting: null pointer");
+  if (P <= 0) return DVCP_OK;
+  hipLaunchKernelGGL(dvcp::weighting_kernel, dim3(dvcp::ceil_div(P, 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), feat, P, params, score);
+  return dvcp::launch_status("dvcp_weighting");
+}
+
+extern "C" int dvcp_topk(const float* score, int B, int S, int K, int64_t* idx, void* stream) {
+  DVCP_REQUIRE(score && idx, "dvcp_topk: null pointer");
+  DVCP_REQUIRE(K >= 0 && K <= S, "dvcp_topk: K=%d out of range for S=%d", K, S);
+  if (B == 0 || K == 0) return DVCP_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int ppt = dvcp::ceil_div(S, 1024);
+#define DVCP_TOPK(P)                                                                                   \
+  if (ppt <= P) {                                                                                      \
+    hipLaunchKernelGGL((dvcp::topk_kernel<P>), dim3(B), dim3(1024), 0, st, score, S, K, idx);          \
+    return dvcp::launch_status("dvcp_topk");                                                           \
+  }
+  DVCP_TOPK(1)
+  DVCP_TOPK(4)
+  DVCP_TOPK(10)
+  DVCP_TOPK(16)
+#undef DVCP_TOPK
+  dvcp::set_error("dvcp_topk: S=%d exceeds 16384", S);
+  return DVCP_EINVAL;
+}

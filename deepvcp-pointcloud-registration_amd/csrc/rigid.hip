@@ -1,0 +1,238 @@
+// rigid.hip -- pose solve (deepVCP_loss.py:13-121), one workgroup per cloud pair, fp64.
+//
+//   get_rigid_transform (:13-44): centroids, H = (x - cx)(y - cy)^T, torch.svd(H) = U S V^T,
+//     R = V U^T with NO reflection fix (Q13), t = cy + (-R) cx.  The 3x3 SVD is a one-sided
+//     Jacobi iteration in fp64; R = V U^T is invariant to the SVD's sign/order freedom.
+//   svd_optimization (:57-90): R1,t1 -> y1 = R1 x + t1 -> 1-NN distance (fp32, knn_cuda
+//     contract) of every y_true point against y1 -> keep the int(0.8 n) smallest (ascending,
+//     ties to the lower index) -> R2,t2 = Kabsch(x1, y1[inliers]) (Q12) -> y2 = R2 x1 + t2.
+//   deepVCP_loss (:105-121) needs sum|y2 - y_true1| and sum(y2 - y_true1): written per pair.
+#include "common.h"
+
+namespace dvcp {
+
+constexpr int kRgThreads = 256;
+constexpr int kRgMaxN = 1024;
+
+struct Mat3 {
+  double m[3][3];
+};
+
+// One-sided Jacobi SVD of A (3x3): A V = U diag(s).  Returns R = V U^T.
+__device__ void kabsch_rotation(const double (&H)[3][3], double (&R)[3][3]) {
+  double A[3][3], V[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      A[i][j] = H[i][j];
+      V[i][j] = i == j ? 1.0 : 0.0;
+    }
+  for (int sweep = 0; sweep < 40; ++sweep) {
+    bool rotated = false;
+    for (int pq = 0; pq < 3; ++pq) {
+      const int p = pq == 2 ? 1 : 0, q = pq == 0 ? 1 : 2;
+      double alpha = 0, beta = 0, gamma = 0;
+      for (int i = 0; i < 3; ++i) {
+        alpha += A[i][p] * A[i][p];
+        beta += A[i][q] * A[i][q];
+        gamma += A[i][p] * A[i][q];
+      }
+      if (fabs(gamma) <= 1e-300 || fabs(gamma) <= 1e-17 * sqrt(alpha * beta)) continue;
+      rotated = true;
+      const double zeta = (beta - alpha) / (2.0 * gamma);
+      const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+      const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+      for (int i = 0; i < 3; ++i) {
+        const double ap = A[i][p], aq = A[i][q];
+        A[i][p] = c * ap - s * aq;
+        A[i][q] = s * ap + c * aq;
+        const double vp = V[i][p], vq = V[i][q];
+        V[i][p] = c * vp - s * vq;
+        V[i][q] = s * vp + c * vq;
+      }
+    }
+    if (!rotated) break;
+  }
+  double U[3][3], sig[3];
+  for (int j = 0; j < 3; ++j) sig[j] = sqrt(A[0][j] * A[0][j] + A[1][j] * A[1][j] + A[2][j] * A[2][j]);
+  const double smax = fmax(sig[0], fmax(sig[1], sig[2]));
+  int bad = -1;
+  for (int j = 0; j < 3; ++j) {
+    if (sig[j] > 1e-14 * smax && sig[j] > 0) {
+      for (int i = 0; i < 3; ++i) U[i][j] = A[i][j] / sig[j];
+    } else {
+      bad = j;
+    }
+  }
+  if (bad >= 0) {  // rank-deficient H: complete U with the cross product of the other columns
+    const int a = (bad + 1) % 3, b = (bad + 2) % 3;
+    U[0][bad] = U[1][a] * U[2][b] - U[2][a] * U[1][b];
+    U[1][bad] = U[2][a] * U[0][b] - U[0][a] * U[2][b];
+    U[2][bad] = U[0][a] * U[1][b] - U[1][a] * U[0][b];
+  }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) R[i][j] = V[i][0] * U[j][0] + V[i][1] * U[j][1] + V[i][2] * U[j][2];
+}
+
+// Kabsch on the columns listed in sel[0..m) (or 0..m-1 when sel == nullptr) of x, y (3 x n
+// in LDS).  Block-wide; every thread returns R, t.
+__device__ void block_kabsch(const double* x, const double* y, int n, const int* sel, int m, double (&R)[3][3],
+                             double (&t)[3], double* scratch, double* shared_rt) {
+  const int tid = threadIdx.x;
+  double c[6];
+  for (int a = 0; a < 6; ++a) c[a] = 0;
+  for (int k = tid; k < m; k += blockDim.x) {
+    const int j = sel ? sel[k] : k;
+    for (int a = 0; a < 3; ++a) {
+      c[a] += x[a * n + j];
+      c[3 + a] += y[a * n + j];
+    }
+  }
+  double cen[6];
+  for (int a = 0; a < 6; ++a) cen[a] = block_sum(c[a], scratch) / static_cast<double>(m);
+  double h[9];
+  for (int a = 0; a < 9; ++a) h[a] = 0;
+  for (int k = tid; k < m; k += blockDim.x) {
+    const int j = sel ? sel[k] : k;
+    double dx[3], dy[3];
+    for (int a = 0; a < 3; ++a) {
+      dx[a] = x[a * n + j] - cen[a];
+      dy[a] = y[a * n + j] - cen[3 + a];
+    }
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) h[a * 3 + b] = fma(dx[a], dy[b], h[a * 3 + b]);
+  }
+  double H[3][3];
+  for (int a = 0; a < 9; ++a) H[a / 3][a % 3] = block_sum(h[a], scratch);
+  if (tid == 0) {
+    double Rm[3][3];
+    kabsch_rotation(H, Rm);
+    for (int a = 0; a < 3; ++a) {
+      for (int b = 0; b < 3; ++b) shared_rt[a * 3 + b] = Rm[a][b];
+      // t = cy + (-R) @ cx
+      shared_rt[9 + a] = cen[3 + a] + dot3_blas<double>(-Rm[a][0], -Rm[a][1], -Rm[a][2], cen[0], cen[1], cen[2]);
+    }
+  }
+  __syncthreads();
+  for (int a = 0; a < 9; ++a) R[a / 3][a % 3] = shared_rt[a];
+  for (int a = 0; a < 3; ++a) t[a] = shared_rt[9 + a];
+  __syncthreads();
+}
+
+__device__ __forceinline__ double affine_row(const double (&R)[3][3], const double (&t)[3], int a, double x0, double x1,
+                                             double x2) {
+  return dot3_blas<double>(R[a][0], R[a][1], R[a][2], x0, x1, x2) + t[a];
+}
+
+__global__ __launch_bounds__(kRgThreads) void rigid_transform_kernel(const double* __restrict__ x,
+                                                                     const double* __restrict__ y, int n,
+                                                                     double* __restrict__ Rout,
+                                                                     double* __restrict__ tout) {
+  __shared__ double scratch[16];
+  __shared__ double rt[12];
+  const int b = blockIdx.x;
+  double R[3][3], t[3];
+  block_kabsch(x + static_cast<int64_t>(b) * 3 * n, y + static_cast<int64_t>(b) * 3 * n, n, nullptr, n, R, t, scratch,
+               rt);
+  if (threadIdx.x == 0) {
+    for (int a = 0; a < 9; ++a) Rout[b * 9 + a] = R[a / 3][a % 3];
+    for (int a = 0; a < 3; ++a) tout[b * 3 + a] = t[a];
+  }
+}
+
+__global__ __launch_bounds__(kRgThreads) void svd_opt_kernel(const double* __restrict__ xg, const double* __restrict__ yg,
+                                                             const double* __restrict__ Rtrue,
+                                                             const double* __restrict__ ttrue, int n, int n_in,
+                                                             double* __restrict__ R2out, double* __restrict__ t2out,
+                                                             double* __restrict__ x1out, double* __restrict__ y2out,
+                                                             double* __restrict__ partial) {
+  __shared__ double xs[3 * kRgMaxN], ys[3 * kRgMaxN], y1[3 * kRgMaxN];
+  __shared__ float nn[kRgMaxN];
+  __shared__ int sel[kRgMaxN];
+  __shared__ double scratch[16];
+  __shared__ double rt[12];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  for (int e = tid; e < 3 * n; e += kRgThreads) {
+    xs[e] = xg[static_cast<int64_t>(b) * 3 * n + e];
+    ys[e] = yg[static_cast<int64_t>(b) * 3 * n + e];
+  }
+  __syncthreads();
+  double R1[3][3], t1[3];
+  block_kabsch(xs, ys, n, nullptr, n, R1, t1, scratch, rt);
+  for (int j = tid; j < n; j += kRgThreads)
+    for (int a = 0; a < 3; ++a) y1[a * n + j] = affine_row(R1, t1, a, xs[j], xs[n + j], xs[2 * n + j]);
+  double Rt[3][3], tt[3];
+  for (int a = 0; a < 9; ++a) Rt[a / 3][a % 3] = Rtrue[b * 9 + a];
+  for (int a = 0; a < 3; ++a) tt[a] = ttrue[b * 3 + a];
+  __syncthreads();
+  // 1-NN (knn_cuda: both inputs .float()) of y_true_j against y1
+  for (int j = tid; j < n; j += kRgThreads) {
+    const float qx = static_cast<float>(affine_row(Rt, tt, 0, xs[j], xs[n + j], xs[2 * n + j]));
+    const float qy = static_cast<float>(affine_row(Rt, tt, 1, xs[j], xs[n + j], xs[2 * n + j]));
+    const float qz = static_cast<float>(affine_row(Rt, tt, 2, xs[j], xs[n + j], xs[2 * n + j]));
+    float best = __builtin_huge_valf();
+    for (int i = 0; i < n; ++i) {
+      const float dx = static_cast<float>(y1[i]) - qx, dy = static_cast<float>(y1[n + i]) - qy,
+                  dz = static_cast<float>(y1[2 * n + i]) - qz;
+      const float d2 = (dx * dx + dy * dy) + dz * dz;
+      best = d2 < best ? d2 : best;
+    }
+    nn[j] = __fsqrt_rn(best);
+  }
+  __syncthreads();
+  // inliers: rank by (distance, index); rank < n_in lands at position rank
+  for (int j = tid; j < n; j += kRgThreads) {
+    const float dj = nn[j];
+    int rank = 0;
+    for (int i = 0; i < n; ++i) rank += (nn[i] < dj || (nn[i] == dj && i < j)) ? 1 : 0;
+    if (rank < n_in) sel[rank] = j;
+  }
+  __syncthreads();
+  double R2[3][3], t2[3];
+  block_kabsch(xs, y1, n, sel, n_in, R2, t2, scratch, rt);
+  double sabs = 0, sdif = 0;
+  for (int k = tid; k < n_in; k += kRgThreads) {
+    const int j = sel[k];
+    for (int a = 0; a < 3; ++a) {
+      const double v2 = affine_row(R2, t2, a, xs[j], xs[n + j], xs[2 * n + j]);
+      const double vt = affine_row(Rt, tt, a, xs[j], xs[n + j], xs[2 * n + j]);
+      if (x1out) x1out[(static_cast<int64_t>(b) * 3 + a) * n_in + k] = xs[a * n + j];
+      if (y2out) y2out[(static_cast<int64_t>(b) * 3 + a) * n_in + k] = v2;
+      sabs += fabs(v2 - vt);
+      sdif += v2 - vt;
+    }
+  }
+  sabs = block_sum(sabs, scratch);
+  sdif = block_sum(sdif, scratch);
+  if (tid == 0) {
+    for (int a = 0; a < 9; ++a) R2out[b * 9 + a] = R2[a / 3][a % 3];
+    for (int a = 0; a < 3; ++a) t2out[b * 3 + a] = t2[a];
+    if (partial) {
+      partial[b * 2] = sabs;
+      partial[b * 2 + 1] = sdif;
+    }
+  }
+}
+
+}  // namespace dvcp
+
+extern "C" int dvcp_rigid_transform(const double* x, const double* y, int B, int n, double* R, double* t, void* stream) {
+  DVCP_REQUIRE(x && y && R && t, "dvcp_rigid_transform: null pointer");
+  DVCP_REQUIRE(n > 0, "dvcp_rigid_transform: n=%d", n);
+  if (B == 0) return DVCP_OK;
+  hipLaunchKernelGGL(dvcp::rigid_transform_kernel, dim3(B), dim3(dvcp::kRgThreads), 0, static_cast<hipStream_t>(stream), x,
+                     y, n, R, t);
+  return dvcp::launch_status("dvcp_rigid_transform");
+}
+
+extern "C" int dvcp_svd_optimization(const double* x, const double* y_pred, const double* R_true, const double* t_true,
+                                     int B, int n, double* R2, double* t2, double* x1, double* y2, double* partial,
+                                     void* stream) {
+  DVCP_REQUIRE(x && y_pred && R_true && t_true && R2 && t2, "dvcp_svd_optimization: null pointer");
+  DVCP_REQUIRE(n > 0 && n <= dvcp::kRgMaxN, "dvcp_svd_optimization: n=%d unsupported (1..1024)", n);
+  const int n_in = static_cast<int>(n * 0.8);  // deepVCP_loss.py:76 int(N*0.8)
+  DVCP_REQUIRE(n_in > 0, "dvcp_svd_optimization: int(0.8 n) == 0");
+  if (B == 0) return DVCP_OK;
+  hipLaunchKernelGGL(dvcp::svd_opt_kernel, dim3(B), dim3(dvcp::kRgThreads), 0, static_cast<hipStream_t>(stream), x,
+                     y_pred, R_true, t_true, n, n_in, R2, t2, x1, y2, partial);
+  return dvcp::launch_status("dvcp_svd_optimization");
+}

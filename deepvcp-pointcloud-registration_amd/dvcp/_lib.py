@@ -1,0 +1,124 @@
+"""ctypes binding of libdvcp_hip.so (the C ABI declared in include/dvcp.h).
+
+The library is built in-tree (``make`` in deepvcp-pointcloud-registration_amd/, or
+``__graft_entry__.build()``) and loaded after ``import torch`` so that it binds to the same
+HIP runtime (SONAME libamdhip64.so.7) that owns torch's device memory and streams.  There is
+no fallback: if the library is missing or no GPU is present, every op raises.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdvcp_hip.so")
+
+F32, F64 = 0, 1
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_int64
+_D = ctypes.c_double
+
+# name -> argtypes (every entry point returns int, 0 on success)
+SIGNATURES = {
+    "dvcp_fps": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P],
+    "dvcp_ball_query": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _D, _I, _P, _P, _P, _P],
+    "dvcp_square_distance": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _P, _P],
+    "dvcp_sa_group_mlp": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _L, _L, _L, _I,
+                          _P, _P, _I, _I, _P, _P, _P, _P],
+    "dvcp_fe_head": [_P, _I, _P, _P, _P, _P],
+    "dvcp_weighting": [_P, _I, _P, _P, _P],
+    "dvcp_topk": [_P, _I, _I, _I, _P, _P],
+    "dvcp_src_keypoints": [_I, _P, _P, _I, _P, _I, _I, _P, _D, _I, _P, _L, _P, _P, _P, _P],
+    "dvcp_voxelize": [_I, _P, _L, _L, _L, _I, _I, _D, _D, _I, _P, _P, _P],
+    "dvcp_knn": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P],
+    "dvcp_dfe": [_I, _P, _L, _P, _P, _P],
+    "dvcp_dfe_tgt": [_I, _P, _L, _L, _L, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P],
+    "dvcp_cpg": [_P, _P, _L, _L, _L, _P, _I, _I, _P, _P, _P, _P],
+    "dvcp_rigid_transform": [_P, _P, _I, _I, _P, _P, _P],
+    "dvcp_svd_optimization": [_P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P],
+}
+
+_lib = None
+
+
+def load():
+    """Load the HIP library (once) and declare its prototypes."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"dvcp: HIP library not built ({LIB_PATH} missing). Run `make -j16` in "
+            "deepvcp-pointcloud-registration_amd/ or __graft_entry__.build().")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    lib.dvcp_last_error.restype = ctypes.c_char_p
+    lib.dvcp_last_error.argtypes = []
+    lib.dvcp_abi_version.restype = ctypes.c_int
+    lib.dvcp_abi_version.argtypes = []
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = ctypes.c_int
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return ["dvcp_last_error", "dvcp_abi_version"] + list(SIGNATURES)
+
+
+# When a list, every entry-point call appends (name, start_event, end_event) recorded on
+# torch's current stream (the stream the kernel is launched on) -- bench.py's live per-kernel
+# HIP-event timing.  None (the default) costs nothing.
+EVENT_LOG = None
+
+
+def call(name, *args):
+    """Call an entry point; raise RuntimeError with the library's message on failure."""
+    lib = load()
+    if EVENT_LOG is not None:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rc = getattr(lib, name)(*args)
+        e1.record()
+        EVENT_LOG.append((name, e0, e1))
+    else:
+        rc = getattr(lib, name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed ({rc}): {lib.dvcp_last_error().decode()}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (or None)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def dtype_code(t):
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.float64:
+        return F64
+    raise TypeError(f"dvcp: coordinates must be float32 or float64, got {t.dtype}")
+
+
+def require_gpu(*tensors):
+    """The product path has no CPU fallback: every operand must already live on a GPU."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("dvcp: no GPU available -- the HIP path has no CPU fallback")
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("dvcp: expected a GPU tensor, got one on " + str(t.device))
+
+
+def point_strides(t, point_dim, coord_dim):
+    """Element strides (batch, coord, point) of a 3-D point tensor."""
+    st = t.stride()
+    return st[0], st[coord_dim], st[point_dim]

@@ -1,0 +1,74 @@
+"""DeepVCP on the HIP path -- drop-in for deepVCP.py:16-110 (REF-R semantics).
+
+Same constructor, submodule names (FE1, WL, DFE, cpg) and state_dict keys as the reference
+(with the R1 shape changes of FE1.sa2/sa3), same forward signature and outputs:
+
+    forward(src_pts (B, C_in, N), tgt_pts (B, C_in, N), R_init (B|1, 3, 3) fp64, t_init)
+        -> (src_keypts (B, K, 3), tgt_vcp (B, K, 3) fp32)
+
+Pipeline (every stage a gfx950 HIP kernel, all on torch's current stream):
+    FE(src) [fps, ball query, grouped MLP x3, fc + weighting] -> top-K
+    -> key-point stage [gather, FPS among key points, ball query, Get_Cat_Feat_Src, R_init]
+    -> DFE(src) -> FE(tgt) -> candidate grid -> kNN(k=32) -> fused gather + DFE(tgt) -> CPG.
+The seven FPS start indices are drawn up front with torch.randint on the CPU generator in the
+reference's order (src sa1, sa2, sa3, key points, tgt sa1, sa2, sa3), so a seeded run draws the
+same starts as the reference.  t_init is unused, as in the reference (deepVCP.py:86).
+"""
+import torch
+import torch.nn as nn
+
+from . import ops
+from .cpg import cpg
+from .deep_feat_embedding import feat_embedding_layer
+from .deep_feat_extraction import feat_extraction_layer
+from .pointnet2_utils import _inference_only
+from .voxelize import grid_side
+from .weighting_layer import weighting_layer
+
+
+class DeepVCP(nn.Module):
+    def __init__(self, use_normal, K=64, r=1.0, s=0.4, fe_npoint=10000):
+        super().__init__()
+        self.FE1 = feat_extraction_layer(use_normal=use_normal, npoint=fe_npoint)
+        self.WL = weighting_layer()
+        self.DFE = feat_embedding_layer()
+        self.cpg = cpg()
+        self.K, self.r, self.s = K, r, s
+
+    def draw_starts(self, B, n_src, n_tgt):
+        """The reference's seven torch.randint(0, n, (B,)) draws, in call order."""
+        S1, S2, S3 = self.FE1.sa1.npoint, self.FE1.sa2.npoint, self.FE1.sa3.npoint
+        sizes = (n_src, S1, S2, self.K, n_tgt, S1, S2)
+        del S3
+        return torch.stack([torch.randint(0, n, (B,), dtype=torch.long) for n in sizes])
+
+    def forward(self, src_pts, tgt_pts, R_init, t_init, starts=None, trace=None):
+        _inference_only(self)
+        B = src_pts.shape[0]
+        K, r, s = self.K, self.r, self.s
+        dev = src_pts.device
+        if starts is None:
+            starts = self.draw_starts(B, src_pts.shape[2], tgt_pts.shape[2])
+        starts = starts.to(dev, non_blocking=True)
+
+        src_xyz, src_feat, score = self.FE1.run(src_pts, starts[0:3], wl=self.WL)
+        top = ops.topk(score, K)
+        keypts, src_cat, moved = ops.src_keypoints(src_xyz, src_feat, top, starts[3], R_init, radius=1.0, nsample=32)
+        src_dfe = ops.dfe(src_cat, self.DFE.packed_params())
+        tgt_xyz, tgt_feat, _ = self.FE1.run(tgt_pts, starts[4:7])
+
+        G = int((2 * r) / s + 1)                    # cpg.py:29
+        if grid_side(r, s) != G:
+            raise AssertionError("cpg.py:30: candidate count != grid_size^3")
+        cand, _ = ops.voxelize(moved, r, s, G, pdim=1)
+        C = G * G * G
+        qry = cand.view(B, K * C, 3)
+        dist, idx, _ = ops.knn(tgt_xyz, qry, 32, ref_pdim=2, qry_pdim=1, want_idx64=False)
+        tgt_dfe = ops.dfe_tgt(tgt_xyz, tgt_feat, qry, dist, idx, self.DFE.packed_params(), ref_pdim=2)
+        tgt_dfe = tgt_dfe.view(B, K, C, 32)
+        vcp = ops.cpg(src_dfe, tgt_dfe.permute(0, 1, 3, 2), cand, G, self.cpg.packed_params())
+        if trace is not None:
+            trace.update(src_xyz=src_xyz, src_feat=src_feat, score=score, topk=top, keypts=keypts,
+                         src_cat=src_cat, moved=moved, src_dfe=src_dfe, tgt_xyz=tgt_xyz, tgt_feat=tgt_feat,
+                         cand=cand, knn_dist=dist, knn_idx=idx, tgt_dfe=tgt_dfe)
+        return keypts, vcp

@@ -1,0 +1,35 @@
+"""Pose solve on the HIP path -- drop-in for deepVCP_loss.py:13-121.
+
+get_rigid_transform: Kabsch in fp64 (R = V U^T, no reflection fix, Q13).
+svd_optimization: SVD -> 1-NN inlier rejection (keep int(0.8 n)) -> SVD on (x1, R1 x1 + t1) (Q12).
+deepVCP_loss: alpha * L1 + (1 - alpha) * |mean|, one workgroup per pair (dvcp_svd_optimization).
+Set PRINT_LOSS = True to reproduce the reference's ``Loss: ...`` stdout line (:120), which the
+reference's loss_vis.py scrapes; it forces a host sync, so it is off by default.
+"""
+import torch
+
+from . import ops
+
+PRINT_LOSS = False
+
+
+def get_rigid_transform(x, y):
+    """(B, 3, n) fp64 pairs -> R (B, 3, 3), t (B, 3, 1)."""
+    return ops.rigid_transform(x, y)
+
+
+def svd_optimization(x, y_pred, R_true, t_true):
+    R2, t2, x1, y2, _ = ops.svd_optimization(x, y_pred, R_true, t_true)
+    return R2, t2, x1, y2
+
+
+def deepVCP_loss(x, y_pred, R_true, t_true, alpha):
+    """x, y_pred (B, K, 3); R_true (B, 3, 3); t_true (B, 3, 1) -> (loss, R (B,3,3), t (B,3,1))."""
+    x = x.permute(0, 2, 1).double()
+    y_pred = y_pred.permute(0, 2, 1).double()
+    R, t, x1, _, partial = ops.svd_optimization(x, y_pred, R_true, t_true)
+    denom = float(x1.numel())
+    loss = alpha * (partial[:, 0].sum() / denom) + (1 - alpha) * torch.abs(partial[:, 1].sum() / denom)
+    if PRINT_LOSS:
+        print(f"Loss: {loss}")
+    return loss, R, t

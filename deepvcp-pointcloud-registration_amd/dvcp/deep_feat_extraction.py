@@ -1,0 +1,64 @@
+"""Feature extraction layer on the HIP path -- drop-in for deep_feat_extraction.py (REF-R R1).
+
+Three set-abstraction layers (npoint 10000; r 0.1/0.2/0.4; nsample 256/128/64) chained on the
+previous layer's features, then ``fc`` 64 -> 32 (deep_feat_extraction.py:10-32 as repaired:
+the reference feeds sa2/sa3 the raw normals and never applies ``fc``, which crashes, C1/C2).
+"""
+import torch
+import torch.nn as nn
+
+from . import ops
+from ._params import cached_pack, linear_pack, linear_tensors
+from .pointnet2_utils import PointNetSetAbstraction, _inference_only
+
+
+def fe_config(use_normal=True, npoint=10000):
+    """deep_feat_extraction.py:10-13 (+R1 channels); npoint defaults to the literal 10000."""
+    c_in = 6 if use_normal else 3
+    return [
+        dict(npoint=npoint, radius=0.1, nsample=256, in_channel=c_in, mlp=[16, 16, 32]),
+        dict(npoint=npoint, radius=0.2, nsample=128, in_channel=32 + 3, mlp=[32, 64]),
+        dict(npoint=npoint, radius=0.4, nsample=64, in_channel=64 + 3, mlp=[64, 64]),
+    ]
+
+
+class feat_extraction_layer(nn.Module):
+    """deep_feat_extraction.py:5-32.  forward(pts (B, C_in, N)) -> (xyz (B, S, 3), feat (B, S, 32))."""
+
+    def __init__(self, use_normal=True, npoint=10000):
+        super().__init__()
+        self.use_normal = use_normal
+        cfg = fe_config(use_normal, npoint)
+        self.sa1 = PointNetSetAbstraction(**cfg[0])
+        self.sa2 = PointNetSetAbstraction(**cfg[1])
+        self.sa3 = PointNetSetAbstraction(**cfg[2])
+        self.fc = nn.Linear(64, 32)
+
+    def fc_params(self, wl=None):
+        lins = [self.fc] + ([wl.fc1[0], wl.fc2[0], wl.fc3[0]] if wl is not None else [])
+        return cached_pack(self, "head" if wl is None else "head_wl", linear_tensors(*lins),
+                           lambda: linear_pack(*lins))
+
+    def run(self, pts, starts=None, wl=None):
+        """Fused forward.  starts: (3, B) FPS start indices (drawn like the reference if None).
+        Returns xyz (B, 3, S) contiguous, feat (B, S, 32), score (B, S) when ``wl`` is given."""
+        _inference_only(self)
+        B, _, N = pts.shape
+        if self.use_normal:
+            xyz, feat = pts[:, :3, :], pts[:, 3:, :]
+        else:
+            xyz, feat = pts, None
+        if starts is None:
+            starts = [torch.randint(0, n, (B,), dtype=torch.long)
+                      for n in (N, self.sa1.npoint, self.sa2.npoint)]
+        xyz, feat = self.sa1(xyz, feat, start=starts[0])
+        xyz, feat = self.sa2(xyz, feat, start=starts[1])
+        xyz, feat = self.sa3(xyz, feat, start=starts[2])
+        S = xyz.shape[2]
+        f3 = feat.permute(0, 2, 1).reshape(B * S, 64)  # sa output is (B, S, 64) in memory
+        out, score = ops.fe_head(f3, self.fc_params(wl), with_score=wl is not None)
+        return xyz, out.view(B, S, 32), (score.view(B, S) if score is not None else None)
+
+    def forward(self, pts):
+        xyz, feat, _ = self.run(pts)
+        return xyz.permute(0, 2, 1), feat

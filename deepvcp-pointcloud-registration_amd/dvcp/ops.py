@@ -1,0 +1,243 @@
+"""Tensor-level wrappers of the HIP entry points (one function per C-ABI call).
+
+Every function takes GPU tensors, allocates its outputs with torch's caching allocator and
+launches on torch's current stream.  Point tensors are passed as strided views: ``pdim`` is
+the dimension that indexes points (1 for (B, N, 3), 2 for the reference's (B, 3, N)).
+"""
+import torch
+
+from . import _lib
+from ._lib import call, dtype_code, ptr, stream
+
+
+def _pts(t, pdim):
+    cdim = 3 - pdim
+    if t.dim() != 3 or t.shape[cdim] < 3:
+        raise ValueError(f"dvcp: expected a (B, N, 3)/(B, 3, N) point tensor, got {tuple(t.shape)}")
+    sb, sc, sn = _lib.point_strides(t, pdim, cdim)
+    return t.shape[pdim], sb, sc, sn
+
+
+def fps(xyz, npoint, start, pdim=1):
+    """pointnet2_utils.py:63-84.  Returns (idx (B, npoint) int64, centres (B, 3, npoint))."""
+    _lib.require_gpu(xyz, start)
+    B = xyz.shape[0]
+    N, sb, sc, sn = _pts(xyz, pdim)
+    start = start.to(device=xyz.device, dtype=torch.int64).contiguous()
+    idx = torch.empty(B, npoint, dtype=torch.int64, device=xyz.device)
+    ctr = torch.empty(B, 3, npoint, dtype=xyz.dtype, device=xyz.device)
+    call("dvcp_fps", dtype_code(xyz), ptr(xyz), sb, sc, sn, B, N, npoint, ptr(start), ptr(idx), ptr(ctr), stream())
+    return idx, ctr
+
+
+def ball_query(xyz, ctr, radius, nsample, pdim=1, cdim_pts=1, compact=True, padded=False):
+    """pointnet2_utils.py:87-107.  ``ctr`` uses point dim ``cdim_pts``.  Returns
+    (count (B,S) int32, list (B,S,ns) int32) and/or padded (B,S,ns) int64."""
+    _lib.require_gpu(xyz, ctr)
+    if xyz.dtype != ctr.dtype:
+        raise TypeError("dvcp.ball_query: xyz and centres must share a dtype")
+    B = xyz.shape[0]
+    N, sb, sc, sn = _pts(xyz, pdim)
+    S, cb, cc, cn = _pts(ctr, cdim_pts)
+    dev = xyz.device
+    count = torch.empty(B, S, dtype=torch.int32, device=dev) if compact else None
+    lst = torch.empty(B, S, nsample, dtype=torch.int32, device=dev) if compact else None
+    pad = torch.empty(B, S, nsample, dtype=torch.int64, device=dev) if padded else None
+    call("dvcp_ball_query", dtype_code(xyz), ptr(xyz), sb, sc, sn, N, ptr(ctr), cb, cc, cn, S, B, float(radius),
+         int(nsample), ptr(count), ptr(lst), ptr(pad), stream())
+    return count, lst, pad
+
+
+def square_distance(src, dst):
+    """pointnet2_utils.py:19-40 on (B, S, 3) / (B, N, 3)."""
+    _lib.require_gpu(src, dst)
+    B = src.shape[0]
+    S, sb, sc, sn = _pts(src, 1)
+    N, db, dc, dn = _pts(dst, 1)
+    out = torch.empty(B, S, N, dtype=src.dtype, device=src.device)
+    call("dvcp_square_distance", dtype_code(src), ptr(src), sb, sc, sn, S, ptr(dst), db, dc, dn, N, B, ptr(out),
+         stream())
+    return out
+
+
+def sa_group_mlp(xyz, ctr, feat, count, lst, nsample, chans, params, xyz_pdim=2, feat_ddim=1, feat_pdim=2):
+    """Grouping + [Conv1x1, BN, ReLU]* + max (pointnet2_utils.py:122-132, :195-200).
+    ``feat`` is None or a (B, D, N)-indexable strided view; output (B, S, C_last) fp32."""
+    _lib.require_gpu(xyz, ctr, count, lst, params)
+    B = xyz.shape[0]
+    N, sb, sc, sn = _pts(xyz, xyz_pdim)
+    S, cb, cc, cn = _pts(ctr, 2)
+    if feat is not None:
+        st = feat.stride()
+        D = feat.shape[feat_ddim]
+        fb, fd, fn = st[0], st[feat_ddim], st[feat_pdim]
+        fdt = dtype_code(feat)
+    else:
+        D, fb, fd, fn, fdt = 0, 0, 0, 0, _lib.F32
+    ch = torch.tensor(list(chans), dtype=torch.int32)  # host array, read by the launcher only
+    out = torch.empty(B, S, chans[-1], dtype=torch.float32, device=xyz.device)
+    call("dvcp_sa_group_mlp", dtype_code(xyz), ptr(xyz), sb, sc, sn, N, ptr(ctr), cb, cc, cn, S, B, fdt, ptr(feat),
+         fb, fd, fn, D, ptr(count), ptr(lst), int(nsample), len(chans) - 1, ptr(ch), ptr(params), ptr(out), stream())
+    return out
+
+
+def fe_head(x, params, with_score):
+    """deep_feat_extraction.py:15 fc (+ weighting_layer.py:26-30).  x (P, 64) fp32."""
+    _lib.require_gpu(x, params)
+    P = x.shape[0]
+    feat = torch.empty(P, 32, dtype=torch.float32, device=x.device)
+    score = torch.empty(P, dtype=torch.float32, device=x.device) if with_score else None
+    call("dvcp_fe_head", ptr(x), P, ptr(params), ptr(feat), ptr(score), stream())
+    return feat, score
+
+
+def weighting(feat, params):
+    _lib.require_gpu(feat, params)
+    P = feat.shape[0]
+    score = torch.empty(P, dtype=torch.float32, device=feat.device)
+    call("dvcp_weighting", ptr(feat), P, ptr(params), ptr(score), stream())
+    return score
+
+
+def topk(score, K):
+    """weighting_layer.py:31 on (B, S) scores -> (B, K) int64 (descending, ties -> lower index)."""
+    _lib.require_gpu(score)
+    B, S = score.shape
+    idx = torch.empty(B, K, dtype=torch.int64, device=score.device)
+    call("dvcp_topk", ptr(score), B, S, K, ptr(idx), stream())
+    return idx
+
+
+def src_keypoints(fe_xyz, fe_feat, topk_idx, kstart, R_init, radius=1.0, nsample=32):
+    """deepVCP.py:44-68 + get_cat_feat_src.py + deepVCP.py:86-91 (REF-R R2/R3)."""
+    _lib.require_gpu(fe_xyz, fe_feat, topk_idx, kstart, R_init)
+    B, _, S = fe_xyz.shape
+    K = topk_idx.shape[1]
+    if R_init.dtype != torch.float64:
+        # deepVCP.py:90 multiplies R_init with a .double() tensor; any other dtype raises there.
+        raise RuntimeError(f"expected R_init of dtype torch.float64, got {R_init.dtype}")
+    R = R_init.reshape(-1, 3, 3).contiguous()
+    if R.shape[0] not in (1, B):
+        raise RuntimeError(f"R_init batch {R.shape[0]} does not broadcast to B={B}")
+    r_b = 9 if R.shape[0] == B and B > 1 else 0
+    dev = fe_xyz.device
+    # keep every temporary alive across the launch (a freed block could be handed to the next
+    # allocation in the same argument list)
+    xyz_c, feat_c = fe_xyz.contiguous(), fe_feat.contiguous()
+    top_c, ks_c = topk_idx.contiguous(), kstart.to(device=dev, dtype=torch.int64).contiguous()
+    keypts = torch.empty(B, K, 3, dtype=fe_xyz.dtype, device=dev)
+    src_cat = torch.empty(B, K, nsample, 35, dtype=torch.float32, device=dev)
+    moved = torch.empty(B, K, 3, dtype=torch.float64, device=dev)
+    call("dvcp_src_keypoints", dtype_code(fe_xyz), ptr(xyz_c), ptr(feat_c), S, ptr(top_c), B, K, ptr(ks_c),
+         float(radius), int(nsample), ptr(R), r_b, ptr(keypts), ptr(src_cat), ptr(moved), stream())
+    return keypts, src_cat, moved
+
+
+def voxelize(pts, r, s, G, pdim=1):
+    """voxelize.py:19-83: (B, Kp, 3) -> (B, Kp, G^3, 3) fp32 candidates, plus an error flag."""
+    _lib.require_gpu(pts)
+    B = pts.shape[0]
+    Kp, pb, pc, pn = _pts(pts, pdim)
+    cand = torch.empty(B, Kp, G * G * G, 3, dtype=torch.float32, device=pts.device)
+    err = torch.zeros(1, dtype=torch.int32, device=pts.device)
+    call("dvcp_voxelize", dtype_code(pts), ptr(pts), pb, pc, pn, B, Kp, float(r), float(s), int(G), ptr(cand),
+         ptr(err), stream())
+    return cand, err
+
+
+def knn(ref, qry, k, ref_pdim=1, qry_pdim=1, want_idx64=True):
+    """Exact kNN (knn_cuda.KNN replacement).  Returns dist (B,Q,k) fp32, idx int32, idx64."""
+    _lib.require_gpu(ref, qry)
+    if ref.dtype != qry.dtype:
+        qry = qry.to(ref.dtype)  # both sides are cast to fp32 inside, like knn_cuda's .float()
+    B = ref.shape[0]
+    M, rb, rc, rn = _pts(ref, ref_pdim)
+    Q, qb, qc, qn = _pts(qry, qry_pdim)
+    dev = ref.device
+    dist = torch.empty(B, Q, k, dtype=torch.float32, device=dev)
+    idx = torch.empty(B, Q, k, dtype=torch.int32, device=dev)
+    idx64 = torch.empty(B, Q, k, dtype=torch.int64, device=dev) if want_idx64 else None
+    call("dvcp_knn", dtype_code(ref), ptr(ref), rb, rc, rn, M, ptr(qry), qb, qc, qn, Q, B, int(k), ptr(dist), ptr(idx),
+         ptr(idx64), stream())
+    return dist, idx, idx64
+
+
+def dfe(X, params):
+    """deep_feat_embedding.py on materialised rows: X (..., 32, 35) -> (..., 32) fp32."""
+    _lib.require_gpu(X, params)
+    lead = X.shape[:-2]
+    if tuple(X.shape[-2:]) != (32, 35):
+        raise RuntimeError(f"feat_embedding_layer expects (..., 32, 35), got {tuple(X.shape)}")
+    Xc = X.contiguous()
+    R = Xc.numel() // (32 * 35)
+    out = torch.empty(R, 32, dtype=torch.float32, device=X.device)
+    call("dvcp_dfe", dtype_code(Xc), ptr(Xc), R, ptr(params), ptr(out), stream())
+    return out.view(*lead, 32)
+
+
+def dfe_tgt(ref_xyz, ref_feat, cand, dist, idx, params, ref_pdim=2):
+    """get_cat_feat_tgt.py:54-96 fused with deep_feat_embedding.py:47-60.  cand (B, Q, 3)."""
+    _lib.require_gpu(ref_xyz, ref_feat, cand, dist, idx, params)
+    B = ref_xyz.shape[0]
+    M, rb, rc, rn = _pts(ref_xyz, ref_pdim)
+    Q = cand.shape[1]
+    feat_c, cand_c, dist_c, idx_c = ref_feat.contiguous(), cand.contiguous(), dist.contiguous(), idx.contiguous()
+    out = torch.empty(B, Q, 32, dtype=torch.float32, device=ref_xyz.device)
+    call("dvcp_dfe_tgt", dtype_code(ref_xyz), ptr(ref_xyz), rb, rc, rn, M, ptr(feat_c), ptr(cand_c), ptr(dist_c),
+         ptr(idx_c), B, Q, ptr(params), ptr(out), stream())
+    return out
+
+
+def cpg(src, tgt, cand, G, params, want_weight=False):
+    """cpg.py:27-60.  src (B, K, 32) or (B, K, 1, 32); tgt: the reference's (B, K, 32, C)
+    (any strides); cand (B, K, C, 3).  Returns vcp (B, K, 3) [, weights (B, K, C)]."""
+    _lib.require_gpu(src, tgt, cand, params)
+    B, K, C, _ = cand.shape
+    if tgt.dim() != 4 or tuple(tgt.shape) != (B, K, 32, C):
+        raise RuntimeError(f"cpg: tgt_dfe_feat must be (B, K, 32, C), got {tuple(tgt.shape)}")
+    if tgt.stride(0) != K * tgt.stride(1):
+        tgt = tgt.contiguous()
+    srcc = src.reshape(B * K, 32).contiguous().float()
+    candc = cand.contiguous()
+    vcp = torch.empty(B, K, 3, dtype=torch.float32, device=cand.device)
+    w = torch.empty(B, K, C, dtype=torch.float32, device=cand.device) if want_weight else None
+    call("dvcp_cpg", ptr(srcc), ptr(tgt), tgt.stride(1), tgt.stride(2), tgt.stride(3), ptr(candc), B * K, int(G),
+         ptr(params), ptr(vcp), ptr(w), stream())
+    return (vcp, w) if want_weight else vcp
+
+
+def rigid_transform(x, y):
+    """deepVCP_loss.py:13-44 on (B, 3, n) fp64."""
+    _lib.require_gpu(x, y)
+    x = x.double().contiguous()
+    y = y.double().contiguous()
+    B, _, n = x.shape
+    R = torch.empty(B, 3, 3, dtype=torch.float64, device=x.device)
+    t = torch.empty(B, 3, 1, dtype=torch.float64, device=x.device)
+    call("dvcp_rigid_transform", ptr(x), ptr(y), B, n, ptr(R), ptr(t), stream())
+    return R, t
+
+
+def svd_optimization(x, y_pred, R_true, t_true):
+    """deepVCP_loss.py:57-90 (+ the per-pair loss sums of :110-119)."""
+    _lib.require_gpu(x, y_pred, R_true, t_true)
+    x = x.double().contiguous()
+    y_pred = y_pred.double().contiguous()
+    B, _, n = x.shape
+    Rt = R_true.double().expand(B, 3, 3).contiguous()
+    tt = t_true.double()
+    if tt.dim() == 2:
+        tt = tt.unsqueeze(0)
+    if tt.shape[-1] != 1:
+        raise RuntimeError("t_true must broadcast as (B, 3, 1)")
+    tt = tt.expand(B, 3, 1).contiguous()
+    n_in = int(n * 0.8)
+    dev = x.device
+    R2 = torch.empty(B, 3, 3, dtype=torch.float64, device=dev)
+    t2 = torch.empty(B, 3, 1, dtype=torch.float64, device=dev)
+    x1 = torch.empty(B, 3, n_in, dtype=torch.float64, device=dev)
+    y2 = torch.empty(B, 3, n_in, dtype=torch.float64, device=dev)
+    partial = torch.empty(B, 2, dtype=torch.float64, device=dev)
+    call("dvcp_svd_optimization", ptr(x), ptr(y_pred), ptr(Rt), ptr(tt), B, n, ptr(R2), ptr(t2), ptr(x1), ptr(y2),
+         ptr(partial), stream())
+    return R2, t2, x1, y2, partial

@@ -1,0 +1,178 @@
+/* dvcp.h -- C ABI of libdvcp_hip.so, the MI355X (gfx950) DeepVCP registration hot path.
+ *
+ * The reference (vccheng2001/DeepVCP-Pointcloud-Registration) has no FFI: its boundary is
+ * the Python nn.Module / free-function surface.  Each entry point below
+ * replaces one reference interface, cited as file:line.  The Python host package
+ * (deepvcp-pointcloud-registration_amd/dvcp) binds them with ctypes and mirrors the
+ * reference module surface on top.
+ *
+ * Conventions
+ *   - Plain pointers and sizes, no torch types.  All buffers are device pointers allocated
+ *     by the caller; the library never allocates, frees or retains them.
+ *   - Strided point inputs: coordinate c (0..2) of point n of batch b lives at
+ *     p[b*sb + c*sc + n*sn] (element strides).  This covers both the reference's
+ *     channel-first (B,C,N) tensors and (B,N,3) rows without a copy.
+ *   - dtype: DVCP_F32 or DVCP_F64 for coordinate tensors (feature tensors are fp32, as the
+ *     reference's .float() casts make them).
+ *   - Every call is asynchronous on `stream` (a hipStream_t; NULL = default stream), never
+ *     synchronises the host and is safe to capture into a hipGraph.
+ *   - Return 0 on success, a negative DVCP_E* code otherwise; dvcp_last_error() gives a
+ *     thread-local message.
+ */
+#ifndef DVCP_H
+#define DVCP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DVCP_F32 0
+#define DVCP_F64 1
+
+#define DVCP_OK 0
+#define DVCP_EINVAL (-1)    /* bad argument / unsupported shape */
+#define DVCP_EHIP (-2)      /* HIP launch error */
+
+const char* dvcp_last_error(void);
+int dvcp_abi_version(void);
+
+/* Farthest point sampling.  Replaces pointnet2_utils.py:63-84 farthest_point_sample.
+ * xyz: B x N points (strided, dtype); start: B int64 start indices (the reference draws them
+ * with torch.randint on the CPU generator, :75 -- the caller does the same);
+ * out_idx: B x npoint int64; out_xyz (optional, may be NULL): B x 3 x npoint of dtype
+ * (the sampled centres, channel-first = the reference's new_xyz.permute(0,2,1)).
+ * Running minimum kept in fp32 for both dtypes (:74,:82), strict '<' update (:81),
+ * first-index argmax (:83). */
+int dvcp_fps(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N,
+             int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz, void* stream);
+
+/* Ball query.  Replaces pointnet2_utils.py:87-107 query_ball_point (and the
+ * square_distance expansion it uses, :19-40): the first `nsample` ascending point indices
+ * whose d2 = ((-2*dot) + |c|^2) + |p|^2 is not > radius^2 (dot = MKL's fma chain).
+ * xyz: B x N points, ctr: B x S centres (both strided, dtype).
+ * Outputs (each optional): count B x S int32 (number of distinct hits, <= nsample),
+ * list B x S x nsample int32 (the hits, ascending; entries >= count undefined),
+ * padded B x S x nsample int64 (reference format: padded with the first hit, or N if
+ * there is none). */
+int dvcp_ball_query(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
+                    const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
+                    double radius, int nsample, int32_t* count, int32_t* list,
+                    int64_t* padded, void* stream);
+
+/* Dense expansion-form squared distance, pointnet2_utils.py:19-40 (API completeness).
+ * out: B x S x N of dtype. */
+int dvcp_square_distance(int dtype, const void* src, int64_t sb, int64_t sc, int64_t sn, int S,
+                         const void* dst, int64_t db, int64_t dc, int64_t dn, int N, int B,
+                         void* out, void* stream);
+
+/* Grouped set-abstraction MLP.  Replaces pointnet2_utils.py:122-132 (grouping) +
+ * :195-200 ([Conv2d 1x1 + BN2d(eval) + ReLU] x L, max over nsample).  Rows are the
+ * distinct ball-query hits (count/list of dvcp_ball_query): the reference's padded
+ * duplicates repeat the first hit, so the max is identical.
+ * Row input = [ (p - c) cast to fp32 (3), feature (D) ]; features are read as
+ * feat[b*fb + d*fd + n*fn] of dtype feat_dtype (fp32 or fp64, cast to fp32), or NULL when D=0.
+ * Layers: nlayer in {2,3}; chans = {C0=3+D, C1, ..., C_nlayer}; for layer l:
+ * W_l (C_{l+1} x C_l), bias_l, bn_scale_l, bn_shift_l (all fp32) packed back-to-back in
+ * `params` in that order, layer by layer.  y = relu((W x + bias) * scale + shift).
+ * out: B x S x C_last fp32 (row-major per centre). */
+int dvcp_sa_group_mlp(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
+                      const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
+                      int feat_dtype, const void* feat, int64_t fb, int64_t fd, int64_t fn, int D,
+                      const int32_t* count, const int32_t* list, int nsample,
+                      int nlayer, const int* chans, const float* params, float* out,
+                      void* stream);
+
+/* Per-point affine + weighting MLP.  Replaces deep_feat_extraction.py:15 (fc, applied per
+ * REF-R R1) and weighting_layer.py:26-30 (Linear 32-16-8-1, ReLU, ReLU, Softplus).
+ * x: P x 64 fp32 -> feat: P x 32 fp32 (= fc(x)); score (optional, may be NULL): P fp32.
+ * params: fc.W(32x64), fc.b(32) [, wl1.W(16x32), wl1.b, wl2.W(8x16), wl2.b, wl3.W(1x8), wl3.b]. */
+int dvcp_fe_head(const float* x, int P, const float* params, float* feat, float* score,
+                 void* stream);
+
+/* Weighting layer alone.  Replaces weighting_layer.py:26-30 on given features:
+ * feat: P x 32 fp32 -> score: P fp32.  params: wl1.W(16x32), wl1.b, wl2.W(8x16), wl2.b,
+ * wl3.W(1x8), wl3.b. */
+int dvcp_weighting(const float* feat, int P, const float* params, float* score, void* stream);
+
+/* Top-K per row (descending value, ties to the lower index).  Replaces
+ * weighting_layer.py:31 torch.topk(X, K, dim=1).  score: B x S fp32 -> idx: B x K int64. */
+int dvcp_topk(const float* score, int B, int S, int K, int64_t* idx, void* stream);
+
+/* Source key-point stage, one workgroup per pair.  Replaces deepVCP.py:44-68 +
+ * get_cat_feat_src.py:16-55 with REF-R R2/R7 and deepVCP.py:86-91 (R3):
+ *   keypts = fe_xyz[topk]; FPS among the K key points (start = kstart[b]);
+ *   ball query r=radius, nsample among them; src_cat = [grouped - keypt, F[picked]*w] (Q4,Q5);
+ *   moved = R_init[b] @ keypts (fp64).
+ * fe_xyz: B x 3 x S (dtype, channel-first), fe_feat: B x S x 32 fp32, topk: B x K int64,
+ * R_init: B x 3 x 3 fp64 (row stride r_b: 0 broadcasts one matrix).
+ * Outputs: keypts B x K x 3 (dtype), src_cat B x K x nsample x 35 fp32 (the DFE input after
+ * its .float()), moved B x K x 3 fp64. */
+int dvcp_src_keypoints(int dtype, const void* fe_xyz, const float* fe_feat, int S,
+                       const int64_t* topk, int B, int K, const int64_t* kstart,
+                       double radius, int nsample, const double* R_init, int64_t r_b,
+                       void* keypts, float* src_cat, double* moved, void* stream);
+
+/* Candidate grid.  Replaces voxelize.py:19-83: cand[b,k,(ix*G+iy)*G+iz,a] =
+ * fp32(((c_a - r) - s/2) + s*i_a) evaluated in fp64 (torch.arange, Q9).
+ * pts: B x Kp points (strided, dtype) -> cand: B x Kp x G^3 x 3 fp32.
+ * err (optional int32): set to 1 if a point's per-axis arange length differs from G. */
+int dvcp_voxelize(int dtype, const void* pts, int64_t pb, int64_t pc, int64_t pn, int B, int Kp,
+                  double r, double s, int G, float* cand, int32_t* err, void* stream);
+
+/* Exact k-nearest neighbours (R6 contract: fp32 d2 = (dx*dx+dy*dy)+dz*dz, ascending, ties to
+ * the lower index, dist = sqrt(d2)).  Replaces knn_cuda.KNN (get_cat_feat_tgt.py:45,52;
+ * deepVCP_loss.py:70,72).  ref: B x M points, qry: B x Q points (both strided, dtype; cast to
+ * fp32 like knn_cuda).  Outputs (B x Q x k): dist fp32, idx int32 and/or idx64 int64 (any may
+ * be NULL).  k <= 32. */
+int dvcp_knn(int dtype, const void* ref, int64_t rb, int64_t rc, int64_t rn, int M,
+             const void* qry, int64_t qb, int64_t qc, int64_t qn, int Q, int B, int k,
+             float* dist, int32_t* idx, int64_t* idx64, void* stream);
+
+/* Deep feature embedding on a materialised input.  Replaces deep_feat_embedding.py:23-61
+ * (X.float(); Linear 35-32-32-32, no activations; MaxPool1d(32) over the neighbour axis).
+ * X: R x 32 x 35 rows of x_dtype (fp32/fp64) contiguous -> out: R x 32 fp32.
+ * params: fc1.W(32x35), fc1.b, fc2.W(32x32), fc2.b, fc3.W(32x32), fc3.b. */
+int dvcp_dfe(int x_dtype, const void* X, int64_t R, const float* params, float* out,
+             void* stream);
+
+/* Target-side fused gather + DFE.  Replaces get_cat_feat_tgt.py:54-96 (R4, R5, Q10) +
+ * deep_feat_embedding.py:47-60 without materialising the (B,K,C,32,35) fp64 tensor.
+ * For query q with neighbours j (idx/dist from dvcp_knn, k = 32):
+ *   X[j] = [ (ref[idx_j] - cand_q) -> fp32 (3),
+ *            fp32( F[idx_j, f] * (double(dist_f) / sum_j double(dist_j)) ) (32) ]
+ * ref_xyz: B x M (strided, dtype), ref_feat: B x M x 32 fp32, cand: B x Q x 3 fp32.
+ * out: B x Q x 32 fp32. */
+int dvcp_dfe_tgt(int dtype, const void* ref_xyz, int64_t rb, int64_t rc, int64_t rn, int M,
+                 const float* ref_feat, const float* cand, const float* dist, const int32_t* idx,
+                 int B, int Q, const float* params, float* out, void* stream);
+
+/* Corresponding point generation.  Replaces cpg.py:27-60: cost volume
+ * (src - scrambled tgt)^2 (Q11), Conv3d 32-16-4-1 (k3, p1, no activations), softmax over C,
+ * vcp = sum(w*cand)/sum(w).
+ * src: P x 32 fp32 (P = B*K key points); tgt: the reference's (B,K,32,C) tensor given by
+ * element strides (t_p per key point, t_f per feature, t_c per candidate);
+ * cand: P x C x 3 fp32; params: conv1.W(16x32x27), conv1.b, conv2.W(4x16x27), conv2.b,
+ * conv3.W(1x4x27), conv3.b.  out: P x 3 fp32; weight (optional): P x C softmax weights. */
+int dvcp_cpg(const float* src, const float* tgt, int64_t t_p, int64_t t_f, int64_t t_c,
+             const float* cand, int P, int G, const float* params, float* vcp, float* weight,
+             void* stream);
+
+/* Kabsch.  Replaces deepVCP_loss.py:13-44 get_rigid_transform: x, y: B x 3 x n fp64
+ * (contiguous) -> R: B x 3 x 3, t: B x 3 x 1 (fp64). R = V U^T, no reflection fix (Q13). */
+int dvcp_rigid_transform(const double* x, const double* y, int B, int n, double* R, double* t,
+                         void* stream);
+
+/* Two-pass pose solve.  Replaces deepVCP_loss.py:57-90 svd_optimization (+ the loss terms of
+ * :105-121).  x, y_pred: B x 3 x n fp64; R_true: B x 3 x 3; t_true: B x 3 x 1 (fp64).
+ * Outputs: R2 B x 3 x 3, t2 B x 3 x 1, x1 / y_pred2 (optional) B x 3 x n_in with
+ * n_in = int(n * 0.8); partial (optional) B x 2: per pair sum|y_pred2 - y_true1| and
+ * sum(y_pred2 - y_true1) for the loss. */
+int dvcp_svd_optimization(const double* x, const double* y_pred, const double* R_true,
+                          const double* t_true, int B, int n, double* R2, double* t2,
+                          double* x1, double* y2, double* partial, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DVCP_H */

@@ -1,0 +1,66 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library loads, exports every entry point
+declared in include/dvcp.h, the ctypes prototypes cover them all, and the product path has no
+CPU fallback (ops raise instead of computing when no GPU is present)."""
+import os
+import re
+import subprocess
+
+import pytest
+import torch
+
+from conftest import PKG, ROOT
+
+HEADER = os.path.join(ROOT, "include", "dvcp.h")
+
+
+def declared():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(dvcp_\w+)\s*\(", text, re.M)))
+
+
+def test_header_declares_entry_points():
+    names = declared()
+    assert "dvcp_fps" in names and "dvcp_knn" in names and "dvcp_svd_optimization" in names
+    assert len(names) >= 17
+
+
+def test_library_exports_every_declared_symbol():
+    import dvcp
+    from dvcp import _lib
+    lib = dvcp.load_library()
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (dvcp_\w+)", out))
+    missing = [n for n in declared() if n not in exported]
+    assert not missing, missing
+    assert sorted(_lib.exported_symbols()) == declared()
+    assert lib.dvcp_abi_version() == 1
+
+
+def test_error_path_reports_message():
+    import dvcp
+    from dvcp import _lib
+    dvcp.load_library()
+    with pytest.raises(RuntimeError, match="null pointer"):
+        _lib.call("dvcp_fps", 7, None, 0, 0, 0, 1, 1, 1, _lib.ctypes.c_void_p(8), _lib.ctypes.c_void_p(8), None, None)
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU behaviour")
+def test_no_cpu_fallback():
+    import dvcp
+    import dvcp.pointnet2_utils as P
+    x = torch.rand(1, 100, 3)
+    with pytest.raises(RuntimeError, match="no GPU"):
+        P.farthest_point_sample(x, 10)
+    with pytest.raises(RuntimeError, match="no GPU"):
+        dvcp.KNN(k=4, transpose_mode=True)(x, x)
+    m = dvcp.DeepVCP(use_normal=False, fe_npoint=16).eval()
+    with pytest.raises(RuntimeError):
+        m(torch.rand(1, 3, 64), torch.rand(1, 3, 64), torch.eye(3, dtype=torch.float64)[None], torch.zeros(1, 3))
+
+
+def test_product_never_imports_oracle():
+    for dirpath, _, files in os.walk(os.path.join(PKG, "dvcp")):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                assert "import oracle" not in src and "from oracle" not in src, f

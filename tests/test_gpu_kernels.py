@@ -1,0 +1,348 @@
+"""GPU parity of every HIP kernel against the oracle (golden fixtures + live, seeded).
+
+Bars: bit-exact for indices (FPS, ball query, kNN, top-k, candidate grid) and kNN distances;
+fp32 feature stages within rtol 1e-5 / atol 1e-5 of the oracle's torch CPU ops (different fp32
+summation order); fp64 pose solve within 1e-9.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def golden(name):
+    return np.load(os.path.join(GOLDEN, name + ".npz"))
+
+
+def T(a, dev=None):
+    t = torch.from_numpy(np.asarray(a))
+    return t.to(dev) if dev is not None else t
+
+
+def ball_mismatch_ok(xyz, ctr, got, want, radius, ulps=4):
+    """Rows that differ may only differ by points whose d2 sits within `ulps` of radius^2."""
+    import oracle as O
+    bad = (got != want).any(-1)
+    if not bad.any():
+        return True
+    d2 = O.square_distance(ctr, xyz)
+    r2 = torch.tensor(radius ** 2, dtype=xyz.dtype)
+    tol = ulps * torch.finfo(xyz.dtype).eps * float(r2)
+    for b, s in bad.nonzero().tolist():
+        a, w = set(got[b, s].tolist()), set(want[b, s].tolist())
+        for n in a ^ w:
+            if n < xyz.shape[1] and abs(float(d2[b, s, n]) - float(r2)) > tol:
+                return False
+    return True
+
+
+# ---------------------------------------------------------------------------------------- FPS
+@pytest.mark.parametrize("name", ["fps_f32", "fps_dyadic", "fps_f64"])
+def test_fps_golden(cuda, name):
+    import dvcp.pointnet2_utils as P
+    from dvcp import ops
+    z = golden(name)
+    xyz = T(z["xyz"], cuda)
+    idx = P.farthest_point_sample(xyz, int(z["npoint"]), start=T(z["start"]))
+    assert torch.equal(idx.cpu(), T(z["idx"]))
+    # channel-first layout + sampled centres
+    idx2, ctr = ops.fps(xyz.transpose(1, 2).contiguous(), int(z["npoint"]), T(z["start"], cuda), pdim=2)
+    assert torch.equal(idx2, idx)
+    gathered = torch.stack([xyz[b, idx[b]] for b in range(xyz.shape[0])]).transpose(1, 2)
+    assert torch.equal(ctr, gathered)
+
+
+def test_fps_live_vs_oracle(cuda):
+    import oracle as O
+    import dvcp.pointnet2_utils as P
+    g = torch.Generator().manual_seed(101)
+    for N, npoint in ((16384, 2000), (10000, 10000), (333, 1000), (5, 7)):
+        xyz = torch.rand(2, N, 3, generator=g) * 2 - 1
+        start = torch.randint(0, N, (2,), generator=g)
+        want = O.farthest_point_sample(xyz, npoint, start)
+        got = P.farthest_point_sample(xyz.to(cuda), npoint, start=start).cpu()
+        assert torch.equal(got, want), (N, npoint)
+
+
+def test_fps_full_size_property(cuda):
+    """C3 scale: 16384 -> 10000; the min-distance of each newly picked point to the already
+    picked set never increases (the defining FPS invariant), and no index repeats."""
+    from dvcp import ops
+    g = torch.Generator().manual_seed(102)
+    xyz = (torch.rand(4, 16384, 3, generator=g) * 2 - 1).to(cuda)
+    idx, _ = ops.fps(xyz, 10000, torch.tensor([0, 1, 16383, 7]).to(cuda), pdim=1)
+    for b in range(4):
+        assert idx[b].unique().numel() == 10000
+        sel = xyz[b, idx[b]].double()
+        dmin = torch.full((16384,), float("inf"), dtype=torch.float64, device=cuda)
+        prev = []
+        x64 = xyz[b].double()
+        for i in range(0, 400):
+            p = sel[i]
+            if i > 0:
+                prev.append(float(dmin[idx[b, i]]))
+            dmin = torch.minimum(dmin, ((x64 - p) ** 2).sum(-1))
+        prev = torch.tensor(prev)
+        assert (prev[1:] <= prev[:-1] * (1 + 1e-6) + 1e-12).all()
+
+
+# --------------------------------------------------------------------------------- ball query
+@pytest.mark.parametrize("name,radii", [("ball_f32", [(0.1, 256), (0.2, 128), (0.4, 64)]),
+                                         ("ball_dyadic", [(0.25, 32), (0.25, 200)]),
+                                         ("ball_f64", [(0.2, 128)])])
+def test_ball_query_golden(cuda, name, radii):
+    import dvcp.pointnet2_utils as P
+    z = golden(name)
+    xyz, ctr = T(z["xyz"]), T(z["ctr"])
+    for r, ns in radii:
+        got = P.query_ball_point(r, ns, xyz.to(cuda), ctr.to(cuda)).cpu()
+        want = T(z[f"idx_{ns}"])
+        if "dyadic" in name:
+            assert torch.equal(got, want)
+        else:
+            assert ball_mismatch_ok(xyz, ctr, got, want, r)
+
+
+def test_ball_query_compact_matches_padded(cuda):
+    from dvcp import ops
+    g = torch.Generator().manual_seed(103)
+    xyz = (torch.rand(2, 5000, 3, generator=g) * 2 - 1).to(cuda)
+    ctr = xyz[:, :700].contiguous()
+    cnt, lst, pad = ops.ball_query(xyz, ctr, 0.2, 128, padded=True)
+    for b in range(2):
+        for s in range(0, 700, 37):
+            c = int(cnt[b, s])
+            assert 1 <= c <= 128
+            hits = lst[b, s, :c].long()
+            assert torch.equal(pad[b, s, :c], hits)
+            assert (pad[b, s, c:] == hits[0]).all()
+            assert (hits[1:] > hits[:-1]).all()
+
+
+def test_ball_query_no_hit_pads_with_N(cuda):
+    import dvcp.pointnet2_utils as P
+    xyz = torch.zeros(1, 10, 3, device=cuda)
+    ctr = torch.full((1, 2, 3), 5.0, device=cuda)
+    assert (P.query_ball_point(0.5, 4, xyz, ctr) == 10).all()
+
+
+def test_square_distance(cuda):
+    import oracle as O
+    import dvcp.pointnet2_utils as P
+    g = torch.Generator().manual_seed(104)
+    a, b = torch.rand(2, 300, 3, generator=g), torch.rand(2, 700, 3, generator=g)
+    got = P.square_distance(a.to(cuda), b.to(cuda)).cpu()
+    assert torch.equal(got, O.square_distance(a, b))
+
+
+# ---------------------------------------------------------------------------------------- kNN
+@pytest.mark.parametrize("name", ["knn_f32", "knn_dyadic"])
+def test_knn_golden(cuda, name):
+    from dvcp.knn import KNN
+    z = golden(name)
+    d, i = KNN(k=32, transpose_mode=True)(T(z["ref"], cuda), T(z["qry"], cuda))
+    assert torch.equal(i.cpu(), T(z["idx"]))
+    assert torch.equal(d.cpu(), T(z["dist"]))
+
+
+def test_knn_k1_transpose_false(cuda):
+    from dvcp.knn import KNN
+    z = golden("knn_k1")
+    ref, qry = T(z["ref"], cuda).transpose(1, 2), T(z["qry"], cuda).transpose(1, 2)
+    d, i = KNN(k=1, transpose_mode=False)(ref, qry)
+    assert torch.equal(i.cpu(), T(z["idx"])) and torch.equal(d.cpu(), T(z["dist"]))
+
+
+def test_knn_f64_reference_is_cast(cuda):
+    import oracle as O
+    from dvcp.knn import KNN
+    g = torch.Generator().manual_seed(105)
+    ref = torch.rand(1, 800, 3, generator=g, dtype=torch.float64)
+    qry = torch.rand(1, 900, 3, generator=g, dtype=torch.float64)
+    dw, iw = O.KNN(k=16, transpose_mode=True)(ref, qry)
+    d, i = KNN(k=16, transpose_mode=True)(ref.to(cuda), qry.to(cuda))
+    assert torch.equal(i.cpu(), iw) and torch.equal(d.cpu(), dw)
+
+
+# ------------------------------------------------------------------------------- voxel grid
+def test_voxelize_golden(cuda):
+    import dvcp
+    z = golden("voxel")
+    pts = T(z["pts"], cuda)
+    assert torch.equal(dvcp.voxelize(pts, 2.0, 0.4).cpu(), T(z["cand_r2"]))
+    assert torch.equal(dvcp.voxelize(pts, 1.0, 0.4).cpu(), T(z["cand_r1"]))
+    assert torch.equal(dvcp.voxelize_point(pts[0, 1], 2.0, 0.4).cpu(), T(z["cand_r2"])[0, 1])
+
+
+# ------------------------------------------------------------------------ set abstraction
+@pytest.mark.parametrize("normals", [False, True])
+def test_set_abstraction_vs_oracle(cuda, normals):
+    import oracle as O
+    import dvcp.pointnet2_utils as P
+    from tests_helpers import randomize_bn
+    g = torch.Generator().manual_seed(106)
+    B, N, S = 2, 3000, 700
+    dt = torch.float64 if normals else torch.float32
+    for cfg in O.fe_config(use_normal=normals, npoint=S):
+        torch.manual_seed(7)
+        ref = O.PointNetSetAbstraction(**cfg).eval()
+        randomize_bn(ref)
+        mine = P.PointNetSetAbstraction(**cfg).eval()
+        mine.load_state_dict(ref.state_dict())
+        mine.to(cuda)
+        xyz = (torch.rand(B, 3, N, generator=g, dtype=torch.float64) * 2 - 1).to(dt)
+        D = cfg["in_channel"] - 3
+        feats = torch.randn(B, D, N, generator=g, dtype=dt if D == 3 else torch.float32) if D else None
+        start = torch.randint(0, N, (B,), generator=g)
+        with torch.no_grad():
+            O_xyz, O_f = _sa_oracle(ref, xyz, feats, start)
+            G_xyz, G_f = mine(xyz.to(cuda), feats.to(cuda) if feats is not None else None, start=start)
+        assert torch.equal(G_xyz.cpu(), O_xyz)
+        torch.testing.assert_close(G_f.cpu(), O_f, rtol=1e-5, atol=1e-5)
+
+
+def _sa_oracle(ref, xyz, feats, start):
+    import oracle as O
+    orig = O.ref_r.farthest_point_sample
+
+    def fps_fixed(x, npoint, start_=None):
+        return orig(x, npoint, start)
+
+    O.ref_r.farthest_point_sample = fps_fixed
+    try:
+        return ref(xyz, feats)
+    finally:
+        O.ref_r.farthest_point_sample = orig
+
+
+# ------------------------------------------------------------------------------ heads, top-k
+def test_fe_head_and_weighting(cuda):
+    import oracle as O
+    import dvcp
+    g = torch.Generator().manual_seed(107)
+    torch.manual_seed(3)
+    fe = O.feat_extraction_layer(use_normal=False, npoint=16)
+    wl = O.weighting_layer()
+    x = torch.randn(5000, 64, generator=g)
+    mine_fe = dvcp.feat_extraction_layer(use_normal=False, npoint=16).eval()
+    mine_fe.load_state_dict(fe.state_dict())
+    mine_wl = dvcp.weighting_layer().eval()
+    mine_wl.load_state_dict(wl.state_dict())
+    mine_fe.to(cuda), mine_wl.to(cuda)
+    from dvcp import ops
+    feat, score = ops.fe_head(x.to(cuda), mine_fe.fc_params(mine_wl), with_score=True)
+    with torch.no_grad():
+        f_ref = fe.fc(x)
+        s_ref = wl.fc3(wl.fc2(wl.fc1(f_ref)))[:, 0]
+    torch.testing.assert_close(feat.cpu(), f_ref, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(score.cpu(), s_ref, rtol=1e-5, atol=1e-6)
+    s2 = mine_wl.scores(f_ref.view(1, 5000, 32).to(cuda))
+    torch.testing.assert_close(s2.cpu()[0], s_ref, rtol=1e-5, atol=1e-6)
+
+
+def test_topk(cuda):
+    from dvcp import ops
+    g = torch.Generator().manual_seed(108)
+    s = torch.rand(3, 10000, generator=g)
+    got = ops.topk(s.to(cuda), 64).cpu()
+    assert torch.equal(got, torch.topk(s, 64, dim=1).indices)
+    tied = torch.tensor([[1.0, 5.0, 5.0, 2.0, 5.0, 0.0]])
+    assert ops.topk(tied.to(cuda), 4).cpu().tolist() == [[1, 2, 4, 3]]  # value desc, index asc
+
+
+# ------------------------------------------------------------------------------ DFE / CPG
+def test_dfe_vs_oracle(cuda):
+    import oracle as O
+    import dvcp
+    g = torch.Generator().manual_seed(109)
+    torch.manual_seed(4)
+    ref = O.feat_embedding_layer()
+    mine = dvcp.feat_embedding_layer().eval()
+    mine.load_state_dict(ref.state_dict())
+    mine.to(cuda)
+    Xs = torch.randn(2, 64, 32, 35, generator=g, dtype=torch.float64)
+    Xt = torch.randn(2, 5, 27, 32, 35, generator=g)
+    with torch.no_grad():
+        torch.testing.assert_close(mine(Xs.to(cuda), src=True).cpu(), ref(Xs, src=True), rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(mine(Xt.to(cuda), src=False).cpu(), ref(Xt, src=False), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("f64", [False, True])
+def test_dfe_tgt_fused_vs_oracle(cuda, f64):
+    import oracle as O
+    import dvcp
+    from dvcp import ops
+    g = torch.Generator().manual_seed(110)
+    dt = torch.float64 if f64 else torch.float32
+    B, K, G, M = 2, 3, 6, 900
+    C = G ** 3
+    torch.manual_seed(5)
+    dfe_ref = O.feat_embedding_layer()
+    mine = dvcp.feat_embedding_layer().eval()
+    mine.load_state_dict(dfe_ref.state_dict())
+    mine.to(cuda)
+    ref_xyz = (torch.rand(B, M, 3, generator=g, dtype=torch.float64) * 2 - 1).to(dt)
+    ref_feat = torch.randn(B, M, 32, generator=g)
+    cand = O.voxelize(torch.rand(B, K, 3, generator=g, dtype=torch.float64) - 0.5, 1.0, 0.4)
+    with torch.no_grad():
+        cat = O.Get_Cat_Feat_Tgt()(cand, torch.zeros(B, K, 3), ref_xyz, ref_feat)
+        want = dfe_ref(cat, src=False)
+    qry = cand.view(B, K * C, 3).to(cuda)
+    dist, idx, _ = ops.knn(ref_xyz.to(cuda), qry, 32, ref_pdim=1, qry_pdim=1)
+    got = ops.dfe_tgt(ref_xyz.to(cuda), ref_feat.to(cuda), qry, dist, idx, mine.packed_params(), ref_pdim=1)
+    torch.testing.assert_close(got.view(B, K, C, 32).cpu(), want, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("r", [1.0, 2.0])
+def test_cpg_vs_oracle(cuda, r):
+    import oracle as O
+    import dvcp
+    g = torch.Generator().manual_seed(111)
+    torch.manual_seed(6)
+    ref = O.cpg()
+    mine = dvcp.cpg().eval()
+    mine.load_state_dict(ref.state_dict())
+    mine.to(cuda)
+    G = int(2 * r / 0.4 + 1)
+    C = G ** 3
+    B, K = 2, 8
+    src = torch.randn(B, K, 1, 32, generator=g)
+    tgt = torch.randn(B, K, C, 32, generator=g).permute(0, 1, 3, 2)   # the reference's permuted view
+    cand = torch.randn(B, K, C, 3, generator=g)
+    with torch.no_grad(), O.tracing() as tr:
+        want = ref(src, tgt, cand, r, 0.4)
+    got, w = mine(src.to(cuda), tgt.to(cuda), cand.to(cuda), r, 0.4, return_weights=True)
+    torch.testing.assert_close(got.cpu(), want, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(w.cpu(), dict(tr)["cpg_weight"], rtol=1e-4, atol=1e-7)
+
+
+# ------------------------------------------------------------------------------ pose solve
+def test_rigid_golden(cuda):
+    import dvcp
+    z = golden("rigid")
+    x, y = T(z["x"], cuda), T(z["y"], cuda)
+    Rt, tt = T(z["R_true"], cuda), T(z["t_true"], cuda)
+    loss, R, t = dvcp.deepVCP_loss(x, y, Rt, tt, 0.5)
+    torch.testing.assert_close(R.cpu(), T(z["R"]), rtol=0, atol=1e-9)
+    torch.testing.assert_close(t.cpu(), T(z["t"]), rtol=0, atol=1e-9)
+    torch.testing.assert_close(loss.cpu(), T(z["loss"]), rtol=1e-9, atol=1e-12)
+    R1, t1 = dvcp.get_rigid_transform(x.transpose(1, 2), y.double().transpose(1, 2))
+    torch.testing.assert_close(R1.cpu(), T(z["R1"]), rtol=0, atol=1e-9)
+    torch.testing.assert_close(t1.cpu(), T(z["t1"]), rtol=0, atol=1e-9)
+
+
+def test_rigid_exact_rotation_and_reflection(cuda):
+    import dvcp
+    from dvcp.synthetic import rot_xyz
+    g = torch.Generator().manual_seed(112)
+    x = torch.randn(2, 3, 50, generator=g, dtype=torch.float64)
+    R = torch.from_numpy(np.stack([rot_xyz(0.3, 1.2, -2.0), np.diag([1.0, 1.0, -1.0])]))
+    t = torch.tensor([[[0.5], [-1.0], [2.0]], [[0.0], [0.0], [0.0]]], dtype=torch.float64)
+    Rg, tg = dvcp.get_rigid_transform(x.to(cuda), (R @ x + t).to(cuda))
+    torch.testing.assert_close(Rg.cpu(), R, rtol=0, atol=1e-12)     # Q13: the reflection is returned as-is
+    torch.testing.assert_close(tg.cpu(), t, rtol=0, atol=1e-12)
