@@ -34,6 +34,11 @@ __device__ __forceinline__ float fma_rn<float>(float a, float b, float c) { retu
 template <>
 __device__ __forceinline__ double fma_rn<double>(double a, double b, double c) { return __fma_rn(a, b, c); }
 
+// Correctly rounded fp32 sqrt (torch's CPU sqrt is IEEE): fp64 sqrt then narrowing is exact
+// for fp32 inputs (53 >= 2*24 + 2), and the fp64 sqrt is correctly rounded.
+__device__ __forceinline__ float sqrt_rn(float x) { return static_cast<float>(__dsqrt_rn(static_cast<double>(x))); }
+__device__ __forceinline__ double sqrt_rn(double x) { return __dsqrt_rn(x); }
+
 // |p|^2 as torch.sum(p ** 2, -1) rounds it: ((x*x + y*y) + z*z), no fma.
 template <typename T>
 __device__ __forceinline__ T sumsq3(T x, T y, T z) { return (x * x + y * y) + z * z; }

@@ -101,7 +101,7 @@ __global__ __launch_bounds__(kKpThreads) void src_keypoints_kernel(
     const int c = fidx[i], p = pidx[e];
     const T gx = kx[p] - kx[c], gy = ky[p] - ky[c], gz = kz[p] - kz[c];
     const T ex = (kx[i] - gx) + eps, ey = (ky[i] - gy) + eps, ez = (kz[i] - gz) + eps;
-    dist[e] = sqrt(fma_rn<T>(ez, ez, fma_rn<T>(ey, ey, ex * ex)));
+    dist[e] = sqrt_rn(fma_rn<T>(ez, ez, fma_rn<T>(ey, ey, ex * ex)));
   }
   __syncthreads();
   if (tid < K) {

@@ -72,15 +72,16 @@ __global__ __launch_bounds__(kKnnThreads) void knn_kernel(PointsView<T> ref, int
 #pragma unroll
   for (int t = 0; t < KT; ++t) {
     if (t < k) {
-      if (dist) dist[o + t] = __fsqrt_rn(kd[t]);
+      if (dist) dist[o + t] = sqrt_rn(kd[t]);
       if (idx) idx[o + t] = ki[t];
       if (idx64) idx64[o + t] = ki[t];
     }
   }
 }
 
-// torch.arange(start, end, s) values fp32(start + s*i) with start = (c - r) - s/2, end = c + r,
-// all in fp64 (voxelize.py:62-64); length ceil((end - start)/s) must equal G (cpg.py:29-30).
+// torch.arange(start, end, s) values fp32(fma(s, i, start)) with start = (c - r) - s/2,
+// end = c + r, all in fp64 (voxelize.py:62-64; torch's CPU arange kernel is compiled with fma
+// contraction, visible at zero crossings); length ceil((end - start)/s) must equal G (cpg.py:29-30).
 template <typename T>
 __global__ void voxelize_kernel(PointsView<T> pts, int Kp, double r, double s, int G, float* __restrict__ cand,
                                 int32_t* __restrict__ err) {
@@ -97,7 +98,7 @@ __global__ void voxelize_kernel(PointsView<T> pts, int Kp, double r, double s, i
     const double lo = m - r, hi = m + r;
     const double start = lo - s / 2;
     if (err && c == 0 && static_cast<int>(ceil((hi - start) / s)) != G) *err = 1;
-    o[a] = static_cast<float>(start + s * static_cast<double>(ii[a]));
+    o[a] = static_cast<float>(__fma_rn(s, static_cast<double>(ii[a]), start));
   }
 }
 

@@ -176,7 +176,7 @@ __global__ __launch_bounds__(kRgThreads) void svd_opt_kernel(const double* __res
       const float d2 = (dx * dx + dy * dy) + dz * dz;
       best = d2 < best ? d2 : best;
     }
-    nn[j] = __fsqrt_rn(best);
+    nn[j] = sqrt_rn(best);
   }
   __syncthreads();
   // inliers: rank by (distance, index); rank < n_in lands at position rank

@@ -1,7 +1,7 @@
 """Candidate grid on the HIP path -- drop-in for voxelize.py:19-83.
 
-cand[b, n, (ix*G + iy)*G + iz, a] = fp32(((c_a - r) - s/2) + s*i_a), evaluated in fp64 like
-torch.arange (Q9: the grid is offset by -s/2, no sphere rejection).
+cand[b, n, (ix*G + iy)*G + iz, a] = fp32(fma(s, i_a, (c_a - r) - s/2)), evaluated in fp64 like
+torch's CPU arange (Q9: the grid is offset by -s/2, no sphere rejection).
 """
 import math
 

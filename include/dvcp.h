@@ -114,7 +114,7 @@ int dvcp_src_keypoints(int dtype, const void* fe_xyz, const float* fe_feat, int 
                        void* keypts, float* src_cat, double* moved, void* stream);
 
 /* Candidate grid.  Replaces voxelize.py:19-83: cand[b,k,(ix*G+iy)*G+iz,a] =
- * fp32(((c_a - r) - s/2) + s*i_a) evaluated in fp64 (torch.arange, Q9).
+ * fp32(fma(s, i_a, (c_a - r) - s/2)) evaluated in fp64 (torch.arange, Q9).
  * pts: B x Kp points (strided, dtype) -> cand: B x Kp x G^3 x 3 fp32.
  * err (optional int32): set to 1 if a point's per-axis arange length differs from G. */
 int dvcp_voxelize(int dtype, const void* pts, int64_t pb, int64_t pc, int64_t pn, int B, int Kp,

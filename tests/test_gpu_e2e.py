@@ -14,10 +14,15 @@ from tests_helpers import golden, golden_state_dict
 pytestmark = pytest.mark.gpu
 
 
-def _near_tie(score, K):
-    s, _ = torch.sort(score.double(), dim=-1, descending=True)
-    gap = (s[:, K - 1] - s[:, K]).abs() / s[:, K - 1].abs().clamp_min(1e-30)
-    return bool((gap < 1e-5).any())
+def _near_tie(score, K, rel=1e-5):
+    """True if two distinct values among the oracle's top K+1 scores are closer than `rel`
+    (relative): then the reference's own top-k order/set is decided by fp32 rounding.  Exactly
+    equal scores come from duplicated FE points (N < npoint, Q1) and are value-identical."""
+    for row in score.double():
+        s = torch.unique(torch.sort(row, descending=True).values[: K + 1])
+        if s.numel() > 1 and bool(((s[1:] - s[:-1]) / s[1:].abs().clamp_min(1e-30) < rel).any()):
+            return True
+    return False
 
 
 def _run_fixture(cuda, name):
@@ -69,11 +74,14 @@ def test_e2e_live_full_size_pair(cuda):
     import oracle as O
     import dvcp
     from dvcp.synthetic import make_pairs
-    from tests_helpers import randomize_bn
+    from dvcp.synthetic import condition_weights, randomize_bn
     src, tgt, R_gt, t_gt = make_pairs(1, 16384, seed=777)
     torch.manual_seed(0)
     ref = O.DeepVCP(use_normal=False, K=64, r=2.0, s=0.4).eval()
     randomize_bn(ref)
+    with torch.no_grad():
+        _, calib = ref.FE1(src)
+    condition_weights(ref, feats=calib)
     mine = dvcp.DeepVCP(use_normal=False, K=64, r=2.0, s=0.4).eval()
     mine.load_state_dict(ref.state_dict())
     mine.to(cuda)

@@ -210,8 +210,8 @@ def _sa_oracle(ref, xyz, feats, start):
     import oracle as O
     orig = O.ref_r.farthest_point_sample
 
-    def fps_fixed(x, npoint, start_=None):
-        return orig(x, npoint, start)
+    def fps_fixed(x, npoint, start=None, _fixed=start):
+        return orig(x, npoint, _fixed)
 
     O.ref_r.farthest_point_sample = fps_fixed
     try:
