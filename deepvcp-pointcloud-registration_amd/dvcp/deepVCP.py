@@ -35,6 +35,12 @@ class DeepVCP(nn.Module):
         self.cpg = cpg()
         self.K, self.r, self.s = K, r, s
 
+    def _side_stream(self, dev):
+        cache = self.__dict__.setdefault("_dvcp_streams", {})
+        if dev not in cache:
+            cache[dev] = torch.cuda.Stream(device=dev)
+        return cache[dev]
+
     def draw_starts(self, B, n_src, n_tgt):
         """The reference's seven torch.randint(0, n, (B,)) draws, in call order."""
         S1, S2, S3 = self.FE1.sa1.npoint, self.FE1.sa2.npoint, self.FE1.sa3.npoint
@@ -42,7 +48,10 @@ class DeepVCP(nn.Module):
         del S3
         return torch.stack([torch.randint(0, n, (B,), dtype=torch.long) for n in sizes])
 
-    def forward(self, src_pts, tgt_pts, R_init, t_init, starts=None, trace=None):
+    def forward(self, src_pts, tgt_pts, R_init, t_init, starts=None, trace=None, keypoint_idx=None):
+        """``starts`` (7, B): FPS start indices (drawn like the reference when None).
+        ``trace``: dict filled with the stage outputs.  ``keypoint_idx`` (B, K): stage override
+        for parity testing -- use these FE-space key-point indices instead of the top-k."""
         _inference_only(self)
         B = src_pts.shape[0]
         K, r, s = self.K, self.r, self.s
@@ -51,11 +60,22 @@ class DeepVCP(nn.Module):
             starts = self.draw_starts(B, src_pts.shape[2], tgt_pts.shape[2])
         starts = starts.to(dev, non_blocking=True)
 
-        src_xyz, src_feat, score = self.FE1.run(src_pts, starts[0:3], wl=self.WL)
-        top = ops.topk(score, K)
+        side = self._side_stream(dev)
+        if src_pts.shape == tgt_pts.shape and src_pts.dtype == tgt_pts.dtype:
+            # src and tgt share FE1's weights and eval-mode FE is per cloud: one 2B-cloud pass
+            # (the serial FPS chain then runs once for both clouds, on 2B workgroups)
+            both = torch.cat([src_pts, tgt_pts], 0)
+            fe_starts = [torch.cat([starts[i], starts[4 + i]]) for i in range(3)]
+            xyz2, feat2, score2 = self.FE1.run(both, fe_starts, wl=self.WL, side_stream=side)
+            src_xyz, tgt_xyz = xyz2[:B], xyz2[B:]
+            src_feat, tgt_feat = feat2[:B], feat2[B:]
+            score = score2[:B]
+        else:
+            src_xyz, src_feat, score = self.FE1.run(src_pts, starts[0:3], wl=self.WL, side_stream=side)
+            tgt_xyz, tgt_feat, _ = self.FE1.run(tgt_pts, starts[4:7], side_stream=side)
+        top = ops.topk(score, K) if keypoint_idx is None else keypoint_idx.to(dev, torch.int64).contiguous()
         keypts, src_cat, moved = ops.src_keypoints(src_xyz, src_feat, top, starts[3], R_init, radius=1.0, nsample=32)
         src_dfe = ops.dfe(src_cat, self.DFE.packed_params())
-        tgt_xyz, tgt_feat, _ = self.FE1.run(tgt_pts, starts[4:7])
 
         G = int((2 * r) / s + 1)                    # cpg.py:29
         if grid_side(r, s) != G:

@@ -39,9 +39,13 @@ class feat_extraction_layer(nn.Module):
         return cached_pack(self, "head" if wl is None else "head_wl", linear_tensors(*lins),
                            lambda: linear_pack(*lins))
 
-    def run(self, pts, starts=None, wl=None):
+    def run(self, pts, starts=None, wl=None, side_stream=None):
         """Fused forward.  starts: (3, B) FPS start indices (drawn like the reference if None).
-        Returns xyz (B, 3, S) contiguous, feat (B, S, 32), score (B, S) when ``wl`` is given."""
+        Returns xyz (B, 3, S) contiguous, feat (B, S, 32), score (B, S) when ``wl`` is given.
+
+        FPS of layer l+1 depends only on layer l's sampled centres, not on its features, so the
+        three FPS launches (the serial critical path) run back to back on the current stream
+        while each layer's ball query + grouped MLP runs on ``side_stream`` behind an event."""
         _inference_only(self)
         B, _, N = pts.shape
         if self.use_normal:
@@ -51,13 +55,38 @@ class feat_extraction_layer(nn.Module):
         if starts is None:
             starts = [torch.randint(0, n, (B,), dtype=torch.long)
                       for n in (N, self.sa1.npoint, self.sa2.npoint)]
-        xyz, feat = self.sa1(xyz, feat, start=starts[0])
-        xyz, feat = self.sa2(xyz, feat, start=starts[1])
-        xyz, feat = self.sa3(xyz, feat, start=starts[2])
-        S = xyz.shape[2]
-        f3 = feat.permute(0, 2, 1).reshape(B * S, 64)  # sa output is (B, S, 64) in memory
-        out, score = ops.fe_head(f3, self.fc_params(wl), with_score=wl is not None)
-        return xyz, out.view(B, S, 32), (score.view(B, S) if score is not None else None)
+        layers = (self.sa1, self.sa2, self.sa3)
+        main = torch.cuda.current_stream()
+        side = side_stream if side_stream is not None else main
+        centres, events = [], []
+        prev = xyz
+        for sa, st in zip(layers, starts):
+            _inference_only(sa)
+            _, c = ops.fps(prev, sa.npoint, st.to(prev.device), pdim=2)
+            centres.append(c)
+            ev = torch.cuda.Event()
+            ev.record(main)
+            events.append(ev)
+            prev = c
+        with torch.cuda.stream(side):
+            pts_l, f = xyz, feat
+            for sa, c, ev in zip(layers, centres, events):
+                side.wait_event(ev)
+                n_l = pts_l.shape[2]
+                ns = min(int(sa.nsample), n_l)
+                count, lst, _ = ops.ball_query(pts_l, c, sa.radius, ns, pdim=2, cdim_pts=2)
+                out = ops.sa_group_mlp(pts_l, c, f, count, lst, ns, sa.chans, sa.packed_params(),
+                                       xyz_pdim=2, feat_ddim=1, feat_pdim=2)
+                pts_l, f = c, out.permute(0, 2, 1)
+            S = pts_l.shape[2]
+            f3 = f.permute(0, 2, 1).reshape(B * S, 64)  # sa output is (B, S, 64) in memory
+            head, score = ops.fe_head(f3, self.fc_params(wl), with_score=wl is not None)
+        if side is not main:
+            main.wait_stream(side)
+            for t in (head, score):
+                if t is not None:
+                    t.record_stream(main)  # allocated on the side stream, consumed on main
+        return pts_l, head.view(B, S, 32), (score.view(B, S) if score is not None else None)
 
     def forward(self, pts):
         xyz, feat, _ = self.run(pts)

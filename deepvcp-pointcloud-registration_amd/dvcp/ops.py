@@ -18,6 +18,10 @@ def _pts(t, pdim):
     return t.shape[pdim], sb, sc, sn
 
 
+# largest cloud the register-resident FPS kernel takes (csrc/fps.hip); beyond it a workspace
+FPS_REG_LIMIT = {torch.float32: 16384, torch.float64: 12288}
+
+
 def fps(xyz, npoint, start, pdim=1):
     """pointnet2_utils.py:63-84.  Returns (idx (B, npoint) int64, centres (B, 3, npoint))."""
     _lib.require_gpu(xyz, start)
@@ -26,7 +30,10 @@ def fps(xyz, npoint, start, pdim=1):
     start = start.to(device=xyz.device, dtype=torch.int64).contiguous()
     idx = torch.empty(B, npoint, dtype=torch.int64, device=xyz.device)
     ctr = torch.empty(B, 3, npoint, dtype=xyz.dtype, device=xyz.device)
-    call("dvcp_fps", dtype_code(xyz), ptr(xyz), sb, sc, sn, B, N, npoint, ptr(start), ptr(idx), ptr(ctr), stream())
+    limit = FPS_REG_LIMIT[xyz.dtype]
+    ws = torch.empty(B, N, dtype=torch.float32, device=xyz.device) if N > limit else None
+    call("dvcp_fps_ws", dtype_code(xyz), ptr(xyz), sb, sc, sn, B, N, npoint, ptr(start), ptr(idx), ptr(ctr), ptr(ws),
+         stream())
     return idx, ctr
 
 

@@ -47,6 +47,12 @@ int dvcp_abi_version(void);
 int dvcp_fps(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N,
              int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz, void* stream);
 
+/* dvcp_fps with a B x N fp32 workspace, required when N exceeds the register-resident limit
+ * (16384 fp32 / 12288 fp64 points per cloud); smaller clouds ignore it. */
+int dvcp_fps_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N,
+                int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz, float* ws,
+                void* stream);
+
 /* Ball query.  Replaces pointnet2_utils.py:87-107 query_ball_point (and the
  * square_distance expansion it uses, :19-40): the first `nsample` ascending point indices
  * whose d2 = ((-2*dot) + |c|^2) + |p|^2 is not > radius^2 (dot = MKL's fma chain).

@@ -285,7 +285,9 @@ def _knn_rows(ref, qry, k, chunk=2048):
         key = d2.contiguous().view(torch.int32).to(torch.int64) * (1 << 32) + ar
         best = torch.topk(key, k, dim=1, largest=False, sorted=True).values
         sel = best & 0xFFFFFFFF
-        dists.append(torch.sqrt(torch.gather(d2, 1, sel)))
+        # correctly rounded sqrt (the contract; knn_cuda's CUDA sqrtf is IEEE): torch's fp32
+        # CPU sqrt is up to 1 ulp off, its fp64 sqrt narrowed to fp32 is exact
+        dists.append(torch.sqrt(torch.gather(d2, 1, sel).double()).float())
         idxs.append(sel)
     return torch.cat(dists, 0), torch.cat(idxs, 0)
 
