@@ -17,7 +17,7 @@ same starts as the reference.  t_init is unused, as in the reference (deepVCP.py
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import _lib, ops
 from .cpg import cpg
 from .deep_feat_embedding import feat_embedding_layer
 from .deep_feat_extraction import feat_extraction_layer
@@ -53,6 +53,7 @@ class DeepVCP(nn.Module):
         ``trace``: dict filled with the stage outputs.  ``keypoint_idx`` (B, K): stage override
         for parity testing -- use these FE-space key-point indices instead of the top-k."""
         _inference_only(self)
+        _lib.require_gpu(src_pts, tgt_pts)   # no CPU fallback
         B = src_pts.shape[0]
         K, r, s = self.K, self.r, self.s
         dev = src_pts.device
