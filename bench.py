@@ -48,26 +48,6 @@ def parse():
     return p.parse_args()
 
 
-# ---------------------------------------------------------------------------------------------
-# Algorithmic work per launch, by entry point (DESIGN.md "Roofline accounting").  Flops count
-# the reference op graph's arithmetic for the work one launch performs.
-def algorithmic_flops(name, cfg):
-    B, N, K, S, C = cfg["B"], cfg["N"], cfg["K"], cfg["S"], cfg["C"]
-    if name == "dvcp_fps":          # per launch: npoint x N point updates (3 sub, 3 mul, 2 add, 1 min)
-        return None  # per-launch N differs (16384 for sa1, 10000 for sa2/sa3): handled below
-    if name == "dvcp_knn":          # Q x M distance evaluations, 8 flops each
-        return B * K * C * S * 8.0
-    if name == "dvcp_dfe_tgt":      # rows x (35*32 + 32*32 + 32*32) MACs
-        return B * K * C * 32 * 2.0 * (35 * 32 + 32 * 32 + 32 * 32)
-    if name == "dvcp_cpg":          # per key point: C x (32*16 + 16*4 + 4*1) x 27 MACs
-        return B * K * C * 2.0 * 27 * (32 * 16 + 16 * 4 + 4)
-    return None
-
-
-def fps_flops(n, npoint, B):
-    return B * float(npoint) * n * 9.0
-
-
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,21 +106,23 @@ def main():
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         elapsed = float(tmax.item())
 
-    # per-kernel live HIP-event timing over the timed region
+    # per-kernel live HIP-event timing over the timed region (events on the launching stream)
     S = model.FE1.sa1.npoint
     C = int((2 * r) / s + 1) ** 3
-    cfg = dict(B=B, N=N, K=K, S=S, C=C)
-    per = {}
-    for name, e0, e1 in log:
+    per, work = {}, {}
+    for name, e0, e1, w in log:
         per.setdefault(name, []).append(e0.elapsed_time(e1))
+        if w is not None:
+            acc = work.setdefault(name, [0.0, 0.0])
+            acc[0] += w[0]
+            acc[1] += w[1]
     tot = {k: sum(v) for k, v in per.items()}
     dom = max(tot, key=tot.get)
-    if dom == "dvcp_fps":
-        # launches alternate sa1 (N -> S), sa2 (S -> S), sa3 (S -> S) per cloud
-        works = [fps_flops(N if (i % 3) == 0 else S, S, B) for i in range(len(per[dom]))]
-        achieved = sum(works) / (sum(per[dom]) * 1e-3) / 1e12
-    else:
-        achieved = algorithmic_flops(dom, cfg) / (sum(per[dom]) / len(per[dom]) * 1e-3) / 1e12
+    n_launch = len(per[dom])
+    avg_ms = tot[dom] / n_launch
+    flops = work.get(dom, [0.0, 0.0])[0] / n_launch
+    nbytes = work.get(dom, [0.0, 0.0])[1] / n_launch
+    achieved = flops / (avg_ms * 1e-3) / 1e12
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if os.path.exists(pmc):
@@ -150,11 +132,15 @@ def main():
             traffic = None
     roofline = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 4), "peak": PEAK_FP32_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 6), "traffic": traffic,
-                "avg_launch_ms": round(tot[dom] / len(per[dom]), 4),
-                "note": "fp32 arithmetic (VALU/MFMA share one 157.3 TF peak); FPS is a serial chain of "
-                        "npoint dependent argmax steps per cloud (latency-bound)"}
+                "avg_launch_ms": round(avg_ms, 4), "algorithmic_flops_per_launch": flops,
+                "algorithmic_bytes_per_launch": nbytes,
+                "hbm_GBs_algorithmic": round(nbytes / (avg_ms * 1e-3) / 1e9, 2),
+                "note": "fp32 arithmetic (VALU and MFMA share the 157.3 TF fp32 peak); algorithmic flops per "
+                        "launch as defined in DESIGN.md (reference op graph)"}
     stages = {k: {"launches": len(v), "total_ms_per_step": round(sum(v) / args.steps, 3),
-                  "avg_ms": round(sum(v) / len(v), 4)} for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1]))}
+                  "avg_ms": round(sum(v) / len(v), 4),
+                  "tflops": round(work.get(k, [0, 0])[0] / (sum(v) * 1e-3) / 1e12, 3) if k in work else None}
+              for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1]))}
 
     pairs = B * world * args.steps
     value = pairs / elapsed

@@ -69,13 +69,14 @@ def exported_symbols():
     return ["dvcp_last_error", "dvcp_abi_version"] + list(SIGNATURES)
 
 
-# When a list, every entry-point call appends (name, start_event, end_event) recorded on
+# When a list, every entry-point call appends (name, start_event, end_event, work) recorded on
 # torch's current stream (the stream the kernel is launched on) -- bench.py's live per-kernel
-# HIP-event timing.  None (the default) costs nothing.
+# HIP-event timing.  `work` = (algorithmic flops, algorithmic bytes) of that launch, as defined
+# in DESIGN.md "Roofline accounting".  None (the default) costs nothing.
 EVENT_LOG = None
 
 
-def call(name, *args):
+def call(name, *args, work=None):
     """Call an entry point; raise RuntimeError with the library's message on failure."""
     lib = load()
     if EVENT_LOG is not None:
@@ -84,7 +85,7 @@ def call(name, *args):
         e0.record()
         rc = getattr(lib, name)(*args)
         e1.record()
-        EVENT_LOG.append((name, e0, e1))
+        EVENT_LOG.append((name, e0, e1, work))
     else:
         rc = getattr(lib, name)(*args)
     if rc != 0:

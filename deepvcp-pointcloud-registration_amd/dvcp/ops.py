@@ -32,8 +32,9 @@ def fps(xyz, npoint, start, pdim=1):
     ctr = torch.empty(B, 3, npoint, dtype=xyz.dtype, device=xyz.device)
     limit = FPS_REG_LIMIT[xyz.dtype]
     ws = torch.empty(B, N, dtype=torch.float32, device=xyz.device) if N > limit else None
+    es = xyz.element_size()
     call("dvcp_fps_ws", dtype_code(xyz), ptr(xyz), sb, sc, sn, B, N, npoint, ptr(start), ptr(idx), ptr(ctr), ptr(ws),
-         stream())
+         stream(), work=(9.0 * B * npoint * N, B * (3 * N * es + npoint * (8 + 3 * es))))
     return idx, ctr
 
 
@@ -50,8 +51,11 @@ def ball_query(xyz, ctr, radius, nsample, pdim=1, cdim_pts=1, compact=True, padd
     count = torch.empty(B, S, dtype=torch.int32, device=dev) if compact else None
     lst = torch.empty(B, S, nsample, dtype=torch.int32, device=dev) if compact else None
     pad = torch.empty(B, S, nsample, dtype=torch.int64, device=dev) if padded else None
+    es = xyz.element_size()
+    out_b = (4 + 4 * nsample if compact else 0) + (8 * nsample if padded else 0)
     call("dvcp_ball_query", dtype_code(xyz), ptr(xyz), sb, sc, sn, N, ptr(ctr), cb, cc, cn, S, B, float(radius),
-         int(nsample), ptr(count), ptr(lst), ptr(pad), stream())
+         int(nsample), ptr(count), ptr(lst), ptr(pad), stream(),
+         work=(9.0 * B * S * N, B * (3 * es * (N + S) + S * out_b)))
     return count, lst, pad
 
 
@@ -83,8 +87,10 @@ def sa_group_mlp(xyz, ctr, feat, count, lst, nsample, chans, params, xyz_pdim=2,
         D, fb, fd, fn, fdt = 0, 0, 0, 0, _lib.F32
     ch = torch.tensor(list(chans), dtype=torch.int32)  # host array, read by the launcher only
     out = torch.empty(B, S, chans[-1], dtype=torch.float32, device=xyz.device)
+    macs = sum(a * b for a, b in zip(chans[:-1], chans[1:]))
     call("dvcp_sa_group_mlp", dtype_code(xyz), ptr(xyz), sb, sc, sn, N, ptr(ctr), cb, cc, cn, S, B, fdt, ptr(feat),
-         fb, fd, fn, D, ptr(count), ptr(lst), int(nsample), len(chans) - 1, ptr(ch), ptr(params), ptr(out), stream())
+         fb, fd, fn, D, ptr(count), ptr(lst), int(nsample), len(chans) - 1, ptr(ch), ptr(params), ptr(out), stream(),
+         work=(2.0 * macs * B * S * nsample, B * S * (4 * nsample + 4 * chans[-1]) + B * N * 4 * (3 + D)))
     return out
 
 
@@ -165,7 +171,7 @@ def knn(ref, qry, k, ref_pdim=1, qry_pdim=1, want_idx64=True):
     idx = torch.empty(B, Q, k, dtype=torch.int32, device=dev)
     idx64 = torch.empty(B, Q, k, dtype=torch.int64, device=dev) if want_idx64 else None
     call("dvcp_knn", dtype_code(ref), ptr(ref), rb, rc, rn, M, ptr(qry), qb, qc, qn, Q, B, int(k), ptr(dist), ptr(idx),
-         ptr(idx64), stream())
+         ptr(idx64), stream(), work=(9.0 * B * Q * M, B * (12 * (M + Q) + Q * k * (8 + (8 if want_idx64 else 0)))))
     return dist, idx, idx64
 
 
@@ -178,7 +184,8 @@ def dfe(X, params):
     Xc = X.contiguous()
     R = Xc.numel() // (32 * 35)
     out = torch.empty(R, 32, dtype=torch.float32, device=X.device)
-    call("dvcp_dfe", dtype_code(Xc), ptr(Xc), R, ptr(params), ptr(out), stream())
+    call("dvcp_dfe", dtype_code(Xc), ptr(Xc), R, ptr(params), ptr(out), stream(),
+         work=(2.0 * 3168 * 32 * R, Xc.numel() * Xc.element_size() + 128 * R))
     return out.view(*lead, 32)
 
 
@@ -191,7 +198,8 @@ def dfe_tgt(ref_xyz, ref_feat, cand, dist, idx, params, ref_pdim=2):
     feat_c, cand_c, dist_c, idx_c = ref_feat.contiguous(), cand.contiguous(), dist.contiguous(), idx.contiguous()
     out = torch.empty(B, Q, 32, dtype=torch.float32, device=ref_xyz.device)
     call("dvcp_dfe_tgt", dtype_code(ref_xyz), ptr(ref_xyz), rb, rc, rn, M, ptr(feat_c), ptr(cand_c), ptr(dist_c),
-         ptr(idx_c), B, Q, ptr(params), ptr(out), stream())
+         ptr(idx_c), B, Q, ptr(params), ptr(out), stream(),
+         work=(2.0 * 3168 * 32 * B * Q, B * (M * (12 + 128) + Q * (12 + 32 * 8 + 128))))
     return out
 
 
@@ -209,7 +217,8 @@ def cpg(src, tgt, cand, G, params, want_weight=False):
     vcp = torch.empty(B, K, 3, dtype=torch.float32, device=cand.device)
     w = torch.empty(B, K, C, dtype=torch.float32, device=cand.device) if want_weight else None
     call("dvcp_cpg", ptr(srcc), ptr(tgt), tgt.stride(1), tgt.stride(2), tgt.stride(3), ptr(candc), B * K, int(G),
-         ptr(params), ptr(vcp), ptr(w), stream())
+         ptr(params), ptr(vcp), ptr(w), stream(),
+         work=(2.0 * 27 * (32 * 16 + 16 * 4 + 4) * B * K * C, B * K * (128 + C * (128 + 12) + 12)))
     return (vcp, w) if want_weight else vcp
 
 
