@@ -94,6 +94,15 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
+// Workgroup barrier that orders LDS only.  __syncthreads() is a workgroup release/acquire: it
+// also waits for every outstanding global store (vmcnt(0)), which in a serial per-step loop
+// that streams its outputs puts an HBM write round trip on every step.  Here only LDS traffic
+// crosses the barrier, so wait for LDS (lgkmcnt) and barrier; "memory" keeps the compiler from
+// moving LDS accesses across it.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Block-wide sum of one value per thread (blockDim multiple of 64, <= 1024).  `scratch`
 // holds >= 16 T.  Every thread returns the total.  The summation order is fixed.
 template <typename T>

@@ -278,7 +278,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_kernel(PointsView<T> pts, int
     }
     FpsSlot<T>* buf = slots[step & 1];
     if (lane == 0) buf[wave] = FpsSlot<T>{empty_wave ? -2.0f : wv, empty_wave ? 0x7FFFFFFF : wi, wx, wy, wz};
-    __syncthreads();
+    lds_barrier();  // the output stores above stay in flight across the barrier
     // block argmax over the 16 slots in lanes 0..15 (row 0): value desc, then index asc
     const FpsSlot<T> mine = buf[lane & (kFpsWaves - 1)];
     float v = mine.v;

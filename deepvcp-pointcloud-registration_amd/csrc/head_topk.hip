@@ -94,7 +94,7 @@ __global__ __launch_bounds__(1024) void topk_kernel(const float* __restrict__ sc
     for (int p = 0; p < PPT; ++p) best = key[p] > best ? key[p] : best;
     const uint64_t w = wave_max_u64(best);
     if (lane == 0) slots[k & 1][wave] = w;
-    __syncthreads();
+    lds_barrier();
     uint64_t m = slots[k & 1][0];
 #pragma unroll
     for (int q = 1; q < NT / kWave; ++q) m = slots[k & 1][q] > m ? slots[k & 1][q] : m;

@@ -70,7 +70,7 @@ __global__ __launch_bounds__(kKpThreads) void src_keypoints_kernel(
     const uint64_t mine = dmin >= 0.0f ? argmax_key(dmin, static_cast<uint32_t>(tid)) : 0ull;
     const uint64_t w = wave_max_u64(mine);
     if (lane == 0) slots[step & 1][wave] = w;
-    __syncthreads();
+    lds_barrier();
     uint64_t m = slots[step & 1][0];
 #pragma unroll
     for (int q = 1; q < kKpThreads / kWave; ++q) m = slots[step & 1][q] > m ? slots[step & 1][q] : m;
