@@ -18,6 +18,8 @@
 //     wave publishes {value, index, x, y, z} to a double-buffered LDS slot, and every wave
 //     reduces the 16 slots with a 16-lane DPP max.  No global memory in the loop except the
 //     output stores.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace dvcp {
@@ -92,7 +94,7 @@ __device__ __forceinline__ uint32_t spread4(uint32_t v) {  // 4 bits -> every th
   return (v & 1u) | ((v & 2u) << 2) | ((v & 4u) << 4) | ((v & 8u) << 6);
 }
 
-template <typename T, int PPT>
+template <typename T, int PPT, bool PRUNE = true>
 __global__ __launch_bounds__(kFpsThreads) void fps_kernel(PointsView<T> pts, int N, int npoint,
                                                           const int64_t* __restrict__ start,
                                                           int64_t* __restrict__ out_idx, T* __restrict__ out_xyz) {
@@ -245,7 +247,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_kernel(PointsView<T> pts, int
         ox[2 * npoint + step] = cz;
       }
     }
-    const bool active = !empty_wave && !(box_lb2(cx, cy, cz, wb) >= static_cast<T>(wv));
+    const bool active = !empty_wave && (!PRUNE || !(box_lb2(cx, cy, cz, wb) >= static_cast<T>(wv)));
     if (active) {
       float bv = -1.0f;
       int bi = 0x7FFFFFFF;
@@ -375,10 +377,18 @@ static int launch_fps(const T* xyz, int64_t sb, int64_t sc, int64_t sn, int B, i
   PointsView<T> v{xyz, sb, sc, sn};
   const int ppt = ceil_div(N, kFpsThreads);
   dim3 grid(B), block(kFpsThreads);
-#define DVCP_FPS_CASE(P)                                                                                     \
-  if (ppt <= P) {                                                                                            \
-    hipLaunchKernelGGL((fps_kernel<T, P>), grid, block, 0, st, v, N, npoint, start, out_idx, out_xyz);       \
-    return launch_status("dvcp_fps");                                                                        \
+  // diagnostics only: DVCP_FPS_NOPRUNE=1 disables the exact box pruning (identical results)
+  static const bool noprune = [] {
+    const char* e = getenv("DVCP_FPS_NOPRUNE");
+    return e && e[0] == '1';
+  }();
+#define DVCP_FPS_CASE(P)                                                                                      \
+  if (ppt <= P) {                                                                                             \
+    if (noprune)                                                                                              \
+      hipLaunchKernelGGL((fps_kernel<T, P, false>), grid, block, 0, st, v, N, npoint, start, out_idx, out_xyz); \
+    else                                                                                                      \
+      hipLaunchKernelGGL((fps_kernel<T, P, true>), grid, block, 0, st, v, N, npoint, start, out_idx, out_xyz);  \
+    return launch_status("dvcp_fps");                                                                         \
   }
   DVCP_FPS_CASE(1)
   DVCP_FPS_CASE(2)

@@ -158,7 +158,12 @@ def voxelize(pts, r, s, G, pdim=1):
     return cand, err
 
 
-def knn(ref, qry, k, ref_pdim=1, qry_pdim=1, want_idx64=True):
+# reference sets at least this large use the cell-grid kNN (dvcp_knn_grid); smaller ones the
+# brute-force scan (dvcp_knn).  Both are exact and return identical results.
+KNN_GRID_MIN_M = 2048
+
+
+def knn(ref, qry, k, ref_pdim=1, qry_pdim=1, want_idx64=True, method=None):
     """Exact kNN (knn_cuda.KNN replacement).  Returns dist (B,Q,k) fp32, idx int32, idx64."""
     _lib.require_gpu(ref, qry)
     if ref.dtype != qry.dtype:
@@ -170,8 +175,15 @@ def knn(ref, qry, k, ref_pdim=1, qry_pdim=1, want_idx64=True):
     dist = torch.empty(B, Q, k, dtype=torch.float32, device=dev)
     idx = torch.empty(B, Q, k, dtype=torch.int32, device=dev)
     idx64 = torch.empty(B, Q, k, dtype=torch.int64, device=dev) if want_idx64 else None
-    call("dvcp_knn", dtype_code(ref), ptr(ref), rb, rc, rn, M, ptr(qry), qb, qc, qn, Q, B, int(k), ptr(dist), ptr(idx),
-         ptr(idx64), stream(), work=(9.0 * B * Q * M, B * (12 * (M + Q) + Q * k * (8 + (8 if want_idx64 else 0)))))
+    work = (9.0 * B * Q * M, B * (12 * (M + Q) + Q * k * (8 + (8 if want_idx64 else 0))))
+    method = method or ("grid" if M >= KNN_GRID_MIN_M else "brute")
+    if method == "grid":
+        ws = torch.empty(int(_lib.load().dvcp_knn_grid_workspace_bytes(B, M)), dtype=torch.uint8, device=dev)
+        call("dvcp_knn_grid", dtype_code(ref), ptr(ref), rb, rc, rn, M, ptr(qry), qb, qc, qn, Q, B, int(k), ptr(ws),
+             ptr(dist), ptr(idx), ptr(idx64), stream(), work=work)
+    else:
+        call("dvcp_knn", dtype_code(ref), ptr(ref), rb, rc, rn, M, ptr(qry), qb, qc, qn, Q, B, int(k), ptr(dist),
+             ptr(idx), ptr(idx64), stream(), work=work)
     return dist, idx, idx64
 
 

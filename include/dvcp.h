@@ -135,6 +135,15 @@ int dvcp_knn(int dtype, const void* ref, int64_t rb, int64_t rc, int64_t rn, int
              const void* qry, int64_t qb, int64_t qc, int64_t qn, int Q, int B, int k,
              float* dist, int32_t* idx, int64_t* idx64, void* stream);
 
+/* Exact kNN through a uniform cell grid (same contract and outputs as dvcp_knn).  The reference
+ * set is counting-sorted into cells once per cloud, then each query scans Chebyshev shells of
+ * cells around its home cell until no unscanned cell can hold a point at or below its k-th
+ * distance.  workspace: dvcp_knn_grid_workspace_bytes(B, M) bytes of device memory. */
+int dvcp_knn_grid(int dtype, const void* ref, int64_t rb, int64_t rc, int64_t rn, int M,
+                  const void* qry, int64_t qb, int64_t qc, int64_t qn, int Q, int B, int k,
+                  void* workspace, float* dist, int32_t* idx, int64_t* idx64, void* stream);
+int64_t dvcp_knn_grid_workspace_bytes(int B, int M);
+
 /* Deep feature embedding on a materialised input.  Replaces deep_feat_embedding.py:23-61
  * (X.float(); Linear 35-32-32-32, no activations; MaxPool1d(32) over the neighbour axis).
  * X: R x 32 x 35 rows of x_dtype (fp32/fp64) contiguous -> out: R x 32 fp32.

@@ -15,7 +15,7 @@ HEADER = os.path.join(ROOT, "include", "dvcp.h")
 
 def declared():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(dvcp_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(dvcp_\w+)\s*\(", text, re.M)))
 
 
 def test_header_declares_entry_points():

@@ -150,6 +150,33 @@ def test_knn_golden(cuda, name):
     assert torch.equal(d.cpu(), T(z["dist"]))
 
 
+@pytest.mark.parametrize("name", ["knn_f32", "knn_dyadic"])
+def test_knn_grid_golden(cuda, name):
+    """The cell-grid kNN on the golden fixtures (forced even though M is small)."""
+    from dvcp import ops
+    z = golden(name)
+    d, _, i = ops.knn(T(z["ref"], cuda), T(z["qry"], cuda), 32, method="grid")
+    assert torch.equal(i.cpu(), T(z["idx"]))
+    assert torch.equal(d.cpu(), T(z["dist"]))
+
+
+@pytest.mark.parametrize("k", [1, 5, 32])
+def test_knn_grid_equals_brute_full_size(cuda, k):
+    """C3 shape: 10000 target FE-like points, candidate-grid queries partly far outside the
+    cloud (as the R_init-only transform produces) and exact duplicates (ties)."""
+    from dvcp import ops
+    from dvcp.synthetic import rot_xyz
+    g = torch.Generator().manual_seed(113)
+    ref = (torch.rand(2, 10000, 3, generator=g) * 2 - 1)
+    ref = ref @ torch.from_numpy(rot_xyz(0.4, 1.1, 2.0)).float().T + 0.7
+    ref[:, 5000:5100] = ref[:, 100:200]                       # duplicated points -> equal distances
+    qry = torch.rand(2, 20000, 3, generator=g) * 8 - 4           # many queries outside the cloud
+    ref, qry = ref.to(cuda), qry.to(cuda)
+    d1, i1, _ = ops.knn(ref, qry, k, method="brute")
+    d2, i2, _ = ops.knn(ref, qry, k, method="grid")
+    assert torch.equal(i1, i2) and torch.equal(d1, d2)
+
+
 def test_knn_k1_transpose_false(cuda):
     from dvcp.knn import KNN
     z = golden("knn_k1")
