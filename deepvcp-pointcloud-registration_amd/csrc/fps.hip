@@ -69,12 +69,13 @@ __device__ __forceinline__ double readlane_t<double>(double v, int lane) {
   return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
 }
 
-// Lower bound of the distance from c to an axis-aligned box, rounded like a point distance.
+// Lower bound of the distance from c to an axis-aligned box, rounded like a point distance
+// (branch-free: outside the slab exactly one difference is positive, inside both are <= 0).
 template <typename T>
 __device__ __forceinline__ T box_lb2(T cx, T cy, T cz, const T (&bx)[6]) {
-  const T ex = cx < bx[0] ? bx[0] - cx : (cx > bx[3] ? cx - bx[3] : static_cast<T>(0));
-  const T ey = cy < bx[1] ? bx[1] - cy : (cy > bx[4] ? cy - bx[4] : static_cast<T>(0));
-  const T ez = cz < bx[2] ? bx[2] - cz : (cz > bx[5] ? cz - bx[5] : static_cast<T>(0));
+  const T ex = fmax(fmax(bx[0] - cx, cx - bx[3]), static_cast<T>(0));
+  const T ey = fmax(fmax(bx[1] - cy, cy - bx[4]), static_cast<T>(0));
+  const T ez = fmax(fmax(bx[2] - cz, cz - bx[5]), static_cast<T>(0));
   return (ex * ex + ey * ey) + ez * ez;
 }
 
@@ -256,8 +257,9 @@ __global__ __launch_bounds__(kFpsThreads) void fps_kernel(PointsView<T> pts, int
       for (int p = 0; p < PPT; ++p) {
         const T dx = px[p] - cx, dy = py[p] - cy, dz = pz[p] - cz;
         const T d = (dx * dx + dy * dy) + dz * dz;  // torch.sum((xyz - c) ** 2, -1), :80
-        if (d < static_cast<T>(dmin[p])) dmin[p] = static_cast<float>(d);
-        const bool better = dmin[p] > bv || (dmin[p] == bv && pid[p] < bi);
+        dmin[p] = d < static_cast<T>(dmin[p]) ? static_cast<float>(d) : dmin[p];
+        // branch-free lexicographic (value desc, original index asc): bitwise, not short-circuit
+        const bool better = (dmin[p] > bv) | ((dmin[p] == bv) & (pid[p] < bi));
         bv = better ? dmin[p] : bv;
         bi = better ? pid[p] : bi;
         bx = better ? px[p] : bx;

@@ -222,15 +222,14 @@ template <int KT>
 __device__ __forceinline__ void topk_insert_lex(float (&kd)[KT], int (&ki)[KT], float d, int i) {
 #pragma unroll
   for (int t = KT - 1; t > 0; --t) {
-    const bool here = d < kd[t] || (d == kd[t] && i < ki[t]);
-    const bool before = d < kd[t - 1] || (d == kd[t - 1] && i < ki[t - 1]);
+    const bool here = (d < kd[t]) | ((d == kd[t]) & (i < ki[t]));
+    const bool before = (d < kd[t - 1]) | ((d == kd[t - 1]) & (i < ki[t - 1]));
     kd[t] = before ? kd[t - 1] : (here ? d : kd[t]);
     ki[t] = before ? ki[t - 1] : (here ? i : ki[t]);
   }
-  if (d < kd[0] || (d == kd[0] && i < ki[0])) {
-    kd[0] = d;
-    ki[0] = i;
-  }
+  const bool first = (d < kd[0]) | ((d == kd[0]) & (i < ki[0]));
+  kd[0] = first ? d : kd[0];
+  ki[0] = first ? i : ki[0];
 }
 
 __device__ __forceinline__ float axis_gap(float q, float lo, float hi) {
@@ -289,7 +288,7 @@ __global__ __launch_bounds__(kKnnThreads) void knn_grid_query_kernel(const KnnGr
             const float dx = p.x - qv[0], dy = p.y - qv[1], dz = p.z - qv[2];
             const float d2 = (dx * dx + dy * dy) + dz * dz;
             const int pi = __float_as_int(p.w);
-            if (d2 < kd[KT - 1] || (d2 == kd[KT - 1] && pi < ki[KT - 1])) topk_insert_lex<KT>(kd, ki, d2, pi);
+            if ((d2 < kd[KT - 1]) | ((d2 == kd[KT - 1]) & (pi < ki[KT - 1]))) topk_insert_lex<KT>(kd, ki, d2, pi);
           }
         }
       }
