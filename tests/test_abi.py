@@ -36,6 +36,17 @@ def test_library_exports_every_declared_symbol():
     assert lib.dvcp_abi_version() == 1
 
 
+def test_ctypes_prototypes_match_header_arity():
+    """Every ctypes prototype in dvcp/_lib.py has as many arguments as the header declares."""
+    from dvcp import _lib
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    protos = dict(re.findall(r"(?:int|int64_t|const char\*)\s+(dvcp_\w+)\s*\(([^)]*)\)\s*;", text))
+    for name, argtypes in _lib.SIGNATURES.items():
+        params = protos[name].strip()
+        n = 0 if params in ("", "void") else params.count(",") + 1
+        assert n == len(argtypes), (name, n, len(argtypes))
+
+
 def test_error_path_reports_message():
     import dvcp
     from dvcp import _lib
