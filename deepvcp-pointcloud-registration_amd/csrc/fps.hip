@@ -69,6 +69,11 @@ __device__ __forceinline__ double readlane_t<double>(double v, int lane) {
   return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
 }
 
+template <typename T>
+__device__ __forceinline__ T readfirstlane_t(T v) {
+  return readlane_t(v, 0);
+}
+
 // Lower bound of the distance from c to an axis-aligned box, rounded like a point distance
 // (branch-free: outside the slab exactly one difference is positive, inside both are <= 0).
 template <typename T>
@@ -86,32 +91,46 @@ struct alignas(16) FpsSlot {
   T x, y, z;
 };
 
-constexpr int kFpsThreads = 1024;
-constexpr int kFpsWaves = kFpsThreads / kWave;
+constexpr int kFpsThreads = 512;  // 8 waves: 2 per SIMD, up to 256 VGPRs each
 constexpr int kMortonBins = 4096;
+constexpr int kFpsProf = 8;       // timing probe words per wave (fps_kernel<..., TIMING=true>)
 
 __device__ __forceinline__ uint32_t spread4(uint32_t v) {  // 4 bits -> every third bit
   v &= 0xF;
   return (v & 1u) | ((v & 2u) << 2) | ((v & 4u) << 4) | ((v & 8u) << 6);
 }
 
-template <typename T, int PPT, bool PRUNE = true>
-__global__ __launch_bounds__(kFpsThreads) void fps_kernel(PointsView<T> pts, int N, int npoint,
-                                                          const int64_t* __restrict__ start,
-                                                          int64_t* __restrict__ out_idx, T* __restrict__ out_xyz) {
+__device__ __forceinline__ uint64_t fps_clock() {
+  const uint64_t t = __builtin_amdgcn_s_memtime();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  return t;
+}
+
+// THREADS threads (W = THREADS/64 waves) per cloud; PPT points per lane in VGPRs.
+// TIMING (diagnostics, tools/fps_lab): per-wave sums of the step phases in shader clocks.
+template <typename T, int THREADS, int PPT, bool PRUNE, bool TIMING = false>
+__global__ __launch_bounds__(THREADS) void fps_kernel(PointsView<T> pts, int N, int npoint,
+                                                      const int64_t* __restrict__ start,
+                                                      int64_t* __restrict__ out_idx, T* __restrict__ out_xyz,
+                                                      unsigned long long* __restrict__ prof) {
+  constexpr int W = THREADS / kWave;
+  constexpr int RANGE = kWave * PPT;  // sorted positions per wave
+  static_assert(W <= 16 && (W & (W - 1)) == 0, "slot reduction covers one DPP row");
+  static_assert(PPT % 2 == 0 || PPT == 1, "original indices are packed two per VGPR");
   __shared__ uint32_t bins[kMortonBins];
-  __shared__ uint16_t perm[kFpsThreads * PPT];
-  __shared__ FpsSlot<T> slots[2][kFpsWaves];
-  __shared__ T red[2][6][kFpsWaves];
-  __shared__ uint32_t wsum[kFpsWaves];
+  __shared__ uint16_t perm[THREADS * PPT];
+  __shared__ uint8_t owner[THREADS * PPT];
+  __shared__ FpsSlot<T> slots[2][W];
+  __shared__ T red[2][3][W];
+  __shared__ uint32_t wsum[W];
 
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
-  // ---- setup 1: cloud bounding box (natural layout) ----------------------------------------
+  // ---- setup 1: cloud bounding box ------------------------------------------------------------
   T lo[3] = {static_cast<T>(__builtin_huge_val()), static_cast<T>(__builtin_huge_val()),
              static_cast<T>(__builtin_huge_val())};
   T hi[3] = {-lo[0], -lo[1], -lo[2]};
-  for (int n = tid; n < N; n += kFpsThreads) {
+  for (int n = tid; n < N; n += THREADS) {
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
       const T v = pts.at(b, a, n);
@@ -131,13 +150,13 @@ __global__ __launch_bounds__(kFpsThreads) void fps_kernel(PointsView<T> pts, int
       red[1][a][wave] = hi[a];
     }
   }
-  for (int i = tid; i < kMortonBins; i += kFpsThreads) bins[i] = 0u;
+  for (int i = tid; i < kMortonBins; i += THREADS) bins[i] = 0u;
   __syncthreads();
   T blo[3], bscale[3];
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     T l = red[0][a][0], h = red[1][a][0];
-    for (int w = 1; w < kFpsWaves; ++w) {
+    for (int w = 1; w < W; ++w) {
       l = red[0][a][w] < l ? red[0][a][w] : l;
       h = red[1][a][w] > h ? red[1][a][w] : h;
     }
@@ -145,7 +164,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_kernel(PointsView<T> pts, int
     bscale[a] = h > l ? static_cast<T>(16) / (h - l) : static_cast<T>(0);
   }
 
-  // ---- setup 2: counting sort by Morton cell (only the point->slot map depends on it) --------
+  // ---- setup 2: counting sort by Morton cell -> each wave owns a compact region ---------------
   auto cell_of = [&](int n) -> uint32_t {
     uint32_t c = 0;
 #pragma unroll
@@ -156,13 +175,14 @@ __global__ __launch_bounds__(kFpsThreads) void fps_kernel(PointsView<T> pts, int
     }
     return c;
   };
-  for (int n = tid; n < N; n += kFpsThreads) atomicAdd(&bins[cell_of(n)], 1u);
+  for (int n = tid; n < N; n += THREADS) atomicAdd(&bins[cell_of(n)], 1u);
   __syncthreads();
-  {  // exclusive scan of 4096 bins: 4 per thread, wave scan, then across waves
-    uint32_t v[4], s = 0;
+  {  // exclusive scan of the bins: PER per thread, wave scan, then across waves
+    constexpr int PER = kMortonBins / THREADS;
+    uint32_t v[PER], s = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      v[k] = bins[tid * 4 + k];
+    for (int k = 0; k < PER; ++k) {
+      v[k] = bins[tid * PER + k];
       s += v[k];
     }
     uint32_t incl = s;
@@ -176,19 +196,38 @@ __global__ __launch_bounds__(kFpsThreads) void fps_kernel(PointsView<T> pts, int
     for (int w = 0; w < wave; ++w) base += wsum[w];
     uint32_t run = base + incl - s;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      bins[tid * 4 + k] = run;
+    for (int k = 0; k < PER; ++k) {
+      bins[tid * PER + k] = run;
       run += v[k];
     }
   }
   __syncthreads();
-  for (int n = tid; n < N; n += kFpsThreads) perm[atomicAdd(&bins[cell_of(n)], 1u)] = static_cast<uint16_t>(n);
+  for (int n = tid; n < N; n += THREADS) perm[atomicAdd(&bins[cell_of(n)], 1u)] = static_cast<uint16_t>(n);
+  __syncthreads();
+  for (int pos = tid; pos < N; pos += THREADS) owner[perm[pos]] = static_cast<uint8_t>(pos / RANGE);
+  __syncthreads();
+  // ---- setup 3: each wave lists its points in ascending original index (stream compaction) ---
+  // Slot p of a lane then holds the wave's (p*64 + lane)-th smallest index, so a lane meets its
+  // points in index order and a strict '>' keeps the lowest index among equal maxima (:83).
+  {
+    int k = 0;
+    for (int base = 0; base < N; base += kWave) {
+      const int n = base + lane;
+      const bool mine = (n < N) && owner[n] == wave;
+      const uint64_t m = __ballot(mine);
+      if (mine) perm[wave * RANGE + k + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0))] =
+          static_cast<uint16_t>(n);
+      k += __popcll(m);
+    }
+  }
   __syncthreads();
 
-  // ---- setup 3: this thread's points (wave-contiguous sorted ranges) and the wave's box ------
+  // ---- setup 4: this lane's points, running minima, packed indices; the wave's box -----------
+  const int count = min(RANGE, max(0, N - wave * RANGE));
   T px[PPT], py[PPT], pz[PPT];
   float dmin[PPT];
-  int pid[PPT];
+  uint32_t pidp[(PPT + 1) / 2];
   T wb[6];
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
@@ -196,11 +235,13 @@ __global__ __launch_bounds__(kFpsThreads) void fps_kernel(PointsView<T> pts, int
     wb[3 + a] = -wb[a];
   }
 #pragma unroll
+  for (int p = 0; p < (PPT + 1) / 2; ++p) pidp[p] = 0u;
+#pragma unroll
   for (int p = 0; p < PPT; ++p) {
-    const int pos = wave * (kWave * PPT) + p * kWave + lane;
-    if (pos < N) {
-      const int n = perm[pos];
-      pid[p] = n;
+    const int k = p * kWave + lane;
+    if (k < count) {
+      const uint32_t n = perm[wave * RANGE + k];
+      pidp[p >> 1] |= n << ((p & 1) * 16);
       px[p] = pts.at(b, 0, n);
       py[p] = pts.at(b, 1, n);
       pz[p] = pts.at(b, 2, n);
@@ -212,7 +253,6 @@ __global__ __launch_bounds__(kFpsThreads) void fps_kernel(PointsView<T> pts, int
       wb[4] = py[p] > wb[4] ? py[p] : wb[4];
       wb[5] = pz[p] > wb[5] ? pz[p] : wb[5];
     } else {
-      pid[p] = 0x7FFFFFFF;
       px[p] = py[p] = pz[p] = static_cast<T>(0);
       dmin[p] = -1.0f;  // never updated (d >= 0) and never selected
     }
@@ -224,6 +264,8 @@ __global__ __launch_bounds__(kFpsThreads) void fps_kernel(PointsView<T> pts, int
       wb[a] = ol < wb[a] ? ol : wb[a];
       wb[3 + a] = oh > wb[3 + a] ? oh : wb[3 + a];
     }
+    wb[a] = readfirstlane_t(wb[a]);
+    wb[3 + a] = readfirstlane_t(wb[3 + a]);
   }
 
   int64_t cur = start[b];
@@ -237,9 +279,12 @@ __global__ __launch_bounds__(kFpsThreads) void fps_kernel(PointsView<T> pts, int
   float wv = __builtin_huge_valf();  // forces the first step to update
   int wi = 0x7FFFFFFF;
   T wx = 0, wy = 0, wz = 0;
-  const bool empty_wave = wave * (kWave * PPT) >= N;
+  const bool empty_wave = count == 0;
+  uint64_t ph[4] = {0, 0, 0, 0}, nact = 0;
 
   for (int step = 0; step < npoint; ++step) {
+    uint64_t t0 = 0, t1 = 0, t2 = 0;
+    if constexpr (TIMING) t0 = fps_clock();
     if (tid == 0) {
       oi[step] = cur;
       if (ox) {
@@ -248,66 +293,98 @@ __global__ __launch_bounds__(kFpsThreads) void fps_kernel(PointsView<T> pts, int
         ox[2 * npoint + step] = cz;
       }
     }
-    const bool active = !empty_wave && (!PRUNE || !(box_lb2(cx, cy, cz, wb) >= static_cast<T>(wv)));
+    const bool active = !empty_wave & (!PRUNE || !(box_lb2(cx, cy, cz, wb) >= static_cast<T>(wv)));
     if (active) {
       float bv = -1.0f;
-      int bi = 0x7FFFFFFF;
-      T bx = 0, by = 0, bz = 0;
+      int bp = 0;
 #pragma unroll
       for (int p = 0; p < PPT; ++p) {
         const T dx = px[p] - cx, dy = py[p] - cy, dz = pz[p] - cz;
         const T d = (dx * dx + dy * dy) + dz * dz;  // torch.sum((xyz - c) ** 2, -1), :80
-        dmin[p] = d < static_cast<T>(dmin[p]) ? static_cast<float>(d) : dmin[p];
-        // branch-free lexicographic (value desc, original index asc): bitwise, not short-circuit
-        const bool better = (dmin[p] > bv) | ((dmin[p] == bv) & (pid[p] < bi));
-        bv = better ? dmin[p] : bv;
-        bi = better ? pid[p] : bi;
-        bx = better ? px[p] : bx;
-        by = better ? py[p] : by;
-        bz = better ? pz[p] : bz;
+        if constexpr (sizeof(T) == 4) {
+          dmin[p] = fminf(d, dmin[p]);  // == (d < dmin ? d : dmin) for finite values, :81-82
+        } else {
+          dmin[p] = d < static_cast<T>(dmin[p]) ? static_cast<float>(d) : dmin[p];
+        }
+        const bool c = dmin[p] > bv;  // strict: the first (lowest-index) of equal maxima stays
+        bp = c ? p : bp;
+        bv = c ? dmin[p] : bv;
       }
+      if constexpr (TIMING) t1 = fps_clock();
       wv = wave_maxf_dpp(bv);
       const uint64_t tied = __ballot(bv == wv);
       int wl;
       if ((tied & (tied - 1)) == 0) {
         wl = __ffsll(static_cast<long long>(tied)) - 1;
-      } else {  // equal maxima in several lanes: lowest original index
-        const int mi = wave_mini_dpp(bv == wv ? bi : 0x7FFFFFFF);
-        wl = __ffsll(static_cast<long long>(__ballot(bv == wv && bi == mi))) - 1;
+      } else {  // equal maxima in several lanes: the lowest original index among them
+        uint32_t mine = 0x7FFFFFFFu;
+#pragma unroll
+        for (int p = 0; p < PPT; ++p) mine = bp == p ? ((pidp[p >> 1] >> ((p & 1) * 16)) & 0xFFFFu) : mine;
+        const int mi = wave_mini_dpp(bv == wv ? static_cast<int>(mine) : 0x7FFFFFFF);
+        wl = __ffsll(static_cast<long long>(__ballot((bv == wv) & (static_cast<int>(mine) == mi)))) - 1;
       }
-      wi = __builtin_amdgcn_readlane(bi, wl);
-      wx = readlane_t(bx, wl);
-      wy = readlane_t(by, wl);
-      wz = readlane_t(bz, wl);
+      // the winning lane's slot index is wave-uniform: indexed register reads (s_set_gpr_idx)
+      const int wp = __builtin_amdgcn_readlane(bp, wl);
+      wi = static_cast<int>((static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(pidp[wp >> 1]), wl)) >>
+                             ((wp & 1) * 16)) & 0xFFFFu);
+      wx = readlane_t(px[wp], wl);
+      wy = readlane_t(py[wp], wl);
+      wz = readlane_t(pz[wp], wl);
+      if constexpr (TIMING) ++nact;
+    } else if constexpr (TIMING) {
+      t1 = fps_clock();
     }
     FpsSlot<T>* buf = slots[step & 1];
     if (lane == 0) buf[wave] = FpsSlot<T>{empty_wave ? -2.0f : wv, empty_wave ? 0x7FFFFFFF : wi, wx, wy, wz};
+    if constexpr (TIMING) t2 = fps_clock();
     lds_barrier();  // the output stores above stay in flight across the barrier
-    // block argmax over the 16 slots in lanes 0..15 (row 0): value desc, then index asc
-    const FpsSlot<T> mine = buf[lane & (kFpsWaves - 1)];
+    uint64_t t3 = 0;
+    if constexpr (TIMING) t3 = fps_clock();
+    // block argmax over the W slots in lanes 0..W-1 (row 0): value desc, then index asc
+    const FpsSlot<T> mine = buf[lane & (W - 1)];
     float v = mine.v;
-    v = dpp_maxf<0x111, 0x1>(v);
-    v = dpp_maxf<0x112, 0x1>(v);
-    v = dpp_maxf<0x114, 0x1>(v);
-    v = dpp_maxf<0x118, 0x1>(v);
-    const float gv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 15));
-    const uint64_t tied = __ballot(lane < kFpsWaves && mine.v == gv);
+    if constexpr (W > 1) v = dpp_maxf<0x111, 0x1>(v);
+    if constexpr (W > 2) v = dpp_maxf<0x112, 0x1>(v);
+    if constexpr (W > 4) v = dpp_maxf<0x114, 0x1>(v);
+    if constexpr (W > 8) v = dpp_maxf<0x118, 0x1>(v);
+    const float gv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), W - 1));
+    const uint64_t tied = __ballot((lane < W) & (mine.v == gv));
     int ws;
     if ((tied & (tied - 1)) == 0) {
       ws = __ffsll(static_cast<long long>(tied)) - 1;
     } else {
-      int ii = (lane < kFpsWaves && mine.v == gv) ? mine.i : 0x7FFFFFFF;
-      ii = dpp_mini<0x111, 0x1>(ii);
-      ii = dpp_mini<0x112, 0x1>(ii);
-      ii = dpp_mini<0x114, 0x1>(ii);
-      ii = dpp_mini<0x118, 0x1>(ii);
-      const int mi = __builtin_amdgcn_readlane(ii, 15);
-      ws = __ffsll(static_cast<long long>(__ballot(lane < kFpsWaves && mine.v == gv && mine.i == mi))) - 1;
+      int ii = ((lane < W) & (mine.v == gv)) ? mine.i : 0x7FFFFFFF;
+      if constexpr (W > 1) ii = dpp_mini<0x111, 0x1>(ii);
+      if constexpr (W > 2) ii = dpp_mini<0x112, 0x1>(ii);
+      if constexpr (W > 4) ii = dpp_mini<0x114, 0x1>(ii);
+      if constexpr (W > 8) ii = dpp_mini<0x118, 0x1>(ii);
+      const int mi = __builtin_amdgcn_readlane(ii, W - 1);
+      ws = __ffsll(static_cast<long long>(__ballot((lane < W) & (mine.v == gv) & (mine.i == mi)))) - 1;
     }
-    cur = buf[ws].i;
-    cx = buf[ws].x;
-    cy = buf[ws].y;
-    cz = buf[ws].z;
+    cur = __builtin_amdgcn_readlane(mine.i, ws);
+    cx = readlane_t(mine.x, ws);
+    cy = readlane_t(mine.y, ws);
+    cz = readlane_t(mine.z, ws);
+    if constexpr (TIMING) {
+      const uint64_t t4 = fps_clock();
+      ph[0] += t1 - t0;  // box test + point update
+      ph[1] += t2 - t1;  // wave argmax + slot publish
+      ph[2] += t3 - t2;  // barrier wait
+      ph[3] += t4 - t3;  // slot reduction
+    }
+  }
+  if constexpr (TIMING) {
+    if (prof && lane == 0) {
+      unsigned long long* o = prof + (static_cast<int64_t>(b) * W + wave) * kFpsProf;
+      o[0] = ph[0];
+      o[1] = ph[1];
+      o[2] = ph[2];
+      o[3] = ph[3];
+      o[4] = nact;
+      o[5] = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);  // HW_ID: wave slot, SIMD, CU
+      o[6] = static_cast<unsigned long long>(count);
+      o[7] = 0;
+    }
   }
 }
 
@@ -317,7 +394,8 @@ __global__ __launch_bounds__(kFpsThreads) void fps_dense_kernel(PointsView<T> pt
                                                                 const int64_t* __restrict__ start,
                                                                 int64_t* __restrict__ out_idx, T* __restrict__ out_xyz,
                                                                 float* __restrict__ ws) {
-  __shared__ FpsSlot<T> slots[2][kFpsWaves];
+  constexpr int kDenseWaves = kFpsThreads / kWave;
+  __shared__ FpsSlot<T> slots[2][kDenseWaves];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float* dmin = ws + static_cast<int64_t>(b) * N;
   for (int n = tid; n < N; n += kFpsThreads) dmin[n] = 1e10f;
@@ -358,7 +436,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_dense_kernel(PointsView<T> pt
     __syncthreads();
     float gv = -2.0f;
     int gi = 0x7FFFFFFF;
-    for (int w = 0; w < kFpsWaves; ++w) {
+    for (int w = 0; w < kDenseWaves; ++w) {
       const float v = slots[step & 1][w].v;
       const int i = slots[step & 1][w].i;
       if (v > gv || (v == gv && i < gi)) {
@@ -384,23 +462,23 @@ static int launch_fps(const T* xyz, int64_t sb, int64_t sc, int64_t sn, int B, i
     const char* e = getenv("DVCP_FPS_NOPRUNE");
     return e && e[0] == '1';
   }();
-#define DVCP_FPS_CASE(P)                                                                                      \
-  if (ppt <= P) {                                                                                             \
-    if (noprune)                                                                                              \
-      hipLaunchKernelGGL((fps_kernel<T, P, false>), grid, block, 0, st, v, N, npoint, start, out_idx, out_xyz); \
-    else                                                                                                      \
-      hipLaunchKernelGGL((fps_kernel<T, P, true>), grid, block, 0, st, v, N, npoint, start, out_idx, out_xyz);  \
-    return launch_status("dvcp_fps");                                                                         \
+#define DVCP_FPS_CASE(P)                                                                             \
+  if (ppt <= P) {                                                                                    \
+    if (noprune)                                                                                     \
+      hipLaunchKernelGGL((fps_kernel<T, kFpsThreads, P, false>), grid, block, 0, st, v, N, npoint, start, \
+                         out_idx, out_xyz, nullptr);                                                 \
+    else                                                                                             \
+      hipLaunchKernelGGL((fps_kernel<T, kFpsThreads, P, true>), grid, block, 0, st, v, N, npoint, start,  \
+                         out_idx, out_xyz, nullptr);                                                 \
+    return launch_status("dvcp_fps");                                                                \
   }
-  DVCP_FPS_CASE(1)
   DVCP_FPS_CASE(2)
   DVCP_FPS_CASE(4)
   DVCP_FPS_CASE(8)
-  if (sizeof(T) == 4 || N <= 12 * kFpsThreads) {
-    DVCP_FPS_CASE(12)
-  }
-  if (sizeof(T) == 4) {
-    DVCP_FPS_CASE(16)
+  DVCP_FPS_CASE(16)
+  if constexpr (sizeof(T) == 4) {
+    DVCP_FPS_CASE(24)
+    DVCP_FPS_CASE(32)
   }
 #undef DVCP_FPS_CASE
   if (!ws) {

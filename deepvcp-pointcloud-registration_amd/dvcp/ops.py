@@ -19,7 +19,7 @@ def _pts(t, pdim):
 
 
 # largest cloud the register-resident FPS kernel takes (csrc/fps.hip); beyond it a workspace
-FPS_REG_LIMIT = {torch.float32: 16384, torch.float64: 12288}
+FPS_REG_LIMIT = {torch.float32: 16384, torch.float64: 8192}
 
 
 def fps(xyz, npoint, start, pdim=1):
@@ -158,9 +158,11 @@ def voxelize(pts, r, s, G, pdim=1):
     return cand, err
 
 
-# reference sets at least this large use the cell-grid kNN (dvcp_knn_grid); smaller ones the
-# brute-force scan (dvcp_knn).  Both are exact and return identical results.
-KNN_GRID_MIN_M = 2048
+# Default kNN method.  Both are exact and return identical results.  The cell grid
+# (dvcp_knn_grid) loses on the forward's workload: most voxel candidates lie outside the target
+# cloud, so the shell search visits most cells (profiles/round1: 35.8 ms vs 12.4 ms brute per
+# C3 step).
+KNN_DEFAULT_METHOD = "brute"
 
 
 def knn(ref, qry, k, ref_pdim=1, qry_pdim=1, want_idx64=True, method=None):
@@ -176,7 +178,7 @@ def knn(ref, qry, k, ref_pdim=1, qry_pdim=1, want_idx64=True, method=None):
     idx = torch.empty(B, Q, k, dtype=torch.int32, device=dev)
     idx64 = torch.empty(B, Q, k, dtype=torch.int64, device=dev) if want_idx64 else None
     work = (9.0 * B * Q * M, B * (12 * (M + Q) + Q * k * (8 + (8 if want_idx64 else 0))))
-    method = method or ("grid" if M >= KNN_GRID_MIN_M else "brute")
+    method = method or KNN_DEFAULT_METHOD
     if method == "grid":
         ws = torch.empty(int(_lib.load().dvcp_knn_grid_workspace_bytes(B, M)), dtype=torch.uint8, device=dev)
         call("dvcp_knn_grid", dtype_code(ref), ptr(ref), rb, rc, rn, M, ptr(qry), qb, qc, qn, Q, B, int(k), ptr(ws),

@@ -48,7 +48,7 @@ int dvcp_fps(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int
              int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz, void* stream);
 
 /* dvcp_fps with a B x N fp32 workspace, required when N exceeds the register-resident limit
- * (16384 fp32 / 12288 fp64 points per cloud); smaller clouds ignore it. */
+ * (16384 fp32 / 8192 fp64 points per cloud); smaller clouds ignore it. */
 int dvcp_fps_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N,
                 int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz, float* ws,
                 void* stream);
