@@ -1,0 +1,458 @@
+// knn_tiled.hip -- exact kNN over spatially sorted reference tiles (replaces knn_cuda.KNN at
+// get_cat_feat_tgt.py:45,52; same contract as dvcp_knn in knn.hip: fp32 d2 = (dx*dx + dy*dy) +
+// dz*dz with dx = ref - query, ascending, ties to the lower index, dist = correctly rounded sqrt).
+//
+// Why: the brute-force scan meets reference points in index order, so a lane keeps inserting into
+// its sorted top-32 and the wave executes the 32-deep insertion network on almost every point.
+// Here both sets are sorted by a 12-bit Morton cell, references into 64-point tiles with boxes.
+// Each wave takes 64 Morton-consecutive queries (a compact box), sorts the tiles by the lower
+// bound of the distance between its query box and each tile box, and scans tiles nearest first:
+//   * tile data is wave-uniform, so points come through the scalar cache as SGPR operands;
+//   * a tile is skipped when no lane's own lower bound reaches its current k-th distance;
+//   * the scan stops when the next tile's bound exceeds every lane's k-th distance.
+// Exactness: round-to-nearest is monotone, so a bound computed from box faces with the same
+// float ops never exceeds the computed d2 of any point in the box; tiles are dropped only when the
+// bound is strictly above the k-th distance, so every point that could enter or tie the top k is
+// examined, and insertion orders by (d2, index) explicitly.
+#include "common.h"
+
+namespace dvcp {
+
+constexpr int kTile = 64;             // reference points per tile
+constexpr int kMaxTiles = 256;        // per cloud: M <= 16384
+constexpr int kTiledThreads = 256;    // 4 independent waves per workgroup
+constexpr int kSortBins = 4096;       // 12-bit Morton cells
+constexpr int kBuildThreads = 1024;
+
+struct TiledLayout {
+  float4* sorted;  // B x T*64: x, y, z, original index bits (padding: NaN, index 0x7FFFFFFF)
+  float4* tbox;    // B x T x 2: {lo.xyz, _}, {hi.xyz, _}
+  int32_t* qperm;  // B x Q: query index by Morton position
+};
+
+__device__ __forceinline__ float float_unorder(uint32_t u) {  // inverse of float_order
+  const uint32_t flip = (u >> 31) ? 0x80000000u : 0xFFFFFFFFu;
+  return __uint_as_float(u ^ flip);
+}
+
+// Wave-uniform reads through the constant address space: the compiler emits scalar loads
+// (s_load_dwordx*), so tile data arrives in SGPRs and feeds the VALU as scalar operands.
+typedef __attribute__((address_space(4))) const float const_float;
+
+// A pointer known to be wave-uniform (the compiler can lose that through divergent phis).
+template <typename P>
+__device__ __forceinline__ P* uniform_ptr(P* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v & 0xFFFFFFFFull)));
+  const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v >> 32)));
+  return reinterpret_cast<P*>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
+
+inline TiledLayout tiled_layout(void* ws, int B, int M, int Q) {
+  const int64_t T = ceil_div(M, kTile);
+  char* p = static_cast<char*>(ws);
+  TiledLayout L;
+  L.sorted = reinterpret_cast<float4*>(p);
+  p += align256(16 * int64_t(B) * T * kTile);
+  L.tbox = reinterpret_cast<float4*>(p);
+  p += align256(32 * int64_t(B) * T);
+  L.qperm = reinterpret_cast<int32_t*>(p);
+  return L;
+}
+
+__device__ __forceinline__ uint32_t spread4b(uint32_t v) {
+  v &= 0xF;
+  return (v & 1u) | ((v & 2u) << 2) | ((v & 4u) << 4) | ((v & 8u) << 6);
+}
+
+// Block-wide bounding box of n points (1024 threads).
+template <typename GET>
+__device__ void block_bbox(int n, GET get, float (&lo)[3], float (&hi)[3], float (*red)[3][16]) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    lo[a] = __builtin_huge_valf();
+    hi[a] = -__builtin_huge_valf();
+  }
+  for (int i = tid; i < n; i += kBuildThreads) {
+    float v[3];
+    get(i, v);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = fminf(lo[a], v[a]);
+      hi[a] = fmaxf(hi[a], v[a]);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    for (int off = 32; off > 0; off >>= 1) {
+      lo[a] = fminf(lo[a], __shfl_xor(lo[a], off, kWave));
+      hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], off, kWave));
+    }
+    if (lane == 0) {
+      red[0][a][wave] = lo[a];
+      red[1][a][wave] = hi[a];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    float l = red[0][a][0], h = red[1][a][0];
+    for (int w = 1; w < kBuildThreads / kWave; ++w) {
+      l = fminf(l, red[0][a][w]);
+      h = fmaxf(h, red[1][a][w]);
+    }
+    lo[a] = l;
+    hi[a] = h;
+  }
+  __syncthreads();
+}
+
+// Counting sort of n items by 12-bit Morton cell over [lo, hi]; emit(pos, i, v) for each item.
+template <typename GET, typename EMIT>
+__device__ void morton_sort(int n, GET get, EMIT emit, const float (&lo)[3], const float (&hi)[3], uint32_t* bins,
+                            uint32_t* wsum) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float scale[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) scale[a] = hi[a] > lo[a] ? 16.0f / (hi[a] - lo[a]) : 0.0f;
+  auto cell = [&](const float (&v)[3]) -> uint32_t {
+    uint32_t c = 0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      int q = static_cast<int>((v[a] - lo[a]) * scale[a]);
+      q = q < 0 ? 0 : (q > 15 ? 15 : q);
+      c |= spread4b(static_cast<uint32_t>(q)) << a;
+    }
+    return c;
+  };
+  for (int i = tid; i < kSortBins; i += kBuildThreads) bins[i] = 0u;
+  __syncthreads();
+  for (int i = tid; i < n; i += kBuildThreads) {
+    float v[3];
+    get(i, v);
+    atomicAdd(&bins[cell(v)], 1u);
+  }
+  __syncthreads();
+  {
+    constexpr int PER = kSortBins / kBuildThreads;
+    uint32_t c[PER], s = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      c[k] = bins[tid * PER + k];
+      s += c[k];
+    }
+    uint32_t incl = s;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t u = __shfl_up(incl, off, kWave);
+      if (lane >= off) incl += u;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t run = incl - s;
+    for (int w = 0; w < wave; ++w) run += wsum[w];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      bins[tid * PER + k] = run;
+      run += c[k];
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < n; i += kBuildThreads) {
+    float v[3];
+    get(i, v);
+    emit(static_cast<int>(atomicAdd(&bins[cell(v)], 1u)), i, v);
+  }
+  __syncthreads();
+}
+
+template <typename CT>
+__global__ __launch_bounds__(kBuildThreads) void knn_tiled_build_kernel(PointsView<CT> ref, int M, PointsView<CT> qry,
+                                                                        int Q, TiledLayout L) {
+  __shared__ uint32_t bins[kSortBins];
+  __shared__ uint32_t boxk[kMaxTiles][6];  // order-preserving float keys: lo.xyz (min), hi.xyz (max)
+  __shared__ uint32_t wsum[16];
+  __shared__ float red[2][3][16];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int T = (M + kTile - 1) / kTile;
+  float4* so = L.sorted + static_cast<int64_t>(b) * T * kTile;
+  // knn_cuda casts both inputs with .float()
+  auto get_ref = [&](int i, float (&v)[3]) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) v[a] = static_cast<float>(ref.at(b, a, i));
+  };
+  auto get_qry = [&](int i, float (&v)[3]) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) v[a] = static_cast<float>(qry.at(b, a, i));
+  };
+  for (int i = tid; i < T * 6; i += kBuildThreads) boxk[i / 6][i % 6] = (i % 6) < 3 ? 0xFFFFFFFFu : 0u;
+  float lo[3], hi[3];
+  block_bbox(M, get_ref, lo, hi, red);
+  morton_sort(
+      M, get_ref,
+      [&](int pos, int i, const float (&v)[3]) {
+        so[pos] = make_float4(v[0], v[1], v[2], __int_as_float(i));
+        const int t = pos / kTile;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          atomicMin(&boxk[t][a], float_order(v[a]));
+          atomicMax(&boxk[t][3 + a], float_order(v[a]));
+        }
+      },
+      lo, hi, bins, wsum);
+  for (int pos = M + tid; pos < T * kTile; pos += kBuildThreads)
+    so[pos] = make_float4(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __int_as_float(0x7FFFFFFF));
+  for (int t = tid; t < T; t += kBuildThreads) {
+    float4* tb = L.tbox + (static_cast<int64_t>(b) * T + t) * 2;
+    tb[0] = make_float4(float_unorder(boxk[t][0]), float_unorder(boxk[t][1]), float_unorder(boxk[t][2]), 0.f);
+    tb[1] = make_float4(float_unorder(boxk[t][3]), float_unorder(boxk[t][4]), float_unorder(boxk[t][5]), 0.f);
+  }
+  // queries: Morton order over their own bounding box
+  block_bbox(Q, get_qry, lo, hi, red);
+  int32_t* qp = L.qperm + static_cast<int64_t>(b) * Q;
+  morton_sort(
+      Q, get_qry, [&](int pos, int i, const float (&)[3]) { qp[pos] = i; }, lo, hi, bins, wsum);
+}
+
+// Lower bound of the computed d2 between a point in box [a_lo, a_hi] and a point in box
+// [b_lo, b_hi] (per axis gap fl(b_lo - a_hi) or fl(a_lo - b_hi), then the d2 formula).
+__device__ __forceinline__ float box_box_lb2(float alx, float aly, float alz, float ahx, float ahy, float ahz,
+                                             float blx, float bly, float blz, float bhx, float bhy, float bhz) {
+  const float gx = fmaxf(fmaxf(blx - ahx, alx - bhx), 0.0f);
+  const float gy = fmaxf(fmaxf(bly - ahy, aly - bhy), 0.0f);
+  const float gz = fmaxf(fmaxf(blz - ahz, alz - bhz), 0.0f);
+  return (gx * gx + gy * gy) + gz * gz;
+}
+
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_max_u(uint32_t v) {
+  return max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, ROWS, 0xF, false)));
+}
+// max over the wave of non-negative float bits (k-th distances; +inf allowed)
+__device__ __forceinline__ float wave_max_nonneg(float x) {
+  uint32_t v = __float_as_uint(x);
+  v = dpp_max_u<0x111, 0xF>(v);
+  v = dpp_max_u<0x112, 0xF>(v);
+  v = dpp_max_u<0x114, 0xF>(v);
+  v = dpp_max_u<0x118, 0xF>(v);
+  v = dpp_max_u<0x142, 0xA>(v);
+  v = dpp_max_u<0x143, 0xC>(v);
+  return __uint_as_float(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63)));
+}
+
+// Bitonic sort (ascending) of 64*R keys held as keys[r] at position r*64 + lane.
+template <int R>
+__device__ __forceinline__ void wave_bitonic(uint32_t (&keys)[R]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 2; k <= 64 * R; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j >= 64) {  // partner is another register of the same lane
+        const int jr = j >> 6;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if ((r & jr) == 0) {
+            const int i = r * 64 + lane;
+            const bool up = (i & k) == 0;
+            const uint32_t a = keys[r], c = keys[r + jr];
+            const bool sw = up ? (a > c) : (a < c);
+            keys[r] = sw ? c : a;
+            keys[r + jr] = sw ? a : c;
+          }
+        }
+      } else {  // partner lane = lane ^ j, same register
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int i = r * 64 + lane;
+          const uint32_t o = static_cast<uint32_t>(__shfl_xor(static_cast<int>(keys[r]), j, kWave));
+          const bool lower = (lane & j) == 0;  // this lane holds the lower index of the pair
+          const bool up = (i & k) == 0;
+          const uint32_t mn = min(keys[r], o), mx = max(keys[r], o);
+          keys[r] = (lower == up) ? mn : mx;
+        }
+      }
+    }
+  }
+}
+
+template <int KT, int R>
+__global__ __launch_bounds__(kTiledThreads) void knn_tiled_query_kernel(const float4* __restrict__ sorted,
+                                                                        const float4* __restrict__ tbox,
+                                                                        const int32_t* __restrict__ qperm, int M,
+                                                                        const void* __restrict__ qry_raw,
+                                                                        int64_t qb, int64_t qc, int64_t qn, int qf64,
+                                                                        int Q, int k, float* __restrict__ dist,
+                                                                        int32_t* __restrict__ idx,
+                                                                        int64_t* __restrict__ idx64) {
+  const int b = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int T = (M + kTile - 1) / kTile;
+  const int sq = (blockIdx.x * (kTiledThreads / kWave) + wave) * kWave + lane;
+  if ((blockIdx.x * (kTiledThreads / kWave) + wave) * kWave >= Q) return;  // whole wave past the end
+  const bool live = sq < Q;
+  const int q = live ? qperm[static_cast<int64_t>(b) * Q + sq] : 0;
+  float qx, qy, qz;
+  if (qf64) {
+    const double* p = static_cast<const double*>(qry_raw);
+    qx = static_cast<float>(p[b * qb + 0 * qc + q * qn]);
+    qy = static_cast<float>(p[b * qb + 1 * qc + q * qn]);
+    qz = static_cast<float>(p[b * qb + 2 * qc + q * qn]);
+  } else {
+    const float* p = static_cast<const float*>(qry_raw);
+    qx = p[b * qb + 0 * qc + q * qn];
+    qy = p[b * qb + 1 * qc + q * qn];
+    qz = p[b * qb + 2 * qc + q * qn];
+  }
+  // the wave's query box (live lanes only)
+  float wl[3] = {live ? qx : __builtin_huge_valf(), live ? qy : __builtin_huge_valf(),
+                 live ? qz : __builtin_huge_valf()};
+  float wh[3] = {live ? qx : -__builtin_huge_valf(), live ? qy : -__builtin_huge_valf(),
+                 live ? qz : -__builtin_huge_valf()};
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+    for (int off = 32; off > 0; off >>= 1) {
+      wl[a] = fminf(wl[a], __shfl_xor(wl[a], off, kWave));
+      wh[a] = fmaxf(wh[a], __shfl_xor(wh[a], off, kWave));
+    }
+  const float4* tb = tbox + static_cast<int64_t>(b) * T * 2;
+  // tile keys: lb2(query box, tile box) with the low 8 mantissa bits replaced by the tile id.
+  // Truncation only lowers a non-negative float, so key value <= the true bound.
+  uint32_t keys[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int t = r * 64 + lane;
+    if (t < T) {
+      const float4 lo = tb[2 * t], hi = tb[2 * t + 1];
+      const float lb = box_box_lb2(wl[0], wl[1], wl[2], wh[0], wh[1], wh[2], lo.x, lo.y, lo.z, hi.x, hi.y, hi.z);
+      keys[r] = (__float_as_uint(lb) & 0xFFFFFF00u) | static_cast<uint32_t>(t);
+    } else {
+      keys[r] = 0xFFFFFFFFu;
+    }
+  }
+  wave_bitonic<R>(keys);
+
+  float kd[KT];
+  int ki[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    kd[t] = __builtin_huge_valf();
+    ki[t] = 0x7FFFFFFF;
+  }
+  const int kk = k - 1;  // wave-uniform: kd[kk] is an indexed register read
+  float kth = live ? __builtin_huge_valf() : 0.0f;  // dead lanes never need more points
+  float wkth = wave_max_nonneg(kth);
+  const float4* P = uniform_ptr(sorted + static_cast<int64_t>(b) * T * kTile);
+  const float4* tbu = uniform_ptr(tb);
+  bool stop = false;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    for (int i = 0; i < 64 && !stop; ++i) {
+      if (r * 64 + i >= T) break;
+      const uint32_t key = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(keys[r]), i));
+      if (__uint_as_float(key & 0xFFFFFF00u) > wkth) {  // every later tile is farther
+        stop = true;
+        break;
+      }
+      const int t = static_cast<int>(key & 0xFFu);
+      const const_float* bx = (const const_float*)(tbu + 2 * t);
+      const float lbq = box_box_lb2(qx, qy, qz, qx, qy, qz, bx[0], bx[1], bx[2], bx[4], bx[5], bx[6]);
+      const bool act = live & (lbq <= kth);
+      if (__ballot(act) == 0) continue;
+      const const_float* tp = (const const_float*)(P + t * kTile);
+      uint64_t ins = 0;
+      for (int j0 = 0; j0 < kTile; j0 += 16) {
+        // the whole 16-point chunk is loaded (scalar loads, one wait) before any branch
+        float c[64];
+#pragma unroll
+        for (int u = 0; u < 64; ++u) c[u] = tp[4 * j0 + u];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const float px = c[4 * j], py = c[4 * j + 1], pz = c[4 * j + 2];
+          const int pi = __float_as_int(c[4 * j + 3]);
+          const float dx = px - qx, dy = py - qy, dz = pz - qz;
+          const float d2 = (dx * dx + dy * dy) + dz * dz;
+          const bool cand = act & (d2 <= kth) & (d2 < __builtin_huge_valf());
+          const uint64_t m = __ballot(cand);
+          if (m != 0) {  // wave-uniform branch; lanes without a candidate keep their lists
+            ins |= m;
+#pragma unroll
+            for (int u = KT - 1; u > 0; --u) {
+              const bool here = cand & ((d2 < kd[u]) | ((d2 == kd[u]) & (pi < ki[u])));
+              const bool before = cand & ((d2 < kd[u - 1]) | ((d2 == kd[u - 1]) & (pi < ki[u - 1])));
+              kd[u] = before ? kd[u - 1] : (here ? d2 : kd[u]);
+              ki[u] = before ? ki[u - 1] : (here ? pi : ki[u]);
+            }
+            const bool first = cand & ((d2 < kd[0]) | ((d2 == kd[0]) & (pi < ki[0])));
+            kd[0] = first ? d2 : kd[0];
+            ki[0] = first ? pi : ki[0];
+            kth = live ? (KT == 1 ? kd[0] : kd[kk]) : 0.0f;
+          }
+        }
+      }
+      if (ins != 0) wkth = wave_max_nonneg(kth);
+    }
+  }
+  if (!live) return;
+  const int64_t o = (static_cast<int64_t>(b) * Q + q) * k;
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    if (t < k) {
+      const bool ok = ki[t] != 0x7FFFFFFF;  // fewer than k finite points: like dvcp_knn (inf, -1)
+      if (dist) dist[o + t] = ok ? sqrt_rn(kd[t]) : __builtin_huge_valf();
+      if (idx) idx[o + t] = ok ? ki[t] : -1;
+      if (idx64) idx64[o + t] = ok ? ki[t] : -1;
+    }
+  }
+}
+
+}  // namespace dvcp
+
+extern "C" int64_t dvcp_knn_tiled_workspace_bytes(int B, int M, int Q) {
+  if (B < 0 || M < 0 || Q < 0) return -1;
+  const int64_t T = dvcp::ceil_div(M, dvcp::kTile);
+  return dvcp::align256(16 * int64_t(B) * T * dvcp::kTile) + dvcp::align256(32 * int64_t(B) * T) +
+         dvcp::align256(4 * int64_t(B) * Q);
+}
+
+extern "C" int dvcp_knn_tiled(int dtype, const void* ref, int64_t rb, int64_t rc, int64_t rn, int M, const void* qry,
+                              int64_t qb, int64_t qc, int64_t qn, int Q, int B, int k, void* workspace, float* dist,
+                              int32_t* idx, int64_t* idx64, void* stream) {
+  DVCP_REQUIRE(ref && qry && workspace, "dvcp_knn_tiled: null pointer");
+  DVCP_REQUIRE(k > 0 && k <= 32 && M >= 0 && Q >= 0 && B >= 0 && B <= 65535, "dvcp_knn_tiled: bad sizes");
+  DVCP_REQUIRE(M <= dvcp::kMaxTiles * dvcp::kTile, "dvcp_knn_tiled: M=%d > %d", M, dvcp::kMaxTiles * dvcp::kTile);
+  DVCP_REQUIRE(dtype == DVCP_F32 || dtype == DVCP_F64, "dvcp_knn_tiled: bad dtype %d", dtype);
+  if (B == 0 || Q == 0) return DVCP_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const dvcp::TiledLayout L = dvcp::tiled_layout(workspace, B, M, Q);
+  if (dtype == DVCP_F32)
+    hipLaunchKernelGGL((dvcp::knn_tiled_build_kernel<float>), dim3(B), dim3(dvcp::kBuildThreads), 0, st,
+                       dvcp::PointsView<float>{static_cast<const float*>(ref), rb, rc, rn}, M,
+                       dvcp::PointsView<float>{static_cast<const float*>(qry), qb, qc, qn}, Q, L);
+  else
+    hipLaunchKernelGGL((dvcp::knn_tiled_build_kernel<double>), dim3(B), dim3(dvcp::kBuildThreads), 0, st,
+                       dvcp::PointsView<double>{static_cast<const double*>(ref), rb, rc, rn}, M,
+                       dvcp::PointsView<double>{static_cast<const double*>(qry), qb, qc, qn}, Q, L);
+  if (int e = dvcp::launch_status("dvcp_knn_tiled(build)")) return e;
+  const int T = dvcp::ceil_div(M, dvcp::kTile);
+  const int qf64 = dtype == DVCP_F64;
+  dim3 grid(dvcp::ceil_div(Q, dvcp::kTiledThreads), B);
+#define DVCP_KNNT(KK, RR)                                                                                          \
+  if (k <= KK && T <= 64 * RR) {                                                                                   \
+    hipLaunchKernelGGL((dvcp::knn_tiled_query_kernel<KK, RR>), grid, dim3(dvcp::kTiledThreads), 0, st, L.sorted,   \
+                       L.tbox, L.qperm, M, qry, qb, qc, qn, qf64, Q, k, dist, idx, idx64);                                                                                \
+    return dvcp::launch_status("dvcp_knn_tiled(query)");                                                           \
+  }
+  DVCP_KNNT(1, 1)
+  DVCP_KNNT(1, 4)
+  DVCP_KNNT(8, 1)
+  DVCP_KNNT(8, 4)
+  DVCP_KNNT(16, 4)
+  DVCP_KNNT(32, 1)
+  DVCP_KNNT(32, 2)
+  DVCP_KNNT(32, 4)
+#undef DVCP_KNNT
+  dvcp::set_error("dvcp_knn_tiled: unsupported k=%d", k);
+  return DVCP_EINVAL;
+}

@@ -34,6 +34,7 @@ SIGNATURES = {
     "dvcp_voxelize": [_I, _P, _L, _L, _L, _I, _I, _D, _D, _I, _P, _P, _P],
     "dvcp_knn": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P],
     "dvcp_knn_grid": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P],
+    "dvcp_knn_tiled": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P],
     "dvcp_dfe": [_I, _P, _L, _P, _P, _P],
     "dvcp_dfe_tgt": [_I, _P, _L, _L, _L, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P],
     "dvcp_cpg": [_P, _P, _L, _L, _L, _P, _I, _I, _P, _P, _P, _P],
@@ -60,6 +61,8 @@ def load():
     lib.dvcp_abi_version.argtypes = []
     lib.dvcp_knn_grid_workspace_bytes.restype = ctypes.c_int64
     lib.dvcp_knn_grid_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.dvcp_knn_tiled_workspace_bytes.restype = ctypes.c_int64
+    lib.dvcp_knn_tiled_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
     for name, args in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = ctypes.c_int
@@ -69,7 +72,8 @@ def load():
 
 
 def exported_symbols():
-    return ["dvcp_last_error", "dvcp_abi_version", "dvcp_knn_grid_workspace_bytes"] + list(SIGNATURES)
+    return ["dvcp_last_error", "dvcp_abi_version", "dvcp_knn_grid_workspace_bytes",
+            "dvcp_knn_tiled_workspace_bytes"] + list(SIGNATURES)
 
 
 # When a list, every entry-point call appends (name, start_event, end_event, work) recorded on

@@ -158,11 +158,19 @@ def voxelize(pts, r, s, G, pdim=1):
     return cand, err
 
 
-# Default kNN method.  Both are exact and return identical results.  The cell grid
-# (dvcp_knn_grid) loses on the forward's workload: most voxel candidates lie outside the target
-# cloud, so the shell search visits most cells (profiles/round1: 35.8 ms vs 12.4 ms brute per
-# C3 step).
-KNN_DEFAULT_METHOD = "brute"
+# kNN method choice.  All three are exact and return identical results.
+#   tiled: Morton-sorted reference tiles scanned nearest-first per wave (dvcp_knn_tiled);
+#          M <= KNN_TILED_MAX_M.
+#   brute: index-order scan of every reference point (dvcp_knn); best for small M.
+#   grid:  per-query cell-shell search (dvcp_knn_grid); loses on the forward's workload, where
+#          most voxel candidates lie outside the target cloud (profiles/round1: 35.8 ms vs 12.4 ms
+#          brute per C3 step).  Kept as an option.
+KNN_TILED_MIN_M = 512
+KNN_TILED_MAX_M = 16384
+
+
+def knn_method(M):
+    return "tiled" if KNN_TILED_MIN_M <= M <= KNN_TILED_MAX_M else "brute"
 
 
 def knn(ref, qry, k, ref_pdim=1, qry_pdim=1, want_idx64=True, method=None):
@@ -178,8 +186,12 @@ def knn(ref, qry, k, ref_pdim=1, qry_pdim=1, want_idx64=True, method=None):
     idx = torch.empty(B, Q, k, dtype=torch.int32, device=dev)
     idx64 = torch.empty(B, Q, k, dtype=torch.int64, device=dev) if want_idx64 else None
     work = (9.0 * B * Q * M, B * (12 * (M + Q) + Q * k * (8 + (8 if want_idx64 else 0))))
-    method = method or KNN_DEFAULT_METHOD
-    if method == "grid":
+    method = method or knn_method(M)
+    if method == "tiled":
+        ws = torch.empty(int(_lib.load().dvcp_knn_tiled_workspace_bytes(B, M, Q)), dtype=torch.uint8, device=dev)
+        call("dvcp_knn_tiled", dtype_code(ref), ptr(ref), rb, rc, rn, M, ptr(qry), qb, qc, qn, Q, B, int(k), ptr(ws),
+             ptr(dist), ptr(idx), ptr(idx64), stream(), work=work)
+    elif method == "grid":
         ws = torch.empty(int(_lib.load().dvcp_knn_grid_workspace_bytes(B, M)), dtype=torch.uint8, device=dev)
         call("dvcp_knn_grid", dtype_code(ref), ptr(ref), rb, rc, rn, M, ptr(qry), qb, qc, qn, Q, B, int(k), ptr(ws),
              ptr(dist), ptr(idx), ptr(idx64), stream(), work=work)

@@ -150,30 +150,62 @@ def test_knn_golden(cuda, name):
     assert torch.equal(d.cpu(), T(z["dist"]))
 
 
+@pytest.mark.parametrize("method", ["tiled", "brute", "grid"])
 @pytest.mark.parametrize("name", ["knn_f32", "knn_dyadic"])
-def test_knn_grid_golden(cuda, name):
-    """The cell-grid kNN on the golden fixtures (forced even though M is small)."""
+def test_knn_methods_golden(cuda, name, method):
+    """Every kNN method on the golden fixtures (forced regardless of M)."""
     from dvcp import ops
     z = golden(name)
-    d, _, i = ops.knn(T(z["ref"], cuda), T(z["qry"], cuda), 32, method="grid")
+    d, _, i = ops.knn(T(z["ref"], cuda), T(z["qry"], cuda), 32, method=method)
     assert torch.equal(i.cpu(), T(z["idx"]))
     assert torch.equal(d.cpu(), T(z["dist"]))
 
 
-@pytest.mark.parametrize("k", [1, 5, 32])
-def test_knn_grid_equals_brute_full_size(cuda, k):
-    """C3 shape: 10000 target FE-like points, candidate-grid queries partly far outside the
-    cloud (as the R_init-only transform produces) and exact duplicates (ties)."""
-    from dvcp import ops
+def _c3_knn_inputs(cuda, M=10000, Q=20000, B=2, seed=113):
+    """C3 shape: FE-like target points, candidate-grid-like queries partly far outside the cloud
+    (as the R_init-only transform produces), and exact duplicates (ties)."""
     from dvcp.synthetic import rot_xyz
-    g = torch.Generator().manual_seed(113)
-    ref = (torch.rand(2, 10000, 3, generator=g) * 2 - 1)
+    g = torch.Generator().manual_seed(seed)
+    ref = (torch.rand(B, M, 3, generator=g) * 2 - 1)
     ref = ref @ torch.from_numpy(rot_xyz(0.4, 1.1, 2.0)).float().T + 0.7
-    ref[:, 5000:5100] = ref[:, 100:200]                       # duplicated points -> equal distances
-    qry = torch.rand(2, 20000, 3, generator=g) * 8 - 4           # many queries outside the cloud
-    ref, qry = ref.to(cuda), qry.to(cuda)
+    if M >= 5100:
+        ref[:, 5000:5100] = ref[:, 100:200]                   # duplicated points -> equal distances
+    qry = torch.rand(B, Q, 3, generator=g) * 8 - 4             # many queries outside the cloud
+    return ref.to(cuda), qry.to(cuda)
+
+
+@pytest.mark.parametrize("method", ["tiled", "grid"])
+@pytest.mark.parametrize("k", [1, 5, 32])
+def test_knn_method_equals_brute_full_size(cuda, k, method):
+    from dvcp import ops
+    ref, qry = _c3_knn_inputs(cuda)
     d1, i1, _ = ops.knn(ref, qry, k, method="brute")
-    d2, i2, _ = ops.knn(ref, qry, k, method="grid")
+    d2, i2, _ = ops.knn(ref, qry, k, method=method)
+    assert torch.equal(i1, i2) and torch.equal(d1, d2)
+
+
+@pytest.mark.parametrize("M,Q,k", [(16384, 3001, 32), (8193, 777, 16), (100, 1000, 32), (20, 300, 32), (1, 65, 4),
+                                   (64, 64, 32), (4096, 1, 8)])
+def test_knn_tiled_edges_equal_brute(cuda, M, Q, k):
+    """Tile-count boundaries (1, 2, 129, 256 tiles; partial last tile), fewer references than k
+    (slots past M are (inf, -1) like knn.hip), a single query, ragged wave tails."""
+    from dvcp import ops
+    ref, qry = _c3_knn_inputs(cuda, M=M, Q=Q, B=3, seed=M + Q)
+    qry[:, : Q // 3] = qry[:, :1]                              # many identical queries
+    d1, i1, _ = ops.knn(ref, qry, k, method="brute")
+    d2, i2, i64 = ops.knn(ref, qry, k, method="tiled")
+    assert torch.equal(i1, i2) and torch.equal(d1, d2)
+    assert torch.equal(i64, i2.long())
+
+
+def test_knn_tiled_dyadic_ties_full(cuda):
+    """Coordinates on a 1/8 grid: nearly every distance is tied; order must be (d2, index)."""
+    from dvcp import ops
+    g = torch.Generator().manual_seed(7)
+    ref = (torch.randint(-16, 17, (2, 12000, 3), generator=g).float() / 8).to(cuda)
+    qry = (torch.randint(-20, 21, (2, 5000, 3), generator=g).float() / 8).to(cuda)
+    d1, i1, _ = ops.knn(ref, qry, 32, method="brute")
+    d2, i2, _ = ops.knn(ref, qry, 32, method="tiled")
     assert torch.equal(i1, i2) and torch.equal(d1, d2)
 
 
