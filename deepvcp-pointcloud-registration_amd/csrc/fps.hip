@@ -106,27 +106,14 @@ __device__ __forceinline__ uint64_t fps_clock() {
   return t;
 }
 
-// THREADS threads (W = THREADS/64 waves) per cloud; PPT points per lane in VGPRs.
-// TIMING (diagnostics, tools/fps_lab): per-wave sums of the step phases in shader clocks.
-template <typename T, int THREADS, int PPT, bool PRUNE, bool TIMING = false>
-__global__ __launch_bounds__(THREADS) void fps_kernel(PointsView<T> pts, int N, int npoint,
-                                                      const int64_t* __restrict__ start,
-                                                      int64_t* __restrict__ out_idx, T* __restrict__ out_xyz,
-                                                      unsigned long long* __restrict__ prof) {
+// Setup shared by the FPS kernels: counting sort of the cloud by 12-bit Morton cell (16^3 cells
+// over its bounding box) in LDS.  perm[pos] = original index of sorted position pos.  Only the
+// point -> wave/group assignment depends on it, never a result.
+template <typename T, int THREADS>
+__device__ void fps_morton_sort(const PointsView<T>& pts, int b, int N, uint32_t* bins, uint16_t* perm,
+                                T (*red)[3][THREADS / kWave], uint32_t* wsum) {
   constexpr int W = THREADS / kWave;
-  constexpr int RANGE = kWave * PPT;  // sorted positions per wave
-  static_assert(W <= 16 && (W & (W - 1)) == 0, "slot reduction covers one DPP row");
-  static_assert(PPT % 2 == 0 || PPT == 1, "original indices are packed two per VGPR");
-  __shared__ uint32_t bins[kMortonBins];
-  __shared__ uint16_t perm[THREADS * PPT];
-  __shared__ uint8_t owner[THREADS * PPT];
-  __shared__ FpsSlot<T> slots[2][W];
-  __shared__ T red[2][3][W];
-  __shared__ uint32_t wsum[W];
-
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-
-  // ---- setup 1: cloud bounding box ------------------------------------------------------------
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   T lo[3] = {static_cast<T>(__builtin_huge_val()), static_cast<T>(__builtin_huge_val()),
              static_cast<T>(__builtin_huge_val())};
   T hi[3] = {-lo[0], -lo[1], -lo[2]};
@@ -163,8 +150,6 @@ __global__ __launch_bounds__(THREADS) void fps_kernel(PointsView<T> pts, int N, 
     blo[a] = l;
     bscale[a] = h > l ? static_cast<T>(16) / (h - l) : static_cast<T>(0);
   }
-
-  // ---- setup 2: counting sort by Morton cell -> each wave owns a compact region ---------------
   auto cell_of = [&](int n) -> uint32_t {
     uint32_t c = 0;
 #pragma unroll
@@ -204,6 +189,28 @@ __global__ __launch_bounds__(THREADS) void fps_kernel(PointsView<T> pts, int N, 
   __syncthreads();
   for (int n = tid; n < N; n += THREADS) perm[atomicAdd(&bins[cell_of(n)], 1u)] = static_cast<uint16_t>(n);
   __syncthreads();
+}
+
+// THREADS threads (W = THREADS/64 waves) per cloud; PPT points per lane in VGPRs.
+// TIMING (diagnostics, tools/fps_lab): per-wave sums of the step phases in shader clocks.
+template <typename T, int THREADS, int PPT, bool PRUNE, bool TIMING = false>
+__global__ __launch_bounds__(THREADS) void fps_kernel(PointsView<T> pts, int N, int npoint,
+                                                      const int64_t* __restrict__ start,
+                                                      int64_t* __restrict__ out_idx, T* __restrict__ out_xyz,
+                                                      unsigned long long* __restrict__ prof) {
+  constexpr int W = THREADS / kWave;
+  constexpr int RANGE = kWave * PPT;  // sorted positions per wave
+  static_assert(W <= 16 && (W & (W - 1)) == 0, "slot reduction covers one DPP row");
+  static_assert(PPT % 2 == 0 || PPT == 1, "original indices are packed two per VGPR");
+  __shared__ uint32_t bins[kMortonBins];
+  __shared__ uint16_t perm[THREADS * PPT];
+  __shared__ uint8_t owner[THREADS * PPT];
+  __shared__ FpsSlot<T> slots[2][W];
+  __shared__ T red[2][3][W];
+  __shared__ uint32_t wsum[W];
+
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  fps_morton_sort<T, THREADS>(pts, b, N, bins, perm, red, wsum);
   for (int pos = tid; pos < N; pos += THREADS) owner[perm[pos]] = static_cast<uint8_t>(pos / RANGE);
   __syncthreads();
   // ---- setup 3: each wave lists its points in ascending original index (stream compaction) ---
@@ -388,6 +395,346 @@ __global__ __launch_bounds__(THREADS) void fps_kernel(PointsView<T> pts, int N, 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Exact batched FPS (numpy model: tools/fps_lab/batched_fps_proto.py).
+//
+// Groups: slot p of wave w = 64 Morton-consecutive points (a compact box).  Each group publishes
+// its best point (value desc, index asc), the second largest running minimum (an upper bound on
+// the rest of the group) and keeps its box.  Per round, wave 0 ("the walker") lists the best group
+// of each of its lanes (groups l, l+64, ...) and bounds every unlisted group by the largest
+// unlisted candidate value T.  It then accepts centres one by one:
+//   next = argmax over listed candidates of (value desc, index asc), values updated exactly by
+//          every centre accepted so far (same float formula as the point update);
+//   accept if it is the first of the round, or if its value is strictly above
+//          UB = max(T, bounds of the listed groups), each bound lowered by every accepted centre to
+//          the rounding-safe max distance from the centre to the group box.
+// A strictly larger value than every possibly-unlisted running minimum, and the argmax of the
+// listed ones, is exactly the serial FPS's next centre.  Then every wave applies the round's
+// centres to its points (wave- and group-box pruning), re-reduces the groups it touched, and
+// republishes.  Two barriers per round; rounds ~ npoint / 9 on C3 clouds.  Ties and clouds with
+// fewer points than npoint degrade to one centre per round, still exact.
+template <typename T>
+struct alignas(16) FpsGroup {
+  float cv;  // group max running minimum
+  int pid;   // its original index (lowest among equal maxima)
+  float ub;  // second largest running minimum of the group
+  float pad;
+  T x, y, z;
+};
+
+template <typename T>
+struct alignas(16) FpsCentre {
+  int pid;
+  int pad;
+  T x, y, z;
+};
+
+constexpr int kFpsMaxBatch = 64;
+
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_umax(uint32_t v) {
+  return max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, ROWS, 0xF, false)));
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_umin(uint32_t v) {
+  return min(v, static_cast<uint32_t>(
+                    __builtin_amdgcn_update_dpp(static_cast<int>(0xFFFFFFFFu), static_cast<int>(v), CTRL, ROWS, 0xF, false)));
+}
+__device__ __forceinline__ uint32_t wave_umax(uint32_t v) {
+  v = dpp_umax<0x111, 0xF>(v);
+  v = dpp_umax<0x112, 0xF>(v);
+  v = dpp_umax<0x114, 0xF>(v);
+  v = dpp_umax<0x118, 0xF>(v);
+  v = dpp_umax<0x142, 0xA>(v);
+  v = dpp_umax<0x143, 0xC>(v);
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+}
+__device__ __forceinline__ uint32_t wave_umin(uint32_t v) {
+  v = dpp_umin<0x111, 0xF>(v);
+  v = dpp_umin<0x112, 0xF>(v);
+  v = dpp_umin<0x114, 0xF>(v);
+  v = dpp_umin<0x118, 0xF>(v);
+  v = dpp_umin<0x142, 0xA>(v);
+  v = dpp_umin<0x143, 0xC>(v);
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+}
+__device__ __forceinline__ float float_unorder_fps(uint32_t u) {  // inverse of float_order
+  const uint32_t flip = (u >> 31) ? 0x80000000u : 0xFFFFFFFFu;
+  return __uint_as_float(u ^ flip);
+}
+
+// Rounding-safe upper bound of the computed d2(p, c) over p in [lo, hi]: per axis the larger of
+// |fl(lo - c)| and |fl(hi - c)| (round-to-nearest is monotone), then the d2 formula.
+template <typename T>
+__device__ __forceinline__ T box_ub2(T cx, T cy, T cz, const T (&bx)[6]) {
+  const T ex = fmax(fabs(bx[0] - cx), fabs(bx[3] - cx));
+  const T ey = fmax(fabs(bx[1] - cy), fabs(bx[4] - cy));
+  const T ez = fmax(fabs(bx[2] - cz), fabs(bx[5] - cz));
+  return (ex * ex + ey * ey) + ez * ez;
+}
+
+// The reference's running-minimum update (:80-82): d in the coordinate dtype, strict '<', stored fp32.
+template <typename T>
+__device__ __forceinline__ float fps_update(float m, T px, T py, T pz, T cx, T cy, T cz) {
+  const T dx = px - cx, dy = py - cy, dz = pz - cz;
+  const T d = (dx * dx + dy * dy) + dz * dz;
+  if constexpr (sizeof(T) == 4) {
+    return d < m ? d : m;
+  } else {
+    return d < static_cast<T>(m) ? static_cast<float>(d) : m;
+  }
+}
+
+template <typename T, int PPT, bool TIMING = false>
+__global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> pts, int N, int npoint,
+                                                                  const int64_t* __restrict__ start,
+                                                                  int64_t* __restrict__ out_idx,
+                                                                  T* __restrict__ out_xyz,
+                                                                  unsigned long long* __restrict__ prof) {
+  constexpr int W = kFpsThreads / kWave;
+  constexpr int RANGE = kWave * PPT;
+  constexpr int G = W * PPT;               // groups
+  constexpr int GPL = (G + kWave - 1) / kWave;  // groups per walker lane
+  static_assert(PPT <= 32, "group masks are 32-bit");
+  __shared__ uint32_t bins[kMortonBins];
+  __shared__ uint16_t perm[kFpsThreads * PPT];
+  __shared__ T red[2][3][W];
+  __shared__ uint32_t wsum[W];
+  __shared__ FpsGroup<T> groups[G];
+  __shared__ T gbox[G][6];
+  __shared__ FpsCentre<T> centres[kFpsMaxBatch];
+  __shared__ int ncentre;
+
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  fps_morton_sort<T, kFpsThreads>(pts, b, N, bins, perm, red, wsum);
+
+  // ---- this lane's points: slot p = sorted position wave*RANGE + p*64 + lane ----------------
+  T px[PPT], py[PPT], pz[PPT];
+  float dmin[PPT];
+  T gb[6];  // lane p < PPT: box of group (wave, p)
+  T wb[6];  // the wave's box (uniform)
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    gb[a] = wb[a] = static_cast<T>(__builtin_huge_val());
+    gb[3 + a] = wb[3 + a] = -static_cast<T>(__builtin_huge_val());
+  }
+  // Setup runs one slot at a time (uniform dynamic register indexing, s_set_gpr_idx): unrolled,
+  // every slot's loads and box reductions would be in flight together and set the VGPR peak.
+#pragma unroll 1
+  for (int p = 0; p < PPT; ++p) {
+    const int pos = wave * RANGE + p * kWave + lane;
+    const bool real = pos < N;
+    const uint32_t n = perm[real ? pos : 0];
+    const T x = pts.at(b, 0, n), y = pts.at(b, 1, n), z = pts.at(b, 2, n);
+    px[p] = real ? x : static_cast<T>(0);
+    py[p] = real ? y : static_cast<T>(0);
+    pz[p] = real ? z : static_cast<T>(0);
+    dmin[p] = real ? 1e10f : -1.0f;  // torch.ones(B, N) * 1e10 (fp32), :74; padding: never selected
+    const T inf = static_cast<T>(__builtin_huge_val());
+    T l[3] = {real ? x : inf, real ? y : inf, real ? z : inf};
+    T h[3] = {real ? x : -inf, real ? y : -inf, real ? z : -inf};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      for (int off = 32; off > 0; off >>= 1) {
+        const T ol = __shfl_xor(l[a], off, kWave), oh = __shfl_xor(h[a], off, kWave);
+        l[a] = ol < l[a] ? ol : l[a];
+        h[a] = oh > h[a] ? oh : h[a];
+      }
+      wb[a] = l[a] < wb[a] ? l[a] : wb[a];
+      wb[3 + a] = h[a] > wb[3 + a] ? h[a] : wb[3 + a];
+      gb[a] = lane == p ? l[a] : gb[a];
+      gb[3 + a] = lane == p ? h[a] : gb[3 + a];
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        gbox[wave * PPT + p][a] = l[a];
+        gbox[wave * PPT + p][3 + a] = h[a];
+      }
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 6; ++a) wb[a] = readfirstlane_t(wb[a]);
+
+  int64_t* oi = out_idx + static_cast<int64_t>(b) * npoint;
+  T* ox = out_xyz ? out_xyz + static_cast<int64_t>(b) * 3 * npoint : nullptr;
+
+  // ---- step 0: the start point --------------------------------------------------------------
+  int64_t cur = start[b];
+  if (cur < 0 || cur >= N) cur = 0;  // host validates; keep the kernel in bounds regardless
+  {
+    const T cx = pts.at(b, 0, cur), cy = pts.at(b, 1, cur), cz = pts.at(b, 2, cur);
+    if (tid == 0) {
+      oi[0] = cur;
+      if (ox) {
+        ox[0] = cx;
+        ox[npoint] = cy;
+        ox[2 * npoint] = cz;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < PPT; ++p) dmin[p] = fps_update<T>(dmin[p], px[p], py[p], pz[p], cx, cy, cz);
+  }
+  uint32_t touched = (PPT >= 32) ? 0xFFFFFFFFu : ((1u << PPT) - 1u);
+  float gcv = -2.0f;    // lane p < PPT: current max of group (wave, p); others below any value
+  float wgmax = -2.0f;  // max over the wave's groups (uniform)
+  int step = 1;
+  uint64_t rounds = 0, t_walk = 0, t_update = 0;
+
+  while (true) {
+    // ---- re-reduce the groups this wave touched and republish them -------------------------
+    if (touched) {
+#pragma unroll
+      for (int p = 0; p < PPT; ++p) {
+        if ((touched >> p) & 1u) {
+          const uint32_t vk = float_order(dmin[p]);
+          const uint32_t m1 = wave_umax(vk);
+          const uint64_t tied = __ballot(vk == m1);
+          int L;
+          if ((tied & (tied - 1)) == 0) {
+            L = __ffsll(static_cast<long long>(tied)) - 1;
+          } else {  // equal maxima: the lowest original index (sorted position -> index in LDS)
+            const uint32_t mypid = perm[wave * RANGE + p * kWave + lane];
+            const uint32_t mi = wave_umin(vk == m1 ? mypid : 0xFFFFFFFFu);
+            L = __ffsll(static_cast<long long>(__ballot((vk == m1) & (mypid == mi)))) - 1;
+          }
+          const uint32_t m2 = wave_umax(lane == L ? 0u : vk);
+          const float cv = float_unorder_fps(m1);
+          FpsGroup<T> g;
+          g.cv = cv;
+          g.pid = perm[wave * RANGE + p * kWave + L];
+          g.ub = float_unorder_fps(m2);
+          g.pad = 0.f;
+          g.x = readlane_t(px[p], L);
+          g.y = readlane_t(py[p], L);
+          g.z = readlane_t(pz[p], L);
+          if (lane == 0) groups[wave * PPT + p] = g;
+          gcv = lane == p ? cv : gcv;
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      wgmax = float_unorder_fps(wave_umax(lane < PPT ? float_order(gcv) : 0u));
+    }
+    lds_barrier();
+    if (step >= npoint) break;
+
+    // ---- the walk (wave 0) ---------------------------------------------------------------
+    uint64_t tw0 = 0;
+    if constexpr (TIMING) tw0 = fps_clock();
+    if (wave == 0) {
+      // this lane's listed group: its best of groups lane, lane+64, ... ; T over the others
+      int mg = -1;
+      uint32_t mk = 0, mpid = 0xFFFFFFFFu, tk = 0;
+#pragma unroll
+      for (int k = 0; k < GPL; ++k) {
+        const int g = k * kWave + lane;
+        if (g < G) {
+          const uint32_t key = float_order(groups[g].cv);
+          const uint32_t gp = static_cast<uint32_t>(groups[g].pid);
+          const bool better = (mg < 0) | (key > mk) | ((key == mk) & (gp < mpid));
+          const uint32_t loser = better ? mk : key;
+          tk = (mg >= 0) ? max(tk, loser) : tk;
+          mk = better ? key : mk;
+          mpid = better ? gp : mpid;
+          mg = better ? g : mg;
+        }
+      }
+      const uint32_t T_all = wave_umax(tk);
+      bool alive = mg >= 0;
+      float cv = alive ? float_unorder_fps(mk) : -3.0f;
+      float ub = alive ? groups[mg].ub : -3.0f;
+      T gx = 0, gy = 0, gz = 0, bx[6];
+#pragma unroll
+      for (int a = 0; a < 6; ++a) bx[a] = alive ? gbox[mg][a] : static_cast<T>(0);
+      if (alive) {
+        gx = groups[mg].x;
+        gy = groups[mg].y;
+        gz = groups[mg].z;
+      }
+      const int listed_pid = static_cast<int>(mpid);
+      int acc = 0;
+      int a_pid = 0;
+      T a_x = 0, a_y = 0, a_z = 0;
+      while (step + acc < npoint && acc < kFpsMaxBatch) {
+        const uint32_t key = alive ? float_order(cv) : 0u;
+        const uint32_t km = wave_umax(key);
+        const uint64_t tied = __ballot(alive & (key == km));
+        int j;
+        if ((tied & (tied - 1)) == 0) {
+          j = __ffsll(static_cast<long long>(tied)) - 1;
+        } else {
+          const uint32_t mi = wave_umin((alive & (key == km)) ? static_cast<uint32_t>(listed_pid) : 0xFFFFFFFFu);
+          j = __ffsll(static_cast<long long>(__ballot(alive & (key == km) & (static_cast<uint32_t>(listed_pid) == mi)))) - 1;
+        }
+        if (acc > 0) {
+          const uint32_t ubk = max(T_all, wave_umax(mg >= 0 ? float_order(ub) : 0u));
+          if (!(km > ubk)) break;
+        }
+        const int cpid = __builtin_amdgcn_readlane(listed_pid, j);
+        const T cx = readlane_t(gx, j), cy = readlane_t(gy, j), cz = readlane_t(gz, j);
+        if (lane == acc) {
+          a_pid = cpid;
+          a_x = cx;
+          a_y = cy;
+          a_z = cz;
+        }
+        alive = alive & (lane != j);
+        cv = fps_update<T>(cv, gx, gy, gz, cx, cy, cz);
+        const float u2 = static_cast<float>(box_ub2<T>(cx, cy, cz, bx));
+        ub = u2 < ub ? u2 : ub;
+        ++acc;
+      }
+      if (lane < acc) {
+        centres[lane] = FpsCentre<T>{a_pid, 0, a_x, a_y, a_z};
+        oi[step + lane] = a_pid;
+        if (ox) {
+          ox[step + lane] = a_x;
+          ox[npoint + step + lane] = a_y;
+          ox[2 * npoint + step + lane] = a_z;
+        }
+      }
+      if (lane == 0) ncentre = acc;
+    }
+    lds_barrier();
+    uint64_t tw1 = 0;
+    if constexpr (TIMING) tw1 = fps_clock();
+
+    // ---- apply the round's centres ---------------------------------------------------------
+    const int nc = ncentre;
+    step += nc;
+    ++rounds;
+    const FpsCentre<T> mc = centres[lane < nc ? lane : 0];
+    touched = 0u;
+    for (int i = 0; i < nc; ++i) {
+      const T cx = readlane_t(mc.x, i), cy = readlane_t(mc.y, i), cz = readlane_t(mc.z, i);
+      if (box_lb2(cx, cy, cz, wb) >= static_cast<T>(wgmax)) continue;  // no running minimum of the wave can drop
+      const uint32_t m = static_cast<uint32_t>(
+          __ballot((lane < PPT) & !(box_lb2(cx, cy, cz, gb) >= static_cast<T>(gcv))));
+      touched |= m;
+#pragma unroll
+      for (int p = 0; p < PPT; ++p)
+        if ((m >> p) & 1u) dmin[p] = fps_update<T>(dmin[p], px[p], py[p], pz[p], cx, cy, cz);
+    }
+    if constexpr (TIMING) {
+      t_walk += tw1 - tw0;
+      t_update += fps_clock() - tw1;
+    }
+  }
+  if constexpr (TIMING) {
+    if (prof && lane == 0) {
+      unsigned long long* o = prof + (static_cast<int64_t>(b) * W + wave) * kFpsProf;
+      o[0] = t_walk;
+      o[1] = t_update;
+      o[2] = rounds;
+      o[3] = 0;
+      o[4] = 0;
+      o[5] = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
+      o[6] = 0;
+      o[7] = 0;
+    }
+  }
+}
+
 // Dense fallback (no sort, no pruning) for clouds larger than the sorted kernel's VGPR budget.
 template <typename T>
 __global__ __launch_bounds__(kFpsThreads) void fps_dense_kernel(PointsView<T> pts, int N, int npoint,
@@ -457,20 +804,24 @@ static int launch_fps(const T* xyz, int64_t sb, int64_t sc, int64_t sn, int B, i
   PointsView<T> v{xyz, sb, sc, sn};
   const int ppt = ceil_div(N, kFpsThreads);
   dim3 grid(B), block(kFpsThreads);
-  // diagnostics only: DVCP_FPS_NOPRUNE=1 disables the exact box pruning (identical results)
-  static const bool noprune = [] {
-    const char* e = getenv("DVCP_FPS_NOPRUNE");
-    return e && e[0] == '1';
+  // diagnostics only (identical results): DVCP_FPS_SERIAL=1 runs the one-centre-per-step kernel,
+  // DVCP_FPS_SERIAL=2 that kernel without box pruning
+  static const int mode = [] {
+    const char* e = getenv("DVCP_FPS_SERIAL");
+    return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
   }();
-#define DVCP_FPS_CASE(P)                                                                             \
-  if (ppt <= P) {                                                                                    \
-    if (noprune)                                                                                     \
-      hipLaunchKernelGGL((fps_kernel<T, kFpsThreads, P, false>), grid, block, 0, st, v, N, npoint, start, \
-                         out_idx, out_xyz, nullptr);                                                 \
-    else                                                                                             \
-      hipLaunchKernelGGL((fps_kernel<T, kFpsThreads, P, true>), grid, block, 0, st, v, N, npoint, start,  \
-                         out_idx, out_xyz, nullptr);                                                 \
-    return launch_status("dvcp_fps");                                                                \
+#define DVCP_FPS_CASE(P)                                                                                   \
+  if (ppt <= P) {                                                                                          \
+    if (mode == 0)                                                                                         \
+      hipLaunchKernelGGL((fps_batched_kernel<T, P>), grid, block, 0, st, v, N, npoint, start, out_idx, out_xyz, \
+                         nullptr);                                                                         \
+    else if (mode == 1)                                                                                    \
+      hipLaunchKernelGGL((fps_kernel<T, kFpsThreads, P, true>), grid, block, 0, st, v, N, npoint, start,        \
+                         out_idx, out_xyz, nullptr);                                                       \
+    else                                                                                                   \
+      hipLaunchKernelGGL((fps_kernel<T, kFpsThreads, P, false>), grid, block, 0, st, v, N, npoint, start,       \
+                         out_idx, out_xyz, nullptr);                                                       \
+    return launch_status("dvcp_fps");                                                                      \
   }
   DVCP_FPS_CASE(2)
   DVCP_FPS_CASE(4)

@@ -60,6 +60,8 @@ struct Config {
 };
 
 #define CFG(T, P, PR, TM, NAME) Config{NAME, dvcp::fps_kernel<float, T, P, PR, TM>, T, P, TM}
+#define BAT(P, NAME) Config{NAME, dvcp::fps_batched_kernel<float, P, false>, 512, P, false}
+#define BATT(P, NAME) Config{NAME, dvcp::fps_batched_kernel<float, P, true>, 512, P, true}
 
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 16;
@@ -92,6 +94,11 @@ int main(int argc, char** argv) {
   const PointsView<float> view{dx, 3LL * N, N, 1};
 
   const std::vector<Config> cfgs = {
+      BAT(32, "batched 512x32"),
+      BATT(32, "batched 512x32 +timing"),
+      BAT(24, "batched 512x24"),
+      BAT(16, "batched 512x16"),
+      BAT(2, "batched 512x2"),
       CFG(512, 32, true, false, "v3 512x32 prune"),
       CFG(512, 32, true, true, "v3 512x32 prune +timing"),
       CFG(512, 32, false, false, "v3 512x32 noprune"),
@@ -103,6 +110,7 @@ int main(int argc, char** argv) {
       CFG(256, 16, true, false, "v3 256x16 prune"),
   };
   std::vector<int64_t> got(static_cast<size_t>(B) * npoint);
+  const std::vector<unsigned long long> pr_dummy(1);
   for (const auto& c : cfgs) {
     if (N > c.threads * c.ppt) continue;
     CK(hipMemset(dprof, 0, prof_words * 8));
@@ -122,7 +130,17 @@ int main(int argc, char** argv) {
       for (int s = 0; s < npoint; ++s) bad += got[static_cast<size_t>(b) * npoint + s] != want[b][s];
     printf("%-28s B %3d N %6d npoint %6d  %8.3f ms  %6.3f us/step  mismatches %d\n", c.name, B, N, npoint, best,
            1e3f * best / npoint, bad);
-    if (c.timing) {
+    if (c.timing && c.fn == reinterpret_cast<KernelFn>(dvcp::fps_batched_kernel<float, 32, true>)) {
+      const unsigned long long* o = &pr_dummy[0];
+      (void)o;
+      std::vector<unsigned long long> pr(prof_words);
+      CK(hipMemcpy(pr.data(), dprof, pr.size() * 8, hipMemcpyDeviceToHost));
+      for (int w = 0; w < 8; ++w) {
+        const unsigned long long* q = &pr[static_cast<size_t>(w) * dvcp::kFpsProf];  // cloud 0
+        printf("   wave %d: rounds %llu  walk %.0f clk/round  update+regroup %.0f clk/round\n", w, q[2],
+               q[2] ? double(q[0]) / q[2] : 0.0, q[2] ? double(q[1]) / q[2] : 0.0);
+      }
+    } else if (c.timing) {
       const int W = c.threads / 64;
       std::vector<unsigned long long> pr(prof_words);
       CK(hipMemcpy(pr.data(), dprof, pr.size() * 8, hipMemcpyDeviceToHost));
