@@ -449,6 +449,23 @@ __device__ __forceinline__ uint32_t wave_umax(uint32_t v) {
   v = dpp_umax<0x143, 0xC>(v);
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
 }
+// Two independent wave maxima; the DPP chains interleave, so they cost about one chain's latency.
+__device__ __forceinline__ void wave_umax2(uint32_t a, uint32_t b, uint32_t& ma, uint32_t& mb) {
+  a = dpp_umax<0x111, 0xF>(a);
+  b = dpp_umax<0x111, 0xF>(b);
+  a = dpp_umax<0x112, 0xF>(a);
+  b = dpp_umax<0x112, 0xF>(b);
+  a = dpp_umax<0x114, 0xF>(a);
+  b = dpp_umax<0x114, 0xF>(b);
+  a = dpp_umax<0x118, 0xF>(a);
+  b = dpp_umax<0x118, 0xF>(b);
+  a = dpp_umax<0x142, 0xA>(a);
+  b = dpp_umax<0x142, 0xA>(b);
+  a = dpp_umax<0x143, 0xC>(a);
+  b = dpp_umax<0x143, 0xC>(b);
+  ma = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(a), 63));
+  mb = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(b), 63));
+}
 __device__ __forceinline__ uint32_t wave_umin(uint32_t v) {
   v = dpp_umin<0x111, 0xF>(v);
   v = dpp_umin<0x112, 0xF>(v);
@@ -575,18 +592,24 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
 #pragma unroll
     for (int p = 0; p < PPT; ++p) dmin[p] = fps_update<T>(dmin[p], px[p], py[p], pz[p], cx, cy, cz);
   }
-  uint32_t touched = (PPT >= 32) ? 0xFFFFFFFFu : ((1u << PPT) - 1u);
-  float gcv = -2.0f;    // lane p < PPT: current max of group (wave, p); others below any value
+  // Groups whose candidate's running minimum changed ("dirty") are re-reduced.  A group whose
+  // candidate kept its value keeps its record: no other point can have risen above it, and its
+  // old second maximum still bounds the rest.
+  uint32_t dirty = (PPT >= 32) ? 0xFFFFFFFFu : ((1u << PPT) - 1u);
+  float gcv = -2.0f;    // lane p < PPT: max of group (wave, p) = its candidate's running minimum
+  T gcx = 0, gcy = 0, gcz = 0;  // lane p < PPT: that candidate's coordinates
   float wgmax = -2.0f;  // max over the wave's groups (uniform)
   int step = 1;
-  uint64_t rounds = 0, t_walk = 0, t_update = 0;
+  uint64_t rounds = 0, t_walk = 0, t_update = 0, t_regroup = 0, t_barrier = 0, n_regroup = 0;
 
   while (true) {
-    // ---- re-reduce the groups this wave touched and republish them -------------------------
-    if (touched) {
+    // ---- re-reduce the groups whose candidate changed and republish them ---------------------
+    uint64_t tr0 = 0;
+    if constexpr (TIMING) tr0 = fps_clock();
+    if (dirty) {
 #pragma unroll
       for (int p = 0; p < PPT; ++p) {
-        if ((touched >> p) & 1u) {
+        if ((dirty >> p) & 1u) {
           const uint32_t vk = float_order(dmin[p]);
           const uint32_t m1 = wave_umax(vk);
           const uint64_t tied = __ballot(vk == m1);
@@ -610,12 +633,23 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
           g.z = readlane_t(pz[p], L);
           if (lane == 0) groups[wave * PPT + p] = g;
           gcv = lane == p ? cv : gcv;
+          gcx = lane == p ? g.x : gcx;
+          gcy = lane == p ? g.y : gcy;
+          gcz = lane == p ? g.z : gcz;
+          if constexpr (TIMING) ++n_regroup;
           __builtin_amdgcn_sched_barrier(0);
         }
       }
       wgmax = float_unorder_fps(wave_umax(lane < PPT ? float_order(gcv) : 0u));
     }
+    uint64_t tr1 = 0;
+    if constexpr (TIMING) tr1 = fps_clock();
     lds_barrier();
+    if constexpr (TIMING) {
+      const uint64_t tr2 = fps_clock();
+      t_regroup += tr1 - tr0;
+      t_barrier += tr2 - tr1;
+    }
     if (step >= npoint) break;
 
     // ---- the walk (wave 0) ---------------------------------------------------------------
@@ -657,7 +691,9 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
       T a_x = 0, a_y = 0, a_z = 0;
       while (step + acc < npoint && acc < kFpsMaxBatch) {
         const uint32_t key = alive ? float_order(cv) : 0u;
-        const uint32_t km = wave_umax(key);
+        uint32_t km, umax;
+        wave_umax2(key, mg >= 0 ? float_order(ub) : 0u, km, umax);
+        if (acc > 0 && !(km > max(T_all, umax))) break;
         const uint64_t tied = __ballot(alive & (key == km));
         int j;
         if ((tied & (tied - 1)) == 0) {
@@ -665,10 +701,6 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
         } else {
           const uint32_t mi = wave_umin((alive & (key == km)) ? static_cast<uint32_t>(listed_pid) : 0xFFFFFFFFu);
           j = __ffsll(static_cast<long long>(__ballot(alive & (key == km) & (static_cast<uint32_t>(listed_pid) == mi)))) - 1;
-        }
-        if (acc > 0) {
-          const uint32_t ubk = max(T_all, wave_umax(mg >= 0 ? float_order(ub) : 0u));
-          if (!(km > ubk)) break;
         }
         const int cpid = __builtin_amdgcn_readlane(listed_pid, j);
         const T cx = readlane_t(gx, j), cy = readlane_t(gy, j), cz = readlane_t(gz, j);
@@ -704,13 +736,14 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
     step += nc;
     ++rounds;
     const FpsCentre<T> mc = centres[lane < nc ? lane : 0];
-    touched = 0u;
+    dirty = 0u;
     for (int i = 0; i < nc; ++i) {
       const T cx = readlane_t(mc.x, i), cy = readlane_t(mc.y, i), cz = readlane_t(mc.z, i);
       if (box_lb2(cx, cy, cz, wb) >= static_cast<T>(wgmax)) continue;  // no running minimum of the wave can drop
-      const uint32_t m = static_cast<uint32_t>(
-          __ballot((lane < PPT) & !(box_lb2(cx, cy, cz, gb) >= static_cast<T>(gcv))));
-      touched |= m;
+      const bool grp = lane < PPT;
+      const uint32_t m = static_cast<uint32_t>(__ballot(grp & !(box_lb2(cx, cy, cz, gb) >= static_cast<T>(gcv))));
+      // the candidate itself drops exactly when the point update would lower it (same formula)
+      dirty |= static_cast<uint32_t>(__ballot(grp & (fps_update<T>(gcv, gcx, gcy, gcz, cx, cy, cz) != gcv)));
 #pragma unroll
       for (int p = 0; p < PPT; ++p)
         if ((m >> p) & 1u) dmin[p] = fps_update<T>(dmin[p], px[p], py[p], pz[p], cx, cy, cz);
@@ -726,10 +759,10 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
       o[0] = t_walk;
       o[1] = t_update;
       o[2] = rounds;
-      o[3] = 0;
-      o[4] = 0;
+      o[3] = t_regroup;
+      o[4] = t_barrier;
       o[5] = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
-      o[6] = 0;
+      o[6] = n_regroup;
       o[7] = 0;
     }
   }

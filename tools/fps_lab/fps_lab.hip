@@ -137,8 +137,10 @@ int main(int argc, char** argv) {
       CK(hipMemcpy(pr.data(), dprof, pr.size() * 8, hipMemcpyDeviceToHost));
       for (int w = 0; w < 8; ++w) {
         const unsigned long long* q = &pr[static_cast<size_t>(w) * dvcp::kFpsProf];  // cloud 0
-        printf("   wave %d: rounds %llu  walk %.0f clk/round  update+regroup %.0f clk/round\n", w, q[2],
-               q[2] ? double(q[0]) / q[2] : 0.0, q[2] ? double(q[1]) / q[2] : 0.0);
+        const double r = q[2] ? double(q[2]) : 1.0;
+        printf("   wave %d: rounds %llu  regroup %.0f  barrierA %.0f  walk+barrierB %.0f  update %.0f clk/round  "
+               "regroups/round %.2f\n",
+               w, q[2], q[3] / r, q[4] / r, q[0] / r, q[1] / r, q[6] / r);
       }
     } else if (c.timing) {
       const int W = c.threads / 64;
