@@ -607,9 +607,11 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
     uint64_t tr0 = 0;
     if constexpr (TIMING) tr0 = fps_clock();
     if (dirty) {
-#pragma unroll
-      for (int p = 0; p < PPT; ++p) {
-        if ((dirty >> p) & 1u) {
+      uint32_t dm = dirty;
+      while (dm) {  // p is wave-uniform -> indexed register access
+        const int p = __ffs(dm) - 1;
+        dm &= dm - 1;
+        {
           const uint32_t vk = float_order(dmin[p]);
           const uint32_t m1 = wave_umax(vk);
           const uint64_t tied = __ballot(vk == m1);
@@ -737,16 +739,21 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
     ++rounds;
     const FpsCentre<T> mc = centres[lane < nc ? lane : 0];
     dirty = 0u;
-    for (int i = 0; i < nc; ++i) {
+    // centres that can lower some running minimum of this wave: one vector test, lane i = centre i
+    uint64_t rel = __ballot((lane < nc) & !(box_lb2(mc.x, mc.y, mc.z, wb) >= static_cast<T>(wgmax)));
+    while (rel) {
+      const int i = __ffsll(static_cast<long long>(rel)) - 1;
+      rel &= rel - 1;
       const T cx = readlane_t(mc.x, i), cy = readlane_t(mc.y, i), cz = readlane_t(mc.z, i);
-      if (box_lb2(cx, cy, cz, wb) >= static_cast<T>(wgmax)) continue;  // no running minimum of the wave can drop
       const bool grp = lane < PPT;
-      const uint32_t m = static_cast<uint32_t>(__ballot(grp & !(box_lb2(cx, cy, cz, gb) >= static_cast<T>(gcv))));
+      uint32_t m = static_cast<uint32_t>(__ballot(grp & !(box_lb2(cx, cy, cz, gb) >= static_cast<T>(gcv))));
       // the candidate itself drops exactly when the point update would lower it (same formula)
       dirty |= static_cast<uint32_t>(__ballot(grp & (fps_update<T>(gcv, gcx, gcy, gcz, cx, cy, cz) != gcv)));
-#pragma unroll
-      for (int p = 0; p < PPT; ++p)
-        if ((m >> p) & 1u) dmin[p] = fps_update<T>(dmin[p], px[p], py[p], pz[p], cx, cy, cz);
+      while (m) {  // touched slots only; p is wave-uniform -> indexed register access
+        const int p = __ffs(m) - 1;
+        m &= m - 1;
+        dmin[p] = fps_update<T>(dmin[p], px[p], py[p], pz[p], cx, cy, cz);
+      }
     }
     if constexpr (TIMING) {
       t_walk += tw1 - tw0;
