@@ -398,7 +398,8 @@ __global__ __launch_bounds__(THREADS) void fps_kernel(PointsView<T> pts, int N, 
 // ---------------------------------------------------------------------------------------------
 // Exact batched FPS (numpy model: tools/fps_lab/batched_fps_proto.py).
 //
-// Groups: slot p of wave w = 64 Morton-consecutive points (a compact box).  Each group publishes
+// Groups: 64 Morton-consecutive points (a compact box); group g lives in slot g / 8 of wave g % 8,
+// so the few neighbouring groups one centre touches fall into different waves (balanced rounds).  Each group publishes
 // its best point (value desc, index asc), the second largest running minimum (an upper bound on
 // the rest of the group) and keeps its box.  Per round, wave 0 ("the walker") lists the best group
 // of each of its lanes (groups l, l+64, ...) and bounds every unlisted group by the largest
@@ -509,7 +510,6 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
                                                                   T* __restrict__ out_xyz,
                                                                   unsigned long long* __restrict__ prof) {
   constexpr int W = kFpsThreads / kWave;
-  constexpr int RANGE = kWave * PPT;
   constexpr int G = W * PPT;               // groups
   constexpr int GPL = (G + kWave - 1) / kWave;  // groups per walker lane
   static_assert(PPT <= 32, "group masks are 32-bit");
@@ -525,7 +525,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   fps_morton_sort<T, kFpsThreads>(pts, b, N, bins, perm, red, wsum);
 
-  // ---- this lane's points: slot p = sorted position wave*RANGE + p*64 + lane ----------------
+  // ---- this lane's points: slot p = sorted position (p*W + wave)*64 + lane ------------------
   T px[PPT], py[PPT], pz[PPT];
   float dmin[PPT];
   T gb[6];  // lane p < PPT: box of group (wave, p)
@@ -539,7 +539,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
   // every slot's loads and box reductions would be in flight together and set the VGPR peak.
 #pragma unroll 1
   for (int p = 0; p < PPT; ++p) {
-    const int pos = wave * RANGE + p * kWave + lane;
+    const int pos = (p * W + wave) * kWave + lane;
     const bool real = pos < N;
     const uint32_t n = perm[real ? pos : 0];
     const T x = pts.at(b, 0, n), y = pts.at(b, 1, n), z = pts.at(b, 2, n);
@@ -565,8 +565,8 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
     if (lane == 0) {
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
-        gbox[wave * PPT + p][a] = l[a];
-        gbox[wave * PPT + p][3 + a] = h[a];
+        gbox[p * W + wave][a] = l[a];
+        gbox[p * W + wave][3 + a] = h[a];
       }
     }
   }
@@ -619,7 +619,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
           if ((tied & (tied - 1)) == 0) {
             L = __ffsll(static_cast<long long>(tied)) - 1;
           } else {  // equal maxima: the lowest original index (sorted position -> index in LDS)
-            const uint32_t mypid = perm[wave * RANGE + p * kWave + lane];
+            const uint32_t mypid = perm[(p * W + wave) * kWave + lane];
             const uint32_t mi = wave_umin(vk == m1 ? mypid : 0xFFFFFFFFu);
             L = __ffsll(static_cast<long long>(__ballot((vk == m1) & (mypid == mi)))) - 1;
           }
@@ -627,13 +627,13 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
           const float cv = float_unorder_fps(m1);
           FpsGroup<T> g;
           g.cv = cv;
-          g.pid = perm[wave * RANGE + p * kWave + L];
+          g.pid = perm[(p * W + wave) * kWave + L];
           g.ub = float_unorder_fps(m2);
           g.pad = 0.f;
           g.x = readlane_t(px[p], L);
           g.y = readlane_t(py[p], L);
           g.z = readlane_t(pz[p], L);
-          if (lane == 0) groups[wave * PPT + p] = g;
+          if (lane == 0) groups[p * W + wave] = g;
           gcv = lane == p ? cv : gcv;
           gcx = lane == p ? g.x : gcx;
           gcy = lane == p ? g.y : gcy;
