@@ -401,9 +401,9 @@ __global__ __launch_bounds__(THREADS) void fps_kernel(PointsView<T> pts, int N, 
 // Groups: 64 Morton-consecutive points (a compact box); wave w holds groups w*PPT .. w*PPT+PPT-1
 // (a compact region, so a centre's update usually concerns one or two waves).  Each group publishes
 // its best point (value desc, index asc), the second largest running minimum (an upper bound on
-// the rest of the group) and keeps its box.  Per round, wave 0 ("the walker") lists the (at most
-// 63) groups whose best value lies above a threshold -- one per lane -- and bounds every unlisted
-// group by the largest unlisted best value T.  It then accepts centres one by one:
+// the rest of the group) and keeps its box.  Per round, wave 0 ("the walker") lists the best group
+// of each of its lanes (groups l, l+64, ...) and bounds every unlisted group by the largest
+// unlisted candidate value T.  It then accepts centres one by one:
 //   next = argmax over listed candidates of (value desc, index asc), values updated exactly by
 //          every centre accepted so far (same float formula as the point update);
 //   accept if it is the first of the round, or if its value is strictly above
@@ -431,6 +431,9 @@ struct alignas(16) FpsCentre {
 };
 
 constexpr int kFpsMaxBatch = 64;
+// Below this cloud size the one-centre-per-step kernel is faster (few groups, short steps; and
+// npoint > N tails, where every running minimum is 0, give batches of one) -- tools/fps_lab.
+constexpr int kFpsBatchedMinN = 2048;
 
 template <int CTRL, int ROWS>
 __device__ __forceinline__ uint32_t dpp_umax(uint32_t v) {
@@ -449,6 +452,23 @@ __device__ __forceinline__ uint32_t wave_umax(uint32_t v) {
   v = dpp_umax<0x142, 0xA>(v);
   v = dpp_umax<0x143, 0xC>(v);
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+}
+// Two independent wave maxima; the DPP chains interleave, so they cost about one chain's latency.
+__device__ __forceinline__ void wave_umax2(uint32_t a, uint32_t b, uint32_t& ma, uint32_t& mb) {
+  a = dpp_umax<0x111, 0xF>(a);
+  b = dpp_umax<0x111, 0xF>(b);
+  a = dpp_umax<0x112, 0xF>(a);
+  b = dpp_umax<0x112, 0xF>(b);
+  a = dpp_umax<0x114, 0xF>(a);
+  b = dpp_umax<0x114, 0xF>(b);
+  a = dpp_umax<0x118, 0xF>(a);
+  b = dpp_umax<0x118, 0xF>(b);
+  a = dpp_umax<0x142, 0xA>(a);
+  b = dpp_umax<0x142, 0xA>(b);
+  a = dpp_umax<0x143, 0xC>(a);
+  b = dpp_umax<0x143, 0xC>(b);
+  ma = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(a), 63));
+  mb = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(b), 63));
 }
 __device__ __forceinline__ uint32_t wave_umin(uint32_t v) {
   v = dpp_umin<0x111, 0xF>(v);
@@ -503,13 +523,12 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
   __shared__ FpsGroup<T> groups[G];
   __shared__ T gbox[G][6];
   __shared__ FpsCentre<T> centres[kFpsMaxBatch];
-  __shared__ int walk_list[kWave];
   __shared__ int ncentre;
 
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   fps_morton_sort<T, kFpsThreads>(pts, b, N, bins, perm, red, wsum);
 
-  // ---- this lane's points: slot p = sorted position (p*W + wave)*64 + lane ------------------
+  // ---- this lane's points: slot p = sorted position (wave*PPT + p)*64 + lane -----------------
   T px[PPT], py[PPT], pz[PPT];
   float dmin[PPT];
   T gb[6];  // lane p < PPT: box of group (wave, p)
@@ -642,87 +661,44 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
     uint64_t tw0 = 0;
     if constexpr (TIMING) tw0 = fps_clock();
     if (wave == 0) {
-      // ---- list the candidates: every group whose running-minimum key is above a threshold t
-      // (at most 63 of them; t from a 12-bit search on the float exponent/leading mantissa), the
-      // rest bounded by T = their largest value.  Keys are fp32 bits of non-negative values,
-      // order-preserving; padding-only groups (cv < 0) get key 0 and never win a tie.
-      uint32_t kb[GPL], kp[GPL];
+      // this lane's listed group: its best of groups lane, lane+64, ... ; T over the others
+      int mg = -1;
+      uint32_t mk = 0, mpid = 0xFFFFFFFFu, tk = 0;
 #pragma unroll
       for (int k = 0; k < GPL; ++k) {
         const int g = k * kWave + lane;
-        const float c = g < G ? groups[g].cv : -1.0f;
-        kb[k] = c > 0.0f ? __float_as_uint(c) : 0u;
-        kp[k] = (g < G && c >= 0.0f) ? static_cast<uint32_t>(groups[g].pid) : 0xFFFFFFFFu;
-      }
-      uint32_t lo = 0, hi = 4096;  // smallest t with #{kb >> 19 > t} <= 63
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        int cnt = 0;
-#pragma unroll
-        for (int k = 0; k < GPL; ++k) cnt += __popcll(__ballot((kb[k] >> 19) > mid));
-        if (cnt <= 63) hi = mid; else lo = mid + 1;
-      }
-      int total = 0;
-      uint32_t tk = 0;  // max key of the unlisted
-#pragma unroll
-      for (int k = 0; k < GPL; ++k) {
-        const bool listed = (kb[k] >> 19) > lo;
-        const uint64_t bm = __ballot(listed);
-        if (listed) {
-          const int slot = total + static_cast<int>(__builtin_amdgcn_mbcnt_hi(
-                                       static_cast<uint32_t>(bm >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bm), 0)));
-          walk_list[slot] = k * kWave + lane;
-        } else {
-          tk = max(tk, kb[k]);
+        if (g < G) {
+          const uint32_t key = float_order(groups[g].cv);
+          const uint32_t gp = static_cast<uint32_t>(groups[g].pid);
+          const bool better = (mg < 0) | (key > mk) | ((key == mk) & (gp < mpid));
+          const uint32_t loser = better ? mk : key;
+          tk = (mg >= 0) ? max(tk, loser) : tk;
+          mk = better ? key : mk;
+          mpid = better ? gp : mpid;
+          mg = better ? g : mg;
         }
-        total += __popcll(bm);
       }
-      uint32_t T_all = wave_umax(tk);
-      if (total == 0) {  // degenerate (>63 groups share the top key bucket, e.g. all zero): the exact best alone
-        uint32_t bk = 0, bp = 0xFFFFFFFFu;
-        int bg = 0;
-#pragma unroll
-        for (int k = 0; k < GPL; ++k) {
-          const bool better = (kb[k] > bk) | ((kb[k] == bk) & (kp[k] < bp));
-          bk = better ? kb[k] : bk;
-          bp = better ? kp[k] : bp;
-          bg = better ? k * kWave + lane : bg;
-        }
-        const uint32_t km = wave_umax(bk);
-        const uint64_t tied = __ballot(bk == km);
-        int L;
-        if ((tied & (tied - 1)) == 0) {
-          L = __ffsll(static_cast<long long>(tied)) - 1;
-        } else {
-          const uint32_t mi = wave_umin(bk == km ? bp : 0xFFFFFFFFu);
-          L = __ffsll(static_cast<long long>(__ballot((bk == km) & (bp == mi)))) - 1;
-        }
-        if (lane == 0) walk_list[0] = __builtin_amdgcn_readlane(bg, L);
-        total = 1;
-        T_all = km;  // nothing beyond the first can be accepted
-      }
-      const bool has = lane < total;
-      const int mg = has ? walk_list[lane] : 0;
-      bool alive = has;
-      float cv = has ? fmaxf(groups[mg].cv, 0.0f) : 0.0f;
-      float ub = has ? fmaxf(groups[mg].ub, 0.0f) : 0.0f;
-      const int listed_pid = has ? groups[mg].pid : 0x7FFFFFFF;
+      const uint32_t T_all = wave_umax(tk);
+      bool alive = mg >= 0;
+      float cv = alive ? float_unorder_fps(mk) : -3.0f;
+      float ub = alive ? groups[mg].ub : -3.0f;
       T gx = 0, gy = 0, gz = 0, bx[6];
 #pragma unroll
-      for (int a = 0; a < 6; ++a) bx[a] = has ? gbox[mg][a] : static_cast<T>(0);
-      if (has) {
+      for (int a = 0; a < 6; ++a) bx[a] = alive ? gbox[mg][a] : static_cast<T>(0);
+      if (alive) {
         gx = groups[mg].x;
         gy = groups[mg].y;
         gz = groups[mg].z;
       }
+      const int listed_pid = static_cast<int>(mpid);
       int acc = 0;
       int a_pid = 0;
       T a_x = 0, a_y = 0, a_z = 0;
       while (step + acc < npoint && acc < kFpsMaxBatch) {
-        const uint32_t key = alive ? __float_as_uint(cv) : 0u;
-        const uint32_t km = wave_umax(key);
-        // accept beyond the first only if strictly above every bound (unlisted and listed groups)
-        if (acc > 0 && (!(km > T_all) || __ballot(has & (__float_as_uint(ub) >= km)) != 0)) break;
+        const uint32_t key = alive ? float_order(cv) : 0u;
+        uint32_t km, umax;
+        wave_umax2(key, mg >= 0 ? float_order(ub) : 0u, km, umax);
+        if (acc > 0 && !(km > max(T_all, umax))) break;
         const uint64_t tied = __ballot(alive & (key == km));
         int j;
         if ((tied & (tied - 1)) == 0) {
@@ -878,10 +854,10 @@ static int launch_fps(const T* xyz, int64_t sb, int64_t sc, int64_t sn, int B, i
   }();
 #define DVCP_FPS_CASE(P)                                                                                   \
   if (ppt <= P) {                                                                                          \
-    if (mode == 0)                                                                                         \
+    if (mode == 0 && N >= kFpsBatchedMinN)                                                                 \
       hipLaunchKernelGGL((fps_batched_kernel<T, P>), grid, block, 0, st, v, N, npoint, start, out_idx, out_xyz, \
                          nullptr);                                                                         \
-    else if (mode == 1)                                                                                    \
+    else if (mode <= 1)                                                                                    \
       hipLaunchKernelGGL((fps_kernel<T, kFpsThreads, P, true>), grid, block, 0, st, v, N, npoint, start,        \
                          out_idx, out_xyz, nullptr);                                                       \
     else                                                                                                   \
