@@ -12,6 +12,8 @@
 // the layer weights read as wave-uniform scalar loads (SGPR operands) and activations in VGPRs.
 // The max over a centre's rows is an LDS atomic max on the fp32 bit pattern (outputs are
 // post-ReLU, hence >= +0, so unsigned order is float order).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace dvcp {
@@ -120,6 +122,12 @@ __global__ __launch_bounds__(kSaThreads) void sa_mlp_kernel(PointsView<T> pts, P
   }
 }
 
+// fp32 MFMA path for the two-layer tables (sa_mlp_mfma.hip)
+template <typename T, int D, int C1, int C2>
+int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, const void* c, int64_t cb, int64_t cc,
+                   int64_t cn, int S, int B, const float* feat, int64_t fb, int64_t fn, const int32_t* count,
+                   const int32_t* list, int nsample, const float* params, float* out, hipStream_t st);
+
 template <typename T, typename FT, int D, int C1, int C2, int C3>
 static int launch_sa(const void* xyz, int64_t sb, int64_t sc, int64_t sn, const void* c, int64_t cb, int64_t cc,
                      int64_t cn, int S, int B, const void* feat, int64_t fb, int64_t fd, int64_t fn,
@@ -136,6 +144,15 @@ static int launch_sa(const void* xyz, int64_t sb, int64_t sc, int64_t sn, const 
 }
 
 }  // namespace dvcp
+
+// diagnostics only: DVCP_SA_VALU=1 keeps the two-layer tables on the row-per-thread kernel
+static bool dvcp_sa_force_valu() {
+  static const bool v = [] {
+    const char* e = getenv("DVCP_SA_VALU");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 
 extern "C" int dvcp_sa_group_mlp(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
                                  const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
@@ -169,8 +186,25 @@ extern "C" int dvcp_sa_group_mlp(int dtype, const void* xyz, int64_t sb, int64_t
     if (D == 0) DVCP_SA_T(0, 16, 16, 32);
     if (D == 3) DVCP_SA_T(3, 16, 16, 32);
   }
-  if (nlayer == 2 && D == 32 && chans[1] == 32 && chans[2] == 64) DVCP_SA_T(32, 32, 64, 0);
-  if (nlayer == 2 && D == 64 && chans[1] == 64 && chans[2] == 64) DVCP_SA_T(64, 64, 64, 0);
+  // two-layer tables: fp32 MFMA when each point's features are a contiguous, 16-B aligned fp32 run
+  const bool mfma_ok = !ff64 && fd == 1 && fb % 4 == 0 && fn % 4 == 0 &&
+                       (reinterpret_cast<uintptr_t>(feat) & 15) == 0 && !dvcp_sa_force_valu();
+#define DVCP_SA_M(DD, A, Bc)                                                                                     \
+  return f64 ? dvcp::launch_sa_mfma<double, DD, A, Bc>(xyz, sb, sc, sn, ctr, cb, cc, cn, S, B,                  \
+                                                     static_cast<const float*>(feat), fb, fn, count, list,      \
+                                                     nsample, params, out, st)                                  \
+             : dvcp::launch_sa_mfma<float, DD, A, Bc>(xyz, sb, sc, sn, ctr, cb, cc, cn, S, B,                   \
+                                                    static_cast<const float*>(feat), fb, fn, count, list, nsample, \
+                                                    params, out, st)
+  if (nlayer == 2 && D == 32 && chans[1] == 32 && chans[2] == 64) {
+    if (mfma_ok) DVCP_SA_M(32, 32, 64);
+    DVCP_SA_T(32, 32, 64, 0);
+  }
+  if (nlayer == 2 && D == 64 && chans[1] == 64 && chans[2] == 64) {
+    if (mfma_ok) DVCP_SA_M(64, 64, 64);
+    DVCP_SA_T(64, 64, 64, 0);
+  }
+#undef DVCP_SA_M
 #undef DVCP_SA_T
 #undef DVCP_SA
   dvcp::set_error("dvcp_sa_group_mlp: unsupported layer table (nlayer=%d, D=%d)", nlayer, D);

@@ -1,0 +1,216 @@
+// sa_mlp_mfma.hip -- the two-layer set-abstraction MLPs (sa2: 35-32-64, sa3: 67-64-64;
+// pointnet2_utils.py:122-132 + :195-200 with REF-R R1) on fp32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+// Per centre the grouped rows form a dense batched GEMM chain, rows x C0 -> C1 -> C2 then a max
+// over rows, which is what the matrix cores are for.  One wave per centre; its rows go through in
+// n-tiles of 32 points (padded rows repeat the first hit, exactly the reference's padding, so
+// the max is unchanged).
+//   layer 1, transposed:  H1^T (C1 x 32) = W1 (C1 x C0) . X^T (C0 x 32)
+//        A = W1 fragment (lane: output channel, k-half), B = X^T fragment (lane: point, k-half).
+//        D has channels in registers and points on lanes...
+//   layer 2:              H2 (32 x C2) = H1 (32 x C1) . W2^T (C1 x C2)
+//        ...so each accumulator register of layer 1 is directly a k-step of layer 2's A operand
+//        (k pair = channels c, c+4 of the register), no LDS round trip;  D has points in
+//        registers and channels on lanes, so the max over points is a per-lane max over
+//        registers plus one exchange between lane halves.
+// Input channel order per k-step s: lane half 0 takes [x, y, z, f0 .. f(D/2-1)], half 1 takes
+// [0, 0, 0, f(D/2) .. f(D-1)], so each half loads one contiguous, 16-B aligned feature run.
+// Bias is the accumulator's initial value; BN (eval) is y = acc * scale + shift with scale/shift
+// folded on the host side of the kernel (scale, shift of dvcp_sa_group_mlp's params); ReLU.
+// The MFMA is a k-ordered fp32 fma chain (exact fp32 products and sums), so the result differs
+// from the row-per-thread kernel only in summation order.
+#include "common.h"
+
+namespace dvcp {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kMfmaWaves = 4;  // centres in flight per workgroup (one per SIMD)
+
+template <int D, int C1, int C2>
+struct SaMfmaShape {
+  static constexpr int C0 = 3 + D;
+  static constexpr int KS = 3 + D / 2;  // k-steps of layer 1
+  static constexpr int MT = C1 / 32;    // layer-1 output tiles
+  static constexpr int CT = C2 / 32;    // layer-2 output tiles
+  static constexpr int K2 = MT * 16;    // k-steps of layer 2
+  static_assert(D % 8 == 0 && C1 % 32 == 0 && C2 % 32 == 0, "MFMA tiling");
+};
+
+// LDS image of the weights in fragment order (staged once per workgroup).
+template <int D, int C1, int C2>
+struct SaMfmaLds {
+  using S = SaMfmaShape<D, C1, C2>;
+  float w1[S::MT][S::KS][64];   // A fragment of layer 1: [tile][k-step][lane]
+  float w2[S::CT][S::K2][64];   // B fragment of layer 2: [tile][k-step][lane]
+  float b1[S::MT][2][16];       // layer-1 bias / BN scale / BN shift by [tile][lane half][register]
+  float s1[S::MT][2][16];
+  float t1[S::MT][2][16];
+};
+
+// channel (index into [xyz, features]) feeding k-step s of lane half h, or -1 (zero)
+template <int D>
+__device__ __forceinline__ int sa_in_channel(int s, int h) {
+  if (s < 3) return h == 0 ? s : -1;
+  return 3 + h * (D / 2) + (s - 3);
+}
+
+// output channel row of accumulator register r for lane half h (32x32 C/D map)
+__device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+template <typename T, int D, int C1, int C2>
+__global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
+    PointsView<T> pts, PointsView<T> ctr, int S, int B, const float* __restrict__ feat, int64_t fb, int64_t fn,
+    const int32_t* __restrict__ count, const int32_t* __restrict__ list, int nsample,
+    const float* __restrict__ params, float* __restrict__ out) {
+  using Sh = SaMfmaShape<D, C1, C2>;
+  constexpr int C0 = Sh::C0, KS = Sh::KS, MT = Sh::MT, CT = Sh::CT;
+  __shared__ SaMfmaLds<D, C1, C2> L;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
+
+  // ---- stage the weights (params: W1, b1, scale1, shift1, W2, b2, scale2, shift2) ---------
+  const float* W1 = params;
+  const float* pb1 = W1 + C1 * C0;
+  const float* ps1 = pb1 + C1;
+  const float* pt1 = ps1 + C1;
+  const float* W2 = pt1 + C1;
+  const float* pb2 = W2 + C2 * C1;
+  const float* ps2 = pb2 + C2;
+  const float* pt2 = ps2 + C2;
+  for (int i = tid; i < MT * KS * 64; i += blockDim.x) {
+    const int l = i % 64, s = (i / 64) % KS, mt = i / (64 * KS);
+    const int ch = sa_in_channel<D>(s, l >> 5);
+    L.w1[mt][s][l] = ch < 0 ? 0.0f : W1[(32 * mt + (l & 31)) * C0 + ch];
+  }
+  for (int i = tid; i < CT * Sh::K2 * 64; i += blockDim.x) {
+    const int l = i % 64, kk = (i / 64) % Sh::K2, ct = i / (64 * Sh::K2);
+    const int mt = kk / 16, r = kk % 16;
+    L.w2[ct][kk][l] = W2[(32 * ct + (l & 31)) * C1 + 32 * mt + acc_row(r, l >> 5)];
+  }
+  for (int i = tid; i < MT * 32; i += blockDim.x) {
+    const int r = i % 16, hh = (i / 16) % 2, mt = i / 32;
+    const int c = 32 * mt + acc_row(r, hh);
+    L.b1[mt][hh][r] = pb1[c];
+    L.s1[mt][hh][r] = ps1[c];
+    L.t1[mt][hh][r] = pt1[c];
+  }
+  float b2[CT], s2[CT], t2[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    b2[ct] = pb2[32 * ct + r32];
+    s2[ct] = ps2[32 * ct + r32];
+    t2[ct] = pt2[32 * ct + r32];
+  }
+  __syncthreads();
+
+  // ---- one centre per wave, grid-strided ------------------------------------------------
+  const int64_t total = static_cast<int64_t>(B) * S;
+  for (int64_t q = static_cast<int64_t>(blockIdx.x) * kMfmaWaves + wave; q < total;
+       q += static_cast<int64_t>(gridDim.x) * kMfmaWaves) {
+    const int b = static_cast<int>(q / S), c = static_cast<int>(q % S);
+    int rows = count[q];
+    rows = rows < 1 ? 1 : (rows > nsample ? nsample : rows);
+    const int32_t* lst = list + q * nsample;
+    const T cx = ctr.at(b, 0, c), cy = ctr.at(b, 1, c), cz = ctr.at(b, 2, c);
+    float mx[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) mx[ct] = 0.0f;  // post-ReLU values are >= +0
+
+    for (int n0 = 0; n0 < rows; n0 += 32) {
+      // B fragment of layer 1: this lane's point (r32) and its half of the input channels
+      const int row = n0 + r32;
+      const int n = lst[row < rows ? row : 0];
+      float x[KS];
+      if (h == 0) {
+        x[0] = static_cast<float>(pts.at(b, 0, n) - cx);
+        x[1] = static_cast<float>(pts.at(b, 1, n) - cy);
+        x[2] = static_cast<float>(pts.at(b, 2, n) - cz);
+      } else {
+        x[0] = x[1] = x[2] = 0.0f;
+      }
+      const float4* fr = reinterpret_cast<const float4*>(feat + b * fb + static_cast<int64_t>(n) * fn + h * (D / 2));
+#pragma unroll
+      for (int v = 0; v < D / 8; ++v) {
+        const float4 f = fr[v];
+        x[3 + 4 * v] = f.x;
+        x[4 + 4 * v] = f.y;
+        x[5 + 4 * v] = f.z;
+        x[6 + 4 * v] = f.w;
+      }
+      // layer 1 (transposed): acc1[mt] rows = output channels, columns = points
+      f32x16 acc1[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc1[mt][r] = L.b1[mt][h][r];
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+          acc1[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(L.w1[mt][s][lane], x[s], acc1[mt], 0, 0, 0);
+      // BN (eval) + ReLU in place
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float v = acc1[mt][r] * L.s1[mt][h][r] + L.t1[mt][h][r];
+          acc1[mt][r] = v > 0.0f ? v : 0.0f;
+        }
+      // layer 2: A operand = the layer-1 registers, B = W2^T fragments
+      f32x16 acc2[CT];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc2[ct][r] = b2[ct];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct)
+            acc2[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(acc1[mt][r], L.w2[ct][mt * 16 + r][lane], acc2[ct], 0, 0, 0);
+      // BN + ReLU, then max over this tile's points (registers)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float v = acc2[ct][r] * s2[ct] + t2[ct];
+          mx[ct] = fmaxf(mx[ct], v > 0.0f ? v : 0.0f);
+        }
+    }
+    // the two lane halves hold different points of the same channel
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const float m = fmaxf(mx[ct], __shfl_xor(mx[ct], 32, kWave));
+      if (h == 0) out[q * C2 + 32 * ct + r32] = m;
+    }
+  }
+}
+
+template <typename T, int D, int C1, int C2>
+int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, const void* c, int64_t cb, int64_t cc,
+                   int64_t cn, int S, int B, const float* feat, int64_t fb, int64_t fn, const int32_t* count,
+                   const int32_t* list, int nsample, const float* params, float* out, hipStream_t st) {
+  PointsView<T> pv{static_cast<const T*>(xyz), sb, sc, sn};
+  PointsView<T> cv{static_cast<const T*>(c), cb, cc, cn};
+  const int64_t centres = static_cast<int64_t>(B) * S;
+  const int grid = static_cast<int>(centres < 4096 * kMfmaWaves ? (centres + kMfmaWaves - 1) / kMfmaWaves : 4096);
+  hipLaunchKernelGGL((sa_mlp_mfma_kernel<T, D, C1, C2>), dim3(grid), dim3(kMfmaWaves * kWave), 0, st, pv, cv, S, B,
+                     feat, fb, fn, count, list, nsample, params, out);
+  return launch_status("dvcp_sa_group_mlp(mfma)");
+}
+
+template int launch_sa_mfma<float, 32, 32, 64>(const void*, int64_t, int64_t, int64_t, const void*, int64_t, int64_t,
+                                               int64_t, int, int, const float*, int64_t, int64_t, const int32_t*,
+                                               const int32_t*, int, const float*, float*, hipStream_t);
+template int launch_sa_mfma<double, 32, 32, 64>(const void*, int64_t, int64_t, int64_t, const void*, int64_t, int64_t,
+                                                int64_t, int, int, const float*, int64_t, int64_t, const int32_t*,
+                                                const int32_t*, int, const float*, float*, hipStream_t);
+template int launch_sa_mfma<float, 64, 64, 64>(const void*, int64_t, int64_t, int64_t, const void*, int64_t, int64_t,
+                                               int64_t, int, int, const float*, int64_t, int64_t, const int32_t*,
+                                               const int32_t*, int, const float*, float*, hipStream_t);
+template int launch_sa_mfma<double, 64, 64, 64>(const void*, int64_t, int64_t, int64_t, const void*, int64_t, int64_t,
+                                                int64_t, int, int, const float*, int64_t, int64_t, const int32_t*,
+                                                const int32_t*, int, const float*, float*, hipStream_t);
+
+}  // namespace dvcp

@@ -69,6 +69,34 @@ def test_fps_live_vs_oracle(cuda):
         assert torch.equal(got, want), (N, npoint)
 
 
+@pytest.mark.parametrize("case", ["dyadic", "duplicates", "surface", "npoint_gt_n", "f64"])
+def test_fps_batched_vs_oracle(cuda, case):
+    """The batched kernel (N >= 2048) on inputs that stress its exactness argument: equal
+    running minima everywhere (dyadic grid), exact duplicate points, a 2-D surface, npoint > N
+    (all minima reach 0), and fp64 coordinates."""
+    import oracle as O
+    import dvcp.pointnet2_utils as P
+    g = torch.Generator().manual_seed(hash(case) % 1000)
+    N, npoint, dt = 4096, 1500, torch.float32
+    if case == "dyadic":
+        xyz = torch.randint(-8, 9, (2, N, 3), generator=g).float() / 8
+    elif case == "duplicates":
+        xyz = (torch.rand(2, N // 4, 3, generator=g) * 2 - 1).repeat_interleave(4, dim=1)
+    elif case == "surface":
+        v = torch.randn(2, N, 3, generator=g)
+        xyz = v / v.norm(dim=2, keepdim=True)
+    elif case == "npoint_gt_n":
+        N, npoint = 2100, 2600
+        xyz = torch.rand(2, N, 3, generator=g) * 2 - 1
+    else:
+        dt = torch.float64
+        xyz = torch.rand(2, N, 3, generator=g, dtype=dt) * 2 - 1
+    start = torch.randint(0, N, (2,), generator=g)
+    want = O.farthest_point_sample(xyz, npoint, start)
+    got = P.farthest_point_sample(xyz.to(cuda), npoint, start=start).cpu()
+    assert torch.equal(got, want), (case, int((got != want).nonzero()[0, 1]) if (got != want).any() else -1)
+
+
 def test_fps_full_size_property(cuda):
     """C3 scale: 16384 -> 10000; the min-distance of each newly picked point to the already
     picked set never increases (the defining FPS invariant), and no index repeats."""
@@ -239,8 +267,12 @@ def test_voxelize_golden(cuda):
 
 
 # ------------------------------------------------------------------------ set abstraction
+@pytest.mark.parametrize("layout", ["channel_first", "point_major"])
 @pytest.mark.parametrize("normals", [False, True])
-def test_set_abstraction_vs_oracle(cuda, normals):
+def test_set_abstraction_vs_oracle(cuda, normals, layout):
+    """All three SA tables.  Channel-first features run the row-per-thread kernel; point-major
+    (each point's channels contiguous, as the forward produces them) the fp32 MFMA kernel for
+    the two-layer tables."""
     import oracle as O
     import dvcp.pointnet2_utils as P
     from tests_helpers import randomize_bn
@@ -258,9 +290,14 @@ def test_set_abstraction_vs_oracle(cuda, normals):
         D = cfg["in_channel"] - 3
         feats = torch.randn(B, D, N, generator=g, dtype=dt if D == 3 else torch.float32) if D else None
         start = torch.randint(0, N, (B,), generator=g)
+        gfeats = None
+        if feats is not None:
+            gfeats = feats.to(cuda)
+            if layout == "point_major":
+                gfeats = gfeats.transpose(1, 2).contiguous().transpose(1, 2)  # (B, D, N) view, fd = 1
         with torch.no_grad():
             O_xyz, O_f = _sa_oracle(ref, xyz, feats, start)
-            G_xyz, G_f = mine(xyz.to(cuda), feats.to(cuda) if feats is not None else None, start=start)
+            G_xyz, G_f = mine(xyz.to(cuda), gfeats, start=start)
         assert torch.equal(G_xyz.cpu(), O_xyz)
         torch.testing.assert_close(G_f.cpu(), O_f, rtol=1e-5, atol=1e-5)
 
