@@ -76,7 +76,7 @@ def test_fps_batched_vs_oracle(cuda, case):
     (all minima reach 0), and fp64 coordinates."""
     import oracle as O
     import dvcp.pointnet2_utils as P
-    g = torch.Generator().manual_seed(hash(case) % 1000)
+    g = torch.Generator().manual_seed(["dyadic", "duplicates", "surface", "npoint_gt_n", "f64"].index(case) + 200)
     N, npoint, dt = 4096, 1500, torch.float32
     if case == "dyadic":
         xyz = torch.randint(-8, 9, (2, N, 3), generator=g).float() / 8
