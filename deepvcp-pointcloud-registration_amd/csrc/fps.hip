@@ -523,7 +523,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
   __shared__ FpsGroup<T> groups[G];
   __shared__ T gbox[G][6];
   __shared__ FpsCentre<T> centres[kFpsMaxBatch];
-  __shared__ uint32_t commit;
+  __shared__ int ncentre;
 
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   fps_morton_sort<T, kFpsThreads>(pts, b, N, bins, perm, red, wsum);
@@ -604,7 +604,6 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
   float wgmax = -2.0f;  // max over the wave's groups (uniform)
   int step = 1;
   uint64_t rounds = 0, t_walk = 0, t_update = 0, t_regroup = 0, t_barrier = 0, n_regroup = 0;
-  if (tid == 0) commit = 0xFFFFFFFFu;  // no round's tag (rounds < 32767 when first overwritten)
 
   while (true) {
     // ---- re-reduce the groups whose candidate changed and republish them ---------------------
@@ -658,26 +657,9 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
     }
     if (step >= npoint) break;
 
-    // ---- the walk (wave 0) publishes centres one by one; the other waves apply them meanwhile --
-    // A centre can lower running minima of this wave only if it is within the wave box's reach.
-    auto apply = [&](T cx, T cy, T cz) {
-      if (box_lb2(cx, cy, cz, wb) >= static_cast<T>(wgmax)) return;
-      const bool grp = lane < PPT;
-      uint32_t m = static_cast<uint32_t>(__ballot(grp & !(box_lb2(cx, cy, cz, gb) >= static_cast<T>(gcv))));
-      // the candidate itself drops exactly when the point update would lower it (same formula)
-      dirty |= static_cast<uint32_t>(__ballot(grp & (fps_update<T>(gcv, gcx, gcy, gcz, cx, cy, cz) != gcv)));
-      while (m) {  // touched slots only; p is wave-uniform -> indexed register access
-        const int p = __ffs(m) - 1;
-        m &= m - 1;
-        dmin[p] = fps_update<T>(dmin[p], px[p], py[p], pz[p], cx, cy, cz);
-      }
-    };
+    // ---- the walk (wave 0) ---------------------------------------------------------------
     uint64_t tw0 = 0;
     if constexpr (TIMING) tw0 = fps_clock();
-    dirty = 0u;
-    // commit word: round tag (bits 31..17) | final flag (bit 16) | centres published (bits 15..0)
-    const uint32_t tag = (static_cast<uint32_t>(rounds) & 0x7FFFu) << 17;
-    int nc = 0;
     if (wave == 0) {
       // this lane's listed group: its best of groups lane, lane+64, ... ; T over the others
       int mg = -1;
@@ -727,11 +709,6 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
         }
         const int cpid = __builtin_amdgcn_readlane(listed_pid, j);
         const T cx = readlane_t(gx, j), cy = readlane_t(gy, j), cz = readlane_t(gz, j);
-        if (lane == 0) {  // publish at once: the other waves apply it while the walk goes on
-          centres[acc] = FpsCentre<T>{cpid, 0, cx, cy, cz};
-          __hip_atomic_store(&commit, tag | static_cast<uint32_t>(acc + 1), __ATOMIC_RELEASE,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
         const bool mine = lane == acc;  // lane acc keeps the acc-th accepted centre (selects, no exec branch)
         a_pid = mine ? cpid : a_pid;
         a_x = mine ? cx : a_x;
@@ -743,10 +720,8 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
         ub = u2 < ub ? u2 : ub;
         ++acc;
       }
-      if (lane == 0)
-        __hip_atomic_store(&commit, tag | 0x10000u | static_cast<uint32_t>(acc), __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
       if (lane < acc) {
+        centres[lane] = FpsCentre<T>{a_pid, 0, a_x, a_y, a_z};
         oi[step + lane] = a_pid;
         if (ox) {
           ox[step + lane] = a_x;
@@ -754,36 +729,38 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
           ox[2 * npoint + step + lane] = a_z;
         }
       }
-      nc = acc;
-      uint64_t tw2 = 0;
-      if constexpr (TIMING) tw2 = fps_clock();
-      for (int i = 0; i < acc; ++i) apply(readlane_t(a_x, i), readlane_t(a_y, i), readlane_t(a_z, i));
-      if constexpr (TIMING) {
-        t_walk += tw2 - tw0;
-        t_update += fps_clock() - tw2;
-      }
-    } else {
-      int seen = 0;
-      while (true) {
-        const uint32_t cval = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(
-            __hip_atomic_load(&commit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP))));
-        const bool current = (cval & 0xFFFE0000u) == tag;
-        const int n = current ? static_cast<int>(cval & 0xFFFFu) : 0;
-        while (seen < n) {
-          const FpsCentre<T> cc = centres[seen];
-          apply(cc.x, cc.y, cc.z);
-          ++seen;
-        }
-        if (current && (cval & 0x10000u)) {
-          nc = n;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if constexpr (TIMING) t_walk += fps_clock() - tw0;
+      if (lane == 0) ncentre = acc;
     }
+    lds_barrier();
+    uint64_t tw1 = 0;
+    if constexpr (TIMING) tw1 = fps_clock();
+
+    // ---- apply the round's centres ---------------------------------------------------------
+    const int nc = ncentre;
     step += nc;
     ++rounds;
+    const FpsCentre<T> mc = centres[lane < nc ? lane : 0];
+    dirty = 0u;
+    // centres that can lower some running minimum of this wave: one vector test, lane i = centre i
+    uint64_t rel = __ballot((lane < nc) & !(box_lb2(mc.x, mc.y, mc.z, wb) >= static_cast<T>(wgmax)));
+    while (rel) {
+      const int i = __ffsll(static_cast<long long>(rel)) - 1;
+      rel &= rel - 1;
+      const T cx = readlane_t(mc.x, i), cy = readlane_t(mc.y, i), cz = readlane_t(mc.z, i);
+      const bool grp = lane < PPT;
+      uint32_t m = static_cast<uint32_t>(__ballot(grp & !(box_lb2(cx, cy, cz, gb) >= static_cast<T>(gcv))));
+      // the candidate itself drops exactly when the point update would lower it (same formula)
+      dirty |= static_cast<uint32_t>(__ballot(grp & (fps_update<T>(gcv, gcx, gcy, gcz, cx, cy, cz) != gcv)));
+      while (m) {  // touched slots only; p is wave-uniform -> indexed register access
+        const int p = __ffs(m) - 1;
+        m &= m - 1;
+        dmin[p] = fps_update<T>(dmin[p], px[p], py[p], pz[p], cx, cy, cz);
+      }
+    }
+    if constexpr (TIMING) {
+      t_walk += tw1 - tw0;
+      t_update += fps_clock() - tw1;
+    }
   }
   if constexpr (TIMING) {
     if (prof && lane == 0) {
