@@ -45,7 +45,9 @@ class feat_extraction_layer(nn.Module):
 
         FPS of layer l+1 depends only on layer l's sampled centres, not on its features, so the
         three FPS launches (the serial critical path) run back to back on the current stream
-        while each layer's ball query + grouped MLP runs on ``side_stream`` behind an event."""
+        while each layer's ball query + grouped MLP runs on ``side_stream``.  A layer whose FPS
+        picks every point (npoint >= its point count, layers 2 and 3 of the reference) is
+        evaluated per point before its FPS finishes and gathered by the FPS order."""
         _inference_only(self)
         B, _, N = pts.shape
         if self.use_normal:
@@ -58,11 +60,12 @@ class feat_extraction_layer(nn.Module):
         layers = (self.sa1, self.sa2, self.sa3)
         main = torch.cuda.current_stream()
         side = side_stream if side_stream is not None else main
-        centres, events = [], []
+        idxs, centres, events = [], [], []
         prev = xyz
         for sa, st in zip(layers, starts):
             _inference_only(sa)
-            _, c = ops.fps(prev, sa.npoint, st.to(prev.device), pdim=2)
+            i, c = ops.fps(prev, sa.npoint, st.to(prev.device), pdim=2)
+            idxs.append(i)
             centres.append(c)
             ev = torch.cuda.Event()
             ev.record(main)
@@ -70,13 +73,27 @@ class feat_extraction_layer(nn.Module):
             prev = c
         with torch.cuda.stream(side):
             pts_l, f = xyz, feat
-            for sa, c, ev in zip(layers, centres, events):
-                side.wait_event(ev)
+            for sa, i, c, ev in zip(layers, idxs, centres, events):
                 n_l = pts_l.shape[2]
                 ns = min(int(sa.nsample), n_l)
-                count, lst, _ = ops.ball_query(pts_l, c, sa.radius, ns, pdim=2, cdim_pts=2)
-                out = ops.sa_group_mlp(pts_l, c, f, count, lst, ns, sa.chans, sa.packed_params(),
-                                       xyz_pdim=2, feat_ddim=1, feat_pdim=2)
+                if sa.npoint >= n_l:
+                    # Every point of the layer becomes a centre (FPS output = a permutation, with
+                    # repeats if npoint > n_l), and a centre's group and MLP depend only on its
+                    # coordinates and the layer's point set.  So evaluate every point as its own
+                    # centre now -- concurrently with this layer's FPS on the main stream -- and
+                    # gather by the FPS indices once they exist.  Bit-identical results.
+                    count, lst, _ = ops.ball_query(pts_l, pts_l, sa.radius, ns, pdim=2, cdim_pts=2)
+                    per_point = ops.sa_group_mlp(pts_l, pts_l, f, count, lst, ns, sa.chans, sa.packed_params(),
+                                                 xyz_pdim=2, feat_ddim=1, feat_pdim=2)
+                    side.wait_event(ev)
+                    i.record_stream(side)
+                    out = torch.gather(per_point, 1, i.unsqueeze(-1).expand(-1, -1, per_point.shape[2]))
+                else:
+                    side.wait_event(ev)
+                    count, lst, _ = ops.ball_query(pts_l, c, sa.radius, ns, pdim=2, cdim_pts=2)
+                    out = ops.sa_group_mlp(pts_l, c, f, count, lst, ns, sa.chans, sa.packed_params(),
+                                           xyz_pdim=2, feat_ddim=1, feat_pdim=2)
+                c.record_stream(side)
                 pts_l, f = c, out.permute(0, 2, 1)
             S = pts_l.shape[2]
             f3 = f.permute(0, 2, 1).reshape(B * S, 64)  # sa output is (B, S, 64) in memory
