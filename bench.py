@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--K", type=int, default=64)
     p.add_argument("--r", type=float, default=2.0)
     p.add_argument("--s", type=float, default=0.4)
+    p.add_argument("--inflight", type=int, default=2,
+                   help="independent batches in flight (one stream each); 1 = strictly serial steps")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--stage-report", action="store_true", help="print the per-kernel table to stderr")
     return p.parse_args()
@@ -63,10 +65,15 @@ def main():
     from dvcp.synthetic import condition_weights, make_pairs, randomize_bn
 
     B, N, K, r, s = args.batch, args.npoints, args.K, args.r, args.s
+    P = max(1, args.inflight)
     torch.manual_seed(0)
     model = dvcp.DeepVCP(use_normal=False, K=K, r=r, s=s).eval().to(dev)
-    src, tgt, R_gt, t_gt = make_pairs(B, N, seed=1234 + 7919 * rank)
-    src, tgt, R_gt, t_gt = src.to(dev), tgt.to(dev), R_gt.to(dev), t_gt.to(dev)
+    # one distinct synthetic batch per in-flight lane
+    batches = []
+    for lane in range(P):
+        src, tgt, R_gt, t_gt = make_pairs(B, N, seed=1234 + 7919 * rank + 104729 * lane)
+        batches.append((src.to(dev), tgt.to(dev), R_gt.to(dev), t_gt.to(dev)))
+    src, tgt, R_gt, t_gt = batches[0]
     # random init, conditioned so key-point scores are separated beyond fp32 noise (the default
     # init's scores are 0.62 +- 1e-4): BN stats randomised, WL calibrated on this batch's features
     randomize_bn(model)
@@ -75,15 +82,27 @@ def main():
     condition_weights(model, feats=calib)
     t_init = torch.zeros(1, 3)
     torch.manual_seed(1 + rank)
+    lanes = [torch.cuda.Stream(device=dev) for _ in range(P)]
 
-    def step(starts=None):
-        with torch.no_grad():
-            kp, vcp = model(src, tgt, R_gt, t_init, starts=starts)
-            loss, Rp, tp = dvcp.deepVCP_loss(kp, vcp, R_gt, t_gt, 0.5)
+    def step(lane=0):
+        """One pass over one batch: DeepVCP.forward + deepVCP_loss, issued on the lane's stream."""
+        b_src, b_tgt, b_R, b_t = batches[lane]
+        with torch.no_grad(), torch.cuda.stream(lanes[lane]):
+            kp, vcp = model(b_src, b_tgt, b_R, t_init)
+            loss, Rp, tp = dvcp.deepVCP_loss(kp, vcp, b_R, b_t, 0.5)
         return Rp, tp, loss
 
+    # warmup, and the single-batch latency (strictly serial steps on one stream)
     for _ in range(args.warmup):
         step()
+    torch.cuda.synchronize()
+    t_lat = time.perf_counter()
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    latency_ms = (time.perf_counter() - t_lat) / 2 * 1e3
+    for lane in range(1, P):
+        step(lane)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -91,7 +110,10 @@ def main():
     _lib.EVENT_LOG = []
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    outs = [step() for _ in range(args.steps)]
+    outs = [step(i % P) for i in range(args.steps)]
+    cur = torch.cuda.current_stream(dev)
+    for ln in lanes:
+        cur.wait_stream(ln)
     res = torch.cat([torch.cat([o[0].reshape(B, 9), o[1].reshape(B, 3)], 1) for o in outs])  # (steps*B, 12)
     if world > 1:
         gathered = [torch.empty_like(res) for _ in range(world)]
@@ -151,7 +173,9 @@ def main():
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": "C3: KITTI-like synthetic pairs, DeepVCP.forward + deepVCP_loss (eval)",
                    "pairs_per_gpu": B, "global_batch": B * world, "n_points": N, "K": K, "r": r, "s": s,
-                   "candidates": C, "fe_npoint": S, "parallelism": f"pairs sharded x{world}, all_gather(R,t)"},
+                   "candidates": C, "fe_npoint": S, "parallelism": f"pairs sharded x{world}, all_gather(R,t)",
+                   "inflight_batches": P},
+        "latency_ms_single_batch": round(latency_ms, 3),
         "roofline": roofline,
         "stages": stages,
     }

@@ -36,10 +36,13 @@ class DeepVCP(nn.Module):
         self.K, self.r, self.s = K, r, s
 
     def _side_stream(self, dev):
+        """The FE side stream paired with the calling stream (independent batches issued on
+        different streams keep independent side streams, so they overlap)."""
         cache = self.__dict__.setdefault("_dvcp_streams", {})
-        if dev not in cache:
-            cache[dev] = torch.cuda.Stream(device=dev)
-        return cache[dev]
+        key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+        if key not in cache:
+            cache[key] = torch.cuda.Stream(device=dev)
+        return cache[key]
 
     def draw_starts(self, B, n_src, n_tgt):
         """The reference's seven torch.randint(0, n, (B,)) draws, in call order."""
