@@ -36,14 +36,14 @@ PEAK_HBM_GBS = 8000.0
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--steps", type=int, default=8)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--batch", type=int, default=8, help="pairs per GPU")
     p.add_argument("--npoints", type=int, default=16384)
     p.add_argument("--K", type=int, default=64)
     p.add_argument("--r", type=float, default=2.0)
     p.add_argument("--s", type=float, default=0.4)
-    p.add_argument("--inflight", type=int, default=2,
+    p.add_argument("--inflight", type=int, default=4,
                    help="independent batches in flight (one stream each); 1 = strictly serial steps")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--stage-report", action="store_true", help="print the per-kernel table to stderr")

@@ -24,6 +24,7 @@ SIGNATURES = {
     "dvcp_fps": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P],
     "dvcp_fps_ws": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P],
     "dvcp_ball_query": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _D, _I, _P, _P, _P, _P],
+    "dvcp_ball_query_ws": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _D, _I, _P, _P, _P, _P, _P],
     "dvcp_square_distance": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _P, _P],
     "dvcp_sa_group_mlp": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _L, _L, _L, _I,
                           _P, _P, _I, _I, _P, _P, _P, _P],

@@ -65,6 +65,13 @@ int dvcp_ball_query(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t 
                     const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
                     double radius, int nsample, int32_t* count, int32_t* list,
                     int64_t* padded, void* stream);
+/* The same with a workspace of B x ((N + 15) & ~15) x 16 bytes (fp32 only; ignored for fp64): points are
+ * packed once as (x, y, z, |p|^2) and each wave of 64 centres streams them in index order as
+ * scalar loads with its own early exit.  Identical results. */
+int dvcp_ball_query_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
+                       const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
+                       double radius, int nsample, int32_t* count, int32_t* list,
+                       int64_t* padded, void* workspace, void* stream);
 
 /* Dense expansion-form squared distance, pointnet2_utils.py:19-40 (API completeness).
  * out: B x S x N of dtype. */
