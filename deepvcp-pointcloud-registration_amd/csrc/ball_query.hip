@@ -10,6 +10,9 @@
 // Rounding matches the reference exactly: d2 = ((-2*dot) + |c|^2) + |p|^2 with
 // dot = MKL's fma chain and |.|^2 without fma; the radius test is `!(d2 > fp(r^2))` (:102).
 #include "common.h"
+#include "morton.h"
+
+#include <cstdlib>
 
 namespace dvcp {
 
@@ -76,15 +79,57 @@ __global__ __launch_bounds__(kBqThreads) void ball_query_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
-// fp32 path: one wave = 64 centres with its own early exit, points streamed in ascending index
-// order as wave-uniform scalar loads of packed (x, y, z, |p|^2) -- no LDS, no block barrier.  A
-// wave stops as soon as each of its centres has `nsample` hits, so dense radii scan only the
-// prefix they need and a sparse wave never waits for a dense one.
-typedef __attribute__((address_space(4))) const float bq_const_float;
+// fp32 paths.  Both produce exactly the index-order result above.
+//
+// bq_wave_kernel (any N): one wave = 64 centres with its own early exit; points are streamed in
+// ascending index order as wave-uniform scalar loads of packed (x, y, z, |p|^2) rows.
+//
+// bq_tiled_kernel (N <= 16384): a sparse radius (most centres far from nsample hits) makes the
+// scan above visit every point for every centre.  bq_build_kernel Morton-sorts the points into
+// 64-point tiles with boxes and the centres into a Morton permutation, so a wave's 64 centres
+// have a compact box.  The wave marks, in an LDS bitmap indexed by ORIGINAL point index, every
+// point whose distance bound to the wave box passes the radius with a rounding margin, then
+// scans the set bits in ascending index order with the same test, append rule and early exit.
+// A point left out of the bitmap provably fails the reference's test (see bq_prune_thr), so the
+// result is identical, and the scan touches only the neighbourhood of the wave.
 
-// Rows are padded to a multiple of 16 points (zeros) so every 16-point chunk of the query loop is one
-// unconditional scalar burst; the padding never hits because the loop tests n < N.
+// Rows are padded to a multiple of 16 points (zeros) so every 16-point chunk of the wave scan is
+// one unconditional scalar burst; the padding never hits because the loop tests n < N.
 __host__ __device__ constexpr int bq_padded_n(int N) { return (N + 15) & ~15; }
+
+constexpr int kBqTile = 64;
+constexpr int kBqMaxTiles = 256;              // tiled path: N <= 16384
+constexpr int kBqWords = kBqMaxTiles * 2;     // bitmap words per wave (N / 32)
+constexpr int kBqCap = 256;                   // candidate points staged in LDS per round
+
+struct BqLayout {
+  float4* packed;   // B x Npad: x, y, z, |p|^2 in original order (zero padding)
+  float4* sorted;   // B x T*64: x, y, z, original index bits (padding: NaN, 0x7FFFFFFF)
+  float4* tbox;     // B x T x 2: lo.xyz, hi.xyz (non-finite member: the whole space)
+  int32_t* cperm;   // B x S: centre index by Morton position
+};
+
+inline int64_t bq_align(int64_t x) { return (x + 255) & ~int64_t(255); }
+
+inline BqLayout bq_layout(void* ws, int B, int N, int S) {
+  const int64_t T = ceil_div(N, kBqTile);
+  char* p = static_cast<char*>(ws);
+  BqLayout L;
+  L.packed = reinterpret_cast<float4*>(p);
+  p += bq_align(16 * int64_t(B) * bq_padded_n(N));
+  L.sorted = reinterpret_cast<float4*>(p);
+  p += bq_align(16 * int64_t(B) * T * kBqTile);
+  L.tbox = reinterpret_cast<float4*>(p);
+  p += bq_align(32 * int64_t(B) * T);
+  L.cperm = reinterpret_cast<int32_t*>(p);
+  return L;
+}
+
+inline int64_t bq_workspace_bytes(int B, int N, int S) {
+  const int64_t T = ceil_div(N, kBqTile);
+  return bq_align(16 * int64_t(B) * bq_padded_n(N)) + bq_align(16 * int64_t(B) * T * kBqTile) +
+         bq_align(32 * int64_t(B) * T) + bq_align(4 * int64_t(B) * S);
+}
 
 __global__ void bq_pack_kernel(PointsView<float> pts, int N, float4* __restrict__ packed) {
   const int b = blockIdx.y;
@@ -99,19 +144,70 @@ __global__ void bq_pack_kernel(PointsView<float> pts, int N, float4* __restrict_
   packed[static_cast<int64_t>(b) * np + n] = v;
 }
 
-template <typename P>
-__device__ __forceinline__ P* bq_uniform_ptr(P* p) {
-  const uint64_t v = reinterpret_cast<uint64_t>(p);
-  const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v & 0xFFFFFFFFull)));
-  const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v >> 32)));
-  return reinterpret_cast<P*>((static_cast<uint64_t>(hi) << 32) | lo);
+// One workgroup per cloud: packed rows, point tiles with boxes, centre Morton permutation.
+__global__ __launch_bounds__(kBuildThreads) void bq_build_kernel(PointsView<float> pts, int N, PointsView<float> ctr,
+                                                                 int S, BqLayout L, int tiled) {
+  __shared__ uint32_t bins[kSortBins];
+  __shared__ uint32_t boxk[kBqMaxTiles][6];  // float_order keys: lo.xyz (min), hi.xyz (max)
+  __shared__ uint32_t wsum[16];
+  __shared__ float red[2][3][16];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int np = bq_padded_n(N);
+  float4* pk = L.packed + static_cast<int64_t>(b) * np;
+  for (int i = tid; i < np; i += kBuildThreads) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < N) {
+      const float x = pts.at(b, 0, i), y = pts.at(b, 1, i), z = pts.at(b, 2, i);
+      v = make_float4(x, y, z, sumsq3(x, y, z));
+    }
+    pk[i] = v;
+  }
+  if (!tiled) return;
+  const int T = (N + kBqTile - 1) / kBqTile;
+  float4* so = L.sorted + static_cast<int64_t>(b) * T * kBqTile;
+  for (int i = tid; i < T * 6; i += kBuildThreads) boxk[i / 6][i % 6] = (i % 6) < 3 ? 0xFFFFFFFFu : 0u;
+  auto get_pt = [&](int i, float (&v)[3]) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) v[a] = pts.at(b, a, i);
+  };
+  auto get_ctr = [&](int i, float (&v)[3]) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) v[a] = ctr.at(b, a, i);
+  };
+  float lo[3], hi[3];
+  block_bbox(N, get_pt, lo, hi, red);
+  morton_sort(
+      N, get_pt,
+      [&](int pos, int i, const float (&v)[3]) {
+        so[pos] = make_float4(v[0], v[1], v[2], __int_as_float(i));
+        const int t = pos / kBqTile;
+        // a non-finite coordinate can pass the reference's test against any centre (NaN d2
+        // is not > r^2), so its tile must never be pruned: give it the whole space
+        const bool fin = __builtin_isfinite(v[0]) && __builtin_isfinite(v[1]) && __builtin_isfinite(v[2]);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          atomicMin(&boxk[t][a], float_order(fin ? v[a] : -__builtin_huge_valf()));
+          atomicMax(&boxk[t][3 + a], float_order(fin ? v[a] : __builtin_huge_valf()));
+        }
+      },
+      lo, hi, bins, wsum);
+  for (int pos = N + tid; pos < T * kBqTile; pos += kBuildThreads)
+    so[pos] = make_float4(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __int_as_float(0x7FFFFFFF));
+  for (int t = tid; t < T; t += kBuildThreads) {
+    float4* tb = L.tbox + (static_cast<int64_t>(b) * T + t) * 2;
+    tb[0] = make_float4(float_unorder(boxk[t][0]), float_unorder(boxk[t][1]), float_unorder(boxk[t][2]), 0.f);
+    tb[1] = make_float4(float_unorder(boxk[t][3]), float_unorder(boxk[t][4]), float_unorder(boxk[t][5]), 0.f);
+  }
+  block_bbox(S, get_ctr, lo, hi, red);
+  int32_t* cp = L.cperm + static_cast<int64_t>(b) * S;
+  morton_sort(
+      S, get_ctr, [&](int pos, int i, const float (&)[3]) { cp[pos] = i; }, lo, hi, bins, wsum);
 }
 
 __global__ __launch_bounds__(256) void bq_wave_kernel(const float4* __restrict__ packed, int N, PointsView<float> ctr,
                                                       int S, float r2, int nsample, int32_t* __restrict__ count,
                                                       int32_t* __restrict__ list, int64_t* __restrict__ padded) {
   const int b = blockIdx.y;
-  const int lane = threadIdx.x & 63;
   const int s = blockIdx.x * 256 + threadIdx.x;
   if ((blockIdx.x * 256 + (threadIdx.x & ~63)) >= S) return;  // whole wave past the end
   const bool live = s < S;
@@ -125,8 +221,7 @@ __global__ __launch_bounds__(256) void bq_wave_kernel(const float4* __restrict__
   const int64_t row = (static_cast<int64_t>(b) * S + s) * nsample;
   int cnt = live ? 0 : nsample;
   int first = N;
-  const bq_const_float* P = (const bq_const_float*)bq_uniform_ptr(packed + static_cast<int64_t>(b) * bq_padded_n(N));
-  (void)lane;
+  const const_float* P = (const const_float*)uniform_ptr(packed + static_cast<int64_t>(b) * bq_padded_n(N));
   for (int n0 = 0; n0 < N; n0 += 16) {
     float c[64];
 #pragma unroll
@@ -150,6 +245,155 @@ __global__ __launch_bounds__(256) void bq_wave_kernel(const float4* __restrict__
     for (int j = cnt; j < nsample; ++j) padded[row + j] = first;
 }
 
+__device__ __forceinline__ float wave_fmin(float v) {
+  for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+__device__ __forceinline__ float wave_fmax(float v) {
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+
+// Prune threshold.  The reference's d2 = ((-2 dot) + |c|^2) + |p|^2 (dot an fma chain) differs
+// from the exact squared distance by at most ~10 u (|c|^2 + |p|^2) (u = 2^-24; each of the six
+// roundings is bounded by u times a magnitude <= 2 (|c|^2 + |p|^2)); a gap-based box bound
+// computed in fp32 exceeds the exact bound by at most (1 + 2^-20).  A point whose computed bound
+// exceeds (r^2 + 16 u (|c|^2max + |p|^2max)) (1 + 2^-19) therefore has computed d2 > r^2.
+__device__ __forceinline__ float bq_prune_thr(float r2, float ssc_max, float ssp_max) {
+  return (r2 + 0x1p-20f * (ssc_max + ssp_max)) * (1.0f + 0x1p-19f);
+}
+
+// |p|^2 upper bound over a box (per axis the larger endpoint magnitude)
+__device__ __forceinline__ float box_ss_max(float lx, float ly, float lz, float hx, float hy, float hz) {
+  const float ax = fmaxf(fabsf(lx), fabsf(hx)), ay = fmaxf(fabsf(ly), fabsf(hy)), az = fmaxf(fabsf(lz), fabsf(hz));
+  return ((ax * ax + ay * ay) + az * az) * (1.0f + 0x1p-20f);
+}
+
+__device__ __forceinline__ float bq_gap(float lo, float hi, float v_lo, float v_hi) {
+  return fmaxf(fmaxf(v_lo - hi, lo - v_hi), 0.0f);
+}
+
+__global__ __launch_bounds__(256) void bq_tiled_kernel(BqLayout L, int N, PointsView<float> ctr, int S, float r2,
+                                                       int nsample, int32_t* __restrict__ count,
+                                                       int32_t* __restrict__ list, int64_t* __restrict__ padded) {
+  __shared__ uint32_t bm[4][kBqWords];
+  __shared__ float4 cpt[4][kBqCap];
+  __shared__ int32_t cid[4][kBqCap];
+  const int b = blockIdx.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int q0 = (blockIdx.x * 4 + wave) * 64;
+  if (q0 >= S) return;
+  const int T = (N + kBqTile - 1) / kBqTile;
+  const int NW = (N + 31) >> 5;
+  const int np = bq_padded_n(N);
+  const bool live = q0 + lane < S;
+  const int s = live ? L.cperm[static_cast<int64_t>(b) * S + q0 + lane] : 0;
+  float cx = 0.f, cy = 0.f, cz = 0.f;
+  if (live) {
+    cx = ctr.at(b, 0, s);
+    cy = ctr.at(b, 1, s);
+    cz = ctr.at(b, 2, s);
+  }
+  const float ssc = sumsq3(cx, cy, cz);
+  // wave box of the centres; a non-finite centre needs every point
+  const bool fin = __builtin_isfinite(cx) && __builtin_isfinite(cy) && __builtin_isfinite(cz);
+  const float inf = __builtin_huge_valf();
+  const float wlx = wave_fmin(live ? (fin ? cx : -inf) : inf), whx = wave_fmax(live ? (fin ? cx : inf) : -inf);
+  const float wly = wave_fmin(live ? (fin ? cy : -inf) : inf), why = wave_fmax(live ? (fin ? cy : inf) : -inf);
+  const float wlz = wave_fmin(live ? (fin ? cz : -inf) : inf), whz = wave_fmax(live ? (fin ? cz : inf) : -inf);
+  const float ssc_max = wave_fmax(live && fin ? ssc : 0.0f);
+
+  uint32_t* mybm = bm[wave];
+  for (int i = lane; i < NW; i += 64) mybm[i] = 0u;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const float4* tb = L.tbox + static_cast<int64_t>(b) * T * 2;
+  const float4* so = L.sorted + static_cast<int64_t>(b) * T * kBqTile;
+  for (int t0 = 0; t0 < T; t0 += 64) {
+    const int t = t0 + lane;
+    bool cand = false;
+    if (t < T) {
+      const float4 lo = tb[2 * t], hi = tb[2 * t + 1];
+      const float gx = bq_gap(lo.x, hi.x, wlx, whx), gy = bq_gap(lo.y, hi.y, wly, why), gz = bq_gap(lo.z, hi.z, wlz, whz);
+      const float lb2 = (gx * gx + gy * gy) + gz * gz;
+      cand = !(lb2 > bq_prune_thr(r2, ssc_max, box_ss_max(lo.x, lo.y, lo.z, hi.x, hi.y, hi.z)));
+    }
+    uint64_t mask = __ballot(cand);
+    while (mask) {
+      const int tt = t0 + __builtin_ctzll(mask);
+      mask &= mask - 1;
+      const float4 q = so[tt * kBqTile + lane];
+      const int idx = __float_as_int(q.w);
+      const float gx = bq_gap(q.x, q.x, wlx, whx), gy = bq_gap(q.y, q.y, wly, why), gz = bq_gap(q.z, q.z, wlz, whz);
+      const float lb2 = (gx * gx + gy * gy) + gz * gz;
+      const float ssp = ((q.x * q.x + q.y * q.y) + q.z * q.z) * (1.0f + 0x1p-20f);
+      // NaN coordinates give NaN bounds, which are kept (never "> thr")
+      if (idx < N && !(lb2 > bq_prune_thr(r2, ssc_max, ssp))) atomicOr(&mybm[idx >> 5], 1u << (idx & 31));
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+
+  const float4* pk = L.packed + static_cast<int64_t>(b) * np;
+  const int64_t row = (static_cast<int64_t>(b) * S + s) * nsample;
+  int cnt = live ? 0 : nsample;
+  int first = N;
+  float4* mypt = cpt[wave];
+  int32_t* myid = cid[wave];
+  for (int c0 = 0; c0 < NW; c0 += 64) {
+    const uint32_t word = (c0 + lane < NW) ? mybm[c0 + lane] : 0u;
+    const int pc = __builtin_popcount(word);
+    int incl = pc;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int u = __shfl_up(incl, off, kWave);
+      if (lane >= off) incl += u;
+    }
+    const int total = __shfl(incl, 63, kWave);
+    const int excl = incl - pc;
+    for (int base = 0; base < total; base += kBqCap) {
+      int p = excl;
+      uint32_t wd = word;
+      while (wd && p < base + kBqCap) {
+        const int bit = __builtin_ctz(wd);
+        wd &= wd - 1;
+        if (p >= base) {
+          const int n = (c0 + lane) * 32 + bit;
+          mypt[p - base] = pk[n];
+          myid[p - base] = n;
+        }
+        ++p;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const int nc = min(kBqCap, total - base);
+      for (int j0 = 0; j0 < nc; j0 += 64) {
+        const int je = min(nc, j0 + 64);
+#pragma unroll 4
+        for (int j = j0; j < je; ++j) {
+          const float4 q = mypt[j];
+          const float d2 = expansion_d2(dot3_blas(cx, cy, cz, q.x, q.y, q.z), ssc, q.w);
+          if (!(d2 > r2) & (cnt < nsample)) {
+            const int n = myid[j];
+            first = cnt == 0 ? n : first;
+            if (list) list[row + cnt] = n;
+            if (padded) padded[row + cnt] = n;
+            ++cnt;
+          }
+        }
+        if (__ballot(cnt < nsample) == 0) goto done;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+done:
+  if (!live) return;
+  if (count) count[static_cast<int64_t>(b) * S + s] = cnt;
+  if (padded)
+    for (int j = cnt; j < nsample; ++j) padded[row + j] = first;
+}
+
 template <typename T>
 __global__ void square_distance_kernel(PointsView<T> src, int S, PointsView<T> dst, int N, T* __restrict__ out) {
   const int b = blockIdx.z;
@@ -162,6 +406,15 @@ __global__ void square_distance_kernel(PointsView<T> src, int S, PointsView<T> d
       expansion_d2(dot3_blas(sx, sy, sz, dx, dy, dz), sumsq3(sx, sy, sz), sumsq3(dx, dy, dz));
 }
 
+// DVCP_BQ_SCAN=1 forces the index-order scan (A/B measurements); read once.
+static bool bq_scan_forced() {
+  static const bool v = [] {
+    const char* e = getenv("DVCP_BQ_SCAN");
+    return e && *e && *e != '0';
+  }();
+  return v;
+}
+
 template <typename T>
 static int launch_bq(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, const void* c, int64_t cb,
                      int64_t cc, int64_t cn, int S, int B, double radius, int nsample, int32_t* count,
@@ -172,11 +425,16 @@ static int launch_bq(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
   const T r2 = static_cast<T>(radius * radius);
   if constexpr (sizeof(T) == 4) {
     if (workspace) {
-      float4* packed = static_cast<float4*>(workspace);
-      hipLaunchKernelGGL(bq_pack_kernel, dim3(ceil_div(bq_padded_n(N), 256), B), dim3(256), 0, st, pv, N, packed);
-      if (int e = launch_status("dvcp_ball_query(pack)")) return e;
-      hipLaunchKernelGGL(bq_wave_kernel, dim3(ceil_div(S, 256), B), dim3(256), 0, st, packed, N, cv, S, r2,
-                         nsample, count, list, padded);
+      const BqLayout L = bq_layout(workspace, B, N, S);
+      const int tiled = N <= kBqMaxTiles * kBqTile && !bq_scan_forced();
+      hipLaunchKernelGGL(bq_build_kernel, dim3(B), dim3(kBuildThreads), 0, st, pv, N, cv, S, L, tiled);
+      if (int e = launch_status("dvcp_ball_query(build)")) return e;
+      if (tiled)
+        hipLaunchKernelGGL(bq_tiled_kernel, dim3(ceil_div(S, 256), B), dim3(256), 0, st, L, N, cv, S, r2, nsample,
+                           count, list, padded);
+      else
+        hipLaunchKernelGGL(bq_wave_kernel, dim3(ceil_div(S, 256), B), dim3(256), 0, st, L.packed, N, cv, S, r2,
+                           nsample, count, list, padded);
       return launch_status("dvcp_ball_query");
     }
   }
@@ -205,6 +463,11 @@ extern "C" int dvcp_ball_query_ws(int dtype, const void* xyz, int64_t sb, int64_
                                    padded, nullptr, st);
   dvcp::set_error("dvcp_ball_query: bad dtype %d", dtype);
   return DVCP_EINVAL;
+}
+
+extern "C" int64_t dvcp_ball_query_workspace_bytes(int B, int N, int S) {
+  if (B < 0 || N < 0 || S < 0) return -1;
+  return dvcp::bq_workspace_bytes(B, N, S);
 }
 
 extern "C" int dvcp_ball_query(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,

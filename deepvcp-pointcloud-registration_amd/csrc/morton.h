@@ -1,0 +1,135 @@
+// morton.h -- helpers shared by the spatially tiled kernels (knn_tiled.hip, ball_query.hip):
+// block-wide bounding box, 12-bit Morton counting sort, and wave-uniform (scalar) loads.
+#pragma once
+#include "common.h"
+
+namespace dvcp {
+
+constexpr int kSortBins = 4096;  // 12-bit Morton cells
+constexpr int kBuildThreads = 1024;
+
+__device__ __forceinline__ float float_unorder(uint32_t u) {  // inverse of float_order
+  const uint32_t flip = (u >> 31) ? 0x80000000u : 0xFFFFFFFFu;
+  return __uint_as_float(u ^ flip);
+}
+
+// Wave-uniform reads through the constant address space: the compiler emits scalar loads
+// (s_load_dwordx*), so tile data arrives in SGPRs and feeds the VALU as scalar operands.
+typedef __attribute__((address_space(4))) const float const_float;
+
+// A pointer known to be wave-uniform (the compiler can lose that through divergent phis).
+template <typename P>
+__device__ __forceinline__ P* uniform_ptr(P* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v & 0xFFFFFFFFull)));
+  const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v >> 32)));
+  return reinterpret_cast<P*>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+__device__ __forceinline__ uint32_t spread4b(uint32_t v) {
+  v &= 0xF;
+  return (v & 1u) | ((v & 2u) << 2) | ((v & 4u) << 4) | ((v & 8u) << 6);
+}
+
+// Block-wide bounding box of n points (1024 threads).
+template <typename GET>
+__device__ void block_bbox(int n, GET get, float (&lo)[3], float (&hi)[3], float (*red)[3][16]) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    lo[a] = __builtin_huge_valf();
+    hi[a] = -__builtin_huge_valf();
+  }
+  for (int i = tid; i < n; i += kBuildThreads) {
+    float v[3];
+    get(i, v);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = fminf(lo[a], v[a]);
+      hi[a] = fmaxf(hi[a], v[a]);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    for (int off = 32; off > 0; off >>= 1) {
+      lo[a] = fminf(lo[a], __shfl_xor(lo[a], off, kWave));
+      hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], off, kWave));
+    }
+    if (lane == 0) {
+      red[0][a][wave] = lo[a];
+      red[1][a][wave] = hi[a];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    float l = red[0][a][0], h = red[1][a][0];
+    for (int w = 1; w < kBuildThreads / kWave; ++w) {
+      l = fminf(l, red[0][a][w]);
+      h = fmaxf(h, red[1][a][w]);
+    }
+    lo[a] = l;
+    hi[a] = h;
+  }
+  __syncthreads();
+}
+
+// Counting sort of n items by 12-bit Morton cell over [lo, hi]; emit(pos, i, v) for each item.
+template <typename GET, typename EMIT>
+__device__ void morton_sort(int n, GET get, EMIT emit, const float (&lo)[3], const float (&hi)[3], uint32_t* bins,
+                            uint32_t* wsum) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float scale[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) scale[a] = hi[a] > lo[a] ? 16.0f / (hi[a] - lo[a]) : 0.0f;
+  auto cell = [&](const float (&v)[3]) -> uint32_t {
+    uint32_t c = 0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      int q = static_cast<int>((v[a] - lo[a]) * scale[a]);
+      q = q < 0 ? 0 : (q > 15 ? 15 : q);
+      c |= spread4b(static_cast<uint32_t>(q)) << a;
+    }
+    return c;
+  };
+  for (int i = tid; i < kSortBins; i += kBuildThreads) bins[i] = 0u;
+  __syncthreads();
+  for (int i = tid; i < n; i += kBuildThreads) {
+    float v[3];
+    get(i, v);
+    atomicAdd(&bins[cell(v)], 1u);
+  }
+  __syncthreads();
+  {
+    constexpr int PER = kSortBins / kBuildThreads;
+    uint32_t c[PER], s = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      c[k] = bins[tid * PER + k];
+      s += c[k];
+    }
+    uint32_t incl = s;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t u = __shfl_up(incl, off, kWave);
+      if (lane >= off) incl += u;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t run = incl - s;
+    for (int w = 0; w < wave; ++w) run += wsum[w];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      bins[tid * PER + k] = run;
+      run += c[k];
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < n; i += kBuildThreads) {
+    float v[3];
+    get(i, v);
+    emit(static_cast<int>(atomicAdd(&bins[cell(v)], 1u)), i, v);
+  }
+  __syncthreads();
+}
+
+}  // namespace dvcp

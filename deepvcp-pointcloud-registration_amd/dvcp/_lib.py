@@ -64,6 +64,8 @@ def load():
     lib.dvcp_knn_grid_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
     lib.dvcp_knn_tiled_workspace_bytes.restype = ctypes.c_int64
     lib.dvcp_knn_tiled_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.dvcp_ball_query_workspace_bytes.restype = ctypes.c_int64
+    lib.dvcp_ball_query_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
     for name, args in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = ctypes.c_int
@@ -74,7 +76,7 @@ def load():
 
 def exported_symbols():
     return ["dvcp_last_error", "dvcp_abi_version", "dvcp_knn_grid_workspace_bytes",
-            "dvcp_knn_tiled_workspace_bytes"] + list(SIGNATURES)
+            "dvcp_knn_tiled_workspace_bytes", "dvcp_ball_query_workspace_bytes"] + list(SIGNATURES)
 
 
 # When a list, every entry-point call appends (name, start_event, end_event, work) recorded on

@@ -53,7 +53,10 @@ def ball_query(xyz, ctr, radius, nsample, pdim=1, cdim_pts=1, compact=True, padd
     pad = torch.empty(B, S, nsample, dtype=torch.int64, device=dev) if padded else None
     es = xyz.element_size()
     out_b = (4 + 4 * nsample if compact else 0) + (8 * nsample if padded else 0)
-    ws = torch.empty(B, (N + 15) & ~15, 4, dtype=torch.float32, device=dev) if xyz.dtype == torch.float32 else None
+    ws = None
+    if xyz.dtype == torch.float32:
+        nb = int(_lib.load().dvcp_ball_query_workspace_bytes(B, N, S))
+        ws = torch.empty(nb, dtype=torch.uint8, device=dev)
     call("dvcp_ball_query_ws", dtype_code(xyz), ptr(xyz), sb, sc, sn, N, ptr(ctr), cb, cc, cn, S, B, float(radius),
          int(nsample), ptr(count), ptr(lst), ptr(pad), ptr(ws), stream(),
          work=(9.0 * B * S * N, B * (3 * es * (N + S) + S * out_b)))

@@ -65,9 +65,12 @@ int dvcp_ball_query(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t 
                     const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
                     double radius, int nsample, int32_t* count, int32_t* list,
                     int64_t* padded, void* stream);
-/* The same with a workspace of B x ((N + 15) & ~15) x 16 bytes (fp32 only; ignored for fp64): points are
- * packed once as (x, y, z, |p|^2) and each wave of 64 centres streams them in index order as
- * scalar loads with its own early exit.  Identical results. */
+/* The same with a device workspace of dvcp_ball_query_workspace_bytes(B, N, S) bytes (fp32
+ * only; ignored for fp64).  Identical results.  For N <= 16384 points are Morton-sorted into
+ * 64-point tiles and each wave of 64 Morton-consecutive centres scans, in ascending index order,
+ * only the points a rounding-safe box bound cannot exclude; otherwise each wave streams all points
+ * in index order as scalar loads with its own early exit. */
+int64_t dvcp_ball_query_workspace_bytes(int B, int N, int S);
 int dvcp_ball_query_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
                        const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
                        double radius, int nsample, int32_t* count, int32_t* list,

@@ -159,6 +159,62 @@ def test_ball_query_no_hit_pads_with_N(cuda):
     assert (P.query_ball_point(0.5, 4, xyz, ctr) == 10).all()
 
 
+def _bq_case(case, g):
+    """Inputs that stress the tiled ball query's pruning: far-from-origin coordinates (large
+    |p|^2 rounding margin), dense clusters (early exit inside the candidate scan), ragged sizes,
+    hits exactly on the radius, and non-finite points and centres."""
+    if case == "kitti":
+        xyz = torch.rand(2, 8000, 3, generator=g) * torch.tensor([80.0, 80.0, 4.0]) - torch.tensor([40.0, 40.0, 2.0])
+        return xyz, xyz[:, torch.randperm(8000, generator=g)[:3000]].contiguous(), [(0.4, 64), (1.5, 32)]
+    if case == "clusters":
+        c = torch.rand(2, 20, 3, generator=g) * 2 - 1
+        xyz = (c[:, torch.randint(0, 20, (6000,), generator=g)] + 0.02 * torch.randn(2, 6000, 3, generator=g))
+        xyz[:, ::7] = torch.rand(2, xyz[:, ::7].shape[1], 3, generator=g) * 2 - 1
+        return xyz, xyz[:, :2500].contiguous(), [(0.05, 64), (0.1, 256), (0.3, 16)]
+    if case == "ragged":
+        xyz = torch.rand(3, 1000, 3, generator=g) * 2 - 1
+        return xyz, torch.rand(3, 77, 3, generator=g) * 2 - 1, [(0.2, 128), (0.5, 8)]
+    if case == "boundary":
+        # dyadic grid: every d2 is exact, many exactly equal to r^2
+        xyz = torch.randint(-16, 17, (2, 4096, 3), generator=g).float() / 16
+        return xyz, xyz[:, :1500].contiguous(), [(0.25, 64), (0.125, 32), (0.5, 200)]
+    if case == "nonfinite":
+        xyz = torch.randint(-16, 17, (2, 3000, 3), generator=g).float() / 16
+        ctr = xyz[:, :700].clone()
+        xyz[0, 1234, 1] = float("nan")
+        xyz[1, 2999, 0] = float("inf")
+        ctr[0, 5, 2] = float("nan")
+        ctr[1, 600, 0] = float("-inf")
+        return xyz, ctr, [(0.25, 64), (0.5, 16)]
+    raise ValueError(case)
+
+
+@pytest.mark.parametrize("case", ["kitti", "clusters", "ragged", "boundary", "nonfinite"])
+def test_ball_query_pruned_vs_oracle(cuda, case):
+    """The spatially pruned fp32 ball query (tiles + per-wave candidate bitmap) against the
+    oracle (pointnet2_utils.py:87-107 restated); exact where every d2 is exact (dyadic inputs),
+    else only radius-boundary rounding may differ."""
+    import oracle as O
+    from dvcp import ops
+    g = torch.Generator().manual_seed(["kitti", "clusters", "ragged", "boundary", "nonfinite"].index(case) + 140)
+    xyz, ctr, radii = _bq_case(case, g)
+    for r, ns in radii:
+        ns = min(ns, xyz.shape[1])
+        want = O.query_ball_point(r, ns, xyz, ctr)
+        cnt, lst, pad = ops.ball_query(xyz.to(cuda), ctr.to(cuda), r, ns, padded=True)
+        got = pad.cpu()
+        if case in ("boundary", "nonfinite"):
+            assert torch.equal(got, want), (case, r, ns)
+        else:
+            assert ball_mismatch_ok(xyz, ctr, got, want, r), (case, r, ns)
+        # compact form agrees with the padded one
+        cnt, lst = cnt.cpu(), lst.cpu().long()
+        for b in range(xyz.shape[0]):
+            for s in range(0, ctr.shape[1], 53):
+                c = int(cnt[b, s])
+                assert torch.equal(lst[b, s, :c], got[b, s, :c])
+
+
 def test_square_distance(cuda):
     import oracle as O
     import dvcp.pointnet2_utils as P
