@@ -85,8 +85,8 @@ __global__ __launch_bounds__(kBqThreads) void ball_query_kernel(
 // ascending index order as wave-uniform scalar loads of packed (x, y, z, |p|^2) rows.
 //
 // bq_tiled_kernel (N <= 16384): a sparse radius (most centres far from nsample hits) makes the
-// scan above visit every point for every centre.  bq_build_kernel Morton-sorts the points into
-// 64-point tiles with boxes and the centres into a Morton permutation, so a wave's 64 centres
+// scan above visit every point for every centre.  bq_build_kernel sorts the points along a Hilbert curve into
+// 64-point tiles with boxes and the centres into a Hilbert permutation, so a wave's 64 centres
 // have a compact box.  The wave marks, in an LDS bitmap indexed by ORIGINAL point index, every
 // point whose distance bound to the wave box passes the radius with a rounding margin, then
 // scans the set bits in ascending index order with the same test, append rule and early exit.
@@ -106,7 +106,7 @@ struct BqLayout {
   float4* packed;   // B x Npad: x, y, z, |p|^2 in original order (zero padding)
   float4* sorted;   // B x T*64: x, y, z, original index bits (padding: NaN, 0x7FFFFFFF)
   float4* tbox;     // B x T x 2: lo.xyz, hi.xyz (non-finite member: the whole space)
-  int32_t* cperm;   // B x S: centre index by Morton position
+  int32_t* cperm;   // B x S: centre index by Hilbert position
 };
 
 inline int64_t bq_align(int64_t x) { return (x + 255) & ~int64_t(255); }
@@ -144,7 +144,7 @@ __global__ void bq_pack_kernel(PointsView<float> pts, int N, float4* __restrict_
   packed[static_cast<int64_t>(b) * np + n] = v;
 }
 
-// One workgroup per cloud: packed rows, point tiles with boxes, centre Morton permutation.
+// One workgroup per cloud: packed rows, point tiles with boxes, centre Hilbert permutation.
 __global__ __launch_bounds__(kBuildThreads) void bq_build_kernel(PointsView<float> pts, int N, PointsView<float> ctr,
                                                                  int S, BqLayout L, int tiled) {
   __shared__ uint32_t bins[kSortBins];
@@ -320,15 +320,27 @@ __global__ __launch_bounds__(256) void bq_tiled_kernel(BqLayout L, int N, Points
     }
     uint64_t mask = __ballot(cand);
     while (mask) {
-      const int tt = t0 + __builtin_ctzll(mask);
-      mask &= mask - 1;
-      const float4 q = so[tt * kBqTile + lane];
-      const int idx = __float_as_int(q.w);
-      const float gx = bq_gap(q.x, q.x, wlx, whx), gy = bq_gap(q.y, q.y, wly, why), gz = bq_gap(q.z, q.z, wlz, whz);
-      const float lb2 = (gx * gx + gy * gy) + gz * gz;
-      const float ssp = ((q.x * q.x + q.y * q.y) + q.z * q.z) * (1.0f + 0x1p-20f);
-      // NaN coordinates give NaN bounds, which are kept (never "> thr")
-      if (idx < N && !(lb2 > bq_prune_thr(r2, ssc_max, ssp))) atomicOr(&mybm[idx >> 5], 1u << (idx & 31));
+      // up to four candidate tiles per pass, their loads in flight together
+      int tt[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        tt[u] = mask ? t0 + __builtin_ctzll(mask) : -1;
+        mask &= mask - 1;
+      }
+      float4 q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) q[u] = so[max(tt[u], 0) * kBqTile + lane];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int idx = __float_as_int(q[u].w);
+        const float gx = bq_gap(q[u].x, q[u].x, wlx, whx), gy = bq_gap(q[u].y, q[u].y, wly, why),
+                    gz = bq_gap(q[u].z, q[u].z, wlz, whz);
+        const float lb2 = (gx * gx + gy * gy) + gz * gz;
+        const float ssp = ((q[u].x * q[u].x + q[u].y * q[u].y) + q[u].z * q[u].z) * (1.0f + 0x1p-20f);
+        // NaN coordinates give NaN bounds, which are kept (never "> thr")
+        if (tt[u] >= 0 && idx < N && !(lb2 > bq_prune_thr(r2, ssc_max, ssp)))
+          atomicOr(&mybm[idx >> 5], 1u << (idx & 31));
+      }
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -352,33 +364,42 @@ __global__ __launch_bounds__(256) void bq_tiled_kernel(BqLayout L, int N, Points
     const int total = __shfl(incl, 63, kWave);
     const int excl = incl - pc;
     for (int base = 0; base < total; base += kBqCap) {
+      // this round's candidates (positions [base, base + kBqCap) in index order): indices first,
+      // then the points gathered cooperatively (several loads in flight per lane)
       int p = excl;
       uint32_t wd = word;
       while (wd && p < base + kBqCap) {
         const int bit = __builtin_ctz(wd);
         wd &= wd - 1;
-        if (p >= base) {
-          const int n = (c0 + lane) * 32 + bit;
-          mypt[p - base] = pk[n];
-          myid[p - base] = n;
-        }
+        if (p >= base) myid[p - base] = (c0 + lane) * 32 + bit;
         ++p;
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
       const int nc = min(kBqCap, total - base);
+#pragma unroll
+      for (int u = 0; u < kBqCap / 64; ++u) {
+        const int j = u * 64 + lane;
+        if (j < nc) mypt[j] = pk[myid[j]];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
       for (int j0 = 0; j0 < nc; j0 += 64) {
         const int je = min(nc, j0 + 64);
-#pragma unroll 4
-        for (int j = j0; j < je; ++j) {
-          const float4 q = mypt[j];
-          const float d2 = expansion_d2(dot3_blas(cx, cy, cz, q.x, q.y, q.z), ssc, q.w);
-          if (!(d2 > r2) & (cnt < nsample)) {
-            const int n = myid[j];
-            first = cnt == 0 ? n : first;
-            if (list) list[row + cnt] = n;
-            if (padded) padded[row + cnt] = n;
-            ++cnt;
+        for (int j1 = j0; j1 < je; j1 += 8) {
+          float4 q[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) q[u] = mypt[j1 + u];  // j1 + 7 < kBqCap
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const float d2 = expansion_d2(dot3_blas(cx, cy, cz, q[u].x, q[u].y, q[u].z), ssc, q[u].w);
+            if ((j1 + u < je) & !(d2 > r2) & (cnt < nsample)) {
+              const int n = myid[j1 + u];
+              first = cnt == 0 ? n : first;
+              if (list) list[row + cnt] = n;
+              if (padded) padded[row + cnt] = n;
+              ++cnt;
+            }
           }
         }
         if (__ballot(cnt < nsample) == 0) goto done;

@@ -1,11 +1,11 @@
 // morton.h -- helpers shared by the spatially tiled kernels (knn_tiled.hip, ball_query.hip):
-// block-wide bounding box, 12-bit Morton counting sort, and wave-uniform (scalar) loads.
+// block-wide bounding box, 12-bit space-filling-curve (Hilbert) counting sort, and wave-uniform (scalar) loads.
 #pragma once
 #include "common.h"
 
 namespace dvcp {
 
-constexpr int kSortBins = 4096;  // 12-bit Morton cells
+constexpr int kSortBins = 4096;  // 12-bit curve cells (16^3)
 constexpr int kBuildThreads = 1024;
 
 __device__ __forceinline__ float float_unorder(uint32_t u) {  // inverse of float_order
@@ -29,6 +29,38 @@ __device__ __forceinline__ P* uniform_ptr(P* p) {
 __device__ __forceinline__ uint32_t spread4b(uint32_t v) {
   v &= 0xF;
   return (v & 1u) | ((v & 2u) << 2) | ((v & 4u) << 4) | ((v & 8u) << 6);
+}
+
+// Hilbert index of a 16^3 cell (Skilling's transpose form, 4 bits per axis).  Unlike Morton
+// order it has no jumps -- consecutive indices are face-adjacent cells -- so any run of
+// consecutive items has a compact box (the tiled kernels' pruning depends on that).
+__device__ __forceinline__ uint32_t hilbert3x4(uint32_t x, uint32_t y, uint32_t z) {
+  uint32_t X[3] = {x, y, z};
+#pragma unroll
+  for (uint32_t Q = 8; Q > 1; Q >>= 1) {
+    const uint32_t P = Q - 1;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (X[i] & Q) {
+        X[0] ^= P;
+      } else {
+        const uint32_t t = (X[0] ^ X[i]) & P;
+        X[0] ^= t;
+        X[i] ^= t;
+      }
+    }
+  }
+  X[1] ^= X[0];
+  X[2] ^= X[1];
+  uint32_t t = 0;
+#pragma unroll
+  for (uint32_t Q = 8; Q > 1; Q >>= 1)
+    if (X[2] & Q) t ^= Q - 1;
+  X[0] ^= t;
+  X[1] ^= t;
+  X[2] ^= t;
+  // bit b of X[i] lands at 3b + (2 - i)
+  return spread4b(X[2]) | (spread4b(X[1]) << 1) | (spread4b(X[0]) << 2);
 }
 
 // Block-wide bounding box of n points (1024 threads).
@@ -74,7 +106,7 @@ __device__ void block_bbox(int n, GET get, float (&lo)[3], float (&hi)[3], float
   __syncthreads();
 }
 
-// Counting sort of n items by 12-bit Morton cell over [lo, hi]; emit(pos, i, v) for each item.
+// Counting sort of n items by 12-bit Hilbert cell over [lo, hi]; emit(pos, i, v) for each item.
 template <typename GET, typename EMIT>
 __device__ void morton_sort(int n, GET get, EMIT emit, const float (&lo)[3], const float (&hi)[3], uint32_t* bins,
                             uint32_t* wsum) {
@@ -83,14 +115,13 @@ __device__ void morton_sort(int n, GET get, EMIT emit, const float (&lo)[3], con
 #pragma unroll
   for (int a = 0; a < 3; ++a) scale[a] = hi[a] > lo[a] ? 16.0f / (hi[a] - lo[a]) : 0.0f;
   auto cell = [&](const float (&v)[3]) -> uint32_t {
-    uint32_t c = 0;
+    uint32_t q[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-      int q = static_cast<int>((v[a] - lo[a]) * scale[a]);
-      q = q < 0 ? 0 : (q > 15 ? 15 : q);
-      c |= spread4b(static_cast<uint32_t>(q)) << a;
+      int c = static_cast<int>((v[a] - lo[a]) * scale[a]);
+      q[a] = static_cast<uint32_t>(c < 0 ? 0 : (c > 15 ? 15 : c));
     }
-    return c;
+    return hilbert3x4(q[0], q[1], q[2]);
   };
   for (int i = tid; i < kSortBins; i += kBuildThreads) bins[i] = 0u;
   __syncthreads();

@@ -1,0 +1,44 @@
+"""Ball-query micro-benchmark: the three C3 set-abstraction layers in isolation (16 clouds).
+
+Layer inputs mirror the FE: sa1 = 16384 points -> 10000 FPS centres (r 0.1, ns 256); sa2/sa3 =
+the 10000 centres against themselves (r 0.2 / 0.4, ns 128 / 64).  Prints ms per call (CUDA
+events) and the mean hit count.  DVCP_BQ_SCAN=1 selects the index-order scan for an A/B."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "deepvcp-pointcloud-registration_amd"))
+
+
+def main():
+    from dvcp import ops
+    from dvcp.synthetic import make_pairs
+    dev = torch.device("cuda", 0)
+    src, tgt, _, _ = make_pairs(8, 16384, seed=1234)
+    xyz = torch.cat([src, tgt]).to(dev)  # (16, N, 3) or channel-first
+    if xyz.shape[1] == 3:
+        xyz = xyz.transpose(1, 2)
+    xyz = xyz[..., :3].contiguous()
+    idx, c1 = ops.fps(xyz, 10000, torch.zeros(16, dtype=torch.int64, device=dev), pdim=1)
+    c1 = torch.gather(xyz, 1, idx.unsqueeze(-1).expand(-1, -1, 3)).contiguous()
+    layers = [("sa1", xyz, c1, 0.1, 256), ("sa2", c1, c1, 0.2, 128), ("sa3", c1, c1, 0.4, 64)]
+    for name, pts, ctr, r, ns in layers:
+        for _ in range(3):
+            cnt, lst, _ = ops.ball_query(pts, ctr, r, ns)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 20
+        e0.record()
+        for _ in range(reps):
+            ops.ball_query(pts, ctr, r, ns)
+        e1.record()
+        torch.cuda.synchronize()
+        cf = cnt.float()
+        print(f"{name}: {e0.elapsed_time(e1) / reps:.4f} ms/call  mean hits {cf.mean().item():.1f}"
+              f" max {cf.max().item():.0f} p99 {cf.flatten().quantile(0.99).item():.0f}"
+              f"  scan={os.environ.get('DVCP_BQ_SCAN', '0')}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
