@@ -25,6 +25,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "deepvcp-pointcloud-registration_amd"))
 
+# Hardware queues per process (read when HIP initialises).  Each in-flight batch drives two
+# streams (the FPS chain and its side stream); with HIP's default of 4 queues, streams that share
+# a queue serialise behind each other's multi-millisecond FPS launches.  8 measured +13% over 4.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -36,8 +41,8 @@ PEAK_HBM_GBS = 8000.0
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=8)
-    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--steps", type=int, default=32)
+    p.add_argument("--warmup", type=int, default=4)
     p.add_argument("--batch", type=int, default=8, help="pairs per GPU")
     p.add_argument("--npoints", type=int, default=16384)
     p.add_argument("--K", type=int, default=64)
@@ -174,7 +179,7 @@ def main():
         "config": {"workload": "C3: KITTI-like synthetic pairs, DeepVCP.forward + deepVCP_loss (eval)",
                    "pairs_per_gpu": B, "global_batch": B * world, "n_points": N, "K": K, "r": r, "s": s,
                    "candidates": C, "fe_npoint": S, "parallelism": f"pairs sharded x{world}, all_gather(R,t)",
-                   "inflight_batches": P},
+                   "inflight_batches": P, "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
         "latency_ms_single_batch": round(latency_ms, 3),
         "roofline": roofline,
         "stages": stages,

@@ -117,6 +117,11 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
     for (int ct = 0; ct < CT; ++ct) mx[ct] = 0.0f;  // post-ReLU values are >= +0
 
     for (int n0 = 0; n0 < rows; n0 += 32) {
+      // An opaque zero added to every LDS weight index: the fragments are re-read per tile
+      // (one ds_read per MFMA) instead of being hoisted out of the loop into ~100 registers,
+      // which would cap occupancy at 2 waves per SIMD.
+      int zo = 0;
+      asm volatile("" : "+v"(zo));
       // B fragment of layer 1: this lane's point (r32) and its half of the input channels
       const int row = n0 + r32;
       const int n = lst[row < rows ? row : 0];
@@ -142,18 +147,18 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc1[mt][r] = L.b1[mt][h][r];
+        for (int r = 0; r < 16; ++r) acc1[mt][r] = L.b1[mt][h][r + zo];
 #pragma unroll
       for (int s = 0; s < KS; ++s)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
-          acc1[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(L.w1[mt][s][lane], x[s], acc1[mt], 0, 0, 0);
+          acc1[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(L.w1[mt][s][lane + zo], x[s], acc1[mt], 0, 0, 0);
       // BN (eval) + ReLU in place
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float v = acc1[mt][r] * L.s1[mt][h][r] + L.t1[mt][h][r];
+          const float v = acc1[mt][r] * L.s1[mt][h][r + zo] + L.t1[mt][h][r + zo];
           acc1[mt][r] = v > 0.0f ? v : 0.0f;
         }
       // layer 2: A operand = the layer-1 registers, B = W2^T fragments
@@ -168,7 +173,7 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
         for (int r = 0; r < 16; ++r)
 #pragma unroll
           for (int ct = 0; ct < CT; ++ct)
-            acc2[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(acc1[mt][r], L.w2[ct][mt * 16 + r][lane], acc2[ct], 0, 0, 0);
+            acc2[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(acc1[mt][r], L.w2[ct][mt * 16 + r][lane + zo], acc2[ct], 0, 0, 0);
       // BN + ReLU, then max over this tile's points (registers)
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct)

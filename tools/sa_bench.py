@@ -1,0 +1,55 @@
+"""Grouped-MLP micro-benchmark: the three C3 set-abstraction MLPs in isolation (16 clouds), on
+the real intermediate inputs of a FE pass (random-init weights, randomised BN).  Prints ms per
+dvcp_sa_group_mlp call (CUDA events) and TFLOP/s over the algorithmic MACs of the evaluated rows."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "deepvcp-pointcloud-registration_amd"))
+
+
+def main():
+    import dvcp
+    from dvcp import ops
+    from dvcp.synthetic import make_pairs, randomize_bn
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = dvcp.DeepVCP(use_normal=False, K=64, r=2.0, s=0.4).eval().to(dev)
+    randomize_bn(model)
+    fe = model.FE1
+    src, tgt, _, _ = make_pairs(8, 16384, seed=1234)
+    xyz = torch.cat([src, tgt]).to(dev).contiguous()  # (16, 3, N)
+    B = xyz.shape[0]
+    pts_l, f = xyz, None
+    with torch.no_grad():
+        for li, sa in enumerate((fe.sa1, fe.sa2, fe.sa3)):
+            n_l = pts_l.shape[2]
+            i, c = ops.fps(pts_l, sa.npoint, torch.zeros(B, dtype=torch.long, device=dev), pdim=2)
+            ns = min(int(sa.nsample), n_l)
+            ctr = pts_l if sa.npoint >= n_l else c
+            count, lst, _ = ops.ball_query(pts_l, ctr, sa.radius, ns, pdim=2, cdim_pts=2)
+            args = (pts_l, ctr, f, count, lst, ns, sa.chans, sa.packed_params())
+            kw = dict(xyz_pdim=2, feat_ddim=1, feat_pdim=2)
+            for _ in range(3):
+                out = ops.sa_group_mlp(*args, **kw)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            reps = 20
+            e0.record()
+            for _ in range(reps):
+                ops.sa_group_mlp(*args, **kw)
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / reps
+            rows = count.clamp(1, ns).sum().item()
+            macs = sum(a * b for a, b in zip(sa.chans[:-1], sa.chans[1:]))
+            print(f"sa{li + 1}: {ms:.4f} ms/call  rows {rows}  {2 * macs * rows / ms / 1e9:.1f} TFLOP/s"
+                  f"  valu={os.environ.get('DVCP_SA_VALU', '0')}", flush=True)
+            if sa.npoint >= n_l:
+                out = torch.gather(out, 1, i.unsqueeze(-1).expand(-1, -1, out.shape[2]))
+            pts_l, f = c, out.permute(0, 2, 1)
+
+
+if __name__ == "__main__":
+    main()
