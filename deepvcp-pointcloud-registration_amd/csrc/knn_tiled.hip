@@ -208,15 +208,21 @@ __global__ __launch_bounds__(kTiledThreads) void knn_tiled_query_kernel(const fl
   }
   wave_bitonic<R>(keys);
 
-  float kd[KT];
-  int ki[KT];
+  // The list is kept as 64-bit keys (d2 bits << 32 | index): d2 >= 0 orders like its bits, so
+  // one unsigned compare orders by (d2, index) and an insertion is one compare + two selects
+  // per slot.
+  // (stored as 32-bit halves: a dynamically indexed 64-bit array is not promoted to registers)
+  uint32_t kh[KT], kl[KT];
 #pragma unroll
-  for (int t = 0; t < KT; ++t) {
-    kd[t] = __builtin_huge_valf();
-    ki[t] = 0x7FFFFFFF;
+  for (int t = 0; t < KT; ++t) {  // empty slot: (+inf, 0xFFFFFFFF), above every finite point
+    kh[t] = 0x7F800000u;
+    kl[t] = ~0u;
   }
-  const int kk = k - 1;  // wave-uniform: kd[kk] is an indexed register read
+  constexpr uint64_t kEmpty = (static_cast<uint64_t>(0x7F800000u) << 32) | 0xFFFFFFFFu;
+#define DVCP_KK(t) ((static_cast<uint64_t>(kh[t]) << 32) | kl[t])
+  const int kq = k - 1;  // wave-uniform: kh[kq], kl[kq] are indexed register reads
   float kth = live ? __builtin_huge_valf() : 0.0f;  // dead lanes never need more points
+  uint64_t kkey = live ? kEmpty : 0ull;
   float wkth = wave_max_nonneg(kth);
   const float4* P = uniform_ptr(sorted + static_cast<int64_t>(b) * T * kTile);
   const float4* tbu = uniform_ptr(tb);
@@ -242,28 +248,45 @@ __global__ __launch_bounds__(kTiledThreads) void knn_tiled_query_kernel(const fl
         float c[64];
 #pragma unroll
         for (int u = 0; u < 64; ++u) c[u] = tp[4 * j0 + u];
+        // pass 1 (unrolled): every distance of the chunk, and which points are a candidate for
+        // some lane against the k-th key at chunk start (a superset: the key only decreases)
+        float d2v[16];
+        uint32_t piv[16];
+        uint32_t todo = 0;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          const float px = c[4 * j], py = c[4 * j + 1], pz = c[4 * j + 2];
-          const int pi = __float_as_int(c[4 * j + 3]);
-          const float dx = px - qx, dy = py - qy, dz = pz - qz;
-          const float d2 = (dx * dx + dy * dy) + dz * dz;
-          const bool cand = act & (d2 <= kth) & (d2 < __builtin_huge_valf());
+          const float dx = c[4 * j] - qx, dy = c[4 * j + 1] - qy, dz = c[4 * j + 2] - qz;
+          d2v[j] = (dx * dx + dy * dy) + dz * dz;
+          piv[j] = __float_as_uint(c[4 * j + 3]);
+          const uint64_t pk = (static_cast<uint64_t>(__float_as_uint(d2v[j])) << 32) | piv[j];
+          // d2 < inf also rejects NaN (padding) and infinite distances, as dvcp_knn does
+          const bool cand = act & (d2v[j] < __builtin_huge_valf()) & (pk < kkey);
+          todo |= __ballot(cand) != 0 ? (1u << j) : 0u;
+        }
+        // pass 2: those points in order, each re-tested against the current key, then inserted
+        // (one compare + two selects per slot)
+        while (todo) {
+          const int j = __builtin_ctz(todo);
+          todo &= todo - 1;
+          const float d2 = d2v[j];  // indexed register reads (uniform j)
+          const uint32_t pi = piv[j];
+          const uint64_t pk = (static_cast<uint64_t>(__float_as_uint(d2)) << 32) | pi;
+          const bool cand = act & (d2 < __builtin_huge_valf()) & (pk < kkey);
           const uint64_t m = __ballot(cand);
-          if (m != 0) {  // wave-uniform branch; lanes without a candidate keep their lists
-            ins |= m;
+          if (m == 0) continue;
+          ins |= m;
+          bool lt[KT];
 #pragma unroll
-            for (int u = KT - 1; u > 0; --u) {
-              const bool here = cand & ((d2 < kd[u]) | ((d2 == kd[u]) & (pi < ki[u])));
-              const bool before = cand & ((d2 < kd[u - 1]) | ((d2 == kd[u - 1]) & (pi < ki[u - 1])));
-              kd[u] = before ? kd[u - 1] : (here ? d2 : kd[u]);
-              ki[u] = before ? ki[u - 1] : (here ? pi : ki[u]);
-            }
-            const bool first = cand & ((d2 < kd[0]) | ((d2 == kd[0]) & (pi < ki[0])));
-            kd[0] = first ? d2 : kd[0];
-            ki[0] = first ? pi : ki[0];
-            kth = live ? (KT == 1 ? kd[0] : kd[kk]) : 0.0f;
+          for (int u = 0; u < KT; ++u) lt[u] = cand & (pk < DVCP_KK(u));
+#pragma unroll
+          for (int u = KT - 1; u > 0; --u) {
+            kh[u] = lt[u - 1] ? kh[u - 1] : (lt[u] ? __float_as_uint(d2) : kh[u]);
+            kl[u] = lt[u - 1] ? kl[u - 1] : (lt[u] ? pi : kl[u]);
           }
+          kh[0] = lt[0] ? __float_as_uint(d2) : kh[0];
+          kl[0] = lt[0] ? pi : kl[0];
+          kkey = live ? (KT == 1 ? DVCP_KK(0) : DVCP_KK(kq)) : 0ull;
+          kth = __uint_as_float(static_cast<uint32_t>(kkey >> 32));
         }
       }
       if (ins != 0) wkth = wave_max_nonneg(kth);
@@ -274,12 +297,15 @@ __global__ __launch_bounds__(kTiledThreads) void knn_tiled_query_kernel(const fl
 #pragma unroll
   for (int t = 0; t < KT; ++t) {
     if (t < k) {
-      const bool ok = ki[t] != 0x7FFFFFFF;  // fewer than k finite points: like dvcp_knn (inf, -1)
-      if (dist) dist[o + t] = ok ? sqrt_rn(kd[t]) : __builtin_huge_valf();
-      if (idx) idx[o + t] = ok ? ki[t] : -1;
-      if (idx64) idx64[o + t] = ok ? ki[t] : -1;
+      const bool ok = DVCP_KK(t) != kEmpty;  // fewer than k finite points: like dvcp_knn (inf, -1)
+      const float d2 = __uint_as_float(kh[t]);
+      const int i = static_cast<int>(kl[t]);
+      if (dist) dist[o + t] = ok ? sqrt_rn(d2) : __builtin_huge_valf();
+      if (idx) idx[o + t] = ok ? i : -1;
+      if (idx64) idx64[o + t] = ok ? i : -1;
     }
   }
+#undef DVCP_KK
 }
 
 }  // namespace dvcp

@@ -1,0 +1,40 @@
+"""kNN micro-benchmark on the C3 shape: 8 target clouds of 10000 FE centres, 64 key points each
+with an 11^3 candidate grid (r 2.0, s 0.4) -> 85184 queries per cloud, k = 32.  Prints ms per
+call (CUDA events)."""
+import itertools
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "deepvcp-pointcloud-registration_amd"))
+
+
+def main():
+    from dvcp import ops
+    from dvcp.synthetic import make_pairs
+    dev = torch.device("cuda", 0)
+    src, tgt, _, _ = make_pairs(8, 16384, seed=1234)
+    g = torch.Generator().manual_seed(0)
+    sel = torch.stack([torch.randperm(16384, generator=g)[:10000] for _ in range(8)])
+    ref = torch.gather(tgt, 2, sel.unsqueeze(1).expand(-1, 3, -1)).to(dev).contiguous()  # (8, 3, 10000)
+    kp = torch.gather(src, 2, sel[:, :64].unsqueeze(1).expand(-1, 3, -1)).permute(0, 2, 1)  # (8, 64, 3)
+    ax = torch.arange(-2.0, 2.0001, 0.4)
+    off = torch.tensor(list(itertools.product(ax.tolist(), repeat=3)), dtype=torch.float32)  # (1331, 3)
+    qry = (kp[:, :, None, :] + off[None, None]).reshape(8, -1, 3).to(dev).contiguous()
+    for _ in range(3):
+        dist, idx, _ = ops.knn(ref, qry, 32, ref_pdim=2, qry_pdim=1, want_idx64=False)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 10
+    e0.record()
+    for _ in range(reps):
+        ops.knn(ref, qry, 32, ref_pdim=2, qry_pdim=1, want_idx64=False)
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"knn: {e0.elapsed_time(e1) / reps:.4f} ms/call  queries {qry.shape[0] * qry.shape[1]}  "
+          f"checksum {dist.double().sum().item():.6e} {idx.long().sum().item()}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
