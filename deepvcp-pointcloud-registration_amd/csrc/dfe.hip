@@ -12,7 +12,22 @@
 // are wave-uniform scalar loads; the max over a query's 32 rows goes through LDS.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace dvcp {
+
+// dfe_mfma.hip: the target side on fp32 MFMA (default; DVCP_DFE_VALU=1 selects the kernel below)
+template <typename T>
+int launch_dfe_tgt_mfma(PointsView<T> ref, const float* feat, int M, const float* cand, const float* dist,
+                        const int32_t* idx, int B, int Q, const float* params, float* out, hipStream_t st);
+
+static bool dfe_valu_forced() {
+  static const bool v = [] {
+    const char* e = getenv("DVCP_DFE_VALU");
+    return e && *e && *e != '0';
+  }();
+  return v;
+}
 
 constexpr int kDfeRowsPerQ = 32;
 constexpr int kDfeThreads = 256;
@@ -140,6 +155,15 @@ extern "C" int dvcp_dfe_tgt(int dtype, const void* ref_xyz, int64_t rb, int64_t 
   DVCP_REQUIRE(M > 0 && B <= 65535, "dvcp_dfe_tgt: bad sizes");
   if (B == 0 || Q == 0) return DVCP_OK;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!dvcp::dfe_valu_forced()) {
+    if (dtype == DVCP_F32)
+      return dvcp::launch_dfe_tgt_mfma<float>(dvcp::PointsView<float>{static_cast<const float*>(ref_xyz), rb, rc, rn},
+                                              ref_feat, M, cand, dist, idx, B, Q, params, out, st);
+    if (dtype == DVCP_F64)
+      return dvcp::launch_dfe_tgt_mfma<double>(
+          dvcp::PointsView<double>{static_cast<const double*>(ref_xyz), rb, rc, rn}, ref_feat, M, cand, dist, idx, B,
+          Q, params, out, st);
+  }
   dim3 grid(dvcp::ceil_div(Q, dvcp::kDfeQPerBlock), B);
   if (dtype == DVCP_F32)
     hipLaunchKernelGGL((dvcp::dfe_tgt_kernel<float>), grid, dim3(dvcp::kDfeThreads), 0, st,

@@ -1,0 +1,156 @@
+// dfe_mfma.hip -- the target-side deep feature embedding (get_cat_feat_tgt.py:54-96 fused with
+// deep_feat_embedding.py:47-60) on fp32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+// Per candidate the 32 neighbour rows go through three 32-wide linear layers (35->32->32->32, no
+// nonlinearity, Q14) and a max over the rows: a 32 x 35 -> 32 -> 32 -> 32 GEMM chain per candidate,
+// one wave per candidate.  The 32x32 accumulator layout (lane l, register r holds
+// D[(r&3) + 8(r>>2) + 4(l>>5)][l&31]) lets each layer feed the next without an LDS round trip:
+//   layer 1, transposed: H1^T = W1 . X^T    A = W1 fragment, B = X^T (lane: row j, k-half)
+//                        -> channels in registers, rows on lanes
+//   layer 2, transposed: H2^T = W2 . H1^T   A = W2 fragment, B = the layer-1 registers
+//                        (register r is the k-step over channels (c, c+4), c = acc_row(r, 0))
+//   layer 3:             H3 = H2 . W3^T     A = the layer-2 registers, B = W3^T fragment
+//                        -> rows in registers, output channels on lanes
+// so the max over rows is a per-lane max over registers plus one exchange between lane halves.
+// Input channel order of layer 1's k-step s: lane half 0 takes [dx, dy, dz, f0 .. f15], half 1
+// [0, 0, 0, f16 .. f31] (19 k-steps; see sa_mlp_mfma.hip).
+// Everything before the GEMMs is the reference's arithmetic as in dfe_tgt_kernel (dfe.hip):
+// dist_sum in fp64 summed in neighbour order, w = dist / dist_sum in fp64, feature x w in fp64
+// rounded to fp32, coordinates differenced in the point dtype.  The MFMA is a k-ordered fp32 fma
+// chain; only the summation order differs from the row-per-thread kernel.
+#include "common.h"
+
+#include <cstdlib>
+
+namespace dvcp {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kDfeMfmaWaves = 4;
+constexpr int kDfeKS = 19;  // layer-1 k-steps: 3 + 32/2
+
+__device__ __forceinline__ int dfe_acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+struct DfeMfmaLds {
+  float w1[kDfeKS][64];  // A fragment of layer 1: [k-step][lane]
+  float w2[16][64];      // A fragment of layer 2: [k-step][lane]
+  float w3[16][64];      // B fragment of layer 3: [k-step][lane]
+  float b1[2][16];       // layer 1/2 bias by [lane half][register]
+  float b2[2][16];
+};
+
+template <typename T>
+__global__ __launch_bounds__(kDfeMfmaWaves * kWave) void dfe_tgt_mfma_kernel(
+    PointsView<T> ref, const float* __restrict__ feat, int M, const float* __restrict__ cand,
+    const float* __restrict__ dist, const int32_t* __restrict__ idx, int Q, int B, const float* __restrict__ params,
+    float* __restrict__ out) {
+  __shared__ DfeMfmaLds L;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
+  // params: W1 (32 x 35), b1, W2 (32 x 32), b2, W3 (32 x 32), b3
+  const float* W1 = params;
+  const float* pb1 = W1 + 32 * 35;
+  const float* W2 = pb1 + 32;
+  const float* pb2 = W2 + 32 * 32;
+  const float* W3 = pb2 + 32;
+  const float* pb3 = W3 + 32 * 32;
+  for (int i = tid; i < kDfeKS * 64; i += blockDim.x) {
+    const int l = i % 64, s = i / 64, hh = l >> 5;
+    const int ch = s < 3 ? (hh == 0 ? s : -1) : 3 + hh * 16 + (s - 3);
+    L.w1[s][l] = ch < 0 ? 0.0f : W1[(l & 31) * 35 + ch];
+  }
+  for (int i = tid; i < 16 * 64; i += blockDim.x) {
+    const int l = i % 64, r = i / 64;
+    const int in = dfe_acc_row(r, l >> 5);
+    L.w2[r][l] = W2[(l & 31) * 32 + in];
+    L.w3[r][l] = W3[(l & 31) * 32 + in];
+  }
+  for (int i = tid; i < 32; i += blockDim.x) {
+    const int r = i % 16, hh = i / 16;
+    L.b1[hh][r] = pb1[dfe_acc_row(r, hh)];
+    L.b2[hh][r] = pb2[dfe_acc_row(r, hh)];
+  }
+  const float b3 = pb3[r32];
+  __syncthreads();
+
+  const int64_t total = static_cast<int64_t>(B) * Q;
+  for (int64_t g = static_cast<int64_t>(blockIdx.x) * kDfeMfmaWaves + wave; g < total;
+       g += static_cast<int64_t>(gridDim.x) * kDfeMfmaWaves) {
+    const int b = static_cast<int>(g / Q);
+    // get_cat_feat_tgt.py:57-58: dist_sum in fp64 (neighbour order), w = dist / dist_sum
+    const float dj = dist[g * 32 + r32];
+    double dsum = 0.0;
+#pragma unroll
+    for (int t = 0; t < 32; ++t)
+      dsum += static_cast<double>(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(dj), t)));
+    const double wj = static_cast<double>(dj) / dsum;
+    int n = idx[g * 32 + r32];
+    n = n < 0 ? 0 : (n >= M ? M - 1 : n);
+    const float* cq = cand + g * 3;
+    float x[kDfeKS];
+    if (h == 0) {
+      // candidates_grouped_local = tgt_pts_picked - candidate (point dtype, then .float())
+      x[0] = static_cast<float>(ref.at(b, 0, n) - static_cast<T>(cq[0]));
+      x[1] = static_cast<float>(ref.at(b, 1, n) - static_cast<T>(cq[1]));
+      x[2] = static_cast<float>(ref.at(b, 2, n) - static_cast<T>(cq[2]));
+    } else {
+      x[0] = x[1] = x[2] = 0.0f;
+    }
+    // tgt_feat_norm[j, f] = F[idx_j, f] * w[f]   (Q10: the weight is indexed by the channel)
+    const float4* fr = reinterpret_cast<const float4*>(feat + (static_cast<int64_t>(b) * M + n) * 32 + 16 * h);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const float4 f = fr[v];
+      const float fv[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 4 * v + e;
+        // w of channel i (half 0) or 16 + i (half 1): lanes i and 16 + i hold them
+        const int2 lo = make_int2(__builtin_amdgcn_readlane(__double2loint(wj), i),
+                                  __builtin_amdgcn_readlane(__double2hiint(wj), i));
+        const int2 hi = make_int2(__builtin_amdgcn_readlane(__double2loint(wj), 16 + i),
+                                  __builtin_amdgcn_readlane(__double2hiint(wj), 16 + i));
+        const double wf = h ? __hiloint2double(hi.y, hi.x) : __hiloint2double(lo.y, lo.x);
+        x[3 + i] = static_cast<float>(static_cast<double>(fv[e]) * wf);
+      }
+    }
+    int zo = 0;  // opaque zero: weight fragments are re-read from LDS per candidate, not hoisted
+    asm volatile("" : "+v"(zo));
+    f32x16 a1, a2, a3;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      a1[r] = L.b1[h][r + zo];
+      a2[r] = L.b2[h][r + zo];
+      a3[r] = b3;
+    }
+#pragma unroll
+    for (int s = 0; s < kDfeKS; ++s) a1 = __builtin_amdgcn_mfma_f32_32x32x2f32(L.w1[s][lane + zo], x[s], a1, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) a2 = __builtin_amdgcn_mfma_f32_32x32x2f32(L.w2[r][lane + zo], a1[r], a2, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) a3 = __builtin_amdgcn_mfma_f32_32x32x2f32(a2[r], L.w3[r][lane + zo], a3, 0, 0, 0);
+    // MaxPool1d(32) over the rows: registers, then the other lane half
+    float m = a3[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) m = fmaxf(m, a3[r]);
+    m = fmaxf(m, __shfl_xor(m, 32, kWave));
+    if (h == 0) out[g * 32 + r32] = m;
+  }
+}
+
+template <typename T>
+int launch_dfe_tgt_mfma(PointsView<T> ref, const float* feat, int M, const float* cand, const float* dist,
+                        const int32_t* idx, int B, int Q, const float* params, float* out, hipStream_t st) {
+  const int64_t total = static_cast<int64_t>(B) * Q;
+  const int64_t need = (total + kDfeMfmaWaves - 1) / kDfeMfmaWaves;
+  const int grid = static_cast<int>(need < 4096 ? need : 4096);
+  hipLaunchKernelGGL((dfe_tgt_mfma_kernel<T>), dim3(grid), dim3(kDfeMfmaWaves * kWave), 0, st, ref, feat, M, cand,
+                     dist, idx, Q, B, params, out);
+  return launch_status("dvcp_dfe_tgt(mfma)");
+}
+
+template int launch_dfe_tgt_mfma<float>(PointsView<float>, const float*, int, const float*, const float*,
+                                        const int32_t*, int, int, const float*, float*, hipStream_t);
+template int launch_dfe_tgt_mfma<double>(PointsView<double>, const float*, int, const float*, const float*,
+                                         const int32_t*, int, int, const float*, float*, hipStream_t);
+
+}  // namespace dvcp

@@ -35,6 +35,25 @@ def main():
     print(f"knn: {e0.elapsed_time(e1) / reps:.4f} ms/call  queries {qry.shape[0] * qry.shape[1]}  "
           f"checksum {dist.double().sum().item():.6e} {idx.long().sum().item()}", flush=True)
 
+    # the target-side deep feature embedding on these neighbour lists (features random)
+    import dvcp
+    torch.manual_seed(3)
+    dfe = dvcp.feat_embedding_layer().eval().to(dev)
+    feat = torch.randn(8, ref.shape[2], 32, generator=g).to(dev)
+    params = dfe.packed_params()
+    for _ in range(3):
+        y = ops.dfe_tgt(ref, feat, qry, dist, idx, params, ref_pdim=2)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        ops.dfe_tgt(ref, feat, qry, dist, idx, params, ref_pdim=2)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    flops = 2.0 * (35 * 32 + 32 * 32 + 32 * 32) * 32 * qry.shape[0] * qry.shape[1]
+    print(f"dfe_tgt: {ms:.4f} ms/call  {flops / ms / 1e9:.1f} TFLOP/s  checksum {y.double().sum().item():.6e}"
+          f"  valu={os.environ.get('DVCP_DFE_VALU', '0')}", flush=True)
+
 
 if __name__ == "__main__":
     main()
