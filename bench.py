@@ -25,10 +25,20 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "deepvcp-pointcloud-registration_amd"))
 
-# Hardware queues per process (read when HIP initialises).  Each in-flight batch drives two
-# streams (the FPS chain and its side stream); with HIP's default of 4 queues, streams that share
-# a queue serialise behind each other's multi-millisecond FPS launches.  8 measured +13% over 4.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# Hardware queues per process (read when HIP initialises, so set before torch touches the GPU).
+# Each in-flight batch drives two streams (the FPS chain and its side stream); with HIP's default
+# of 4 queues, streams that share a queue serialise behind each other's multi-millisecond FPS
+# launches.  8 measured +13% over 4 (profiles/README.md).  --hw-queues overrides.
+def _hw_queues(argv):
+    for i, a in enumerate(argv):
+        if a == "--hw-queues" and i + 1 < len(argv):
+            return argv[i + 1]
+        if a.startswith("--hw-queues="):
+            return a.split("=", 1)[1]
+    return "8"
+
+
+os.environ["GPU_MAX_HW_QUEUES"] = _hw_queues(sys.argv)
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -51,6 +61,7 @@ def parse():
     p.add_argument("--inflight", type=int, default=4,
                    help="independent batches in flight (one stream each); 1 = strictly serial steps")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--hw-queues", type=int, default=8, help="GPU_MAX_HW_QUEUES for this process (<= 32)")
     p.add_argument("--stage-report", action="store_true", help="print the per-kernel table to stderr")
     return p.parse_args()
 

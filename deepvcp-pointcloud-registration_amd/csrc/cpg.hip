@@ -5,36 +5,62 @@
 //   Conv3d 32->16 -> 16->4 -> 4->1 (k3, p1, cross-correlation, no activations);
 //   softmax over the C = G^3 logits; vcp = sum(w * cand) / sum(w).
 //
-// LDS plan (G <= 11, C <= 1331): a 16-channel half of the cost volume (85 KB) plus conv1's
-// weights ([ci][tap][co], 55 KB, broadcast b128 reads).  conv1 runs as two input-channel
-// halves accumulating into VGPRs (<= 6 voxels x 16 channels per thread); its output then
-// replaces the cost volume in LDS for conv2, and conv2/conv3 outputs reuse the weight area.
+// Plan (G <= 11, C <= 1331), one 512-thread workgroup per key point: the key point's (C, 32)
+// target block is loaded once into registers; the cost volume is built in LDS one 8-channel
+// quarter at a time with a zero halo (13^3 cells, 70 KB) next to conv1's weights ([ci][tap][co],
+// 55 KB); conv1 runs on the matrix cores (see below), accumulating the quarters in registers;
+// its output (haloed) then replaces volume and weights in LDS for conv2, which runs the same way
+// with its 4 output channels padded to 16; conv2's haloed output feeds conv3 (VALU, maskless),
+// and the softmax and weighted mean finish in registers.
 #include "common.h"
 
 namespace dvcp {
 
-constexpr int kCpgThreads = 256;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kCpgThreads = 512;  // 8 waves: two per SIMD (LDS allows one workgroup per CU)
 constexpr int kCpgMaxC = 1331;
-constexpr int kCpgV = (kCpgMaxC + kCpgThreads - 1) / kCpgThreads;  // voxels per thread
+constexpr int kCpgMaxG = 11;
+constexpr int kCpgV = (kCpgMaxC + kCpgThreads - 1) / kCpgThreads;  // voxels per thread (conv2/3)
+constexpr int kCpgPV = (kCpgMaxG + 2) * (kCpgMaxG + 2) * (kCpgMaxG + 2);  // haloed voxels (13^3)
+constexpr int kCpgQ = 8;                                                  // channels per quarter
+constexpr int kCpgVolF = kCpgQ * kCpgPV;                                  // haloed quarter volume
+constexpr int kCpgW1F = 32 * 27 * 16;
+constexpr int kCpgBigF = 16 * kCpgPV;  // quarter volume + conv1 weights, later haloed conv1 / conv2 outputs
+constexpr int kCpgE = (32 * kCpgMaxC + kCpgThreads - 1) / kCpgThreads;  // target values per thread
+static_assert(kCpgVolF + kCpgW1F <= kCpgBigF, "quarter volume + conv1 weights must fit the area");
 
 __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restrict__ src, const float* __restrict__ tgt,
                                                           int64_t t_p, int64_t t_f, int64_t t_c,
                                                           const float* __restrict__ cand, int G,
                                                           const float* __restrict__ params, float* __restrict__ vcp,
                                                           float* __restrict__ weight) {
-  __shared__ __attribute__((aligned(16))) float vol[16 * kCpgMaxC];  // cost half / conv1 output
-  __shared__ __attribute__((aligned(16))) float w1[32 * 27 * 16];    // conv1 W [ci][tap][co]; later conv2/3 outputs
-  __shared__ __attribute__((aligned(16))) float w2[16 * 27 * 4];     // conv2 W [ci][tap][co]
+  __shared__ __attribute__((aligned(16))) float big[kCpgBigF];
+  __shared__ __attribute__((aligned(16))) float w2[16 * 27 * 4];  // conv2 W [ci][tap][co]
   __shared__ float w3[4 * 27];
   __shared__ float bias[16 + 4 + 1];
   __shared__ float sv[32];
   __shared__ float red[32];
+  float* vol = big;            // conv1 input: a haloed 8-channel quarter of the cost volume
+  float* w1 = big + kCpgVolF;  // conv1 W [ci][tap][co]
+  float* out1 = big;           // after conv1: its output, haloed [co][cell] (16 x PV)
+  float* out2 = big;           // after conv2: its output, haloed [co][cell] (4 x PV)
 
   const int p = blockIdx.x, tid = threadIdx.x;
   const int C = G * G * G, GG = G * G;
+  const int PG = G + 2, PGG = PG * PG, PV = PG * PGG;
   const float* P1 = params;
   const float* P2 = P1 + 16 * 32 * 27 + 16;
   const float* P3 = P2 + 4 * 16 * 27 + 4;
+  // the whole (C, 32) target block of this key point, coalesced, all loads in flight
+  const float* T = tgt + static_cast<int64_t>(p) * t_p;
+  float tv[kCpgE];
+#pragma unroll
+  for (int u = 0; u < kCpgE; ++u) {
+    const int e = u * kCpgThreads + tid;  // memory order (c, f)
+    tv[u] = e < 32 * C ? T[(e % 32) * t_f + (e / 32) * t_c] : 0.f;
+  }
+#pragma unroll 6
   for (int i = tid; i < 16 * 32 * 27; i += kCpgThreads) {  // torch (co, ci, kd, kh, kw)
     const int co = i / (32 * 27), r = i % (32 * 27);
     w1[r * 16 + co] = P1[i];
@@ -49,120 +75,131 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
   if (tid == 0) bias[20] = P3[4 * 27];
   if (tid < 32) sv[tid] = src[static_cast<int64_t>(p) * 32 + tid];
 
-  // per-thread voxels and their 27-tap validity masks (zero padding)
+  // per-thread voxels (conv3, softmax)
   int gv[kCpgV];
-  uint32_t mask[kCpgV];
 #pragma unroll
-  for (int v = 0; v < kCpgV; ++v) {
-    const int g = tid + v * kCpgThreads;
-    gv[v] = g;
-    uint32_t m = 0;
-    if (g < C) {
-      const int x = g / GG, y = (g / G) % G, z = g % G;
+  for (int v = 0; v < kCpgV; ++v) gv[v] = tid + v * kCpgThreads;
+
+  // conv1 (32 -> 16, k3) as an implicit GEMM on v_mfma_f32_16x16x4_f32: rows = 16-voxel tiles,
+  // k = 4 input channels at one tap, columns = the 16 output channels.  Wave w owns tiles
+  // w, w + 8, ... with their accumulators in registers: each k-step is one B fragment (weights)
+  // and up to kTW independent MFMAs.  The input is haloed (zero border), so a tap is a constant
+  // address shift and needs no mask; lane reads voxel 16 t + (lane & 15), channel 4 cg + (lane >> 4).
+  constexpr int kT = (kCpgMaxC + 15) / 16;          // voxel tiles at C = 1331
+  constexpr int kW = kCpgThreads / 64;
+  constexpr int kTW = (kT + kW - 1) / kW;           // per wave
+  const int lane = tid & 63, wave = tid >> 6, kg = lane >> 4, l16 = lane & 15;
+  const int NT = (C + 15) / 16;
+  int vx[kTW];  // haloed address of the lane's voxel per tile (a border cell past the end)
 #pragma unroll
-      for (int t = 0; t < 27; ++t) {
-        const int dx = t / 9 - 1, dy = (t / 3) % 3 - 1, dz = t % 3 - 1;
-        const bool ok = x + dx >= 0 && x + dx < G && y + dy >= 0 && y + dy < G && z + dz >= 0 && z + dz < G;
-        m |= (ok ? 1u : 0u) << t;
-      }
-    }
-    mask[v] = m;
+  for (int i = 0; i < kTW; ++i) {
+    const int g = 16 * (wave + kW * i) + l16;
+    vx[i] = g < C ? ((g / GG) + 1) * PGG + ((g / G) % G + 1) * PG + (g % G + 1) : 0;
   }
-
-  float acc[kCpgV][16];
+  f32x4 acc[kTW];
 #pragma unroll
-  for (int v = 0; v < kCpgV; ++v)
-#pragma unroll
-    for (int co = 0; co < 16; ++co) acc[v][co] = 0.f;
+  for (int i = 0; i < kTW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const float* T = tgt + static_cast<int64_t>(p) * t_p;
-  for (int half = 0; half < 2; ++half) {
+#pragma unroll 1
+  for (int q = 0; q < 32 / kCpgQ; ++q) {
     __syncthreads();
-    // cost volume half: channel f' in [16*half, 16*half+16); iterate the target in memory
-    // order (c, f) and scatter l = f*C + c -> (g = l / 32, f' = l % 32).
-    for (int e = tid; e < 32 * C; e += kCpgThreads) {
+    for (int i = tid; i < kCpgQ * PV; i += kCpgThreads) vol[i] = 0.f;
+    __syncthreads();
+    // cost volume quarter: channels f' in [8q, 8q + 8) of cost[f'][g] = (src[f'] - T[l])^2,
+    // l = g*32 + f' = f*C + c (the reference's reshape, Q11).  (The opaque zero keeps the
+    // compiler from hoisting 84 addresses per thread out of the quarter loop into registers.)
+    int zo = 0;
+    asm volatile("" : "+v"(zo));
+#pragma unroll
+    for (int u = 0; u < kCpgE; ++u) {
+      const int e = u * kCpgThreads + tid + zo;
       const int c = e / 32, f = e % 32;
       const int l = f * C + c;
       const int g = l >> 5, fp = l & 31;
-      if ((fp >> 4) == half) {
-        const float d = sv[fp] - T[f * t_f + c * t_c];
-        vol[(fp & 15) * C + g] = d * d;
+      if (e < 32 * C && (fp >> 3) == q) {
+        const float d = sv[fp] - tv[u];
+        vol[(fp & 7) * PV + ((g / GG) + 1) * PGG + ((g / G) % G + 1) * PG + (g % G + 1)] = d * d;
       }
     }
     __syncthreads();
 #pragma unroll 1
-    for (int cl = 0; cl < 16; ++cl) {
-      const float* vin = vol + cl * C;
-      const float* wrow = w1 + (half * 16 + cl) * 27 * 16;
-#pragma unroll 1
-      for (int t = 0; t < 27; ++t) {
-        const int off = (t / 9 - 1) * GG + ((t / 3) % 3 - 1) * G + (t % 3 - 1);
-        const float4* w4 = reinterpret_cast<const float4*>(wrow + t * 16);
-        const float4 wa = w4[0], wb = w4[1], wc = w4[2], wd = w4[3];
-        const float w[16] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w,
-                             wc.x, wc.y, wc.z, wc.w, wd.x, wd.y, wd.z, wd.w};
-#pragma unroll
-        for (int v = 0; v < kCpgV; ++v) {
-          const float xin = ((mask[v] >> t) & 1u) ? vin[gv[v] + off] : 0.f;
-#pragma unroll
-          for (int co = 0; co < 16; ++co) acc[v][co] = __fmaf_rn(w[co], xin, acc[v][co]);
-        }
-      }
-    }
-  }
-  __syncthreads();
-  // conv1 output -> vol[co][g]
-#pragma unroll
-  for (int v = 0; v < kCpgV; ++v)
-    if (gv[v] < C)
-#pragma unroll
-      for (int co = 0; co < 16; ++co) vol[co * C + gv[v]] = acc[v][co] + bias[co];
-  __syncthreads();
-
-  // conv2: 16 -> 4
-  float a2[kCpgV][4];
-#pragma unroll
-  for (int v = 0; v < kCpgV; ++v)
-#pragma unroll
-    for (int co = 0; co < 4; ++co) a2[v][co] = 0.f;
-#pragma unroll 1
-  for (int ci = 0; ci < 16; ++ci) {
-    const float* vin = vol + ci * C;
-#pragma unroll 1
     for (int t = 0; t < 27; ++t) {
-      const int off = (t / 9 - 1) * GG + ((t / 3) % 3 - 1) * G + (t % 3 - 1);
-      const float4 w = reinterpret_cast<const float4*>(w2 + (ci * 27 + t) * 4)[0];
+      const int off = (t / 9 - 1) * PGG + ((t / 3) % 3 - 1) * PG + (t % 3 - 1);
 #pragma unroll
-      for (int v = 0; v < kCpgV; ++v) {
-        const float xin = ((mask[v] >> t) & 1u) ? vin[gv[v] + off] : 0.f;
-        a2[v][0] = __fmaf_rn(w.x, xin, a2[v][0]);
-        a2[v][1] = __fmaf_rn(w.y, xin, a2[v][1]);
-        a2[v][2] = __fmaf_rn(w.z, xin, a2[v][2]);
-        a2[v][3] = __fmaf_rn(w.w, xin, a2[v][3]);
+      for (int cg = 0; cg < kCpgQ / 4; ++cg) {
+        const int ci = 4 * cg + kg;  // channel within the quarter
+        const float bw = w1[((kCpgQ * q + ci) * 27 + t) * 16 + l16];
+        const float* vin = vol + ci * PV + off;
+#pragma unroll
+        for (int i = 0; i < kTW; ++i)
+          if (wave + kW * i < NT)  // wave-uniform
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(vin[vx[i]], bw, acc[i], 0, 0, 0);
       }
     }
   }
-  float* out2 = w1;  // conv1 weights are dead now
+  __syncthreads();
+  // conv1 output -> out1 (haloed, zero border); accumulator register r of lane l is voxel
+  // 16 t + 4 (l >> 4) + r, output channel l & 15
+  for (int i = tid; i < 16 * PV; i += kCpgThreads) out1[i] = 0.f;
+  __syncthreads();
 #pragma unroll
-  for (int v = 0; v < kCpgV; ++v)
-    if (gv[v] < C)
+  for (int i = 0; i < kTW; ++i) {
+    const int t = wave + kW * i;
 #pragma unroll
-      for (int co = 0; co < 4; ++co) out2[co * C + gv[v]] = a2[v][co] + bias[16 + co];
+    for (int r = 0; r < 4; ++r) {
+      const int g = 16 * t + 4 * kg + r;
+      if (t < NT && g < C)
+        out1[l16 * PV + ((g / GG) + 1) * PGG + ((g / G) % G + 1) * PG + (g % G + 1)] = acc[i][r] + bias[l16];
+    }
+  }
   __syncthreads();
 
-  // conv3: 4 -> 1
+  // conv2 (16 -> 4) the same way, output channels padded to the MFMA's 16 columns
+#pragma unroll
+  for (int i = 0; i < kTW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int t = 0; t < 27; ++t) {
+    const int off = (t / 9 - 1) * PGG + ((t / 3) % 3 - 1) * PG + (t % 3 - 1);
+#pragma unroll
+    for (int cg = 0; cg < 4; ++cg) {
+      const int ci = 4 * cg + kg;
+      const float bw = l16 < 4 ? w2[(ci * 27 + t) * 4 + l16] : 0.f;
+      const float* vin = out1 + ci * PV + off;
+#pragma unroll
+      for (int i = 0; i < kTW; ++i)
+        if (wave + kW * i < NT)
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(vin[vx[i]], bw, acc[i], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < 4 * PV; i += kCpgThreads) out2[i] = 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kTW; ++i) {
+    const int t = wave + kW * i;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int g = 16 * t + 4 * kg + r;
+      if (t < NT && g < C && l16 < 4)
+        out2[l16 * PV + ((g / GG) + 1) * PGG + ((g / G) % G + 1) * PG + (g % G + 1)] = acc[i][r] + bias[16 + l16];
+    }
+  }
+  __syncthreads();
+
+  // conv3: 4 -> 1, one voxel per thread (haloed input: no masks)
   float lg[kCpgV];
   float lmax = -__builtin_huge_valf();
 #pragma unroll
   for (int v = 0; v < kCpgV; ++v) {
+    const int g = gv[v] < C ? gv[v] : 0;
+    const int hv = ((g / GG) + 1) * PGG + ((g / G) % G + 1) * PG + (g % G + 1);
     float a = 0.f;
-#pragma unroll 1
+#pragma unroll
     for (int ci = 0; ci < 4; ++ci)
-#pragma unroll 1
+#pragma unroll
       for (int t = 0; t < 27; ++t) {
-        const int off = (t / 9 - 1) * GG + ((t / 3) % 3 - 1) * G + (t % 3 - 1);
-        const float xin = ((mask[v] >> t) & 1u) ? out2[ci * C + gv[v] + off] : 0.f;
-        a = __fmaf_rn(w3[ci * 27 + t], xin, a);
+        const int off = (t / 9 - 1) * PGG + ((t / 3) % 3 - 1) * PG + (t % 3 - 1);
+        a = __fmaf_rn(w3[ci * 27 + t], out2[ci * PV + hv + off], a);
       }
     lg[v] = a + bias[20];
     if (gv[v] < C) lmax = fmaxf(lmax, lg[v]);

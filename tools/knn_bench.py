@@ -54,6 +54,26 @@ def main():
     print(f"dfe_tgt: {ms:.4f} ms/call  {flops / ms / 1e9:.1f} TFLOP/s  checksum {y.double().sum().item():.6e}"
           f"  valu={os.environ.get('DVCP_DFE_VALU', '0')}", flush=True)
 
+    # corresponding point generation on these embeddings (src side random)
+    cpg = dvcp.cpg().eval().to(dev)
+    K, C = 64, 1331
+    tgt_dfe = y.view(8, K, C, 32)
+    src_dfe = torch.randn(8, K, 32, generator=g).to(dev)
+    cand = qry.view(8, K, C, 3)
+    cp = cpg.packed_params()
+    for _ in range(3):
+        v = ops.cpg(src_dfe, tgt_dfe.permute(0, 1, 3, 2), cand, 11, cp)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        ops.cpg(src_dfe, tgt_dfe.permute(0, 1, 3, 2), cand, 11, cp)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    flops = 2.0 * C * (16 * 32 + 4 * 16 + 1 * 4) * 27 * 8 * K
+    print(f"cpg: {ms:.4f} ms/call  {flops / ms / 1e9:.1f} TFLOP/s  checksum {v[0].double().sum().item():.6e}",
+          flush=True)
+
 
 if __name__ == "__main__":
     main()
