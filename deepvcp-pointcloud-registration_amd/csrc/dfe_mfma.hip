@@ -137,14 +137,143 @@ __global__ __launch_bounds__(kDfeMfmaWaves * kWave) void dfe_tgt_mfma_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Collapsed form (default).  fc1, fc2 and fc3 have no nonlinearity between them (Q14,
+// deep_feat_embedding.py:48-50), so fc3(fc2(fc1 x)) = E x + e with E = W3 W2 W1 (32 x 35) and
+// e = W3 (W2 b1 + b2) + b3.  Each workgroup forms E and e in fp64 from the three layers (a
+// 72 kflop prologue) and rounds them once to fp32; a candidate then costs 19 MFMAs instead of 51.
+// The result differs from the layer-by-layer fp32 chain only by rounding (two fewer fp32
+// roundings of intermediates, one of E); tests hold it to the same 1e-5 bound.
+//   H = X . E^T:  A = X (lane: row j, k-half), B = E^T fragment (lane: output channel, k-half)
+//   -> output channel on lanes, rows in registers, max over rows = registers + one lane swap.
+// dist_sum: 32 fp32 distances summed in fp64 are exact whenever they span less than 2^24 (24-bit
+// mantissas, 5 bits of carry, 53-bit accumulator), so a butterfly sum equals the reference's
+// ordered sum; w_j = dist_j / dist_sum in fp64 is then bit-identical.
+constexpr int kDfe1Waves = 4;
+
+struct Dfe1Lds {
+  double p[32][35];      // W2 . W1 (fp64), prologue only
+  double pb[32];         // W2 . b1 + b2
+  float e[kDfeKS][64];   // E as the B fragment: [k-step][lane]
+  float eb[32];          // e
+  double w[kDfe1Waves][32];  // per-wave w_j of the current candidate
+};
+
+template <typename T>
+__global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
+    PointsView<T> ref, const float* __restrict__ feat, int M, const float* __restrict__ cand,
+    const float* __restrict__ dist, const int32_t* __restrict__ idx, int Q, int B, const float* __restrict__ params,
+    float* __restrict__ out) {
+  __shared__ Dfe1Lds L;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
+  const float* W1 = params;
+  const float* pb1 = W1 + 32 * 35;
+  const float* W2 = pb1 + 32;
+  const float* pb2 = W2 + 32 * 32;
+  const float* W3 = pb2 + 32;
+  const float* pb3 = W3 + 32 * 32;
+  // prologue: P = W2 W1, pb = W2 b1 + b2 (fp64)
+  for (int i = tid; i < 32 * 36; i += blockDim.x) {
+    const int o = i / 36, c = i % 36;
+    double acc = 0.0;
+    if (c < 35) {
+      for (int a = 0; a < 32; ++a) acc = __fma_rn(static_cast<double>(W2[o * 32 + a]), static_cast<double>(W1[a * 35 + c]), acc);
+      L.p[o][c] = acc;
+    } else {
+      for (int a = 0; a < 32; ++a) acc = __fma_rn(static_cast<double>(W2[o * 32 + a]), static_cast<double>(pb1[a]), acc);
+      L.pb[o] = acc + static_cast<double>(pb2[o]);
+    }
+  }
+  __syncthreads();
+  // E = W3 P in fragment order, e = W3 pb + b3
+  for (int i = tid; i < kDfeKS * 64; i += blockDim.x) {
+    const int l = i % 64, s = i / 64, hh = l >> 5, o = l & 31;
+    const int ch = s < 3 ? (hh == 0 ? s : -1) : 3 + hh * 16 + (s - 3);
+    double acc = 0.0;
+    if (ch >= 0)
+      for (int a = 0; a < 32; ++a) acc = __fma_rn(static_cast<double>(W3[o * 32 + a]), L.p[a][ch], acc);
+    L.e[s][l] = static_cast<float>(acc);
+  }
+  for (int o = tid; o < 32; o += blockDim.x) {
+    double acc = 0.0;
+    for (int a = 0; a < 32; ++a) acc = __fma_rn(static_cast<double>(W3[o * 32 + a]), L.pb[a], acc);
+    L.eb[o] = static_cast<float>(acc + static_cast<double>(pb3[o]));
+  }
+  __syncthreads();
+  const float eb = L.eb[r32];
+
+  const int64_t total = static_cast<int64_t>(B) * Q;
+  for (int64_t g = static_cast<int64_t>(blockIdx.x) * kDfe1Waves + wave; g < total;
+       g += static_cast<int64_t>(gridDim.x) * kDfe1Waves) {
+    const int b = static_cast<int>(g / Q);
+    // get_cat_feat_tgt.py:57-58 (lanes 32..63 mirror lanes 0..31)
+    const float dj = dist[g * 32 + r32];
+    double dsum = static_cast<double>(dj);
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) dsum += __shfl_xor(dsum, off, kWave);
+    const double wj = static_cast<double>(dj) / dsum;
+    if (h == 0) L.w[wave][r32] = wj;
+    int n = idx[g * 32 + r32];
+    n = n < 0 ? 0 : (n >= M ? M - 1 : n);
+    const float* cq = cand + g * 3;
+    float x[kDfeKS];
+    if (h == 0) {
+      x[0] = static_cast<float>(ref.at(b, 0, n) - static_cast<T>(cq[0]));
+      x[1] = static_cast<float>(ref.at(b, 1, n) - static_cast<T>(cq[1]));
+      x[2] = static_cast<float>(ref.at(b, 2, n) - static_cast<T>(cq[2]));
+    } else {
+      x[0] = x[1] = x[2] = 0.0f;
+    }
+    const float4* fr = reinterpret_cast<const float4*>(feat + (static_cast<int64_t>(b) * M + n) * 32 + 16 * h);
+    float4 fv4[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) fv4[v] = fr[v];
+    // the wave's own w row: written above by lanes 0..31, read back as 16-byte broadcasts
+    __builtin_amdgcn_wave_barrier();
+    const double2* wr = reinterpret_cast<const double2*>(&L.w[wave][16 * h]);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const float fv[4] = {fv4[v].x, fv4[v].y, fv4[v].z, fv4[v].w};
+      const double2 wa = wr[2 * v], wb = wr[2 * v + 1];
+      const double wf[4] = {wa.x, wa.y, wb.x, wb.y};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[3 + 4 * v + e] = static_cast<float>(static_cast<double>(fv[e]) * wf[e]);
+    }
+    int zo = 0;  // opaque zero: E fragments are re-read from LDS per candidate, not hoisted
+    asm volatile("" : "+v"(zo));
+    f32x16 a;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) a[r] = eb;
+#pragma unroll
+    for (int s = 0; s < kDfeKS; ++s) a = __builtin_amdgcn_mfma_f32_32x32x2f32(x[s], L.e[s][lane + zo], a, 0, 0, 0);
+    float m = a[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) m = fmaxf(m, a[r]);
+    m = fmaxf(m, __shfl_xor(m, 32, kWave));
+    if (h == 0) out[g * 32 + r32] = m;
+    __builtin_amdgcn_wave_barrier();  // w row reused by the next candidate
+  }
+}
+
 template <typename T>
 int launch_dfe_tgt_mfma(PointsView<T> ref, const float* feat, int M, const float* cand, const float* dist,
                         const int32_t* idx, int B, int Q, const float* params, float* out, hipStream_t st) {
   const int64_t total = static_cast<int64_t>(B) * Q;
   const int64_t need = (total + kDfeMfmaWaves - 1) / kDfeMfmaWaves;
-  const int grid = static_cast<int>(need < 4096 ? need : 4096);
-  hipLaunchKernelGGL((dfe_tgt_mfma_kernel<T>), dim3(grid), dim3(kDfeMfmaWaves * kWave), 0, st, ref, feat, M, cand,
-                     dist, idx, Q, B, params, out);
+  static const bool layerwise = [] {
+    const char* e = getenv("DVCP_DFE_LAYERWISE");
+    return e && *e && *e != '0';
+  }();
+  if (layerwise) {
+    const int grid = static_cast<int>(need < 4096 ? need : 4096);
+    hipLaunchKernelGGL((dfe_tgt_mfma_kernel<T>), dim3(grid), dim3(kDfeMfmaWaves * kWave), 0, st, ref, feat, M, cand,
+                       dist, idx, Q, B, params, out);
+  } else {
+    // a few resident workgroups per CU amortise the fp64 prologue over many candidates
+    const int grid = static_cast<int>(need < 2048 ? need : 2048);
+    hipLaunchKernelGGL((dfe_tgt_mfma1_kernel<T>), dim3(grid), dim3(kDfe1Waves * kWave), 0, st, ref, feat, M, cand,
+                       dist, idx, Q, B, params, out);
+  }
   return launch_status("dvcp_dfe_tgt(mfma)");
 }
 
