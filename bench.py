@@ -35,7 +35,7 @@ def _hw_queues(argv):
             return argv[i + 1]
         if a.startswith("--hw-queues="):
             return a.split("=", 1)[1]
-    return "8"
+    return "16"
 
 
 os.environ["GPU_MAX_HW_QUEUES"] = _hw_queues(sys.argv)
@@ -58,10 +58,10 @@ def parse():
     p.add_argument("--K", type=int, default=64)
     p.add_argument("--r", type=float, default=2.0)
     p.add_argument("--s", type=float, default=0.4)
-    p.add_argument("--inflight", type=int, default=4,
+    p.add_argument("--inflight", type=int, default=8,
                    help="independent batches in flight (one stream each); 1 = strictly serial steps")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--hw-queues", type=int, default=8, help="GPU_MAX_HW_QUEUES for this process (<= 32)")
+    p.add_argument("--hw-queues", type=int, default=16, help="GPU_MAX_HW_QUEUES for this process (<= 32)")
     p.add_argument("--stage-report", action="store_true", help="print the per-kernel table to stderr")
     return p.parse_args()
 

@@ -124,9 +124,9 @@ __global__ __launch_bounds__(kSaThreads) void sa_mlp_kernel(PointsView<T> pts, P
 
 // fp32 MFMA path for the two-layer tables (sa_mlp_mfma.hip)
 template <typename T, int D, int C1, int C2>
-int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, const void* c, int64_t cb, int64_t cc,
+int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, const void* c, int64_t cb, int64_t cc,
                    int64_t cn, int S, int B, const float* feat, int64_t fb, int64_t fn, const int32_t* count,
-                   const int32_t* list, int nsample, const float* params, float* out, hipStream_t st);
+                   const int32_t* list, int nsample, const float* params, float* U, float* out, hipStream_t st);
 
 template <typename T, typename FT, int D, int C1, int C2, int C3>
 static int launch_sa(const void* xyz, int64_t sb, int64_t sc, int64_t sn, const void* c, int64_t cb, int64_t cc,
@@ -154,13 +154,21 @@ static bool dvcp_sa_force_valu() {
   return v;
 }
 
-extern "C" int dvcp_sa_group_mlp(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
-                                 const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
-                                 int feat_dtype, const void* feat, int64_t fb, int64_t fd, int64_t fn, int D,
-                                 const int32_t* count, const int32_t* list, int nsample, int nlayer,
-                                 const int* chans, const float* params, float* out, void* stream) {
-  (void)N;
+// Workspace of the decomposed two-layer MFMA path: U = W1f f + b1 per input point, B x N x C1 fp32.
+static int64_t sa_ws_bytes(int B, int N, int nlayer, const int* chans) {
+  if (nlayer != 2 || !chans) return 0;
+  const int D = chans[0] - 3;
+  const bool mfma_table = (D == 32 && chans[1] == 32 && chans[2] == 64) || (D == 64 && chans[1] == 64 && chans[2] == 64);
+  return mfma_table ? static_cast<int64_t>(B) * N * chans[1] * 4 : 0;
+}
+
+static int sa_group_mlp_impl(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, const void* ctr,
+                             int64_t cb, int64_t cc, int64_t cn, int S, int B, int feat_dtype, const void* feat,
+                             int64_t fb, int64_t fd, int64_t fn, int D, const int32_t* count, const int32_t* list,
+                             int nsample, int nlayer, const int* chans, const float* params, float* out, void* ws,
+                             void* stream) {
   DVCP_REQUIRE(xyz && ctr && count && list && chans && params && out, "dvcp_sa_group_mlp: null pointer");
+  DVCP_REQUIRE(N > 0 || ws == nullptr, "dvcp_sa_group_mlp_ws: N must be given with a workspace");
   DVCP_REQUIRE(D == 0 || feat, "dvcp_sa_group_mlp: D=%d but feat is NULL", D);
   DVCP_REQUIRE(chans[0] == 3 + D, "dvcp_sa_group_mlp: chans[0]=%d != 3+D", chans[0]);
   if (B == 0 || S == 0) return DVCP_OK;
@@ -190,12 +198,12 @@ extern "C" int dvcp_sa_group_mlp(int dtype, const void* xyz, int64_t sb, int64_t
   const bool mfma_ok = !ff64 && fd == 1 && fb % 4 == 0 && fn % 4 == 0 &&
                        (reinterpret_cast<uintptr_t>(feat) & 15) == 0 && !dvcp_sa_force_valu();
 #define DVCP_SA_M(DD, A, Bc)                                                                                     \
-  return f64 ? dvcp::launch_sa_mfma<double, DD, A, Bc>(xyz, sb, sc, sn, ctr, cb, cc, cn, S, B,                  \
+  return f64 ? dvcp::launch_sa_mfma<double, DD, A, Bc>(xyz, sb, sc, sn, N, ctr, cb, cc, cn, S, B,               \
                                                      static_cast<const float*>(feat), fb, fn, count, list,      \
-                                                     nsample, params, out, st)                                  \
-             : dvcp::launch_sa_mfma<float, DD, A, Bc>(xyz, sb, sc, sn, ctr, cb, cc, cn, S, B,                   \
+                                                     nsample, params, static_cast<float*>(ws), out, st)         \
+             : dvcp::launch_sa_mfma<float, DD, A, Bc>(xyz, sb, sc, sn, N, ctr, cb, cc, cn, S, B,                \
                                                     static_cast<const float*>(feat), fb, fn, count, list, nsample, \
-                                                    params, out, st)
+                                                    params, static_cast<float*>(ws), out, st)
   if (nlayer == 2 && D == 32 && chans[1] == 32 && chans[2] == 64) {
     if (mfma_ok) DVCP_SA_M(32, 32, 64);
     DVCP_SA_T(32, 32, 64, 0);
@@ -209,4 +217,30 @@ extern "C" int dvcp_sa_group_mlp(int dtype, const void* xyz, int64_t sb, int64_t
 #undef DVCP_SA
   dvcp::set_error("dvcp_sa_group_mlp: unsupported layer table (nlayer=%d, D=%d)", nlayer, D);
   return DVCP_EINVAL;
+}
+
+extern "C" int dvcp_sa_group_mlp(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
+                                 const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
+                                 int feat_dtype, const void* feat, int64_t fb, int64_t fd, int64_t fn, int D,
+                                 const int32_t* count, const int32_t* list, int nsample, int nlayer,
+                                 const int* chans, const float* params, float* out, void* stream) {
+  return sa_group_mlp_impl(dtype, xyz, sb, sc, sn, N, ctr, cb, cc, cn, S, B, feat_dtype, feat, fb, fd, fn, D, count,
+                           list, nsample, nlayer, chans, params, out, nullptr, stream);
+}
+
+extern "C" int64_t dvcp_sa_group_mlp_workspace_bytes(int B, int N, int nlayer, const int* chans) {
+  return sa_ws_bytes(B, N, nlayer, chans);
+}
+
+extern "C" int dvcp_sa_group_mlp_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
+                                    const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
+                                    int feat_dtype, const void* feat, int64_t fb, int64_t fd, int64_t fn, int D,
+                                    const int32_t* count, const int32_t* list, int nsample, int nlayer,
+                                    const int* chans, const float* params, float* out, void* workspace,
+                                    void* stream) {
+  DVCP_REQUIRE(sa_ws_bytes(B, N, nlayer, chans) == 0 || workspace, "dvcp_sa_group_mlp_ws: workspace is NULL");
+  DVCP_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "dvcp_sa_group_mlp_ws: workspace not 16-B aligned");
+  return sa_group_mlp_impl(dtype, xyz, sb, sc, sn, N, ctr, cb, cc, cn, S, B, feat_dtype, feat, fb, fd, fn, D, count,
+                           list, nsample, nlayer, chans, params, out,
+                           sa_ws_bytes(B, N, nlayer, chans) ? workspace : nullptr, stream);
 }

@@ -42,6 +42,7 @@ template <int D, int C1, int C2>
 struct SaMfmaLds {
   using S = SaMfmaShape<D, C1, C2>;
   float w1[S::MT][S::KS][64];   // A fragment of layer 1: [tile][k-step][lane]
+  float wx[S::MT][2][64];       // decomposed layer 1: xyz columns only, k-steps (x|y), (z|0)
   float w2[S::CT][S::K2][64];   // B fragment of layer 2: [tile][k-step][lane]
   float b1[S::MT][2][16];       // layer-1 bias / BN scale / BN shift by [tile][lane half][register]
   float s1[S::MT][2][16];
@@ -58,11 +59,54 @@ __device__ __forceinline__ int sa_in_channel(int s, int h) {
 // output channel row of accumulator register r for lane half h (32x32 C/D map)
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-template <typename T, int D, int C1, int C2>
+// Decomposed layer 1 (PRE = true).  Layer 1 is linear in its input row [p - c, f]:
+//   W1 [p - c; f] + b1 = W1x (p - c) + (W1f f + b1)
+// and the second term depends only on the neighbour point, not on the centre.  sa_pre_kernel
+// evaluates U[n] = W1f f_n + b1 once per input point (N rows instead of S x nsample), and the
+// grouped kernel starts each layer-1 accumulator from the gathered U row and adds the xyz part
+// with two MFMA k-steps.  Only the summation order changes (features first, then xyz); the local
+// coordinates are still formed per (centre, point) pair, so no cancellation is introduced.
+template <int D, int C1>
+__global__ __launch_bounds__(256) void sa_pre_kernel(const float* __restrict__ feat, int64_t fb, int64_t fn, int N,
+                                                     int B, const float* __restrict__ params,
+                                                     float* __restrict__ U) {
+  constexpr int C0 = 3 + D;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= static_cast<int64_t>(B) * N) return;
+  const int b = static_cast<int>(i / N), n = static_cast<int>(i % N);
+  const float4* fr = reinterpret_cast<const float4*>(feat + b * fb + static_cast<int64_t>(n) * fn);
+  float f[D];
+#pragma unroll
+  for (int v = 0; v < D / 4; ++v) {
+    const float4 q = fr[v];
+    f[4 * v] = q.x;
+    f[4 * v + 1] = q.y;
+    f[4 * v + 2] = q.z;
+    f[4 * v + 3] = q.w;
+  }
+  const float* W1 = params;
+  const float* pb1 = W1 + C1 * C0;
+  float4* dst = reinterpret_cast<float4*>(U + i * C1);
+#pragma unroll 4
+  for (int c4 = 0; c4 < C1 / 4; ++c4) {
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = 4 * c4 + e;
+      float acc = pb1[c];
+#pragma unroll
+      for (int k = 0; k < D; ++k) acc = __fmaf_rn(W1[c * C0 + 3 + k], f[k], acc);
+      o[e] = acc;
+    }
+    dst[c4] = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+template <typename T, int D, int C1, int C2, bool PRE>
 __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
     PointsView<T> pts, PointsView<T> ctr, int S, int B, const float* __restrict__ feat, int64_t fb, int64_t fn,
     const int32_t* __restrict__ count, const int32_t* __restrict__ list, int nsample,
-    const float* __restrict__ params, float* __restrict__ out) {
+    const float* __restrict__ params, const float* __restrict__ U, int64_t ub, float* __restrict__ out) {
   using Sh = SaMfmaShape<D, C1, C2>;
   constexpr int C0 = Sh::C0, KS = Sh::KS, MT = Sh::MT, CT = Sh::CT;
   __shared__ SaMfmaLds<D, C1, C2> L;
@@ -82,6 +126,12 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
     const int ch = sa_in_channel<D>(s, l >> 5);
     L.w1[mt][s][l] = ch < 0 ? 0.0f : W1[(32 * mt + (l & 31)) * C0 + ch];
   }
+  if (PRE)
+    for (int i = tid; i < MT * 2 * 64; i += blockDim.x) {
+      const int l = i % 64, s = (i / 64) % 2, mt = i / 128;
+      const int ch = s == 0 ? (l >> 5) : ((l >> 5) == 0 ? 2 : -1);
+      L.wx[mt][s][l] = ch < 0 ? 0.0f : W1[(32 * mt + (l & 31)) * C0 + ch];
+    }
   for (int i = tid; i < CT * Sh::K2 * 64; i += blockDim.x) {
     const int l = i % 64, kk = (i / 64) % Sh::K2, ct = i / (64 * Sh::K2);
     const int mt = kk / 16, r = kk % 16;
@@ -125,34 +175,58 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
       // B fragment of layer 1: this lane's point (r32) and its half of the input channels
       const int row = n0 + r32;
       const int n = lst[row < rows ? row : 0];
-      float x[KS];
-      if (h == 0) {
-        x[0] = static_cast<float>(pts.at(b, 0, n) - cx);
-        x[1] = static_cast<float>(pts.at(b, 1, n) - cy);
-        x[2] = static_cast<float>(pts.at(b, 2, n) - cz);
-      } else {
-        x[0] = x[1] = x[2] = 0.0f;
-      }
-      const float4* fr = reinterpret_cast<const float4*>(feat + b * fb + static_cast<int64_t>(n) * fn + h * (D / 2));
-#pragma unroll
-      for (int v = 0; v < D / 8; ++v) {
-        const float4 f = fr[v];
-        x[3 + 4 * v] = f.x;
-        x[4 + 4 * v] = f.y;
-        x[5 + 4 * v] = f.z;
-        x[6 + 4 * v] = f.w;
-      }
-      // layer 1 (transposed): acc1[mt] rows = output channels, columns = points
       f32x16 acc1[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc1[mt][r] = L.b1[mt][h][r + zo];
-#pragma unroll
-      for (int s = 0; s < KS; ++s)
+      if constexpr (PRE) {
+        // accumulators start from U[n] (channels (r&3) + 8(r>>2) + 4h of each 32-channel tile)
+        const float4* ur = reinterpret_cast<const float4*>(U + b * ub + static_cast<int64_t>(n) * C1 + 4 * h);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
-          acc1[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(L.w1[mt][s][lane + zo], x[s], acc1[mt], 0, 0, 0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float4 u = ur[8 * mt + 2 * i];
+            acc1[mt][4 * i] = u.x;
+            acc1[mt][4 * i + 1] = u.y;
+            acc1[mt][4 * i + 2] = u.z;
+            acc1[mt][4 * i + 3] = u.w;
+          }
+        const float dx = static_cast<float>(pts.at(b, 0, n) - cx);
+        const float dy = static_cast<float>(pts.at(b, 1, n) - cy);
+        const float dz = static_cast<float>(pts.at(b, 2, n) - cz);
+        const float x0 = h == 0 ? dx : dy, x1 = h == 0 ? dz : 0.0f;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          acc1[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(L.wx[mt][0][lane + zo], x0, acc1[mt], 0, 0, 0);
+          acc1[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(L.wx[mt][1][lane + zo], x1, acc1[mt], 0, 0, 0);
+        }
+      } else {
+        float x[KS];
+        if (h == 0) {
+          x[0] = static_cast<float>(pts.at(b, 0, n) - cx);
+          x[1] = static_cast<float>(pts.at(b, 1, n) - cy);
+          x[2] = static_cast<float>(pts.at(b, 2, n) - cz);
+        } else {
+          x[0] = x[1] = x[2] = 0.0f;
+        }
+        const float4* fr = reinterpret_cast<const float4*>(feat + b * fb + static_cast<int64_t>(n) * fn + h * (D / 2));
+#pragma unroll
+        for (int v = 0; v < D / 8; ++v) {
+          const float4 f = fr[v];
+          x[3 + 4 * v] = f.x;
+          x[4 + 4 * v] = f.y;
+          x[5 + 4 * v] = f.z;
+          x[6 + 4 * v] = f.w;
+        }
+        // layer 1 (transposed): acc1[mt] rows = output channels, columns = points
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc1[mt][r] = L.b1[mt][h][r + zo];
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+            acc1[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(L.w1[mt][s][lane + zo], x[s], acc1[mt], 0, 0, 0);
+      }
       // BN (eval) + ReLU in place
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
@@ -193,29 +267,35 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
 }
 
 template <typename T, int D, int C1, int C2>
-int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, const void* c, int64_t cb, int64_t cc,
+int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, const void* c, int64_t cb, int64_t cc,
                    int64_t cn, int S, int B, const float* feat, int64_t fb, int64_t fn, const int32_t* count,
-                   const int32_t* list, int nsample, const float* params, float* out, hipStream_t st) {
+                   const int32_t* list, int nsample, const float* params, float* U, float* out, hipStream_t st) {
   PointsView<T> pv{static_cast<const T*>(xyz), sb, sc, sn};
   PointsView<T> cv{static_cast<const T*>(c), cb, cc, cn};
   const int64_t centres = static_cast<int64_t>(B) * S;
   const int grid = static_cast<int>(centres < 4096 * kMfmaWaves ? (centres + kMfmaWaves - 1) / kMfmaWaves : 4096);
-  hipLaunchKernelGGL((sa_mlp_mfma_kernel<T, D, C1, C2>), dim3(grid), dim3(kMfmaWaves * kWave), 0, st, pv, cv, S, B,
-                     feat, fb, fn, count, list, nsample, params, out);
+  if (U) {
+    const int64_t rows = static_cast<int64_t>(B) * N;
+    hipLaunchKernelGGL((sa_pre_kernel<D, C1>), dim3(ceil_div(rows, 256)), dim3(256), 0, st, feat, fb, fn, N, B, params,
+                       U);
+    hipLaunchKernelGGL((sa_mlp_mfma_kernel<T, D, C1, C2, true>), dim3(grid), dim3(kMfmaWaves * kWave), 0, st, pv, cv,
+                       S, B, feat, fb, fn, count, list, nsample, params, U, static_cast<int64_t>(N) * C1, out);
+  } else {
+    hipLaunchKernelGGL((sa_mlp_mfma_kernel<T, D, C1, C2, false>), dim3(grid), dim3(kMfmaWaves * kWave), 0, st, pv,
+                       cv, S, B, feat, fb, fn, count, list, nsample, params, nullptr, 0, out);
+  }
   return launch_status("dvcp_sa_group_mlp(mfma)");
 }
 
-template int launch_sa_mfma<float, 32, 32, 64>(const void*, int64_t, int64_t, int64_t, const void*, int64_t, int64_t,
-                                               int64_t, int, int, const float*, int64_t, int64_t, const int32_t*,
-                                               const int32_t*, int, const float*, float*, hipStream_t);
-template int launch_sa_mfma<double, 32, 32, 64>(const void*, int64_t, int64_t, int64_t, const void*, int64_t, int64_t,
-                                                int64_t, int, int, const float*, int64_t, int64_t, const int32_t*,
-                                                const int32_t*, int, const float*, float*, hipStream_t);
-template int launch_sa_mfma<float, 64, 64, 64>(const void*, int64_t, int64_t, int64_t, const void*, int64_t, int64_t,
-                                               int64_t, int, int, const float*, int64_t, int64_t, const int32_t*,
-                                               const int32_t*, int, const float*, float*, hipStream_t);
-template int launch_sa_mfma<double, 64, 64, 64>(const void*, int64_t, int64_t, int64_t, const void*, int64_t, int64_t,
-                                                int64_t, int, int, const float*, int64_t, int64_t, const int32_t*,
-                                                const int32_t*, int, const float*, float*, hipStream_t);
+#define DVCP_SA_MFMA_INST(T, D, C1, C2)                                                                          \
+  template int launch_sa_mfma<T, D, C1, C2>(const void*, int64_t, int64_t, int64_t, int, const void*, int64_t,  \
+                                            int64_t, int64_t, int, int, const float*, int64_t, int64_t,         \
+                                            const int32_t*, const int32_t*, int, const float*, float*, float*,  \
+                                            hipStream_t);
+DVCP_SA_MFMA_INST(float, 32, 32, 64)
+DVCP_SA_MFMA_INST(double, 32, 32, 64)
+DVCP_SA_MFMA_INST(float, 64, 64, 64)
+DVCP_SA_MFMA_INST(double, 64, 64, 64)
+#undef DVCP_SA_MFMA_INST
 
 }  // namespace dvcp

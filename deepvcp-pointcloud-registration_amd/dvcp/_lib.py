@@ -28,6 +28,8 @@ SIGNATURES = {
     "dvcp_square_distance": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _P, _P],
     "dvcp_sa_group_mlp": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _L, _L, _L, _I,
                           _P, _P, _I, _I, _P, _P, _P, _P],
+    "dvcp_sa_group_mlp_ws": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _L, _L, _L, _I,
+                             _P, _P, _I, _I, _P, _P, _P, _P, _P],
     "dvcp_fe_head": [_P, _I, _P, _P, _P, _P],
     "dvcp_weighting": [_P, _I, _P, _P, _P],
     "dvcp_topk": [_P, _I, _I, _I, _P, _P],
@@ -66,6 +68,8 @@ def load():
     lib.dvcp_knn_tiled_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
     lib.dvcp_ball_query_workspace_bytes.restype = ctypes.c_int64
     lib.dvcp_ball_query_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.dvcp_sa_group_mlp_workspace_bytes.restype = ctypes.c_int64
+    lib.dvcp_sa_group_mlp_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     for name, args in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = ctypes.c_int
@@ -76,7 +80,8 @@ def load():
 
 def exported_symbols():
     return ["dvcp_last_error", "dvcp_abi_version", "dvcp_knn_grid_workspace_bytes",
-            "dvcp_knn_tiled_workspace_bytes", "dvcp_ball_query_workspace_bytes"] + list(SIGNATURES)
+            "dvcp_knn_tiled_workspace_bytes", "dvcp_ball_query_workspace_bytes",
+            "dvcp_sa_group_mlp_workspace_bytes"] + list(SIGNATURES)
 
 
 # When a list, every entry-point call appends (name, start_event, end_event, work) recorded on
