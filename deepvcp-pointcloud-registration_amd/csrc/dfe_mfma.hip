@@ -202,38 +202,60 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
   __syncthreads();
   const float eb = L.eb[r32];
 
-  const int64_t total = static_cast<int64_t>(B) * Q;
-  for (int64_t g = static_cast<int64_t>(blockIdx.x) * kDfe1Waves + wave; g < total;
-       g += static_cast<int64_t>(gridDim.x) * kDfe1Waves) {
-    const int b = static_cast<int>(g / Q);
-    // get_cat_feat_tgt.py:57-58 (lanes 32..63 mirror lanes 0..31)
-    const float dj = dist[g * 32 + r32];
+  // Software pipeline over this wave's candidates g0, g0 + stride, ...: the kNN row (dist, idx)
+  // is loaded two candidates ahead and the gathered point/feature row one ahead, so the
+  // dependent idx -> gather latency overlaps the MFMAs of the candidate in hand.  Two register
+  // sets (A, B) alternate, so no loaded register is ever copied (a copy would wait for its load).
+  // Loads are unconditional (indices clamped to the last candidate) and a loaded index is only
+  // clamped in the iteration that gathers with it.  Candidate indices are wave-uniform int32
+  // (B * Q < 2^31 is checked by the launcher).
+  const int total = B * Q;
+  const int stride = static_cast<int>(gridDim.x) * kDfe1Waves;
+  int g = static_cast<int>(blockIdx.x) * kDfe1Waves + __builtin_amdgcn_readfirstlane(wave);
+  if (g >= total) return;
+  auto load_row = [&](int gg, float& dj, int& n) {
+    const int gc = gg < total ? gg : total - 1;
+    dj = dist[static_cast<int64_t>(gc) * 32 + r32];
+    n = idx[static_cast<int64_t>(gc) * 32 + r32];
+  };
+  struct Gathered {
+    float4 f[4];
+    T px, py, pz;
+    float cx, cy, cz;
+  };
+  auto gather = [&](int gg, int nraw, Gathered& G) {
+    const int gc = gg < total ? gg : total - 1;
+    const int bb = gc / Q;
+    const int n = nraw < 0 ? 0 : (nraw >= M ? M - 1 : nraw);
+    const float4* fr = reinterpret_cast<const float4*>(feat + (static_cast<int64_t>(bb) * M + n) * 32 + 16 * h);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) G.f[v] = fr[v];
+    G.px = ref.at(bb, 0, n);
+    G.py = ref.at(bb, 1, n);
+    G.pz = ref.at(bb, 2, n);
+    G.cx = cand[static_cast<int64_t>(gc) * 3];
+    G.cy = cand[static_cast<int64_t>(gc) * 3 + 1];
+    G.cz = cand[static_cast<int64_t>(gc) * 3 + 2];
+  };
+  // get_cat_feat_tgt.py:57-58 (lanes 32..63 mirror lanes 0..31): the w row of a candidate
+  auto weights = [&](float dj) {
     double dsum = static_cast<double>(dj);
 #pragma unroll
     for (int off = 16; off > 0; off >>= 1) dsum += __shfl_xor(dsum, off, kWave);
-    const double wj = static_cast<double>(dj) / dsum;
-    if (h == 0) L.w[wave][r32] = wj;
-    int n = idx[g * 32 + r32];
-    n = n < 0 ? 0 : (n >= M ? M - 1 : n);
-    const float* cq = cand + g * 3;
+    L.w[wave][r32] = static_cast<double>(dj) / dsum;  // both lane halves write the same value
+  };
+  auto embed = [&](int gg, const Gathered& G) {
     float x[kDfeKS];
-    if (h == 0) {
-      x[0] = static_cast<float>(ref.at(b, 0, n) - static_cast<T>(cq[0]));
-      x[1] = static_cast<float>(ref.at(b, 1, n) - static_cast<T>(cq[1]));
-      x[2] = static_cast<float>(ref.at(b, 2, n) - static_cast<T>(cq[2]));
-    } else {
-      x[0] = x[1] = x[2] = 0.0f;
-    }
-    const float4* fr = reinterpret_cast<const float4*>(feat + (static_cast<int64_t>(b) * M + n) * 32 + 16 * h);
-    float4 fv4[4];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) fv4[v] = fr[v];
-    // the wave's own w row: written above by lanes 0..31, read back as 16-byte broadcasts
+    // candidates_grouped_local = tgt_pts_picked - candidate (point dtype, then .float()); half 1: 0
+    x[0] = h == 0 ? static_cast<float>(G.px - static_cast<T>(G.cx)) : 0.0f;
+    x[1] = h == 0 ? static_cast<float>(G.py - static_cast<T>(G.cy)) : 0.0f;
+    x[2] = h == 0 ? static_cast<float>(G.pz - static_cast<T>(G.cz)) : 0.0f;
+    // the wave's own w row, read back as 16-byte broadcasts
     __builtin_amdgcn_wave_barrier();
     const double2* wr = reinterpret_cast<const double2*>(&L.w[wave][16 * h]);
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const float fv[4] = {fv4[v].x, fv4[v].y, fv4[v].z, fv4[v].w};
+      const float fv[4] = {G.f[v].x, G.f[v].y, G.f[v].z, G.f[v].w};
       const double2 wa = wr[2 * v], wb = wr[2 * v + 1];
       const double wf[4] = {wa.x, wa.y, wb.x, wb.y};
 #pragma unroll
@@ -250,8 +272,29 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
 #pragma unroll
     for (int r = 1; r < 16; ++r) m = fmaxf(m, a[r]);
     m = fmaxf(m, __shfl_xor(m, 32, kWave));
-    if (h == 0) out[g * 32 + r32] = m;
-    __builtin_amdgcn_wave_barrier();  // w row reused by the next candidate
+    if (h == 0) out[static_cast<int64_t>(gg) * 32 + r32] = m;
+    __builtin_amdgcn_wave_barrier();  // the w row is rewritten for the next candidate
+  };
+  float djA, djB;
+  int nA, nB;
+  Gathered GA, GB;
+  load_row(g, djA, nA);
+  load_row(g + stride, djB, nB);
+  gather(g, nA, GA);
+  for (;;) {
+    // slot A holds candidate g (gathered), slot B the row of g + stride
+    weights(djA);
+    load_row(g + 2 * stride, djA, nA);
+    gather(g + stride, nB, GB);
+    embed(g, GA);
+    g += stride;
+    if (g >= total) break;
+    weights(djB);
+    load_row(g + 2 * stride, djB, nB);
+    gather(g + stride, nA, GA);
+    embed(g, GB);
+    g += stride;
+    if (g >= total) break;
   }
 }
 
@@ -259,6 +302,10 @@ template <typename T>
 int launch_dfe_tgt_mfma(PointsView<T> ref, const float* feat, int M, const float* cand, const float* dist,
                         const int32_t* idx, int B, int Q, const float* params, float* out, hipStream_t st) {
   const int64_t total = static_cast<int64_t>(B) * Q;
+  if (total >= (int64_t(1) << 31) / 32) {
+    set_error("dvcp_dfe_tgt: B*Q=%lld too large", static_cast<long long>(total));
+    return DVCP_EINVAL;
+  }
   const int64_t need = (total + kDfeMfmaWaves - 1) / kDfeMfmaWaves;
   static const bool layerwise = [] {
     const char* e = getenv("DVCP_DFE_LAYERWISE");
