@@ -63,6 +63,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--hw-queues", type=int, default=16, help="GPU_MAX_HW_QUEUES for this process (<= 32)")
     p.add_argument("--stage-report", action="store_true", help="print the per-kernel table to stderr")
+    p.add_argument("--no-kernel-events", action="store_true",
+                   help="diagnostic: no per-launch HIP events in the timed region (no roofline/stages)")
     return p.parse_args()
 
 
@@ -123,10 +125,11 @@ def main():
     if world > 1:
         dist.barrier()
 
-    _lib.EVENT_LOG = []
+    _lib.EVENT_LOG = None if args.no_kernel_events else []
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     outs = [step(i % P) for i in range(args.steps)]
+    t_issue = time.perf_counter() - t0  # host time to issue every step (no sync inside)
     cur = torch.cuda.current_stream(dev)
     for ln in lanes:
         cur.wait_stream(ln)
@@ -137,7 +140,7 @@ def main():
         res = torch.cat(gathered)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    log, _lib.EVENT_LOG = _lib.EVENT_LOG, None
+    log, _lib.EVENT_LOG = _lib.EVENT_LOG or [], None
     if world > 1:
         dist.barrier()
         tmax = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -154,6 +157,8 @@ def main():
             acc = work.setdefault(name, [0.0, 0.0])
             acc[0] += w[0]
             acc[1] += w[1]
+    if not per:  # --no-kernel-events
+        per = {"(no kernel events)": [float("nan")]}
     tot = {k: sum(v) for k, v in per.items()}
     dom = max(tot, key=tot.get)
     n_launch = len(per[dom])
@@ -192,6 +197,7 @@ def main():
                    "candidates": C, "fe_npoint": S, "parallelism": f"pairs sharded x{world}, all_gather(R,t)",
                    "inflight_batches": P, "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
         "latency_ms_single_batch": round(latency_ms, 3),
+        "host_issue_ms_per_step": round(t_issue / args.steps * 1e3, 3),
         "roofline": roofline,
         "stages": stages,
     }
