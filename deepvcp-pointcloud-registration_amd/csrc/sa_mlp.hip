@@ -126,7 +126,8 @@ __global__ __launch_bounds__(kSaThreads) void sa_mlp_kernel(PointsView<T> pts, P
 template <typename T, int D, int C1, int C2>
 int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, const void* c, int64_t cb, int64_t cc,
                    int64_t cn, int S, int B, const float* feat, int64_t fb, int64_t fn, const int32_t* count,
-                   const int32_t* list, int nsample, const float* params, float* U, float* out, hipStream_t st);
+                   const int32_t* list, int nsample, const float* params, float* U, int32_t* order, float* out,
+                   hipStream_t st);
 
 template <typename T, typename FT, int D, int C1, int C2, int C3>
 static int launch_sa(const void* xyz, int64_t sb, int64_t sc, int64_t sn, const void* c, int64_t cb, int64_t cc,
@@ -154,12 +155,19 @@ static bool dvcp_sa_force_valu() {
   return v;
 }
 
-// Workspace of the decomposed two-layer MFMA path: U = W1f f + b1 per input point, B x N x C1 fp32.
-static int64_t sa_ws_bytes(int B, int N, int nlayer, const int* chans) {
-  if (nlayer != 2 || !chans) return 0;
+// Workspace of the two-layer MFMA path: U = W1f f + b1 per input point (B x N x C1 fp32), then
+// the centres' curve order (B x S int32).
+static bool sa_mfma_table(int nlayer, const int* chans) {
+  if (nlayer != 2 || !chans) return false;
   const int D = chans[0] - 3;
-  const bool mfma_table = (D == 32 && chans[1] == 32 && chans[2] == 64) || (D == 64 && chans[1] == 64 && chans[2] == 64);
-  return mfma_table ? static_cast<int64_t>(B) * N * chans[1] * 4 : 0;
+  return (D == 32 && chans[1] == 32 && chans[2] == 64) || (D == 64 && chans[1] == 64 && chans[2] == 64);
+}
+static int64_t sa_u_bytes(int B, int N, const int* chans) {
+  return (static_cast<int64_t>(B) * N * chans[1] * 4 + 255) & ~int64_t(255);
+}
+static int64_t sa_ws_bytes(int B, int N, int S, int nlayer, const int* chans) {
+  if (!sa_mfma_table(nlayer, chans)) return 0;
+  return sa_u_bytes(B, N, chans) + static_cast<int64_t>(B) * S * 4;
 }
 
 static int sa_group_mlp_impl(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, const void* ctr,
@@ -177,6 +185,8 @@ static int sa_group_mlp_impl(int dtype, const void* xyz, int64_t sb, int64_t sc,
   DVCP_REQUIRE(dtype == DVCP_F32 || f64, "dvcp_sa_group_mlp: bad dtype %d", dtype);
   DVCP_REQUIRE(feat_dtype == DVCP_F32 || feat_dtype == DVCP_F64, "dvcp_sa_group_mlp: bad feat dtype");
   const bool ff64 = feat_dtype == DVCP_F64;
+  float* U = ws ? static_cast<float*>(ws) : nullptr;
+  int32_t* order = ws ? reinterpret_cast<int32_t*>(static_cast<char*>(ws) + sa_u_bytes(B, N, chans)) : nullptr;
 #define DVCP_SA(TT, FF, DD, A, Bc, Cc)                                                                     \
   return dvcp::launch_sa<TT, FF, DD, A, Bc, Cc>(xyz, sb, sc, sn, ctr, cb, cc, cn, S, B, feat, fb, fd, fn, \
                                                 count, list, nsample, params, out, st)
@@ -200,10 +210,10 @@ static int sa_group_mlp_impl(int dtype, const void* xyz, int64_t sb, int64_t sc,
 #define DVCP_SA_M(DD, A, Bc)                                                                                     \
   return f64 ? dvcp::launch_sa_mfma<double, DD, A, Bc>(xyz, sb, sc, sn, N, ctr, cb, cc, cn, S, B,               \
                                                      static_cast<const float*>(feat), fb, fn, count, list,      \
-                                                     nsample, params, static_cast<float*>(ws), out, st)         \
+                                                     nsample, params, U, order, out, st)                        \
              : dvcp::launch_sa_mfma<float, DD, A, Bc>(xyz, sb, sc, sn, N, ctr, cb, cc, cn, S, B,                \
                                                     static_cast<const float*>(feat), fb, fn, count, list, nsample, \
-                                                    params, static_cast<float*>(ws), out, st)
+                                                    params, U, order, out, st)
   if (nlayer == 2 && D == 32 && chans[1] == 32 && chans[2] == 64) {
     if (mfma_ok) DVCP_SA_M(32, 32, 64);
     DVCP_SA_T(32, 32, 64, 0);
@@ -228,8 +238,8 @@ extern "C" int dvcp_sa_group_mlp(int dtype, const void* xyz, int64_t sb, int64_t
                            list, nsample, nlayer, chans, params, out, nullptr, stream);
 }
 
-extern "C" int64_t dvcp_sa_group_mlp_workspace_bytes(int B, int N, int nlayer, const int* chans) {
-  return sa_ws_bytes(B, N, nlayer, chans);
+extern "C" int64_t dvcp_sa_group_mlp_workspace_bytes(int B, int N, int S, int nlayer, const int* chans) {
+  return sa_ws_bytes(B, N, S, nlayer, chans);
 }
 
 extern "C" int dvcp_sa_group_mlp_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
@@ -238,9 +248,9 @@ extern "C" int dvcp_sa_group_mlp_ws(int dtype, const void* xyz, int64_t sb, int6
                                     const int32_t* count, const int32_t* list, int nsample, int nlayer,
                                     const int* chans, const float* params, float* out, void* workspace,
                                     void* stream) {
-  DVCP_REQUIRE(sa_ws_bytes(B, N, nlayer, chans) == 0 || workspace, "dvcp_sa_group_mlp_ws: workspace is NULL");
+  DVCP_REQUIRE(sa_ws_bytes(B, N, S, nlayer, chans) == 0 || workspace, "dvcp_sa_group_mlp_ws: workspace is NULL");
   DVCP_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "dvcp_sa_group_mlp_ws: workspace not 16-B aligned");
   return sa_group_mlp_impl(dtype, xyz, sb, sc, sn, N, ctr, cb, cc, cn, S, B, feat_dtype, feat, fb, fd, fn, D, count,
                            list, nsample, nlayer, chans, params, out,
-                           sa_ws_bytes(B, N, nlayer, chans) ? workspace : nullptr, stream);
+                           sa_ws_bytes(B, N, S, nlayer, chans) ? workspace : nullptr, stream);
 }

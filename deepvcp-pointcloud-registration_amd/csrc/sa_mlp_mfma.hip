@@ -20,6 +20,7 @@
 // The MFMA is a k-ordered fp32 fma chain (exact fp32 products and sums), so the result differs
 // from the row-per-thread kernel only in summation order.
 #include "common.h"
+#include "morton.h"
 
 namespace dvcp {
 
@@ -102,11 +103,30 @@ __global__ __launch_bounds__(256) void sa_pre_kernel(const float* __restrict__ f
   }
 }
 
+// Centres of each cloud in 12-bit Hilbert-cell order (one workgroup per cloud), for the MFMA
+// kernel's visiting order.  The order changes only which wave computes which centre.
+template <typename T>
+__global__ __launch_bounds__(kBuildThreads) void sa_order_kernel(PointsView<T> ctr, int S, int32_t* __restrict__ order) {
+  __shared__ uint32_t bins[kSortBins];
+  __shared__ uint32_t wsum[16];
+  __shared__ float red[2][3][16];
+  const int b = blockIdx.x;
+  auto get = [&](int i, float (&v)[3]) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) v[a] = static_cast<float>(ctr.at(b, a, i));
+  };
+  float lo[3], hi[3];
+  block_bbox(S, get, lo, hi, red);
+  int32_t* o = order + static_cast<int64_t>(b) * S;
+  morton_sort(S, get, [&](int pos, int i, const float (&)[3]) { o[pos] = i; }, lo, hi, bins, wsum);
+}
+
 template <typename T, int D, int C1, int C2, bool PRE>
 __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
     PointsView<T> pts, PointsView<T> ctr, int S, int B, const float* __restrict__ feat, int64_t fb, int64_t fn,
     const int32_t* __restrict__ count, const int32_t* __restrict__ list, int nsample,
-    const float* __restrict__ params, const float* __restrict__ U, int64_t ub, float* __restrict__ out) {
+    const float* __restrict__ params, const float* __restrict__ U, int64_t ub, const int32_t* __restrict__ order,
+    float* __restrict__ out) {
   using Sh = SaMfmaShape<D, C1, C2>;
   constexpr int C0 = Sh::C0, KS = Sh::KS, MT = Sh::MT, CT = Sh::CT;
   __shared__ SaMfmaLds<D, C1, C2> L;
@@ -157,10 +177,14 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
   const int64_t total = static_cast<int64_t>(B) * S;
   for (int64_t q = static_cast<int64_t>(blockIdx.x) * kMfmaWaves + wave; q < total;
        q += static_cast<int64_t>(gridDim.x) * kMfmaWaves) {
-    const int b = static_cast<int>(q / S), c = static_cast<int>(q % S);
-    int rows = count[q];
+    // centre in curve order when `order` is given: consecutive waves then gather the U / point
+    // rows of one spatial neighbourhood, which stay in L2 instead of being fetched again
+    const int b = static_cast<int>(q / S);
+    const int c = order ? order[q] : static_cast<int>(q % S);
+    const int64_t fc = static_cast<int64_t>(b) * S + c;
+    int rows = count[fc];
     rows = rows < 1 ? 1 : (rows > nsample ? nsample : rows);
-    const int32_t* lst = list + q * nsample;
+    const int32_t* lst = list + fc * nsample;
     const T cx = ctr.at(b, 0, c), cy = ctr.at(b, 1, c), cz = ctr.at(b, 2, c);
     float mx[CT];
 #pragma unroll
@@ -261,7 +285,7 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const float m = fmaxf(mx[ct], __shfl_xor(mx[ct], 32, kWave));
-      if (h == 0) out[q * C2 + 32 * ct + r32] = m;
+      if (h == 0) out[fc * C2 + 32 * ct + r32] = m;
     }
   }
 }
@@ -269,20 +293,23 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
 template <typename T, int D, int C1, int C2>
 int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, const void* c, int64_t cb, int64_t cc,
                    int64_t cn, int S, int B, const float* feat, int64_t fb, int64_t fn, const int32_t* count,
-                   const int32_t* list, int nsample, const float* params, float* U, float* out, hipStream_t st) {
+                   const int32_t* list, int nsample, const float* params, float* U, int32_t* order, float* out,
+                   hipStream_t st) {
   PointsView<T> pv{static_cast<const T*>(xyz), sb, sc, sn};
   PointsView<T> cv{static_cast<const T*>(c), cb, cc, cn};
   const int64_t centres = static_cast<int64_t>(B) * S;
   const int grid = static_cast<int>(centres < 4096 * kMfmaWaves ? (centres + kMfmaWaves - 1) / kMfmaWaves : 4096);
+  if (order)
+    hipLaunchKernelGGL((sa_order_kernel<T>), dim3(B), dim3(kBuildThreads), 0, st, cv, S, order);
   if (U) {
     const int64_t rows = static_cast<int64_t>(B) * N;
     hipLaunchKernelGGL((sa_pre_kernel<D, C1>), dim3(ceil_div(rows, 256)), dim3(256), 0, st, feat, fb, fn, N, B, params,
                        U);
     hipLaunchKernelGGL((sa_mlp_mfma_kernel<T, D, C1, C2, true>), dim3(grid), dim3(kMfmaWaves * kWave), 0, st, pv, cv,
-                       S, B, feat, fb, fn, count, list, nsample, params, U, static_cast<int64_t>(N) * C1, out);
+                       S, B, feat, fb, fn, count, list, nsample, params, U, static_cast<int64_t>(N) * C1, order, out);
   } else {
     hipLaunchKernelGGL((sa_mlp_mfma_kernel<T, D, C1, C2, false>), dim3(grid), dim3(kMfmaWaves * kWave), 0, st, pv,
-                       cv, S, B, feat, fb, fn, count, list, nsample, params, nullptr, 0, out);
+                       cv, S, B, feat, fb, fn, count, list, nsample, params, nullptr, 0, order, out);
   }
   return launch_status("dvcp_sa_group_mlp(mfma)");
 }
@@ -290,8 +317,8 @@ int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, c
 #define DVCP_SA_MFMA_INST(T, D, C1, C2)                                                                          \
   template int launch_sa_mfma<T, D, C1, C2>(const void*, int64_t, int64_t, int64_t, int, const void*, int64_t,  \
                                             int64_t, int64_t, int, int, const float*, int64_t, int64_t,         \
-                                            const int32_t*, const int32_t*, int, const float*, float*, float*,  \
-                                            hipStream_t);
+                                            const int32_t*, const int32_t*, int, const float*, float*,          \
+                                            int32_t*, float*, hipStream_t);
 DVCP_SA_MFMA_INST(float, 32, 32, 64)
 DVCP_SA_MFMA_INST(double, 32, 32, 64)
 DVCP_SA_MFMA_INST(float, 64, 64, 64)

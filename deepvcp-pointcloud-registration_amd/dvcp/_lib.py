@@ -69,7 +69,8 @@ def load():
     lib.dvcp_ball_query_workspace_bytes.restype = ctypes.c_int64
     lib.dvcp_ball_query_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
     lib.dvcp_sa_group_mlp_workspace_bytes.restype = ctypes.c_int64
-    lib.dvcp_sa_group_mlp_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    lib.dvcp_sa_group_mlp_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                      ctypes.c_void_p]
     for name, args in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = ctypes.c_int

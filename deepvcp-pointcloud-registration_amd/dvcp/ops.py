@@ -92,8 +92,8 @@ def sa_group_mlp(xyz, ctr, feat, count, lst, nsample, chans, params, xyz_pdim=2,
     ch = torch.tensor(list(chans), dtype=torch.int32)  # host array, read by the launcher only
     out = torch.empty(B, S, chans[-1], dtype=torch.float32, device=xyz.device)
     macs = sum(a * b for a, b in zip(chans[:-1], chans[1:]))
-    # two-layer MFMA tables take a B x N x C1 workspace for the per-point half of layer 1
-    ws_bytes = _lib.load().dvcp_sa_group_mlp_workspace_bytes(B, N, len(chans) - 1, ch.data_ptr())
+    # two-layer MFMA tables take a workspace: the per-point half of layer 1 and the centre order
+    ws_bytes = _lib.load().dvcp_sa_group_mlp_workspace_bytes(B, N, S, len(chans) - 1, ch.data_ptr())
     ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=xyz.device) if ws_bytes else None
     call("dvcp_sa_group_mlp_ws", dtype_code(xyz), ptr(xyz), sb, sc, sn, N, ptr(ctr), cb, cc, cn, S, B, fdt,
          ptr(feat), fb, fd, fn, D, ptr(count), ptr(lst), int(nsample), len(chans) - 1, ptr(ch), ptr(params), ptr(out),

@@ -99,12 +99,14 @@ int dvcp_sa_group_mlp(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_
                       int nlayer, const int* chans, const float* params, float* out,
                       void* stream);
 
-/* dvcp_sa_group_mlp with a device workspace of dvcp_sa_group_mlp_workspace_bytes(B, N, nlayer,
- * chans) bytes (16-B aligned; 0 bytes = none needed, NULL allowed).  N = points of xyz/feat.
- * For the two-layer fp32 tables (sa2 35-32-64, sa3 67-64-64) layer 1 is split into its
- * per-point part U = W1[:, 3:] f + b1, evaluated once per input point into the workspace,
- * and the per-(centre, point) part W1[:, :3] (p - c); same results up to fp32 summation order. */
-int64_t dvcp_sa_group_mlp_workspace_bytes(int B, int N, int nlayer, const int* chans);
+/* dvcp_sa_group_mlp with a device workspace of dvcp_sa_group_mlp_workspace_bytes(B, N, S,
+ * nlayer, chans) bytes (16-B aligned; 0 bytes = none needed, NULL allowed).  N = points of
+ * xyz/feat, S = centres.  For the two-layer fp32 tables (sa2 35-32-64, sa3 67-64-64) layer 1 is
+ * split into its per-point part U = W1[:, 3:] f + b1, evaluated once per input point into the
+ * workspace, and the per-(centre, point) part W1[:, :3] (p - c); same results up to fp32
+ * summation order.  Centres are visited in Hilbert-curve order (also kept in the workspace) so
+ * the gathered rows of concurrently running waves stay in L2; the order does not change results. */
+int64_t dvcp_sa_group_mlp_workspace_bytes(int B, int N, int S, int nlayer, const int* chans);
 int dvcp_sa_group_mlp_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
                          const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
                          int feat_dtype, const void* feat, int64_t fb, int64_t fd, int64_t fn, int D,
