@@ -87,6 +87,8 @@ __global__ __launch_bounds__(256) void sa_pre_kernel(const float* __restrict__ f
   }
   const float* W1 = params;
   const float* pb1 = W1 + C1 * C0;
+  const float* ps1 = pb1 + C1;
+  const float* pt1 = ps1 + C1;
   float4* dst = reinterpret_cast<float4*>(U + i * C1);
 #pragma unroll 4
   for (int c4 = 0; c4 < C1 / 4; ++c4) {
@@ -94,9 +96,11 @@ __global__ __launch_bounds__(256) void sa_pre_kernel(const float* __restrict__ f
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int c = 4 * c4 + e;
-      float acc = pb1[c];
+      // BN folded in: (W x + b) s + t = (s W) x + (s b + t)
+      const float sc = ps1[c];
+      float acc = static_cast<float>(static_cast<double>(pb1[c]) * sc + static_cast<double>(pt1[c]));
 #pragma unroll
-      for (int k = 0; k < D; ++k) acc = __fmaf_rn(W1[c * C0 + 3 + k], f[k], acc);
+      for (int k = 0; k < D; ++k) acc = __fmaf_rn(W1[c * C0 + 3 + k] * sc, f[k], acc);
       o[e] = acc;
     }
     dst[c4] = make_float4(o[0], o[1], o[2], o[3]);
@@ -150,12 +154,12 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
     for (int i = tid; i < MT * 2 * 64; i += blockDim.x) {
       const int l = i % 64, s = (i / 64) % 2, mt = i / 128;
       const int ch = s == 0 ? (l >> 5) : ((l >> 5) == 0 ? 2 : -1);
-      L.wx[mt][s][l] = ch < 0 ? 0.0f : W1[(32 * mt + (l & 31)) * C0 + ch];
+      L.wx[mt][s][l] = ch < 0 ? 0.0f : W1[(32 * mt + (l & 31)) * C0 + ch] * ps1[32 * mt + (l & 31)];
     }
   for (int i = tid; i < CT * Sh::K2 * 64; i += blockDim.x) {
     const int l = i % 64, kk = (i / 64) % Sh::K2, ct = i / (64 * Sh::K2);
     const int mt = kk / 16, r = kk % 16;
-    L.w2[ct][kk][l] = W2[(32 * ct + (l & 31)) * C1 + 32 * mt + acc_row(r, l >> 5)];
+    L.w2[ct][kk][l] = W2[(32 * ct + (l & 31)) * C1 + 32 * mt + acc_row(r, l >> 5)] * (PRE ? ps2[32 * ct + (l & 31)] : 1.0f);
   }
   for (int i = tid; i < MT * 32; i += blockDim.x) {
     const int r = i % 16, hh = (i / 16) % 2, mt = i / 32;
@@ -170,6 +174,8 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
     b2[ct] = pb2[32 * ct + r32];
     s2[ct] = ps2[32 * ct + r32];
     t2[ct] = pt2[32 * ct + r32];
+    // PRE: BN2 folded into W2 (above) and the bias: (W h + b) s + t = (s W) h + (s b + t)
+    if (PRE) b2[ct] = static_cast<float>(static_cast<double>(b2[ct]) * s2[ct] + static_cast<double>(t2[ct]));
   }
   __syncthreads();
 
@@ -251,12 +257,12 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
           for (int mt = 0; mt < MT; ++mt)
             acc1[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(L.w1[mt][s][lane + zo], x[s], acc1[mt], 0, 0, 0);
       }
-      // BN (eval) + ReLU in place
+      // BN (eval) + ReLU in place (PRE: BN already folded into U and W1x)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float v = acc1[mt][r] * L.s1[mt][h][r + zo] + L.t1[mt][h][r + zo];
+          const float v = PRE ? acc1[mt][r] : acc1[mt][r] * L.s1[mt][h][r + zo] + L.t1[mt][h][r + zo];
           acc1[mt][r] = v > 0.0f ? v : 0.0f;
         }
       // layer 2: A operand = the layer-1 registers, B = W2^T fragments
@@ -272,13 +278,18 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
 #pragma unroll
           for (int ct = 0; ct < CT; ++ct)
             acc2[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(acc1[mt][r], L.w2[ct][mt * 16 + r][lane + zo], acc2[ct], 0, 0, 0);
-      // BN + ReLU, then max over this tile's points (registers)
+      // BN + ReLU, then max over this tile's points (registers).  PRE: BN is folded, and
+      // max_i relu(v_i) = relu(max_i v_i), so the ReLU is the +0 the running max starts from.
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float v = acc2[ct][r] * s2[ct] + t2[ct];
-          mx[ct] = fmaxf(mx[ct], v > 0.0f ? v : 0.0f);
+          if (PRE) {
+            mx[ct] = fmaxf(mx[ct], acc2[ct][r]);
+          } else {
+            const float v = acc2[ct][r] * s2[ct] + t2[ct];
+            mx[ct] = fmaxf(mx[ct], v > 0.0f ? v : 0.0f);
+          }
         }
     }
     // the two lane halves hold different points of the same channel
