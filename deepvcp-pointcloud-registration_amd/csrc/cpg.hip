@@ -30,6 +30,25 @@ constexpr int kCpgBigF = 16 * kCpgPV;  // quarter volume + conv1 weights, later 
 constexpr int kCpgE = (32 * kCpgMaxC + kCpgThreads - 1) / kCpgThreads;  // target values per thread
 static_assert(kCpgVolF + kCpgW1F <= kCpgBigF, "quarter volume + conv1 weights must fit the area");
 
+// x / d for 0 <= x < 2^16 and 1 <= d <= 2^11 as one mul_hi: m = ceil(2^32 / d) overestimates
+// 1/d by less than 2^-32, so x*m/2^32 exceeds x/d by less than 2^-16, while the fractional part
+// of x/d is at most 1 - 1/d <= 1 - 2^-11: the floor is exact.  (Index math of an 11^3 grid: the
+// generic 32-bit division costs ~25 VALU instructions and dominated this kernel's VALU count.)
+struct FastDiv {
+  uint32_t m, d;
+  __device__ __forceinline__ explicit FastDiv(uint32_t dd)
+      : m(static_cast<uint32_t>((0x100000000ull + dd - 1) / dd)), d(dd) {}
+  __device__ __forceinline__ uint32_t div(uint32_t x) const { return __umulhi(x, m); }
+  __device__ __forceinline__ uint32_t mod(uint32_t x) const { return x - div(x) * d; }
+};
+
+// haloed cell of voxel g = (gz*G + gy)*G + gx in the (G+2)^3 volume
+__device__ __forceinline__ int cpg_halo(int g, const FastDiv& dG, const FastDiv& dGG, int PG, int PGG) {
+  const uint32_t z = dGG.div(g), r = g - z * dGG.d;
+  const uint32_t y = dG.div(r), x = r - y * dG.d;
+  return static_cast<int>((z + 1) * PGG + (y + 1) * PG + (x + 1));
+}
+
 __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restrict__ src, const float* __restrict__ tgt,
                                                           int64_t t_p, int64_t t_f, int64_t t_c,
                                                           const float* __restrict__ cand, int G,
@@ -49,6 +68,7 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
   const int p = blockIdx.x, tid = threadIdx.x;
   const int C = G * G * G, GG = G * G;
   const int PG = G + 2, PGG = PG * PG, PV = PG * PGG;
+  const FastDiv dG(G), dGG(GG);
   const float* P1 = params;
   const float* P2 = P1 + 16 * 32 * 27 + 16;
   const float* P3 = P2 + 4 * 16 * 27 + 4;
@@ -94,7 +114,7 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
 #pragma unroll
   for (int i = 0; i < kTW; ++i) {
     const int g = 16 * (wave + kW * i) + l16;
-    vx[i] = g < C ? ((g / GG) + 1) * PGG + ((g / G) % G + 1) * PG + (g % G + 1) : 0;
+    vx[i] = g < C ? cpg_halo(g, dG, dGG, PG, PGG) : 0;
   }
   f32x4 acc[kTW];
 #pragma unroll
@@ -110,15 +130,18 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
     // compiler from hoisting 84 addresses per thread out of the quarter loop into registers.)
     int zo = 0;
     asm volatile("" : "+v"(zo));
+    // element e = u*512 + tid of the block is (c = e / 32, f = e % 32): f is fixed per thread
+    // (512 % 32 == 0) and c advances by 16 per u, so l = f*C + c advances by 16 as well.
+    const int f0 = tid & 31;
+    const int l0 = f0 * C + (tid >> 5) + zo;
 #pragma unroll
     for (int u = 0; u < kCpgE; ++u) {
-      const int e = u * kCpgThreads + tid + zo;
-      const int c = e / 32, f = e % 32;
-      const int l = f * C + c;
+      const int e = u * kCpgThreads + tid;
+      const int l = l0 + 16 * u;
       const int g = l >> 5, fp = l & 31;
       if (e < 32 * C && (fp >> 3) == q) {
         const float d = sv[fp] - tv[u];
-        vol[(fp & 7) * PV + ((g / GG) + 1) * PGG + ((g / G) % G + 1) * PG + (g % G + 1)] = d * d;
+        vol[(fp & 7) * PV + cpg_halo(g, dG, dGG, PG, PGG)] = d * d;
       }
     }
     __syncthreads();
@@ -148,8 +171,7 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int g = 16 * t + 4 * kg + r;
-      if (t < NT && g < C)
-        out1[l16 * PV + ((g / GG) + 1) * PGG + ((g / G) % G + 1) * PG + (g % G + 1)] = acc[i][r] + bias[l16];
+      if (t < NT && g < C) out1[l16 * PV + cpg_halo(g, dG, dGG, PG, PGG)] = acc[i][r] + bias[l16];
     }
   }
   __syncthreads();
@@ -180,8 +202,7 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int g = 16 * t + 4 * kg + r;
-      if (t < NT && g < C && l16 < 4)
-        out2[l16 * PV + ((g / GG) + 1) * PGG + ((g / G) % G + 1) * PG + (g % G + 1)] = acc[i][r] + bias[16 + l16];
+      if (t < NT && g < C && l16 < 4) out2[l16 * PV + cpg_halo(g, dG, dGG, PG, PGG)] = acc[i][r] + bias[16 + l16];
     }
   }
   __syncthreads();
@@ -192,7 +213,7 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
 #pragma unroll
   for (int v = 0; v < kCpgV; ++v) {
     const int g = gv[v] < C ? gv[v] : 0;
-    const int hv = ((g / GG) + 1) * PGG + ((g / G) % G + 1) * PG + (g % G + 1);
+    const int hv = cpg_halo(g, dG, dGG, PG, PGG);
     float a = 0.f;
 #pragma unroll
     for (int ci = 0; ci < 4; ++ci)
