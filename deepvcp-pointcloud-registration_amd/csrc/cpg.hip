@@ -5,7 +5,7 @@
 //   Conv3d 32->16 -> 16->4 -> 4->1 (k3, p1, cross-correlation, no activations);
 //   softmax over the C = G^3 logits; vcp = sum(w * cand) / sum(w).
 //
-// Plan (G <= 11, C <= 1331), one 512-thread workgroup per key point: the key point's (C, 32)
+// Plan (G <= 11, C <= 1331), one 1024-thread workgroup per key point: the key point's (C, 32)
 // target block is loaded once into registers; the cost volume is built in LDS one 8-channel
 // quarter at a time with a zero halo (13^3 cells, 70 KB) next to conv1's weights ([ci][tap][co],
 // 55 KB); conv1 runs on the matrix cores (see below), accumulating the quarters in registers;
@@ -18,7 +18,7 @@ namespace dvcp {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kCpgThreads = 512;  // 8 waves: two per SIMD (LDS allows one workgroup per CU)
+constexpr int kCpgThreads = 1024;  // 16 waves: four per SIMD (LDS allows one workgroup per CU)
 constexpr int kCpgMaxC = 1331;
 constexpr int kCpgMaxG = 11;
 constexpr int kCpgV = (kCpgMaxC + kCpgThreads - 1) / kCpgThreads;  // voxels per thread (conv2/3)
@@ -130,14 +130,14 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
     // compiler from hoisting 84 addresses per thread out of the quarter loop into registers.)
     int zo = 0;
     asm volatile("" : "+v"(zo));
-    // element e = u*512 + tid of the block is (c = e / 32, f = e % 32): f is fixed per thread
-    // (512 % 32 == 0) and c advances by 16 per u, so l = f*C + c advances by 16 as well.
+    // element e = u*kCpgThreads + tid of the block is (c = e / 32, f = e % 32): f is fixed per
+    // thread (kCpgThreads % 32 == 0) and c advances by kCpgThreads / 32 per u, and so does l = f*C + c.
     const int f0 = tid & 31;
     const int l0 = f0 * C + (tid >> 5) + zo;
 #pragma unroll
     for (int u = 0; u < kCpgE; ++u) {
       const int e = u * kCpgThreads + tid;
-      const int l = l0 + 16 * u;
+      const int l = l0 + (kCpgThreads / 32) * u;
       const int g = l >> 5, fp = l & 31;
       if (e < 32 * C && (fp >> 3) == q) {
         const float d = sv[fp] - tv[u];
