@@ -108,7 +108,8 @@ def main():
         with torch.no_grad(), torch.cuda.stream(lanes[lane]):
             kp, vcp = model(b_src, b_tgt, b_R, t_init)
             loss, Rp, tp = dvcp.deepVCP_loss(kp, vcp, b_R, b_t, 0.5)
-        return Rp, tp, loss
+            rot, trans = dvcp.registration_errors(Rp, tp, b_R, b_t)  # train.py:112-120 harness
+        return Rp, tp, rot, trans
 
     # warmup, and the single-batch latency (strictly serial steps on one stream)
     for _ in range(args.warmup):
@@ -133,7 +134,9 @@ def main():
     cur = torch.cuda.current_stream(dev)
     for ln in lanes:
         cur.wait_stream(ln)
-    res = torch.cat([torch.cat([o[0].reshape(B, 9), o[1].reshape(B, 3)], 1) for o in outs])  # (steps*B, 12)
+    # per pair: R (9), t (3), rotation error (deg), translation error -> (steps*B, 14)
+    res = torch.cat([torch.cat([o[0].reshape(B, 9), o[1].reshape(B, 3), o[2].reshape(B, 1), o[3].reshape(B, 1)], 1)
+                     for o in outs])
     if world > 1:
         gathered = [torch.empty_like(res) for _ in range(world)]
         dist.all_gather(gathered, res)
@@ -185,6 +188,11 @@ def main():
                   "tflops": round(work.get(k, [0, 0])[0] / (sum(v) * 1e-3) / 1e12, 3) if k in work else None}
               for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1]))}
 
+    res_cpu = res.cpu()
+    reg_err = {"rot_deg_mean": float(res_cpu[:, 12].mean()), "rot_deg_max": float(res_cpu[:, 12].max()),
+               "trans_mean": float(res_cpu[:, 13].mean()), "trans_max": float(res_cpu[:, 13].max()),
+               "pairs": int(res_cpu.shape[0]),
+               "note": "vs ground truth (train.py:112-120 metric), random-init weights, R_init = R_gt as train.py:105 passes it"}
     pairs = B * world * args.steps
     value = pairs / elapsed
     out = {
@@ -198,6 +206,7 @@ def main():
                    "inflight_batches": P, "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
         "latency_ms_single_batch": round(latency_ms, 3),
         "host_issue_ms_per_step": round(t_issue / args.steps * 1e3, 3),
+        "registration_error_vs_gt": reg_err,
         "roofline": roofline,
         "stages": stages,
     }
@@ -245,7 +254,11 @@ def cpu_baseline(model, src, tgt, R_gt, t_gt, dev):
     base = {"value": round(1.0 / secs, 5), "unit": "pairs/s", "cores": threads, "kind": "port",
             "sample": f"1 C3 pair (N=16384, K=64, r=2.0), oracle/ref_r.py torch CPU ops, {secs:.1f} s",
             "cpu_model": cpu_model, "os_cpu_count": os.cpu_count()}
+    rot_vs_ref, trans_vs_ref = dvcp.registration_errors(Rg, tg, Ro.to(dev), to.to(dev))
     parity = {"R_maxabs_vs_ref": float((Rg.cpu() - Ro).abs().max()), "t_maxabs_vs_ref": float((tg.cpu() - to).abs().max()),
+              "rot_err_deg_vs_ref": float(rot_vs_ref.max()), "trans_err_vs_ref": float(trans_vs_ref.max()),
+              "rot_trans_err_note": "train.py:112-120 metric between the GPU pose and the oracle pose; "
+                                    "PairwiseDistance's eps contributes sqrt(3)*1e-6 at exact agreement",
               "vcp_maxabs_vs_ref": float((vcp.cpu() - vcpo).abs().max()),
               "keypts_equal": bool(torch.equal(kp.cpu(), kpo)),
               "keypts_same_set": bool(torch.equal(torch.sort(kp.cpu().reshape(-1, 3), 0).values,

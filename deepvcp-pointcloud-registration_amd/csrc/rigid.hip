@@ -213,7 +213,59 @@ __global__ __launch_bounds__(kRgThreads) void svd_opt_kernel(const double* __res
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Registration error of the training harness (train.py:112-120, with C8 fixed as REF-R does):
+//   rot_err   = || euler_xyz_deg(R_pred) - euler_xyz_deg(R_gt) + 1e-6 ||_2
+//   trans_err = || t_pred - t_gt + 1e-6 ||_2          (nn.PairwiseDistance(p=2), eps 1e-6)
+// scipy's Rotation.from_matrix(M).as_euler('xyz', degrees=True) is the extrinsic x-y-z angle
+// triple (a, b, c) of M = Rz(c) Ry(b) Rx(a): a = atan2(M21, M22), b = atan2(-M20, hypot(M21, M22)),
+// c = atan2(M10, M00), which agrees with scipy's quaternion route to ~1e-14 deg away from gimbal
+// lock (|b| -> 90 deg, where scipy warns and zeroes the third angle).  scipy raises for a matrix
+// with det <= 0 (a Kabsch reflection, Q13); the error is NaN there.
+__device__ __forceinline__ bool euler_xyz_deg(const double* M, double (&e)[3]) {
+  const double det = M[0] * (M[4] * M[8] - M[5] * M[7]) - M[1] * (M[3] * M[8] - M[5] * M[6]) +
+                     M[2] * (M[3] * M[7] - M[4] * M[6]);
+  constexpr double k = 57.29577951308232;  // 180 / pi
+  e[0] = atan2(M[7], M[8]) * k;
+  e[1] = atan2(-M[6], sqrt(M[7] * M[7] + M[8] * M[8])) * k;
+  e[2] = atan2(M[3], M[0]) * k;
+  return det > 0.0;
+}
+
+__global__ void registration_error_kernel(const double* __restrict__ Rp, const double* __restrict__ tp,
+                                          const double* __restrict__ Rg, const double* __restrict__ tg, int B,
+                                          int64_t rg_b, int64_t tg_b, double* __restrict__ rot,
+                                          double* __restrict__ trans) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  double ep[3], eg[3];
+  const bool okp = euler_xyz_deg(Rp + b * 9, ep);
+  const bool okg = euler_xyz_deg(Rg + b * rg_b, eg);
+  const bool ok = okp && okg;
+  double sr = 0.0, st = 0.0;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const double dr = (ep[a] - eg[a]) + 1e-6;
+    const double dt = (tp[b * 3 + a] - tg[b * tg_b + a]) + 1e-6;
+    sr += dr * dr;
+    st += dt * dt;
+  }
+  rot[b] = ok ? sqrt(sr) : __builtin_nan("");
+  trans[b] = sqrt(st);
+}
+
 }  // namespace dvcp
+
+extern "C" int dvcp_registration_error(const double* R_pred, const double* t_pred, const double* R_gt, int64_t rg_b,
+                                       const double* t_gt, int64_t tg_b, int B, double* rot_err, double* trans_err,
+                                       void* stream) {
+  DVCP_REQUIRE(R_pred && t_pred && R_gt && t_gt && rot_err && trans_err, "dvcp_registration_error: null pointer");
+  DVCP_REQUIRE(B >= 0 && rg_b >= 0 && tg_b >= 0, "dvcp_registration_error: bad sizes");
+  if (B == 0) return DVCP_OK;
+  hipLaunchKernelGGL(dvcp::registration_error_kernel, dim3(dvcp::ceil_div(B, 64)), dim3(64), 0,
+                     static_cast<hipStream_t>(stream), R_pred, t_pred, R_gt, t_gt, B, rg_b, tg_b, rot_err, trans_err);
+  return dvcp::launch_status("dvcp_registration_error");
+}
 
 extern "C" int dvcp_rigid_transform(const double* x, const double* y, int B, int n, double* R, double* t, void* stream) {
   DVCP_REQUIRE(x && y && R && t, "dvcp_rigid_transform: null pointer");

@@ -291,3 +291,22 @@ def svd_optimization(x, y_pred, R_true, t_true):
     call("dvcp_svd_optimization", ptr(x), ptr(y_pred), ptr(Rt), ptr(tt), B, n, ptr(R2), ptr(t2), ptr(x1), ptr(y2),
          ptr(partial), stream())
     return R2, t2, x1, y2, partial
+
+
+def registration_error(R_pred, t_pred, R_gt, t_gt):
+    """train.py:112-120 (C8 fixed): per-pair rotation error (Euler xyz, degrees) and translation
+    error, both nn.PairwiseDistance(p=2) with eps 1e-6.  R_pred (B,3,3), t_pred (B,3[,1]);
+    R_gt (B|1,3,3), t_gt (B|1,3[,1]).  Returns (rot_err (B,), trans_err (B,)) fp64."""
+    _lib.require_gpu(R_pred, t_pred, R_gt, t_gt)
+    B = R_pred.shape[0]
+    Rp = R_pred.double().reshape(B, 9).contiguous()
+    tp = t_pred.double().reshape(B, 3).contiguous()
+    Rg = R_gt.double().reshape(-1, 9).contiguous()
+    tg = t_gt.double().reshape(-1, 3).contiguous()
+    if Rg.shape[0] not in (1, B) or tg.shape[0] not in (1, B):
+        raise RuntimeError("registration_error: ground truth must have 1 or B poses")
+    rot = torch.empty(B, dtype=torch.float64, device=Rp.device)
+    trans = torch.empty(B, dtype=torch.float64, device=Rp.device)
+    call("dvcp_registration_error", ptr(Rp), ptr(tp), ptr(Rg), 0 if Rg.shape[0] == 1 else 9, ptr(tg),
+         0 if tg.shape[0] == 1 else 3, B, ptr(rot), ptr(trans), stream())
+    return rot, trans

@@ -223,6 +223,18 @@ int dvcp_svd_optimization(const double* x, const double* y_pred, const double* R
                           const double* t_true, int B, int n, double* R2, double* t2,
                           double* x1, double* y2, double* partial, void* stream);
 
+/* Registration error of the reference's training/eval harness (train.py:112-120 and :156-164, with
+ * crash C8 fixed: translation error over the three components).  Per pair b:
+ *   rot_err[b]   = || euler_xyz_deg(R_pred[b]) - euler_xyz_deg(R_gt[b]) + 1e-6 ||_2
+ *   trans_err[b] = || t_pred[b] - t_gt[b] + 1e-6 ||_2
+ * euler_xyz_deg = scipy Rotation.from_matrix(.).as_euler('xyz', degrees=True); nn.PairwiseDistance
+ * adds its eps (1e-6) to the difference.  R_pred: B x 3 x 3, t_pred: B x 3 fp64 (contiguous);
+ * R_gt / t_gt rows at element strides rg_b / tg_b (0 broadcasts one pose).  rot_err is NaN where a
+ * matrix has det <= 0 (scipy raises there). */
+int dvcp_registration_error(const double* R_pred, const double* t_pred, const double* R_gt, int64_t rg_b,
+                            const double* t_gt, int64_t tg_b, int B, double* rot_err, double* trans_err,
+                            void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -39,7 +39,7 @@ __all__ = [
     "weighting_layer", "Get_Cat_Feat_Src", "Get_Cat_Feat_Tgt", "voxelize",
     "voxelize_point", "feat_embedding_layer", "cpg", "DeepVCP", "KNN",
     "get_rigid_transform", "svd_optimization", "deepVCP_loss", "tracing", "fps_starts",
-    "fe_config",
+    "fe_config", "registration_errors",
 ]
 
 # ---------------------------------------------------------------------------
@@ -505,3 +505,26 @@ def deepVCP_loss(x, y_pred, R_true, t_true, alpha):
     l2 = torch.abs(torch.mean(torch.sub(y_opt, y_true_in)))
     loss = alpha * nn.L1Loss(reduction="mean")(y_true_in, y_opt) + (1 - alpha) * l2
     return loss, R, t
+
+
+def registration_errors(R_pred, t_pred, R_gt, t_gt):
+    """train.py:112-120 per pair, C8 fixed (translation norm over the 3 components):
+    rot_err = PairwiseDistance(euler_xyz_deg(R_pred), euler_xyz_deg(R_gt)) via scipy, trans_err =
+    PairwiseDistance(t_pred, t_gt).  scipy raises for det <= 0 (Q13 reflections); NaN there."""
+    import numpy as np
+    from scipy.spatial.transform import Rotation
+    B = R_pred.shape[0]
+    Rp = R_pred.double().reshape(B, 3, 3).numpy()
+    Rg = R_gt.double().reshape(-1, 3, 3).expand(B, 3, 3).numpy()
+    pdist = nn.PairwiseDistance(p=2)
+    rot = []
+    for b in range(B):
+        try:
+            ep = torch.tensor(Rotation.from_matrix(Rp[b]).as_euler('xyz', degrees=True)).reshape(1, 3)
+            eg = torch.tensor(Rotation.from_matrix(Rg[b]).as_euler('xyz', degrees=True)).reshape(1, 3)
+            rot.append(float(pdist(ep, eg).item()))
+        except ValueError:
+            rot.append(float("nan"))
+    tp = t_pred.double().reshape(B, 3)
+    tg = t_gt.double().reshape(-1, 3).expand(B, 3)
+    return torch.tensor(rot, dtype=torch.float64), pdist(tp, tg)

@@ -498,3 +498,28 @@ def test_rigid_exact_rotation_and_reflection(cuda):
     Rg, tg = dvcp.get_rigid_transform(x.to(cuda), (R @ x + t).to(cuda))
     torch.testing.assert_close(Rg.cpu(), R, rtol=0, atol=1e-12)     # Q13: the reflection is returned as-is
     torch.testing.assert_close(tg.cpu(), t, rtol=0, atol=1e-12)
+
+
+# ----------------------------------------------------------------- registration error (harness)
+def test_registration_error_vs_oracle(cuda):
+    """dvcp_registration_error against scipy's Euler angles (train.py:112-120, C8 fixed)."""
+    import oracle as O
+    from scipy.spatial.transform import Rotation
+    from dvcp import ops
+    g = torch.Generator().manual_seed(120)
+    B = 256
+    Rp = torch.tensor(Rotation.random(B, random_state=1).as_matrix())
+    Rg = torch.tensor(Rotation.random(B, random_state=2).as_matrix())
+    Rp[:64] = Rg[:64] @ torch.tensor(Rotation.from_rotvec(1e-3 * torch.randn(64, 3, generator=g,
+                                                                               dtype=torch.float64).numpy()).as_matrix())
+    Rp[7] = torch.diag(torch.tensor([1.0, -1.0, 1.0], dtype=torch.float64))  # reflection: NaN like scipy
+    tp = torch.randn(B, 3, 1, generator=g, dtype=torch.float64)
+    tg = torch.randn(B, 3, 1, generator=g, dtype=torch.float64)
+    want_r, want_t = O.registration_errors(Rp, tp, Rg, tg)
+    got_r, got_t = ops.registration_error(Rp.to(cuda), tp.to(cuda), Rg.to(cuda), tg.to(cuda))
+    torch.testing.assert_close(got_r.cpu(), want_r, rtol=0, atol=1e-9, equal_nan=True)
+    torch.testing.assert_close(got_t.cpu(), want_t, rtol=0, atol=1e-12)
+    # one ground-truth pose broadcast over the batch
+    got_r1, _ = ops.registration_error(Rp.to(cuda), tp.to(cuda), Rg[:1].to(cuda), tg[:1].to(cuda))
+    want_r1, _ = O.registration_errors(Rp, tp, Rg[:1], tg[:1])
+    torch.testing.assert_close(got_r1.cpu(), want_r1, rtol=0, atol=1e-9, equal_nan=True)

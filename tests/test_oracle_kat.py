@@ -173,3 +173,27 @@ def test_e2e_shapes_and_dtypes_small():
         kp, vcp = m(src, src.clone(), torch.eye(3, dtype=torch.float64)[None], torch.zeros(1, 3))
     assert kp.shape == (1, 32, 3) and kp.dtype == torch.float64     # ModelNet: fp64 key points
     assert vcp.shape == (1, 32, 3) and vcp.dtype == torch.float32   # CPG is fp32 (A.4)
+
+
+# ------------------------------------------------------------------ registration error (harness)
+def test_registration_error_kat():
+    """train.py:112-120 (C8 fixed): identity vs identity leaves only PairwiseDistance's eps in each
+    component; Rx(10 deg) vs identity differs by 10 deg in the first Euler angle; a reflection is
+    rejected by scipy (NaN)."""
+    import math
+    import oracle as O
+    I = torch.eye(3, dtype=torch.float64)[None]
+    z = torch.zeros(1, 3, 1, dtype=torch.float64)
+    rot, tr = O.registration_errors(I, z, I, z)
+    assert abs(rot.item() - math.sqrt(3) * 1e-6) < 1e-15 and abs(tr.item() - math.sqrt(3) * 1e-6) < 1e-15
+    a = math.radians(10.0)
+    Rx = torch.tensor([[1, 0, 0], [0, math.cos(a), -math.sin(a)], [0, math.sin(a), math.cos(a)]],
+                      dtype=torch.float64)[None]
+    t = torch.tensor([[[3.0], [4.0], [0.0]]], dtype=torch.float64)
+    rot, tr = O.registration_errors(Rx, t, I, z)
+    want = math.sqrt((10.0 + 1e-6) ** 2 + 2e-12)
+    assert abs(rot.item() - want) < 1e-9
+    assert abs(tr.item() - math.sqrt((3 + 1e-6) ** 2 + (4 + 1e-6) ** 2 + 1e-12)) < 1e-12
+    refl = torch.diag(torch.tensor([1.0, 1.0, -1.0], dtype=torch.float64))[None]
+    rot, _ = O.registration_errors(refl, z, I, z)
+    assert math.isnan(rot.item())
