@@ -19,8 +19,9 @@
 
 namespace dvcp {
 
-constexpr int kTile = 64;             // reference points per tile
-constexpr int kMaxTiles = 256;        // per cloud: M <= 16384
+constexpr int kTile = 32;             // reference points per tile (finer boxes prune and order better)
+constexpr int kMaxTiles = 512;        // per cloud: M <= 16384
+constexpr uint32_t kTileIdBits = 0x1FFu;  // tile id in the low bits of a sort key (kMaxTiles - 1)
 constexpr int kTiledThreads = 256;    // 4 independent waves per workgroup
 
 struct TiledLayout {
@@ -192,7 +193,7 @@ __global__ __launch_bounds__(kTiledThreads) void knn_tiled_query_kernel(const fl
       wh[a] = fmaxf(wh[a], __shfl_xor(wh[a], off, kWave));
     }
   const float4* tb = tbox + static_cast<int64_t>(b) * T * 2;
-  // tile keys: lb2(query box, tile box) with the low 8 mantissa bits replaced by the tile id.
+  // tile keys: lb2(query box, tile box) with the low 9 mantissa bits replaced by the tile id.
   // Truncation only lowers a non-negative float, so key value <= the true bound.
   uint32_t keys[R];
 #pragma unroll
@@ -201,7 +202,7 @@ __global__ __launch_bounds__(kTiledThreads) void knn_tiled_query_kernel(const fl
     if (t < T) {
       const float4 lo = tb[2 * t], hi = tb[2 * t + 1];
       const float lb = box_box_lb2(wl[0], wl[1], wl[2], wh[0], wh[1], wh[2], lo.x, lo.y, lo.z, hi.x, hi.y, hi.z);
-      keys[r] = (__float_as_uint(lb) & 0xFFFFFF00u) | static_cast<uint32_t>(t);
+      keys[r] = (__float_as_uint(lb) & ~kTileIdBits) | static_cast<uint32_t>(t);
     } else {
       keys[r] = 0xFFFFFFFFu;
     }
@@ -232,11 +233,11 @@ __global__ __launch_bounds__(kTiledThreads) void knn_tiled_query_kernel(const fl
     for (int i = 0; i < 64 && !stop; ++i) {
       if (r * 64 + i >= T) break;
       const uint32_t key = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(keys[r]), i));
-      if (__uint_as_float(key & 0xFFFFFF00u) > wkth) {  // every later tile is farther
+      if (__uint_as_float(key & ~kTileIdBits) > wkth) {  // every later tile is farther
         stop = true;
         break;
       }
-      const int t = static_cast<int>(key & 0xFFu);
+      const int t = static_cast<int>(key & kTileIdBits);
       const const_float* bx = (const const_float*)(tbu + 2 * t);
       const float lbq = box_box_lb2(qx, qy, qz, qx, qy, qz, bx[0], bx[1], bx[2], bx[4], bx[5], bx[6]);
       const bool act = live & (lbq <= kth);
@@ -346,13 +347,14 @@ extern "C" int dvcp_knn_tiled(int dtype, const void* ref, int64_t rb, int64_t rc
     return dvcp::launch_status("dvcp_knn_tiled(query)");                                                           \
   }
   DVCP_KNNT(1, 1)
-  DVCP_KNNT(1, 4)
+  DVCP_KNNT(1, 8)
   DVCP_KNNT(8, 1)
-  DVCP_KNNT(8, 4)
-  DVCP_KNNT(16, 4)
+  DVCP_KNNT(8, 8)
+  DVCP_KNNT(16, 8)
   DVCP_KNNT(32, 1)
   DVCP_KNNT(32, 2)
   DVCP_KNNT(32, 4)
+  DVCP_KNNT(32, 8)
 #undef DVCP_KNNT
   dvcp::set_error("dvcp_knn_tiled: unsupported k=%d", k);
   return DVCP_EINVAL;
