@@ -19,9 +19,9 @@
 
 namespace dvcp {
 
-constexpr int kTile = 32;             // reference points per tile (finer boxes prune and order better)
-constexpr int kMaxTiles = 512;        // per cloud: M <= 16384
-constexpr uint32_t kTileIdBits = 0x1FFu;  // tile id in the low bits of a sort key (kMaxTiles - 1)
+constexpr int kTile = 16;             // reference points per tile (finer boxes prune and order better)
+constexpr int kMaxTiles = 1024;       // per cloud: M <= 16384
+constexpr uint32_t kTileIdBits = 0x3FFu;  // tile id in the low bits of a sort key (kMaxTiles - 1)
 constexpr int kTiledThreads = 256;    // 4 independent waves per workgroup
 
 struct TiledLayout {
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(kTiledThreads) void knn_tiled_query_kernel(const fl
       wh[a] = fmaxf(wh[a], __shfl_xor(wh[a], off, kWave));
     }
   const float4* tb = tbox + static_cast<int64_t>(b) * T * 2;
-  // tile keys: lb2(query box, tile box) with the low 9 mantissa bits replaced by the tile id.
+  // tile keys: lb2(query box, tile box) with the low 10 mantissa bits replaced by the tile id.
   // Truncation only lowers a non-negative float, so key value <= the true bound.
   uint32_t keys[R];
 #pragma unroll
@@ -347,14 +347,15 @@ extern "C" int dvcp_knn_tiled(int dtype, const void* ref, int64_t rb, int64_t rc
     return dvcp::launch_status("dvcp_knn_tiled(query)");                                                           \
   }
   DVCP_KNNT(1, 1)
-  DVCP_KNNT(1, 8)
+  DVCP_KNNT(1, 16)
   DVCP_KNNT(8, 1)
-  DVCP_KNNT(8, 8)
-  DVCP_KNNT(16, 8)
+  DVCP_KNNT(8, 16)
+  DVCP_KNNT(16, 16)
   DVCP_KNNT(32, 1)
   DVCP_KNNT(32, 2)
   DVCP_KNNT(32, 4)
   DVCP_KNNT(32, 8)
+  DVCP_KNNT(32, 16)
 #undef DVCP_KNNT
   dvcp::set_error("dvcp_knn_tiled: unsupported k=%d", k);
   return DVCP_EINVAL;
