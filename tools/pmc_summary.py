@@ -11,14 +11,15 @@ import csv
 import json
 import sys
 
-# entry point (bench stage key) -> kernel name substrings it launches
+# entry point (bench stage key) -> (kernels one call launches once each: the call count,
+#                                  helper kernels the same call also launches)
 ENTRY = {
-    "dvcp_fps_ws": ["fps_batched_kernel", "fps_kernel", "fps_serial"],
-    "dvcp_knn_tiled": ["knn_tiled_query_kernel", "knn_tiled_build_kernel"],
-    "dvcp_sa_group_mlp_ws": ["sa_mlp_mfma_kernel", "sa_mlp_kernel", "sa_pre_kernel"],
-    "dvcp_ball_query_ws": ["bq_tiled_kernel", "bq_build_kernel", "bq_wave_kernel", "ball_query_kernel"],
-    "dvcp_dfe_tgt": ["dfe_tgt"],
-    "dvcp_cpg": ["cpg_kernel"],
+    "dvcp_fps_ws": (["fps_batched_kernel", "fps_kernel"], []),
+    "dvcp_knn_tiled": (["knn_tiled_query_kernel"], ["knn_tiled_build_kernel"]),
+    "dvcp_sa_group_mlp_ws": (["sa_mlp_mfma_kernel", "sa_mlp_kernel"], ["sa_pre_kernel", "sa_order_kernel"]),
+    "dvcp_ball_query_ws": (["bq_tiled_kernel", "bq_wave_kernel", "ball_query_kernel"], ["bq_build_kernel"]),
+    "dvcp_dfe_tgt": (["dfe_tgt"], []),
+    "dvcp_cpg": (["cpg_kernel"], []),
 }
 READ_CORRECTION = 2.0
 
@@ -36,22 +37,16 @@ def main():
     out = {"_note": "bytes per launch of each entry point (sum over the kernels it launches), "
                     f"reads = FETCH_SIZE x {READ_CORRECTION} (gfx950 counts 128-B requests at 64 B), "
                     "writes = WRITE_SIZE; bench.py --inflight 1 --steps 4 --warmup 1"}
-    for entry, subs in ENTRY.items():
-        rd = wr = 0.0
-        n = None
-        for name, vals in fetch.items():
-            if any(s in name for s in subs):
-                rd += sum(vals)
-                n = max(n or 0, len(vals))
-        for name, vals in write.items():
-            if any(s in name for s in subs):
-                wr += sum(vals)
-        if not n:
+    for entry, (main_k, helpers) in ENTRY.items():
+        subs = main_k + helpers
+        calls = sum(len(v) for k, v in fetch.items() if any(m in k for m in main_k))
+        if not calls:
             continue
-        # launches of the entry point = launches of its most frequent kernel
-        out[entry] = {"launches": n, "read_bytes_per_launch": READ_CORRECTION * rd / n,
-                      "write_bytes_per_launch": wr / n,
-                      "hbm_bytes_per_launch": READ_CORRECTION * rd / n + wr / n}
+        rd = sum(sum(v) for k, v in fetch.items() if any(m in k for m in subs))
+        wr = sum(sum(v) for k, v in write.items() if any(m in k for m in subs))
+        out[entry] = {"calls": calls, "read_bytes_per_launch": READ_CORRECTION * rd / calls,
+                      "write_bytes_per_launch": wr / calls,
+                      "hbm_bytes_per_launch": READ_CORRECTION * rd / calls + wr / calls}
     print(json.dumps(out, indent=1))
 
 
