@@ -310,3 +310,17 @@ def registration_error(R_pred, t_pred, R_gt, t_gt):
     call("dvcp_registration_error", ptr(Rp), ptr(tp), ptr(Rg), 0 if Rg.shape[0] == 1 else 9, ptr(tg),
          0 if tg.shape[0] == 1 else 3, B, ptr(rot), ptr(trans), stream())
     return rot, trans
+
+
+def rigid_apply(pts, R, t=None, pdim=2):
+    """R @ pts (+ t) in fp64 (KITTIDataset.py:80-81, ModelNet40Dataset.py:74-85).  pts (B, C, N)
+    with C = 3 or 6 (xyz [+ normals, rotated only]); R (B, 3, 3); t (B|1, 3[, 1]) or None."""
+    _lib.require_gpu(pts, R)
+    B, C = pts.shape[0], pts.shape[1]
+    N, sb, sc, sn = pts.shape[pdim], pts.stride(0), pts.stride(1), pts.stride(pdim)
+    Rc = R.double().reshape(B, 9).contiguous()
+    tc = None if t is None else t.double().reshape(-1, 3).contiguous()
+    out = torch.empty(B, C, N, dtype=torch.float64, device=pts.device)
+    call("dvcp_rigid_apply", dtype_code(pts), ptr(pts), sb, sc, sn, B, N, C, ptr(Rc), ptr(tc),
+         0 if tc is None or tc.shape[0] == 1 else 3, ptr(out), stream())
+    return out

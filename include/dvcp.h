@@ -235,6 +235,14 @@ int dvcp_registration_error(const double* R_pred, const double* t_pred, const do
                             const double* t_gt, int64_t tg_b, int B, double* rot_err, double* trans_err,
                             void* stream);
 
+/* Training-pair synthesis: out = R x (+ t) per cloud, in fp64.  Replaces the numpy transform of
+ * KITTIDataset.py:80-81 (target = R @ src + t) and ModelNet40Dataset.py:74-85 (points rotated
+ * and translated, normals rotated).  in: B x C x N (strided, dtype; C = 3 xyz or 6 xyz+normals),
+ * R: B x 3 x 3 fp64, t: B x 3 fp64 at row stride t_b (NULL: no translation; 0 broadcasts),
+ * out: B x C x N fp64 contiguous (channels 0-2 translated, 3-5 rotated only). */
+int dvcp_rigid_apply(int dtype, const void* in, int64_t ib, int64_t ic, int64_t in_n, int B, int N, int C,
+                     const double* R, const double* t, int64_t t_b, double* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
