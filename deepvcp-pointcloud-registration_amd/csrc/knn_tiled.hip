@@ -23,6 +23,7 @@ constexpr int kTile = 16;             // reference points per tile (finer boxes 
 constexpr int kMaxTiles = 1024;       // per cloud: M <= 16384
 constexpr uint32_t kTileIdBits = 0x3FFu;  // tile id in the low bits of a sort key (kMaxTiles - 1)
 constexpr int kTiledThreads = 256;    // 4 independent waves per workgroup
+constexpr int kBoxBatch = 1;          // tiles whose boxes are read (LDS) and tested together
 
 struct TiledLayout {
   float4* sorted;  // B x T*64: x, y, z, original index bits (padding: NaN, index 0x7FFFFFFF)
@@ -165,6 +166,14 @@ __global__ __launch_bounds__(kTiledThreads) void knn_tiled_query_kernel(const fl
                                                                         int64_t* __restrict__ idx64) {
   const int b = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int T = (M + kTile - 1) / kTile;
+  // the cloud's tile boxes in LDS (all four waves scan the same cloud): the per-lane box test
+  // then reads LDS broadcasts kBoxBatch tiles at a time instead of waiting on a scalar load per tile
+  __shared__ float4 sbox[2 * kMaxTiles];
+  {
+    const float4* tbg = tbox + static_cast<int64_t>(b) * T * 2;
+    for (int i = threadIdx.x; i < 2 * T; i += kTiledThreads) sbox[i] = tbg[i];
+    __syncthreads();
+  }
   const int sq = (blockIdx.x * (kTiledThreads / kWave) + wave) * kWave + lane;
   if ((blockIdx.x * (kTiledThreads / kWave) + wave) * kWave >= Q) return;  // whole wave past the end
   const bool live = sq < Q;
@@ -226,20 +235,31 @@ __global__ __launch_bounds__(kTiledThreads) void knn_tiled_query_kernel(const fl
   uint64_t kkey = live ? kEmpty : 0ull;
   float wkth = wave_max_nonneg(kth);
   const float4* P = uniform_ptr(sorted + static_cast<int64_t>(b) * T * kTile);
-  const float4* tbu = uniform_ptr(tb);
   bool stop = false;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    for (int i = 0; i < 64 && !stop; ++i) {
-      if (r * 64 + i >= T) break;
-      const uint32_t key = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(keys[r]), i));
+    for (int i0 = 0; i0 < 64 && !stop; i0 += kBoxBatch) {
+      if (r * 64 + i0 >= T) break;
+      // kBoxBatch tiles of the order: keys, then their boxes (LDS broadcasts) and this lane's bounds
+      uint32_t key4[kBoxBatch];
+      float lb4[kBoxBatch];
+#pragma unroll
+      for (int j = 0; j < kBoxBatch; ++j) {
+        key4[j] = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(keys[r]), i0 + j));
+        const int tj = static_cast<int>(key4[j] & kTileIdBits) < T ? static_cast<int>(key4[j] & kTileIdBits) : 0;
+        const float4 lo = sbox[2 * tj], hi = sbox[2 * tj + 1];
+        lb4[j] = box_box_lb2(qx, qy, qz, qx, qy, qz, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z);
+      }
+#pragma unroll
+      for (int j = 0; j < kBoxBatch; ++j) {
+      if (r * 64 + i0 + j >= T) break;
+      const uint32_t key = key4[j];
       if (__uint_as_float(key & ~kTileIdBits) > wkth) {  // every later tile is farther
         stop = true;
         break;
       }
       const int t = static_cast<int>(key & kTileIdBits);
-      const const_float* bx = (const const_float*)(tbu + 2 * t);
-      const float lbq = box_box_lb2(qx, qy, qz, qx, qy, qz, bx[0], bx[1], bx[2], bx[4], bx[5], bx[6]);
+      const float lbq = lb4[j];
       const bool act = live & (lbq <= kth);
       if (__ballot(act) == 0) continue;
       const const_float* tp = (const const_float*)(P + t * kTile);
@@ -291,6 +311,7 @@ __global__ __launch_bounds__(kTiledThreads) void knn_tiled_query_kernel(const fl
         }
       }
       if (ins != 0) wkth = wave_max_nonneg(kth);
+      }
     }
   }
   if (!live) return;
