@@ -156,7 +156,7 @@ struct Dfe1Lds {
   double pb[32];         // W2 . b1 + b2
   float e[kDfeKS][64];   // E as the B fragment: [k-step][lane]
   float eb[32];          // e
-  double w[kDfe1Waves][32];  // per-wave w_j of the current candidate
+  float w[kDfe1Waves][32];  // per-wave w_j of the current candidate (fp64 quotient rounded to fp32)
 };
 
 template <typename T>
@@ -237,12 +237,15 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
     G.cy = cand[static_cast<int64_t>(gc) * 3 + 1];
     G.cz = cand[static_cast<int64_t>(gc) * 3 + 2];
   };
-  // get_cat_feat_tgt.py:57-58 (lanes 32..63 mirror lanes 0..31): the w row of a candidate
+  // get_cat_feat_tgt.py:57-58 (lanes 32..63 mirror lanes 0..31): the w row of a candidate.
+  // w = dist / dist_sum is formed in fp64 like the reference and rounded once to fp32; the
+  // feature product below is then one fp32 multiply (the reference rounds the fp64 product to
+  // fp32 at the DFE input: the two differ by at most one fp32 ulp of the input).
   auto weights = [&](float dj) {
     double dsum = static_cast<double>(dj);
 #pragma unroll
     for (int off = 16; off > 0; off >>= 1) dsum += __shfl_xor(dsum, off, kWave);
-    L.w[wave][r32] = static_cast<double>(dj) / dsum;  // both lane halves write the same value
+    L.w[wave][r32] = static_cast<float>(static_cast<double>(dj) / dsum);  // both lane halves write the same value
   };
   auto embed = [&](int gg, const Gathered& G) {
     float x[kDfeKS];
@@ -252,14 +255,14 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
     x[2] = h == 0 ? static_cast<float>(G.pz - static_cast<T>(G.cz)) : 0.0f;
     // the wave's own w row, read back as 16-byte broadcasts
     __builtin_amdgcn_wave_barrier();
-    const double2* wr = reinterpret_cast<const double2*>(&L.w[wave][16 * h]);
+    const float4* wr = reinterpret_cast<const float4*>(&L.w[wave][16 * h]);
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const float fv[4] = {G.f[v].x, G.f[v].y, G.f[v].z, G.f[v].w};
-      const double2 wa = wr[2 * v], wb = wr[2 * v + 1];
-      const double wf[4] = {wa.x, wa.y, wb.x, wb.y};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) x[3 + 4 * v + e] = static_cast<float>(static_cast<double>(fv[e]) * wf[e]);
+      const float4 w4 = wr[v];
+      x[3 + 4 * v] = G.f[v].x * w4.x;
+      x[4 + 4 * v] = G.f[v].y * w4.y;
+      x[5 + 4 * v] = G.f[v].z * w4.z;
+      x[6 + 4 * v] = G.f[v].w * w4.w;
     }
     int zo = 0;  // opaque zero: E fragments are re-read from LDS per candidate, not hoisted
     asm volatile("" : "+v"(zo));
