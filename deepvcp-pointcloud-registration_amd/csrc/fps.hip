@@ -506,18 +506,18 @@ __device__ __forceinline__ float fps_update(float m, T px, T py, T pz, T cx, T c
   }
 }
 
-template <typename T, int PPT, bool TIMING = false>
-__global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> pts, int N, int npoint,
+template <typename T, int PPT, bool TIMING = false, int THREADS = kFpsThreads>
+__global__ __launch_bounds__(THREADS) void fps_batched_kernel(PointsView<T> pts, int N, int npoint,
                                                                   const int64_t* __restrict__ start,
                                                                   int64_t* __restrict__ out_idx,
                                                                   T* __restrict__ out_xyz,
                                                                   unsigned long long* __restrict__ prof) {
-  constexpr int W = kFpsThreads / kWave;
+  constexpr int W = THREADS / kWave;
   constexpr int G = W * PPT;               // groups
   constexpr int GPL = (G + kWave - 1) / kWave;  // groups per walker lane
   static_assert(PPT <= 32, "group masks are 32-bit");
   __shared__ uint32_t bins[kMortonBins];
-  __shared__ uint16_t perm[kFpsThreads * PPT];
+  __shared__ uint16_t perm[THREADS * PPT];
   __shared__ T red[2][3][W];
   __shared__ uint32_t wsum[W];
   __shared__ FpsGroup<T> groups[G];
@@ -526,7 +526,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_batched_kernel(PointsView<T> 
   __shared__ int ncentre;
 
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  fps_morton_sort<T, kFpsThreads>(pts, b, N, bins, perm, red, wsum);
+  fps_morton_sort<T, THREADS>(pts, b, N, bins, perm, red, wsum);
 
   // ---- this lane's points: slot p = sorted position (wave*PPT + p)*64 + lane -----------------
   T px[PPT], py[PPT], pz[PPT];
@@ -852,6 +852,23 @@ static int launch_fps(const T* xyz, int64_t sb, int64_t sc, int64_t sn, int B, i
     const char* e = getenv("DVCP_FPS_SERIAL");
     return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
   }();
+  // 16 waves for the batched kernel: half the points per lane in the update/regroup phase
+  static const bool wide = [] {
+    const char* e = getenv("DVCP_FPS_WIDE");
+    return e && e[0] == '1';
+  }();
+  if (wide && sizeof(T) == 4 && mode == 0 && N >= kFpsBatchedMinN) {
+    const int pw = ceil_div(N, 1024);
+#define DVCP_FPS_WIDE(P)                                                                                   \
+    if (pw <= P) {                                                                                         \
+      hipLaunchKernelGGL((fps_batched_kernel<T, P, false, 1024>), grid, dim3(1024), 0, st, v, N, npoint, start, \
+                         out_idx, out_xyz, nullptr);                                                       \
+      return launch_status("dvcp_fps(wide)");                                                              \
+    }
+    DVCP_FPS_WIDE(8)
+    DVCP_FPS_WIDE(16)
+#undef DVCP_FPS_WIDE
+  }
 #define DVCP_FPS_CASE(P)                                                                                   \
   if (ppt <= P) {                                                                                          \
     if (mode == 0 && N >= kFpsBatchedMinN)                                                                 \

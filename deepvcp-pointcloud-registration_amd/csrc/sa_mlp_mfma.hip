@@ -71,40 +71,43 @@ template <int D, int C1>
 __global__ __launch_bounds__(256) void sa_pre_kernel(const float* __restrict__ feat, int64_t fb, int64_t fn, int N,
                                                      int B, const float* __restrict__ params,
                                                      float* __restrict__ U) {
-  constexpr int C0 = 3 + D;
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= static_cast<int64_t>(B) * N) return;
-  const int b = static_cast<int>(i / N), n = static_cast<int>(i % N);
-  const float4* fr = reinterpret_cast<const float4*>(feat + b * fb + static_cast<int64_t>(n) * fn);
-  float f[D];
-#pragma unroll
-  for (int v = 0; v < D / 4; ++v) {
-    const float4 q = fr[v];
-    f[4 * v] = q.x;
-    f[4 * v + 1] = q.y;
-    f[4 * v + 2] = q.z;
-    f[4 * v + 3] = q.w;
-  }
+  // Thread (point, 4-channel group): the C1/4 threads of a point write one contiguous U row
+  // (coalesced float4 stores), and read the BN-folded weights from LDS as [k][c] float4 rows.
+  constexpr int C0 = 3 + D, CG = C1 / 4, PPB = 256 / CG;  // channel groups, points per block
+  __shared__ float4 w[D][CG];
+  __shared__ float4 bias[CG];
   const float* W1 = params;
   const float* pb1 = W1 + C1 * C0;
   const float* ps1 = pb1 + C1;
   const float* pt1 = ps1 + C1;
-  float4* dst = reinterpret_cast<float4*>(U + i * C1);
+  for (int i = threadIdx.x; i < D * C1; i += 256) {  // BN folded in: (W x + b) s + t = (s W) x + (s b + t)
+    const int k = i / C1, c = i % C1;
+    reinterpret_cast<float*>(&w[k][0])[c] = W1[c * C0 + 3 + k] * ps1[c];
+  }
+  for (int c = threadIdx.x; c < C1; c += 256)
+    reinterpret_cast<float*>(&bias[0])[c] =
+        static_cast<float>(static_cast<double>(pb1[c]) * ps1[c] + static_cast<double>(pt1[c]));
+  __syncthreads();
+  const int g = threadIdx.x % CG;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * PPB + threadIdx.x / CG;
+  if (i >= static_cast<int64_t>(B) * N) return;
+  const int b = static_cast<int>(i / N), n = static_cast<int>(i % N);
+  const float4* fr = reinterpret_cast<const float4*>(feat + b * fb + static_cast<int64_t>(n) * fn);
+  float4 acc = bias[g];
 #pragma unroll 4
-  for (int c4 = 0; c4 < C1 / 4; ++c4) {
-    float o[4];
+  for (int v = 0; v < D / 4; ++v) {
+    const float4 q = fr[v];
+    const float fq[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int c = 4 * c4 + e;
-      // BN folded in: (W x + b) s + t = (s W) x + (s b + t)
-      const float sc = ps1[c];
-      float acc = static_cast<float>(static_cast<double>(pb1[c]) * sc + static_cast<double>(pt1[c]));
-#pragma unroll
-      for (int k = 0; k < D; ++k) acc = __fmaf_rn(W1[c * C0 + 3 + k] * sc, f[k], acc);
-      o[e] = acc;
+      const float4 wk = w[4 * v + e][g];
+      acc.x = __fmaf_rn(wk.x, fq[e], acc.x);
+      acc.y = __fmaf_rn(wk.y, fq[e], acc.y);
+      acc.z = __fmaf_rn(wk.z, fq[e], acc.z);
+      acc.w = __fmaf_rn(wk.w, fq[e], acc.w);
     }
-    dst[c4] = make_float4(o[0], o[1], o[2], o[3]);
   }
+  reinterpret_cast<float4*>(U + i * C1)[g] = acc;
 }
 
 // Centres of each cloud in 12-bit Hilbert-cell order (one workgroup per cloud), for the MFMA
@@ -314,8 +317,8 @@ int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, c
     hipLaunchKernelGGL((sa_order_kernel<T>), dim3(B), dim3(kBuildThreads), 0, st, cv, S, order);
   if (U) {
     const int64_t rows = static_cast<int64_t>(B) * N;
-    hipLaunchKernelGGL((sa_pre_kernel<D, C1>), dim3(ceil_div(rows, 256)), dim3(256), 0, st, feat, fb, fn, N, B, params,
-                       U);
+    hipLaunchKernelGGL((sa_pre_kernel<D, C1>), dim3(ceil_div(rows, 256 / (C1 / 4))), dim3(256), 0, st, feat, fb, fn, N,
+                       B, params, U);
     hipLaunchKernelGGL((sa_mlp_mfma_kernel<T, D, C1, C2, true>), dim3(grid), dim3(kMfmaWaves * kWave), 0, st, pv, cv,
                        S, B, feat, fb, fn, count, list, nsample, params, U, static_cast<int64_t>(N) * C1, order, out);
   } else {

@@ -523,3 +523,31 @@ def test_registration_error_vs_oracle(cuda):
     got_r1, _ = ops.registration_error(Rp.to(cuda), tp.to(cuda), Rg[:1].to(cuda), tg[:1].to(cuda))
     want_r1, _ = O.registration_errors(Rp, tp, Rg[:1], tg[:1])
     torch.testing.assert_close(got_r1.cpu(), want_r1, rtol=0, atol=1e-9, equal_nan=True)
+
+
+def test_sa_mlp_plain_entry_matches_workspace_entry(cuda):
+    """dvcp_sa_group_mlp (no workspace: layer 1 per row, BN after the GEMM) and
+    dvcp_sa_group_mlp_ws (per-point U, BN folded, Hilbert visiting order) agree to fp32 rounding
+    on the sa3 table (67-64-64) with per-point centres, as the forward runs it."""
+    import dvcp.pointnet2_utils as P
+    from dvcp import _lib, ops
+    from tests_helpers import randomize_bn
+    g = torch.Generator().manual_seed(121)
+    B, N = 2, 3000
+    torch.manual_seed(8)
+    sa = P.PointNetSetAbstraction(npoint=N, radius=0.4, nsample=64, in_channel=67, mlp=[64, 64]).eval()
+    randomize_bn(sa)
+    sa.to(cuda)
+    xyz = (torch.rand(B, 3, N, generator=g) * 2 - 1).to(cuda)
+    feat = torch.randn(B, N, 64, generator=g).to(cuda).transpose(1, 2)  # (B, 64, N), point-major memory
+    count, lst, _ = ops.ball_query(xyz, xyz, 0.4, 64, pdim=2, cdim_pts=2)
+    got_ws = ops.sa_group_mlp(xyz, xyz, feat, count, lst, 64, sa.chans, sa.packed_params(), xyz_pdim=2,
+                              feat_ddim=1, feat_pdim=2)
+    ch = torch.tensor(list(sa.chans), dtype=torch.int32)
+    plain = torch.empty_like(got_ws)
+    st = feat.stride()
+    _lib.call("dvcp_sa_group_mlp", _lib.F32, _lib.ptr(xyz), xyz.stride(0), xyz.stride(1), xyz.stride(2), N,
+              _lib.ptr(xyz), xyz.stride(0), xyz.stride(1), xyz.stride(2), N, B, _lib.F32, _lib.ptr(feat), st[0],
+              st[1], st[2], 64, _lib.ptr(count), _lib.ptr(lst), 64, 2, _lib.ctypes.c_void_p(ch.data_ptr()),
+              _lib.ptr(sa.packed_params()), _lib.ptr(plain), _lib.stream())
+    torch.testing.assert_close(got_ws, plain, rtol=1e-5, atol=1e-5)
