@@ -887,6 +887,7 @@ static int launch_fps(const T* xyz, int64_t sb, int64_t sc, int64_t sn, int B, i
   DVCP_FPS_CASE(8)
   DVCP_FPS_CASE(16)
   if constexpr (sizeof(T) == 4) {
+    DVCP_FPS_CASE(20)  // N = 10000 (the FE layers 2 and 3): no all-padding slots per lane
     DVCP_FPS_CASE(24)
     DVCP_FPS_CASE(32)
   }

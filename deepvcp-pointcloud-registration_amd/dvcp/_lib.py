@@ -94,9 +94,16 @@ def exported_symbols():
 EVENT_LOG = None
 
 
+# Diagnostic (bench marginal-cost probes): DVCP_DUP=<entry> issues that entry point twice per call
+# (same arguments, idempotent outputs), so the throughput drop is that kernel's marginal cost.
+_DUP = os.environ.get("DVCP_DUP", "")
+
+
 def call(name, *args, work=None):
     """Call an entry point; raise RuntimeError with the library's message on failure."""
     lib = load()
+    if _DUP and name == _DUP:
+        getattr(lib, name)(*args)
     if EVENT_LOG is not None:
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
