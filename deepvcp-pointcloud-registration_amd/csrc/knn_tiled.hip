@@ -119,21 +119,6 @@ __device__ __forceinline__ float wave_max_nonneg(float x) {
   return __uint_as_float(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63)));
 }
 
-template <int CTRL, int ROWS>
-__device__ __forceinline__ uint32_t dpp_or_u(uint32_t v) {
-  return v | static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, ROWS, 0xF, false));
-}
-// OR over the wave (wave-uniform result)
-__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
-  v = dpp_or_u<0x111, 0xF>(v);
-  v = dpp_or_u<0x112, 0xF>(v);
-  v = dpp_or_u<0x114, 0xF>(v);
-  v = dpp_or_u<0x118, 0xF>(v);
-  v = dpp_or_u<0x142, 0xA>(v);
-  v = dpp_or_u<0x143, 0xC>(v);
-  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
-}
-
 // Bitonic sort (ascending) of 64*R keys held as keys[r] at position r*64 + lane.
 template <int R>
 __device__ __forceinline__ void wave_bitonic(uint32_t (&keys)[R]) {
@@ -288,8 +273,6 @@ __global__ __launch_bounds__(kTiledThreads) void knn_tiled_query_kernel(const fl
         // some lane against the k-th key at chunk start (a superset: the key only decreases)
         float d2v[16];
         uint32_t piv[16];
-        // (per-lane candidate bits, OR-reduced across the wave once per chunk: a ballot per point
-        // would put a VALU -> SALU -> VALU dependency on every point)
         uint32_t todo = 0;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
