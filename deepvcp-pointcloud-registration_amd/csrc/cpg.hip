@@ -13,6 +13,7 @@
 // with its 4 output channels padded to 16; conv2's haloed output feeds conv3 (VALU, maskless),
 // and the softmax and weighted mean finish in registers.
 #include "common.h"
+#include "cpg_grid.h"
 
 namespace dvcp {
 
@@ -29,25 +30,6 @@ constexpr int kCpgW1F = 32 * 27 * 16;
 constexpr int kCpgBigF = 16 * kCpgPV;  // quarter volume + conv1 weights, later haloed conv1 / conv2 outputs
 constexpr int kCpgE = (32 * kCpgMaxC + kCpgThreads - 1) / kCpgThreads;  // target values per thread
 static_assert(kCpgVolF + kCpgW1F <= kCpgBigF, "quarter volume + conv1 weights must fit the area");
-
-// x / d for 0 <= x < 2^16 and 1 <= d <= 2^11 as one mul_hi: m = ceil(2^32 / d) overestimates
-// 1/d by less than 2^-32, so x*m/2^32 exceeds x/d by less than 2^-16, while the fractional part
-// of x/d is at most 1 - 1/d <= 1 - 2^-11: the floor is exact.  (Index math of an 11^3 grid: the
-// generic 32-bit division costs ~25 VALU instructions and dominated this kernel's VALU count.)
-struct FastDiv {
-  uint32_t m, d;
-  __device__ __forceinline__ explicit FastDiv(uint32_t dd)
-      : m(static_cast<uint32_t>((0x100000000ull + dd - 1) / dd)), d(dd) {}
-  __device__ __forceinline__ uint32_t div(uint32_t x) const { return __umulhi(x, m); }
-  __device__ __forceinline__ uint32_t mod(uint32_t x) const { return x - div(x) * d; }
-};
-
-// haloed cell of voxel g = (gz*G + gy)*G + gx in the (G+2)^3 volume
-__device__ __forceinline__ int cpg_halo(int g, const FastDiv& dG, const FastDiv& dGG, int PG, int PGG) {
-  const uint32_t z = dGG.div(g), r = g - z * dGG.d;
-  const uint32_t y = dG.div(r), x = r - y * dG.d;
-  return static_cast<int>((z + 1) * PGG + (y + 1) * PG + (x + 1));
-}
 
 __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restrict__ src, const float* __restrict__ tgt,
                                                           int64_t t_p, int64_t t_f, int64_t t_c,

@@ -1,0 +1,398 @@
+// cpg_bwd.hip -- backward of corresponding point generation (cpg.py:27-60) for training
+// (train.py:121 loss.backward()), one 1024-thread workgroup per key point.
+//
+// Forward (cpg.hip): cost[f'][v] = (src[f'] - T[v*32 + f'])^2 (Q11 scramble: T[l] = tgt[f = l / C]
+// [c = l % C]); h1 = conv1(cost) (32 -> 16), h2 = conv2(h1) (16 -> 4), lg = conv3(h2) (4 -> 1), all
+// k3 p1 with no activations; w = softmax(lg); vcp = sum(w * cand) / sum(w).
+// Backward, given dL/dvcp:
+//   dL/dw_v   = sum_a g_a (cand_v,a / S - A_a / S^2)     (A = sum w cand, S = sum w)
+//   dL/dlg_v  = w_v (dL/dw_v - sum_u w_u dL/dw_u)         (softmax)
+//   conv k: dW[co][ci][t] = sum_v gout[co][v] in[ci][v + off_t];  db[co] = sum_v gout[co][v];
+//           gin[ci][u]    = sum_co sum_t W[co][ci][t] gout[co][u - off_t]   (zero padding: taps
+//           that leave the grid are skipped)
+//   dL/dsrc[f'] = sum_v 2 (src[f'] - T) dL/dcost[f'][v];  dL/dT[l] = -2 (src[f'] - T) dL/dcost.
+// The workgroup recomputes the forward activations (conv1 from the cost volume, one input
+// channel at a time) and keeps them in LDS:
+//   A (16 x C): h1, later dL/dh1;    W (13824): conv1 weights [ci][tap][co], in the middle phases
+//   dL/dlg and reduction scratch;    D (4 x C): the cost channel being processed, or h2 / dL/dh2.
+// Parameter gradients are written per key point (fixed order, no atomics) and summed over key
+// points by cpg_bwd_reduce_kernel in fp64.
+#include "common.h"
+#include "cpg_grid.h"
+
+namespace dvcp {
+
+constexpr int kCbThreads = 1024;
+constexpr int kCbMaxC = 1331;
+constexpr int kCbA = 16 * kCbMaxC;
+constexpr int kCbW = 16 * 32 * 27;
+constexpr int kCbD = 4 * kCbMaxC;
+constexpr int kCbV = (kCbMaxC + kCbThreads - 1) / kCbThreads;  // voxels per thread
+// packed parameter layout (= cpg.packed_params()): W1, b1, W2, b2, W3, b3
+constexpr int kCbOffB1 = 16 * 32 * 27;
+constexpr int kCbOffW2 = kCbOffB1 + 16;
+constexpr int kCbOffB2 = kCbOffW2 + 4 * 16 * 27;
+constexpr int kCbOffW3 = kCbOffB2 + 4;
+constexpr int kCbOffB3 = kCbOffW3 + 4 * 27;
+constexpr int kCbParams = kCbOffB3 + 1;
+static_assert(kCbA + kCbW + kCbD + 64 <= 160 * 1024 / 4, "LDS budget");
+
+// tap t of a 3x3x3 kernel: (dz, dy, dx) = (t / 9 - 1, (t / 3) % 3 - 1, t % 3 - 1)
+__device__ __forceinline__ int tap_off(int t, int G, int GG) {
+  return (t / 9 - 1) * GG + ((t / 3) % 3 - 1) * G + (t % 3 - 1);
+}
+
+// bit t set when voxel (z, y, x) + tap t lies inside the G^3 grid
+__device__ __forceinline__ uint32_t tap_mask(int z, int y, int x, int G) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int t = 0; t < 27; ++t) {
+    const int zz = z + t / 9 - 1, yy = y + (t / 3) % 3 - 1, xx = x + t % 3 - 1;
+    const bool ok = (static_cast<unsigned>(zz) < static_cast<unsigned>(G)) &
+                    (static_cast<unsigned>(yy) < static_cast<unsigned>(G)) &
+                    (static_cast<unsigned>(xx) < static_cast<unsigned>(G));
+    m |= static_cast<uint32_t>(ok) << t;
+  }
+  return m;
+}
+
+// sum over output voxels v with z in [z0, z1) of go[v] * in[v + off_t], v + off_t inside the grid
+__device__ __forceinline__ float wgrad_sum(const float* go, const float* in, int G, int GG, int t, int z0, int z1) {
+  const int dz = t / 9 - 1, dy = (t / 3) % 3 - 1, dx = t % 3 - 1;
+  const int zlo = max(z0, -dz), zhi = min(z1, G - dz);
+  const int ylo = max(0, -dy), yhi = min(G, G - dy);
+  const int xlo = max(0, -dx), xhi = min(G, G - dx);
+  const int off = dz * GG + dy * G + dx;
+  float acc = 0.f;
+  for (int z = zlo; z < zhi; ++z)
+    for (int y = ylo; y < yhi; ++y) {
+      const int base = z * GG + y * G;
+      for (int x = xlo; x < xhi; ++x) acc = __fmaf_rn(go[base + x], in[base + x + off], acc);
+    }
+  return acc;
+}
+
+__global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __restrict__ src, const float* __restrict__ tgt,
+                                                             int64_t t_p, int64_t t_f, int64_t t_c,
+                                                             const float* __restrict__ cand, int G,
+                                                             const float* __restrict__ params,
+                                                             const float* __restrict__ gvcp, float* __restrict__ gsrc,
+                                                             float* __restrict__ gtgt, float* __restrict__ gpart) {
+  __shared__ __attribute__((aligned(16))) float lds[kCbA + kCbW + kCbD];
+  __shared__ float red[32];
+  __shared__ float sv[32];
+  float* A = lds;
+  float* Wr = lds + kCbA;
+  float* D = Wr + kCbW;
+  const int p = blockIdx.x, tid = threadIdx.x;
+  const int C = G * G * G, GG = G * G;
+  const FastDiv dG(G), dGG(GG), dC(C);
+  const float* P1 = params;
+  const float* P2 = params + kCbOffW2;
+  const float* P3 = params + kCbOffW3;
+  float* gp = gpart + static_cast<int64_t>(p) * kCbParams;
+  const float* T = tgt + static_cast<int64_t>(p) * t_p;
+  if (tid < 32) sv[tid] = src[static_cast<int64_t>(p) * 32 + tid];
+
+  int vv[kCbV];
+  bool vok[kCbV];
+  uint32_t msk[kCbV];
+#pragma unroll
+  for (int k = 0; k < kCbV; ++k) {
+    const int v = tid + k * kCbThreads;
+    vok[k] = v < C;
+    vv[k] = vok[k] ? v : 0;
+    const uint32_t z = dGG.div(vv[k]), r = vv[k] - z * GG;
+    const uint32_t y = dG.div(r), x = r - y * G;
+    msk[k] = vok[k] ? tap_mask(z, y, x, G) : 0u;
+  }
+  // T[l] of the scrambled target block
+  auto tval = [&](int l) -> float {
+    const uint32_t f = dC.div(static_cast<uint32_t>(l));
+    return T[static_cast<int64_t>(f) * t_f + static_cast<int64_t>(l - static_cast<int>(f) * C) * t_c];
+  };
+
+  // ---- forward: conv1 (one cost channel at a time) -------------------------------------------
+  for (int i = tid; i < kCbW; i += kCbThreads) {  // torch (co, ci, kd, kh, kw) -> [ci][t][co]
+    const int co = i / (32 * 27), r = i % (32 * 27);
+    Wr[r * 16 + co] = P1[i];
+  }
+  float h1[kCbV][16];
+#pragma unroll
+  for (int k = 0; k < kCbV; ++k)
+#pragma unroll
+    for (int co = 0; co < 16; ++co) h1[k][co] = params[kCbOffB1 + co];
+  __syncthreads();
+#pragma unroll 1
+  for (int ci = 0; ci < 32; ++ci) {
+    for (int v = tid; v < C; v += kCbThreads) {
+      const float d = sv[ci] - tval(v * 32 + ci);
+      D[v] = d * d;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kCbV; ++k) {
+      if (!vok[k]) continue;
+#pragma unroll 1
+      for (int t = 0; t < 27; ++t) {
+        if (!((msk[k] >> t) & 1u)) continue;
+        const float c = D[vv[k] + tap_off(t, G, GG)];
+        const float* w = Wr + (ci * 27 + t) * 16;
+#pragma unroll
+        for (int co = 0; co < 16; ++co) h1[k][co] = __fmaf_rn(w[co], c, h1[k][co]);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int k = 0; k < kCbV; ++k)
+    if (vok[k])
+#pragma unroll
+      for (int co = 0; co < 16; ++co) A[co * C + vv[k]] = h1[k][co];
+  __syncthreads();
+
+  // ---- forward: conv2 -> D, conv3 -> logits ------------------------------------------------
+  float h2[kCbV][4];
+#pragma unroll
+  for (int k = 0; k < kCbV; ++k) {
+#pragma unroll
+    for (int co = 0; co < 4; ++co) h2[k][co] = params[kCbOffB2 + co];
+    if (!vok[k]) continue;
+#pragma unroll 1
+    for (int ci = 0; ci < 16; ++ci)
+#pragma unroll 1
+      for (int t = 0; t < 27; ++t) {
+        if (!((msk[k] >> t) & 1u)) continue;
+        const float c = A[ci * C + vv[k] + tap_off(t, G, GG)];
+#pragma unroll
+        for (int co = 0; co < 4; ++co) h2[k][co] = __fmaf_rn(P2[(co * 16 + ci) * 27 + t], c, h2[k][co]);
+      }
+  }
+#pragma unroll
+  for (int k = 0; k < kCbV; ++k)
+    if (vok[k])
+#pragma unroll
+      for (int co = 0; co < 4; ++co) D[co * C + vv[k]] = h2[k][co];
+  __syncthreads();
+  float lg[kCbV];
+  float lmax = -__builtin_huge_valf();
+#pragma unroll
+  for (int k = 0; k < kCbV; ++k) {
+    float a = 0.f;
+    if (vok[k]) {
+#pragma unroll 1
+      for (int ci = 0; ci < 4; ++ci)
+#pragma unroll 1
+        for (int t = 0; t < 27; ++t)
+          if ((msk[k] >> t) & 1u) a = __fmaf_rn(P3[ci * 27 + t], D[ci * C + vv[k] + tap_off(t, G, GG)], a);
+      lmax = fmaxf(lmax, a + params[kCbOffB3]);
+    }
+    lg[k] = a + params[kCbOffB3];
+  }
+
+  // ---- softmax + weighted mean and their backward ------------------------------------------
+  const float m = block_max_f(lmax, red);
+  float w[kCbV];
+  float se = 0.f;
+#pragma unroll
+  for (int k = 0; k < kCbV; ++k) {
+    w[k] = vok[k] ? expf(lg[k] - m) : 0.f;
+    se += w[k];
+  }
+  const float inv = 1.0f / block_sum(se, red);
+  const float* cq = cand + static_cast<int64_t>(p) * C * 3;
+  float sw = 0.f, sx = 0.f, sy = 0.f, sz = 0.f;
+#pragma unroll
+  for (int k = 0; k < kCbV; ++k) {
+    w[k] *= inv;
+    if (vok[k]) {
+      sw += w[k];
+      sx += w[k] * cq[vv[k] * 3 + 0];
+      sy += w[k] * cq[vv[k] * 3 + 1];
+      sz += w[k] * cq[vv[k] * 3 + 2];
+    }
+  }
+  sw = block_sum(sw, red);
+  sx = block_sum(sx, red);
+  sy = block_sum(sy, red);
+  sz = block_sum(sz, red);
+  const float g0 = gvcp[static_cast<int64_t>(p) * 3 + 0], g1 = gvcp[static_cast<int64_t>(p) * 3 + 1],
+              g2 = gvcp[static_cast<int64_t>(p) * 3 + 2];
+  const float gS = -(g0 * sx + g1 * sy + g2 * sz) / (sw * sw);
+  float gw[kCbV];
+  float dot = 0.f;
+#pragma unroll
+  for (int k = 0; k < kCbV; ++k) {
+    gw[k] = vok[k] ? (g0 * cq[vv[k] * 3 + 0] + g1 * cq[vv[k] * 3 + 1] + g2 * cq[vv[k] * 3 + 2]) / sw + gS : 0.f;
+    dot += w[k] * gw[k];
+  }
+  dot = block_sum(dot, red);
+  float* gl = Wr;  // conv1 weights are reloaded before the last phase
+  float gls = 0.f;
+#pragma unroll
+  for (int k = 0; k < kCbV; ++k)
+    if (vok[k]) {
+      const float v = w[k] * (gw[k] - dot);
+      gl[vv[k]] = v;
+      gls += v;
+    }
+  gls = block_sum(gls, red);  // (its barriers also publish gl)
+  if (tid == 0) gp[kCbOffB3] = gls;
+
+  // ---- conv3 backward: dW3 (z-chunked), dL/dh2 -------------------------------------------
+  float* scr = Wr + kCbMaxC + 16;
+  {
+    constexpr int kZc = 9;  // 108 taps x 9 z-chunks
+    if (tid < 108 * kZc) {
+      const int o = tid % 108, zc = tid / 108;
+      const int ci = o / 27, t = o % 27;
+      scr[tid] = wgrad_sum(gl, D + ci * C, G, GG, t, (zc * G) / kZc, ((zc + 1) * G) / kZc);
+    }
+    __syncthreads();
+    if (tid < 108) {
+      float s = 0.f;
+      for (int zc = 0; zc < kZc; ++zc) s += scr[zc * 108 + tid];
+      gp[kCbOffW3 + tid] = s;
+    }
+  }
+  float gh2[kCbV][4];
+#pragma unroll
+  for (int k = 0; k < kCbV; ++k)
+#pragma unroll
+    for (int ci = 0; ci < 4; ++ci) {
+      float a = 0.f;
+      if (vok[k])
+#pragma unroll 1
+        for (int t = 0; t < 27; ++t)
+          if ((msk[k] >> (26 - t)) & 1u) a = __fmaf_rn(P3[ci * 27 + t], gl[vv[k] - tap_off(t, G, GG)], a);
+      gh2[k][ci] = a;
+    }
+  __syncthreads();  // h2 readers done
+#pragma unroll
+  for (int k = 0; k < kCbV; ++k)
+    if (vok[k])
+#pragma unroll
+      for (int ci = 0; ci < 4; ++ci) D[ci * C + vv[k]] = gh2[k][ci];
+#pragma unroll
+  for (int ci = 0; ci < 4; ++ci) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < kCbV; ++k) s += gh2[k][ci];
+    s = block_sum(s, red);
+    if (tid == 0) gp[kCbOffB2 + ci] = s;
+  }
+
+  // ---- conv2 backward: dW2, dL/dh1 -----------------------------------------------------------
+  for (int o = tid; o < 4 * 16 * 27; o += kCbThreads) {
+    const int co = o / (16 * 27), r = o % (16 * 27), ci = r / 27, t = r % 27;
+    gp[kCbOffW2 + o] = wgrad_sum(D + co * C, A + ci * C, G, GG, t, 0, G);
+  }
+  float gh1[kCbV][16];
+#pragma unroll
+  for (int k = 0; k < kCbV; ++k) {
+#pragma unroll
+    for (int ci = 0; ci < 16; ++ci) gh1[k][ci] = 0.f;
+    if (!vok[k]) continue;
+#pragma unroll 1
+    for (int co = 0; co < 4; ++co)
+#pragma unroll 1
+      for (int t = 0; t < 27; ++t) {
+        if (!((msk[k] >> (26 - t)) & 1u)) continue;
+        const float g = D[co * C + vv[k] - tap_off(t, G, GG)];
+#pragma unroll
+        for (int ci = 0; ci < 16; ++ci) gh1[k][ci] = __fmaf_rn(P2[(co * 16 + ci) * 27 + t], g, gh1[k][ci]);
+      }
+  }
+  __syncthreads();  // h1 readers done
+#pragma unroll
+  for (int k = 0; k < kCbV; ++k)
+    if (vok[k])
+#pragma unroll
+      for (int ci = 0; ci < 16; ++ci) A[ci * C + vv[k]] = gh1[k][ci];
+#pragma unroll 1
+  for (int ci = 0; ci < 16; ++ci) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < kCbV; ++k) s += gh1[k][ci];
+    s = block_sum(s, red);
+    if (tid == 0) gp[kCbOffB1 + ci] = s;
+  }
+
+  // ---- conv1 backward (one cost channel at a time): dW1, dL/dcost -> dsrc, dtgt --------------
+  for (int i = tid; i < kCbW; i += kCbThreads) {
+    const int co = i / (32 * 27), r = i % (32 * 27);
+    Wr[r * 16 + co] = P1[i];
+  }
+  float* scr1 = D + kCbMaxC + 16;
+  float* gT = gtgt + static_cast<int64_t>(p) * 32 * C;
+#pragma unroll 1
+  for (int ci = 0; ci < 32; ++ci) {
+    __syncthreads();  // previous channel's readers of D are done
+    for (int v = tid; v < C; v += kCbThreads) {
+      const float d = sv[ci] - tval(v * 32 + ci);
+      D[v] = d * d;
+    }
+    __syncthreads();
+    if (tid < 2 * 432) {  // (co, t) x two z-halves
+      const int o = tid % 432, zc = tid / 432;
+      const int co = o / 27, t = o % 27;
+      scr1[tid] = wgrad_sum(A + co * C, D, G, GG, t, zc ? G / 2 : 0, zc ? G : G / 2);
+    }
+    float gs = 0.f;
+#pragma unroll
+    for (int k = 0; k < kCbV; ++k) {
+      if (!vok[k]) continue;
+      float gc = 0.f;
+#pragma unroll 1
+      for (int t = 0; t < 27; ++t) {
+        if (!((msk[k] >> (26 - t)) & 1u)) continue;
+        const int u = vv[k] - tap_off(t, G, GG);
+        const float* w = Wr + (ci * 27 + t) * 16;
+#pragma unroll
+        for (int co = 0; co < 16; ++co) gc = __fmaf_rn(w[co], A[co * C + u], gc);
+      }
+      const int l = vv[k] * 32 + ci;
+      const float d = sv[ci] - tval(l);
+      const float gd = 2.0f * d * gc;
+      gs += gd;
+      gT[l] = -gd;
+    }
+    gs = block_sum(gs, red);  // (its barriers also order scr1)
+    if (tid == 0) gsrc[static_cast<int64_t>(p) * 32 + ci] = gs;
+    if (tid < 432) {
+      const int co = tid / 27, t = tid % 27;
+      gp[(co * 32 + ci) * 27 + t] = scr1[tid] + scr1[tid + 432];
+    }
+  }
+}
+
+// grad[i] = sum over key points of part[p][i], in fp64, key-point order
+__global__ void cpg_bwd_reduce_kernel(const float* __restrict__ part, int P, float* __restrict__ grad) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= kCbParams) return;
+  double s = 0.0;
+  for (int p = 0; p < P; ++p) s += static_cast<double>(part[static_cast<int64_t>(p) * kCbParams + i]);
+  grad[i] = static_cast<float>(s);
+}
+
+}  // namespace dvcp
+
+extern "C" int64_t dvcp_cpg_backward_workspace_bytes(int P) {
+  return static_cast<int64_t>(P > 0 ? P : 0) * dvcp::kCbParams * static_cast<int64_t>(sizeof(float));
+}
+
+extern "C" int dvcp_cpg_backward(const float* src, const float* tgt, int64_t t_p, int64_t t_f, int64_t t_c,
+                                 const float* cand, int P, int G, const float* params, const float* grad_vcp,
+                                 float* grad_src, float* grad_tgt, float* ws, float* grad_params, void* stream) {
+  DVCP_REQUIRE(params && grad_params, "dvcp_cpg_backward: null pointer");
+  DVCP_REQUIRE(P <= 0 || (src && tgt && cand && grad_vcp && grad_src && grad_tgt && ws),
+               "dvcp_cpg_backward: null pointer");
+  DVCP_REQUIRE(G >= 2 && G * G * G <= dvcp::kCbMaxC, "dvcp_cpg_backward: grid side G=%d unsupported (2..11)", G);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (P > 0)
+    hipLaunchKernelGGL(dvcp::cpg_bwd_kernel, dim3(P), dim3(dvcp::kCbThreads), 0, st, src, tgt, t_p, t_f, t_c, cand, G,
+                       params, grad_vcp, grad_src, grad_tgt, ws);
+  hipLaunchKernelGGL(dvcp::cpg_bwd_reduce_kernel, dim3(dvcp::ceil_div(dvcp::kCbParams, 256)), dim3(256), 0, st, ws,
+                     P > 0 ? P : 0, grad_params);
+  return dvcp::launch_status("dvcp_cpg_backward");
+}

@@ -12,6 +12,7 @@
 // are wave-uniform scalar loads; the max over a query's 32 rows goes through LDS.
 #include "common.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace dvcp {
@@ -77,26 +78,19 @@ __global__ __launch_bounds__(kDfeThreads) void dfe_kernel(const XT* __restrict__
   dfe_pool_store(y, red, q0, R, out);
 }
 
+// Row j = tid % 32 of query q (batch b) of get_cat_feat_tgt.py:54-96 -> x[35], for a block of 8
+// queries x 32 rows (every thread calls; it synchronises).  dsh: kDfeThreads doubles, wq: [8][32].
 template <typename T>
-__global__ __launch_bounds__(kDfeThreads) void dfe_tgt_kernel(PointsView<T> ref, const float* __restrict__ feat, int M,
-                                                              const float* __restrict__ cand,
-                                                              const float* __restrict__ dist,
-                                                              const int32_t* __restrict__ idx, int Q,
-                                                              const float* __restrict__ params,
-                                                              float* __restrict__ out) {
-  __shared__ float red[kDfeThreads][33];
-  __shared__ double wq[kDfeQPerBlock][32];
-  const int b = blockIdx.y;
+__device__ __forceinline__ void dfe_tgt_row(PointsView<T> ref, const float* __restrict__ feat, int M,
+                                            const float* __restrict__ cand, const float* __restrict__ dist,
+                                            const int32_t* __restrict__ idx, int Q, int b, int64_t q, bool live,
+                                            double* dsh, double (*wq)[32], float (&x)[35]) {
   const int tid = threadIdx.x, ql = tid / 32, j = tid % 32;
-  const int64_t q0 = static_cast<int64_t>(blockIdx.x) * kDfeQPerBlock;
-  const int64_t q = q0 + ql;
-  const bool live = q < Q;
   const int64_t kq = (static_cast<int64_t>(b) * Q + (live ? q : 0)) * 32;
   // get_cat_feat_tgt.py:57-58: dist_sum in fp64, w = dist / dist_sum (fp64)
   const float dj = live ? dist[kq + j] : 1.0f;
   double s = static_cast<double>(dj);
   // fixed-order fp64 sum over the query's 32 neighbours (lanes ql*32 .. ql*32+31)
-  __shared__ double dsh[kDfeThreads];
   dsh[tid] = s;
   __syncthreads();
   double acc = 0.0;
@@ -104,7 +98,6 @@ __global__ __launch_bounds__(kDfeThreads) void dfe_tgt_kernel(PointsView<T> ref,
   wq[ql][j] = static_cast<double>(dj) / acc;
   __syncthreads();
 
-  float x[35];
   int n = live ? idx[kq + j] : 0;
   n = n < 0 ? 0 : (n >= M ? M - 1 : n);
   const float* cq = cand + (static_cast<int64_t>(b) * Q + (live ? q : 0)) * 3;
@@ -122,10 +115,167 @@ __global__ __launch_bounds__(kDfeThreads) void dfe_tgt_kernel(PointsView<T> ref,
     x[3 + 4 * f4 + 2] = static_cast<float>(static_cast<double>(v.z) * wq[ql][4 * f4 + 2]);
     x[3 + 4 * f4 + 3] = static_cast<float>(static_cast<double>(v.w) * wq[ql][4 * f4 + 3]);
   }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kDfeThreads) void dfe_tgt_kernel(PointsView<T> ref, const float* __restrict__ feat, int M,
+                                                              const float* __restrict__ cand,
+                                                              const float* __restrict__ dist,
+                                                              const int32_t* __restrict__ idx, int Q,
+                                                              const float* __restrict__ params,
+                                                              float* __restrict__ out) {
+  __shared__ float red[kDfeThreads][33];
+  __shared__ double wq[kDfeQPerBlock][32];
+  __shared__ double dsh[kDfeThreads];
+  const int b = blockIdx.y;
+  const int64_t q0 = static_cast<int64_t>(blockIdx.x) * kDfeQPerBlock;
+  const int64_t q = q0 + threadIdx.x / 32;
+  float x[35];
+  dfe_tgt_row(ref, feat, M, cand, dist, idx, Q, b, q, q < Q, dsh, wq, x);
   float y[32];
   dfe_mlp(x, y, params);
   dfe_pool_store(y, red, static_cast<int64_t>(b) * Q + q0,
                  static_cast<int64_t>(b) * Q + min(static_cast<int64_t>(Q), q0 + kDfeQPerBlock), out);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Backward (train.py:121 loss.backward() through deep_feat_embedding.py:23-61).  The three layers
+// are linear (Q14), so with g3 the gradient the max-pool routes to the arg-max row of each output
+// channel (MaxPool1d: first index among equal values), every weight gradient is a fixed linear
+// map of just two sums over all routed rows:
+//   Gx[f][c] = sum_q g[q,f] x[q, j*(q,f), c]   (32 x 35),     gs[f] = sum_q g[q,f]
+//   Gh1 = Gx W1^T + gs b1^T,  Gh2 = Gh1 W2^T + gs b2^T
+//   dW3 = Gh2, db3 = gs;  dW2 = W3^T Gh1, db2 = W3^T gs;  dW1 = W2^T W3^T Gx, db1 = W2^T W3^T gs.
+// dfe_bwd_kernel re-runs the forward rows layer by layer (the reference's fp32 arithmetic) to find
+// j*, and accumulates Gx, gs per workgroup (fixed grid, fixed order: deterministic);
+// dfe_bwd_finish_kernel sums the workgroup partials in fp64 and applies the map.
+constexpr int kDfeGPart = 32 * 36;  // per workgroup: [f][35 Gx + gs]
+constexpr int kDfeBwdMaxGrid = 2048;
+
+template <int MODE, typename T>  // MODE 0: materialised rows X (R, 32, 35); 1: fused target rows
+__global__ __launch_bounds__(kDfeThreads) void dfe_bwd_kernel(const T* __restrict__ X, PointsView<T> ref,
+                                                              const float* __restrict__ feat, int M,
+                                                              const float* __restrict__ cand,
+                                                              const float* __restrict__ dist,
+                                                              const int32_t* __restrict__ idx, int Q, int64_t R,
+                                                              const float* __restrict__ params,
+                                                              const float* __restrict__ gout, float* __restrict__ part) {
+  __shared__ float ys[kDfeThreads][33];
+  __shared__ float xs[kDfeThreads][37];
+  __shared__ double wq[kDfeQPerBlock][32];
+  __shared__ double dsh[kDfeThreads];
+  const int tid = threadIdx.x, ql = tid / 32, f = tid % 32;
+  float acc[36];
+#pragma unroll
+  for (int i = 0; i < 36; ++i) acc[i] = 0.f;
+  for (int64_t q0 = static_cast<int64_t>(blockIdx.x) * kDfeQPerBlock; q0 < R;
+       q0 += static_cast<int64_t>(gridDim.x) * kDfeQPerBlock) {
+    const int64_t q = q0 + ql;
+    const bool live = q < R;
+    float x[35];
+    if constexpr (MODE == 0) {
+      const T* src = X + ((live ? q : 0) * 32 + f) * 35;
+#pragma unroll
+      for (int i = 0; i < 35; ++i) x[i] = live ? static_cast<float>(src[i]) : 0.f;
+    } else {
+      const int b = static_cast<int>((live ? q : 0) / Q);
+      const int64_t qq = (live ? q : 0) - static_cast<int64_t>(b) * Q;
+      dfe_tgt_row(ref, feat, M, cand, dist, idx, Q, b, qq, live, dsh, wq, x);
+    }
+    float y[32];
+    dfe_mlp(x, y, params);
+    __syncthreads();  // the previous group's readers are done
+#pragma unroll
+    for (int c = 0; c < 32; ++c) ys[tid][c] = y[c];
+#pragma unroll
+    for (int i = 0; i < 35; ++i) xs[tid][i] = x[i];
+    __syncthreads();
+    // thread (ql, f): the row the max-pool picked for channel f
+    float best = ys[ql * 32][f];
+    int bj = 0;
+    for (int r = 1; r < 32; ++r) {
+      const float v = ys[ql * 32 + r][f];
+      if (v > best) {
+        best = v;
+        bj = r;
+      }
+    }
+    const float g = live ? gout[q * 32 + f] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 35; ++i) acc[i] = __fmaf_rn(g, xs[ql * 32 + bj][i], acc[i]);
+    acc[35] += g;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 36; ++i) xs[tid][i] = acc[i];
+  __syncthreads();
+  for (int e = tid; e < kDfeGPart; e += kDfeThreads) {
+    const int ff = e / 36, i = e % 36;
+    float s = 0.f;
+    for (int k = 0; k < kDfeQPerBlock; ++k) s += xs[k * 32 + ff][i];
+    part[static_cast<int64_t>(blockIdx.x) * kDfeGPart + e] = s;
+  }
+}
+
+// One 1024-thread workgroup: partials -> packed parameter gradients (W1, b1, W2, b2, W3, b3).
+__global__ __launch_bounds__(1024) void dfe_bwd_finish_kernel(const float* __restrict__ part, int nblk,
+                                                              const float* __restrict__ params,
+                                                              float* __restrict__ grad) {
+  __shared__ double Gs[kDfeGPart];
+  __shared__ double Gh1[32][33];
+  __shared__ double U[32][36];  // W3^T [Gx | gs]
+  const int tid = threadIdx.x;
+  const float* W1 = params;
+  const float* b1 = W1 + 32 * 35;
+  const float* W2 = b1 + 32;
+  const float* b2 = W2 + 32 * 32;
+  const float* W3 = b2 + 32;
+  float* gW1 = grad;
+  float* gb1 = gW1 + 32 * 35;
+  float* gW2 = gb1 + 32;
+  float* gb2 = gW2 + 32 * 32;
+  float* gW3 = gb2 + 32;
+  float* gb3 = gW3 + 32 * 32;
+  for (int e = tid; e < kDfeGPart; e += 1024) {
+    double s = 0.0;
+    for (int k = 0; k < nblk; ++k) s += static_cast<double>(part[static_cast<int64_t>(k) * kDfeGPart + e]);
+    Gs[e] = s;
+  }
+  __syncthreads();
+  {  // Gh1[f][k] = sum_c Gx[f][c] W1[k][c] + gs[f] b1[k]
+    const int ff = tid / 32, k = tid % 32;
+    double v = Gs[ff * 36 + 35] * b1[k];
+    for (int c = 0; c < 35; ++c) v += Gs[ff * 36 + c] * W1[k * 35 + c];
+    Gh1[ff][k] = v;
+  }
+  for (int e = tid; e < 32 * 36; e += 1024) {  // U[m][c] = sum_f W3[f][m] [Gx | gs][f][c]
+    const int m = e / 36, c = e % 36;
+    double v = 0.0;
+    for (int ff = 0; ff < 32; ++ff) v += static_cast<double>(W3[ff * 32 + m]) * Gs[ff * 36 + c];
+    U[m][c] = v;
+  }
+  __syncthreads();
+  {
+    const int ff = tid / 32, m = tid % 32;
+    // dW3[f][m] = Gh2[f][m] = sum_k Gh1[f][k] W2[m][k] + gs[f] b2[m]
+    double v = Gs[ff * 36 + 35] * b2[m];
+    for (int k = 0; k < 32; ++k) v += Gh1[ff][k] * W2[m * 32 + k];
+    gW3[ff * 32 + m] = static_cast<float>(v);
+    // dW2[m'][k'] = sum_f W3[f][m'] Gh1[f][k']   (thread: m' = ff, k' = m)
+    double w = 0.0;
+    for (int f2 = 0; f2 < 32; ++f2) w += static_cast<double>(W3[f2 * 32 + ff]) * Gh1[f2][m];
+    gW2[ff * 32 + m] = static_cast<float>(w);
+  }
+  for (int e = tid; e < 32 * 36; e += 1024) {  // dW1[k][c] / db1[k] = sum_m W2[m][k] U[m][c]
+    const int k = e / 36, c = e % 36;
+    double v = 0.0;
+    for (int m = 0; m < 32; ++m) v += static_cast<double>(W2[m * 32 + k]) * U[m][c];
+    if (c < 35) gW1[k * 35 + c] = static_cast<float>(v); else gb1[k] = static_cast<float>(v);
+  }
+  if (tid < 32) {
+    gb2[tid] = static_cast<float>(U[tid][35]);
+    gb3[tid] = static_cast<float>(Gs[tid * 36 + 35]);
+  }
 }
 
 }  // namespace dvcp
@@ -178,4 +328,64 @@ extern "C" int dvcp_dfe_tgt(int dtype, const void* ref_xyz, int64_t rb, int64_t 
     return DVCP_EINVAL;
   }
   return dvcp::launch_status("dvcp_dfe_tgt");
+}
+
+extern "C" int64_t dvcp_dfe_backward_workspace_bytes(int64_t R) {
+  const int64_t nblk = R <= 0 ? 1 : std::min<int64_t>(dvcp::kDfeBwdMaxGrid, (R + dvcp::kDfeQPerBlock - 1) / dvcp::kDfeQPerBlock);
+  return nblk * dvcp::kDfeGPart * static_cast<int64_t>(sizeof(float));
+}
+
+// mode 0: X (R, 32, 35) rows (x_dtype); mode 1: fused target rows (the dvcp_dfe_tgt arguments, R = B*Q).
+static int dfe_backward_launch(int mode, int dtype, const void* X, const void* ref_xyz, int64_t rb, int64_t rc,
+                               int64_t rn, int M, const float* ref_feat, const float* cand, const float* dist,
+                               const int32_t* idx, int Q, int64_t R, const float* params, const float* grad_out,
+                               float* ws, float* grad_params, hipStream_t st) {
+  if (R <= 0) {  // no rows: zero gradients
+    hipLaunchKernelGGL(dvcp::dfe_bwd_finish_kernel, dim3(1), dim3(1024), 0, st, ws, 0, params, grad_params);
+    return dvcp::launch_status("dvcp_dfe_backward");
+  }
+  const int nblk = static_cast<int>(dvcp_dfe_backward_workspace_bytes(R) / (dvcp::kDfeGPart * sizeof(float)));
+  const dim3 grid(nblk), block(dvcp::kDfeThreads);
+  if (mode == 0 && dtype == DVCP_F32)
+    hipLaunchKernelGGL((dvcp::dfe_bwd_kernel<0, float>), grid, block, 0, st, static_cast<const float*>(X),
+                       dvcp::PointsView<float>{nullptr, 0, 0, 0}, nullptr, 0, nullptr, nullptr, nullptr, 1, R, params,
+                       grad_out, ws);
+  else if (mode == 0 && dtype == DVCP_F64)
+    hipLaunchKernelGGL((dvcp::dfe_bwd_kernel<0, double>), grid, block, 0, st, static_cast<const double*>(X),
+                       dvcp::PointsView<double>{nullptr, 0, 0, 0}, nullptr, 0, nullptr, nullptr, nullptr, 1, R, params,
+                       grad_out, ws);
+  else if (mode == 1 && dtype == DVCP_F32)
+    hipLaunchKernelGGL((dvcp::dfe_bwd_kernel<1, float>), grid, block, 0, st, nullptr,
+                       dvcp::PointsView<float>{static_cast<const float*>(ref_xyz), rb, rc, rn}, ref_feat, M, cand, dist,
+                       idx, Q, R, params, grad_out, ws);
+  else if (mode == 1 && dtype == DVCP_F64)
+    hipLaunchKernelGGL((dvcp::dfe_bwd_kernel<1, double>), grid, block, 0, st, nullptr,
+                       dvcp::PointsView<double>{static_cast<const double*>(ref_xyz), rb, rc, rn}, ref_feat, M, cand,
+                       dist, idx, Q, R, params, grad_out, ws);
+  else {
+    dvcp::set_error("dvcp_dfe_backward: bad dtype %d", dtype);
+    return DVCP_EINVAL;
+  }
+  hipLaunchKernelGGL(dvcp::dfe_bwd_finish_kernel, dim3(1), dim3(1024), 0, st, ws, nblk, params, grad_params);
+  return dvcp::launch_status("dvcp_dfe_backward");
+}
+
+extern "C" int dvcp_dfe_backward(int x_dtype, const void* X, int64_t R, const float* params, const float* grad_out,
+                                 float* ws, float* grad_params, void* stream) {
+  DVCP_REQUIRE(params && grad_params && (R <= 0 || (X && grad_out && ws)), "dvcp_dfe_backward: null pointer");
+  return dfe_backward_launch(0, x_dtype, X, nullptr, 0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, 1, R, params,
+                             grad_out, ws, grad_params, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dvcp_dfe_tgt_backward(int dtype, const void* ref_xyz, int64_t rb, int64_t rc, int64_t rn, int M,
+                                     const float* ref_feat, const float* cand, const float* dist, const int32_t* idx,
+                                     int B, int Q, const float* params, const float* grad_out, float* ws,
+                                     float* grad_params, void* stream) {
+  DVCP_REQUIRE(params && grad_params, "dvcp_dfe_tgt_backward: null pointer");
+  DVCP_REQUIRE(B == 0 || Q == 0 || (ref_xyz && ref_feat && cand && dist && idx && grad_out && ws),
+               "dvcp_dfe_tgt_backward: null pointer");
+  DVCP_REQUIRE(M > 0 && B >= 0 && Q >= 0, "dvcp_dfe_tgt_backward: bad sizes");
+  return dfe_backward_launch(1, dtype, nullptr, ref_xyz, rb, rc, rn, M, ref_feat, cand, dist, idx, Q > 0 ? Q : 1,
+                             static_cast<int64_t>(B) * Q, params, grad_out, ws, grad_params,
+                             static_cast<hipStream_t>(stream));
 }

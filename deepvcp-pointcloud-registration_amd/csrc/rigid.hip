@@ -18,8 +18,9 @@ struct Mat3 {
   double m[3][3];
 };
 
-// One-sided Jacobi SVD of A (3x3): A V = U diag(s).  Returns R = V U^T.
-__device__ void kabsch_rotation(const double (&H)[3][3], double (&R)[3][3]) {
+// One-sided Jacobi SVD of H (3x3): H V = U diag(sig), i.e. H = U diag(sig) V^T.  Returns R = V U^T
+// and U, sig (the backward needs them).
+__device__ void kabsch_svd(const double (&H)[3][3], double (&R)[3][3], double (&U)[3][3], double (&sig)[3]) {
   double A[3][3], V[3][3];
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) {
@@ -52,7 +53,6 @@ __device__ void kabsch_rotation(const double (&H)[3][3], double (&R)[3][3]) {
     }
     if (!rotated) break;
   }
-  double U[3][3], sig[3];
   for (int j = 0; j < 3; ++j) sig[j] = sqrt(A[0][j] * A[0][j] + A[1][j] * A[1][j] + A[2][j] * A[2][j]);
   const double smax = fmax(sig[0], fmax(sig[1], sig[2]));
   int bad = -1;
@@ -71,6 +71,11 @@ __device__ void kabsch_rotation(const double (&H)[3][3], double (&R)[3][3]) {
   }
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) R[i][j] = V[i][0] * U[j][0] + V[i][1] * U[j][1] + V[i][2] * U[j][2];
+}
+
+__device__ void kabsch_rotation(const double (&H)[3][3], double (&R)[3][3]) {
+  double U[3][3], sig[3];
+  kabsch_svd(H, R, U, sig);
 }
 
 // Kabsch on the columns listed in sel[0..m) (or 0..m-1 when sel == nullptr) of x, y (3 x n
@@ -139,30 +144,29 @@ __global__ __launch_bounds__(kRgThreads) void rigid_transform_kernel(const doubl
   }
 }
 
-__global__ __launch_bounds__(kRgThreads) void svd_opt_kernel(const double* __restrict__ xg, const double* __restrict__ yg,
-                                                             const double* __restrict__ Rtrue,
-                                                             const double* __restrict__ ttrue, int n, int n_in,
-                                                             double* __restrict__ R2out, double* __restrict__ t2out,
-                                                             double* __restrict__ x1out, double* __restrict__ y2out,
-                                                             double* __restrict__ partial) {
-  __shared__ double xs[3 * kRgMaxN], ys[3 * kRgMaxN], y1[3 * kRgMaxN];
-  __shared__ float nn[kRgMaxN];
-  __shared__ int sel[kRgMaxN];
-  __shared__ double scratch[16];
-  __shared__ double rt[12];
+// The forward of svd_optimization up to the second Kabsch: x, y_pred staged in xs, ys (3 x n);
+// y1 = R1 x + t1; sel[0..n_in) the inliers in rank order.  Shared by the forward and the backward.
+struct SvdOptLds {
+  double xs[3 * kRgMaxN], ys[3 * kRgMaxN], y1[3 * kRgMaxN];
+  float nn[kRgMaxN];
+  int sel[kRgMaxN];
+  double scratch[16];
+  double rt[12];
+};
+
+__device__ void svd_opt_front(SvdOptLds& L, const double* __restrict__ xg, const double* __restrict__ yg,
+                              const double (&Rt)[3][3], const double (&tt)[3], int n, int n_in, double (&R1)[3][3],
+                              double (&t1)[3], double (&R2)[3][3], double (&t2)[3]) {
   const int b = blockIdx.x, tid = threadIdx.x;
   for (int e = tid; e < 3 * n; e += kRgThreads) {
-    xs[e] = xg[static_cast<int64_t>(b) * 3 * n + e];
-    ys[e] = yg[static_cast<int64_t>(b) * 3 * n + e];
+    L.xs[e] = xg[static_cast<int64_t>(b) * 3 * n + e];
+    L.ys[e] = yg[static_cast<int64_t>(b) * 3 * n + e];
   }
   __syncthreads();
-  double R1[3][3], t1[3];
-  block_kabsch(xs, ys, n, nullptr, n, R1, t1, scratch, rt);
+  const double* xs = L.xs;
+  block_kabsch(xs, L.ys, n, nullptr, n, R1, t1, L.scratch, L.rt);
   for (int j = tid; j < n; j += kRgThreads)
-    for (int a = 0; a < 3; ++a) y1[a * n + j] = affine_row(R1, t1, a, xs[j], xs[n + j], xs[2 * n + j]);
-  double Rt[3][3], tt[3];
-  for (int a = 0; a < 9; ++a) Rt[a / 3][a % 3] = Rtrue[b * 9 + a];
-  for (int a = 0; a < 3; ++a) tt[a] = ttrue[b * 3 + a];
+    for (int a = 0; a < 3; ++a) L.y1[a * n + j] = affine_row(R1, t1, a, xs[j], xs[n + j], xs[2 * n + j]);
   __syncthreads();
   // 1-NN (knn_cuda: both inputs .float()) of y_true_j against y1
   for (int j = tid; j < n; j += kRgThreads) {
@@ -171,24 +175,41 @@ __global__ __launch_bounds__(kRgThreads) void svd_opt_kernel(const double* __res
     const float qz = static_cast<float>(affine_row(Rt, tt, 2, xs[j], xs[n + j], xs[2 * n + j]));
     float best = __builtin_huge_valf();
     for (int i = 0; i < n; ++i) {
-      const float dx = static_cast<float>(y1[i]) - qx, dy = static_cast<float>(y1[n + i]) - qy,
-                  dz = static_cast<float>(y1[2 * n + i]) - qz;
+      const float dx = static_cast<float>(L.y1[i]) - qx, dy = static_cast<float>(L.y1[n + i]) - qy,
+                  dz = static_cast<float>(L.y1[2 * n + i]) - qz;
       const float d2 = (dx * dx + dy * dy) + dz * dz;
       best = d2 < best ? d2 : best;
     }
-    nn[j] = sqrt_rn(best);
+    L.nn[j] = sqrt_rn(best);
   }
   __syncthreads();
   // inliers: rank by (distance, index); rank < n_in lands at position rank
   for (int j = tid; j < n; j += kRgThreads) {
-    const float dj = nn[j];
+    const float dj = L.nn[j];
     int rank = 0;
-    for (int i = 0; i < n; ++i) rank += (nn[i] < dj || (nn[i] == dj && i < j)) ? 1 : 0;
-    if (rank < n_in) sel[rank] = j;
+    for (int i = 0; i < n; ++i) rank += (L.nn[i] < dj || (L.nn[i] == dj && i < j)) ? 1 : 0;
+    if (rank < n_in) L.sel[rank] = j;
   }
   __syncthreads();
-  double R2[3][3], t2[3];
-  block_kabsch(xs, y1, n, sel, n_in, R2, t2, scratch, rt);
+  block_kabsch(xs, L.y1, n, L.sel, n_in, R2, t2, L.scratch, L.rt);
+}
+
+__global__ __launch_bounds__(kRgThreads) void svd_opt_kernel(const double* __restrict__ xg, const double* __restrict__ yg,
+                                                             const double* __restrict__ Rtrue,
+                                                             const double* __restrict__ ttrue, int n, int n_in,
+                                                             double* __restrict__ R2out, double* __restrict__ t2out,
+                                                             double* __restrict__ x1out, double* __restrict__ y2out,
+                                                             double* __restrict__ partial) {
+  __shared__ SvdOptLds L;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  double Rt[3][3], tt[3];
+  for (int a = 0; a < 9; ++a) Rt[a / 3][a % 3] = Rtrue[b * 9 + a];
+  for (int a = 0; a < 3; ++a) tt[a] = ttrue[b * 3 + a];
+  double R1[3][3], t1[3], R2[3][3], t2[3];
+  svd_opt_front(L, xg, yg, Rt, tt, n, n_in, R1, t1, R2, t2);
+  const double* xs = L.xs;
+  const int* sel = L.sel;
+  double* scratch = L.scratch;
   double sabs = 0, sdif = 0;
   for (int k = tid; k < n_in; k += kRgThreads) {
     const int j = sel[k];
@@ -211,6 +232,163 @@ __global__ __launch_bounds__(kRgThreads) void svd_opt_kernel(const double* __res
       partial[b * 2 + 1] = sdif;
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Backward of deepVCP_loss (deepVCP_loss.py:57-121) with respect to y_pred, for loss.backward()
+// in train.py:121.  The gradient follows the reference's autograd graph: loss <- y2 = R2 x1 + t2
+// <- Kabsch(x1, y1[inliers]) <- y1 = R1 x + t1 <- Kabsch(x, y_pred).  The 1-NN distances and the
+// top-k inlier choice carry no gradient (knn_cuda runs under no_grad; topk indices).
+//
+// Kabsch backward: R = V U^T is the orthogonal polar factor of H^T = R P, P = U diag(s) U^T.  For
+// an incoming gR, with M = skew(R^T gR) and Y the solution of P Y + Y P = M (in U's basis:
+// Y~_ij = M~_ij / (s_i + s_j)), dL/dH = -2 Y R^T.  This is the derivative torch.svd's backward
+// gives for R = V U^T when the singular values are distinct, and it stays finite when they repeat.
+// t = cy - R cx adds gR -= gt cx^T and d/dcy = gt.
+
+// Adds (or writes, when `write`) dL/dy for the selected columns of y.  Block-wide.
+__device__ void block_kabsch_bwd(const double* x, const double* y, int n, const int* sel, int m, const double (&gR)[3][3],
+                                 const double (&gt)[3], double* gy, bool write, double* scratch, double* shared) {
+  const int tid = threadIdx.x;
+  double c[6];
+  for (int a = 0; a < 6; ++a) c[a] = 0;
+  for (int k = tid; k < m; k += blockDim.x) {
+    const int j = sel ? sel[k] : k;
+    for (int a = 0; a < 3; ++a) {
+      c[a] += x[a * n + j];
+      c[3 + a] += y[a * n + j];
+    }
+  }
+  double cen[6];
+  for (int a = 0; a < 6; ++a) cen[a] = block_sum(c[a], scratch) / static_cast<double>(m);
+  double h[9], sdx[3] = {0, 0, 0};
+  for (int a = 0; a < 9; ++a) h[a] = 0;
+  for (int k = tid; k < m; k += blockDim.x) {
+    const int j = sel ? sel[k] : k;
+    double dx[3], dy[3];
+    for (int a = 0; a < 3; ++a) {
+      dx[a] = x[a * n + j] - cen[a];
+      dy[a] = y[a * n + j] - cen[3 + a];
+      sdx[a] += dx[a];
+    }
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) h[a * 3 + b] = fma(dx[a], dy[b], h[a * 3 + b]);
+  }
+  double H[3][3];
+  for (int a = 0; a < 9; ++a) H[a / 3][a % 3] = block_sum(h[a], scratch);
+  for (int a = 0; a < 3; ++a) sdx[a] = block_sum(sdx[a], scratch);
+  if (tid == 0) {
+    double R[3][3], U[3][3], s[3], G[3][3], M[3][3], Mt[3][3], Y[3][3], Q[3][3];
+    kabsch_svd(H, R, U, s);
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) G[a][b] = gR[a][b] - gt[a] * cen[b];
+    // M = (R^T G - G^T R) / 2
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) {
+        double p = 0, q = 0;
+        for (int k = 0; k < 3; ++k) {
+          p += R[k][a] * G[k][b];
+          q += G[k][a] * R[k][b];
+        }
+        M[a][b] = 0.5 * (p - q);
+      }
+    // Mt = U^T M U; Y~ = Mt / (s_i + s_j); Y = U Y~ U^T
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) {
+        double v = 0;
+        for (int k = 0; k < 3; ++k)
+          for (int l = 0; l < 3; ++l) v += U[k][a] * M[k][l] * U[l][b];
+        const double den = s[a] + s[b];
+        Mt[a][b] = den > 0 ? v / den : 0.0;
+      }
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) {
+        double v = 0;
+        for (int k = 0; k < 3; ++k)
+          for (int l = 0; l < 3; ++l) v += U[a][k] * Mt[k][l] * U[b][l];
+        Y[a][b] = v;
+      }
+    // gH = -2 Y R^T
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) {
+        double v = 0;
+        for (int k = 0; k < 3; ++k) v += Y[a][k] * R[b][k];
+        Q[a][b] = -2.0 * v;
+        shared[a * 3 + b] = Q[a][b];
+      }
+  }
+  __syncthreads();
+  double gH[3][3];
+  for (int a = 0; a < 9; ++a) gH[a / 3][a % 3] = shared[a];
+  __syncthreads();
+  // dy_k = y_k - cy: dL/dy_k = gH^T dx_k - mean_k(gH^T dx_k) + gt / m
+  double mean[3];
+  for (int b = 0; b < 3; ++b)
+    mean[b] = (gH[0][b] * sdx[0] + gH[1][b] * sdx[1] + gH[2][b] * sdx[2]) / static_cast<double>(m);
+  for (int k = tid; k < m; k += blockDim.x) {
+    const int j = sel ? sel[k] : k;
+    double dx[3];
+    for (int a = 0; a < 3; ++a) dx[a] = x[a * n + j] - cen[a];
+    for (int b = 0; b < 3; ++b) {
+      const double v = (gH[0][b] * dx[0] + gH[1][b] * dx[1] + gH[2][b] * dx[2]) - mean[b] + gt[b] / static_cast<double>(m);
+      gy[b * n + j] = write ? v : gy[b * n + j] + v;
+    }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kRgThreads) void svd_opt_bwd_kernel(
+    const double* __restrict__ xg, const double* __restrict__ yg, const double* __restrict__ Rtrue,
+    const double* __restrict__ ttrue, int n, int n_in, int B, const double* __restrict__ partial,
+    const double* __restrict__ gloss, double alpha, double inv_count, double* __restrict__ gy_out) {
+  __shared__ SvdOptLds L;
+  __shared__ double gy1[3 * kRgMaxN];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  double Rt[3][3], tt[3];
+  for (int a = 0; a < 9; ++a) Rt[a / 3][a % 3] = Rtrue[b * 9 + a];
+  for (int a = 0; a < 3; ++a) tt[a] = ttrue[b * 3 + a];
+  double R1[3][3], t1[3], R2[3][3], t2[3];
+  svd_opt_front(L, xg, yg, Rt, tt, n, n_in, R1, t1, R2, t2);
+  const double* xs = L.xs;
+  // loss = alpha * mean|y_true1 - y2| + (1 - alpha) * |mean(y2 - y_true1)| over all B*3*n_in values
+  double tot = 0;
+  for (int bb = 0; bb < B; ++bb) tot += partial[bb * 2 + 1];
+  const double sm = tot > 0 ? 1.0 : (tot < 0 ? -1.0 : 0.0);
+  const double G = gloss[0] * inv_count;
+  double gr[12];
+  for (int a = 0; a < 12; ++a) gr[a] = 0;
+  for (int k = tid; k < n_in; k += kRgThreads) {
+    const int j = L.sel[k];
+    for (int a = 0; a < 3; ++a) {
+      const double d = affine_row(R2, t2, a, xs[j], xs[n + j], xs[2 * n + j]) -
+                       affine_row(Rt, tt, a, xs[j], xs[n + j], xs[2 * n + j]);
+      const double sd = d > 0 ? 1.0 : (d < 0 ? -1.0 : 0.0);
+      const double g = G * (alpha * sd + (1.0 - alpha) * sm);
+      for (int c = 0; c < 3; ++c) gr[a * 3 + c] += g * xs[c * n + j];
+      gr[9 + a] += g;
+    }
+  }
+  double gR[3][3], gt[3];
+  for (int a = 0; a < 12; ++a) {
+    const double v = block_sum(gr[a], L.scratch);
+    if (a < 9) gR[a / 3][a % 3] = v; else gt[a - 9] = v;
+  }
+  for (int e = tid; e < 3 * n; e += kRgThreads) gy1[e] = 0;
+  __syncthreads();
+  block_kabsch_bwd(xs, L.y1, n, L.sel, n_in, gR, gt, gy1, false, L.scratch, L.rt);
+  // y1 = R1 x + t1 over all n columns
+  for (int a = 0; a < 12; ++a) gr[a] = 0;
+  for (int j = tid; j < n; j += kRgThreads)
+    for (int a = 0; a < 3; ++a) {
+      const double g = gy1[a * n + j];
+      for (int c = 0; c < 3; ++c) gr[a * 3 + c] += g * xs[c * n + j];
+      gr[9 + a] += g;
+    }
+  for (int a = 0; a < 12; ++a) {
+    const double v = block_sum(gr[a], L.scratch);
+    if (a < 9) gR[a / 3][a % 3] = v; else gt[a - 9] = v;
+  }
+  block_kabsch_bwd(xs, L.ys, n, nullptr, n, gR, gt, gy_out + static_cast<int64_t>(b) * 3 * n, true, L.scratch, L.rt);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -287,4 +465,20 @@ extern "C" int dvcp_svd_optimization(const double* x, const double* y_pred, cons
   hipLaunchKernelGGL(dvcp::svd_opt_kernel, dim3(B), dim3(dvcp::kRgThreads), 0, static_cast<hipStream_t>(stream), x,
                      y_pred, R_true, t_true, n, n_in, R2, t2, x1, y2, partial);
   return dvcp::launch_status("dvcp_svd_optimization");
+}
+
+extern "C" int dvcp_svd_optimization_backward(const double* x, const double* y_pred, const double* R_true,
+                                              const double* t_true, int B, int n, const double* partial,
+                                              const double* grad_loss, double alpha, double* grad_y_pred,
+                                              void* stream) {
+  DVCP_REQUIRE(x && y_pred && R_true && t_true && partial && grad_loss && grad_y_pred,
+               "dvcp_svd_optimization_backward: null pointer");
+  DVCP_REQUIRE(n > 0 && n <= dvcp::kRgMaxN, "dvcp_svd_optimization_backward: n=%d unsupported (1..1024)", n);
+  const int n_in = static_cast<int>(n * 0.8);
+  DVCP_REQUIRE(n_in > 0, "dvcp_svd_optimization_backward: int(0.8 n) == 0");
+  if (B == 0) return DVCP_OK;
+  const double inv_count = 1.0 / (static_cast<double>(B) * 3.0 * n_in);
+  hipLaunchKernelGGL(dvcp::svd_opt_bwd_kernel, dim3(B), dim3(dvcp::kRgThreads), 0, static_cast<hipStream_t>(stream), x,
+                     y_pred, R_true, t_true, n, n_in, B, partial, grad_loss, alpha, inv_count, grad_y_pred);
+  return dvcp::launch_status("dvcp_svd_optimization_backward");
 }

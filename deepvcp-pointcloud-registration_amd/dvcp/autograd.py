@@ -1,0 +1,129 @@
+"""Autograd for the registration head: training drop-in for train.py:105-125.
+
+The reference trains with ``loss.backward()`` through deepVCP_loss (two torch.svd), the corresponding
+point generation (cpg.py), the deep feature embedding (deep_feat_embedding.py, src and tgt) and the
+feature extractor.  Here the head's backward runs in hand-written HIP kernels:
+
+  * ``pose_loss``  -- deepVCP_loss.py:105-121 forward (dvcp_svd_optimization) and backward
+                      (dvcp_svd_optimization_backward, both Kabsch solves differentiated);
+  * ``cpg``        -- cpg.py:27-60 (dvcp_cpg / dvcp_cpg_backward): gradients for the conv
+                      weights and for both DFE outputs;
+  * ``dfe_rows``   -- deep_feat_embedding.py on the source rows (dvcp_dfe / dvcp_dfe_backward);
+  * ``dfe_tgt``    -- the fused target rows (dvcp_dfe_tgt / dvcp_dfe_tgt_backward).
+
+The key points, candidates and kNN indices carry no gradient in the reference either (index
+ops, knn_cuda under no_grad); the weighting layer gets none (only its top-k indices are used).
+The feature extractor must be frozen (eval BN, requires_grad False): its backward (batch-
+statistics BN + set-abstraction backward) is not implemented, and DeepVCP.forward raises
+rather than silently dropping its gradient.  Parameter gradients come back summed over the
+batch in a fixed order (deterministic).
+"""
+import torch
+
+from . import ops
+
+
+def _pack(weights):
+    return torch.cat([w.detach().reshape(-1) for w in weights]).float().contiguous()
+
+
+def _split(gp, weights):
+    """Packed gradient -> one tensor per (shape, dtype) in ``weights``."""
+    out, o = [], 0
+    for shape, dtype in weights:
+        n = shape.numel()
+        out.append(gp[o:o + n].view(shape).to(dtype))
+        o += n
+    return out
+
+
+class _DfeRows(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, X, *weights):
+        params = _pack(weights)
+        ctx.save_for_backward(X, params)
+        ctx.weights = [(w.shape, w.dtype) for w in weights]
+        return ops.dfe(X, params)
+
+    @staticmethod
+    def backward(ctx, g):
+        X, params = ctx.saved_tensors
+        return (None, *_split(ops.dfe_backward(X, params, g), ctx.weights))
+
+
+class _DfeTgt(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ref_xyz, ref_feat, cand, dist, idx, *weights):
+        params = _pack(weights)
+        ctx.save_for_backward(ref_xyz, ref_feat, cand, dist, idx, params)
+        ctx.weights = [(w.shape, w.dtype) for w in weights]
+        return ops.dfe_tgt(ref_xyz, ref_feat, cand, dist, idx, params, ref_pdim=2)
+
+    @staticmethod
+    def backward(ctx, g):
+        ref_xyz, ref_feat, cand, dist, idx, params = ctx.saved_tensors
+        gp = ops.dfe_tgt_backward(ref_xyz, ref_feat, cand, dist, idx, params, g, ref_pdim=2)
+        return (None, None, None, None, None, *_split(gp, ctx.weights))
+
+
+class _Cpg(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, src, tgt, cand, G, *weights):
+        params = _pack(weights)
+        ctx.save_for_backward(src, tgt, cand, params)
+        ctx.G = G
+        ctx.weights = [(w.shape, w.dtype) for w in weights]
+        return ops.cpg(src, tgt, cand, G, params)
+
+    @staticmethod
+    def backward(ctx, g):
+        src, tgt, cand, params = ctx.saved_tensors
+        gsrc, gtgt, gp = ops.cpg_backward(src, tgt, cand, ctx.G, params, g)
+        gsrc = gsrc.view(src.shape).to(src.dtype) if ctx.needs_input_grad[0] else None
+        gtgt = gtgt.to(tgt.dtype) if ctx.needs_input_grad[1] else None
+        return (gsrc, gtgt, None, None, *_split(gp, ctx.weights))
+
+
+class _PoseLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, y_pred, R_true, t_true, alpha):
+        x, y, Rt, tt = ops.pose_inputs(x, y_pred, R_true, t_true)
+        R, t, x1, _, partial = ops.svd_optimization(x, y, Rt, tt)
+        denom = float(x1.numel())
+        loss = alpha * (partial[:, 0].sum() / denom) + (1 - alpha) * torch.abs(partial[:, 1].sum() / denom)
+        ctx.save_for_backward(x, y, Rt, tt, partial)
+        ctx.alpha = alpha
+        ctx.y_dtype = y_pred.dtype
+        ctx.mark_non_differentiable(R, t)
+        return loss, R, t
+
+    @staticmethod
+    def backward(ctx, g_loss, g_R, g_t):
+        x, y, Rt, tt, partial = ctx.saved_tensors
+        gy = ops.svd_optimization_backward(x, y, Rt, tt, partial, g_loss, ctx.alpha)
+        return None, gy.to(ctx.y_dtype), None, None, None
+
+
+def dfe_rows(X, dfe_module):
+    """deep_feat_embedding.py forward on materialised rows (..., 32, 35), differentiable in fc1-3."""
+    return _DfeRows.apply(X, *_linears(dfe_module))
+
+
+def dfe_tgt(ref_xyz, ref_feat, cand, dist, idx, dfe_module):
+    """The fused target rows (get_cat_feat_tgt.py + deep_feat_embedding.py), differentiable in fc1-3."""
+    return _DfeTgt.apply(ref_xyz, ref_feat, cand, dist, idx, *_linears(dfe_module))
+
+
+def cpg(src, tgt, cand, G, cpg_module):
+    """cpg.py:27-60, differentiable in src, tgt and the conv weights."""
+    convs = [cpg_module.conv1, cpg_module.conv2, cpg_module.conv3]
+    return _Cpg.apply(src, tgt, cand, G, *[t for c in convs for t in (c.weight, c.bias)])
+
+
+def pose_loss(x, y_pred, R_true, t_true, alpha):
+    """deepVCP_loss.py:105-121 on (B, 3, n) operands -> (loss, R, t); differentiable in y_pred."""
+    return _PoseLoss.apply(x, y_pred, R_true, t_true, alpha)
+
+
+def _linears(m):
+    return [m.fc1.weight, m.fc1.bias, m.fc2.weight, m.fc2.bias, m.fc3.weight, m.fc3.bias]

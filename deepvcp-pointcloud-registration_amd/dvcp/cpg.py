@@ -7,9 +7,8 @@ candidates.  One gfx950 workgroup per key point (dvcp_cpg).
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import autograd, ops
 from ._params import cached_pack
-from .pointnet2_utils import _inference_only
 
 
 class cpg(nn.Module):
@@ -28,9 +27,17 @@ class cpg(nn.Module):
 
     def forward(self, src_dfe_feat, tgt_dfe_feat, candidates, r, s, return_weights=False):
         """src (B, N, 1, 32), tgt (B, N, 32, C), candidates (B, N, C, 3) -> vcp (B, N, 3)."""
-        _inference_only(self)
         B, N, C, _ = candidates.shape
         grid_size = int((2 * r) / s + 1)
         assert C == grid_size * grid_size * grid_size
+        if not return_weights and _wants_grad(self, src_dfe_feat, tgt_dfe_feat):
+            return autograd.cpg(src_dfe_feat, tgt_dfe_feat, candidates, grid_size, self)
         return ops.cpg(src_dfe_feat, tgt_dfe_feat, candidates, grid_size, self.packed_params(),
                        want_weight=return_weights)
+
+
+def _wants_grad(module, *inputs):
+    """Autograd is on and something upstream of the output requires a gradient."""
+    if not torch.is_grad_enabled():
+        return False
+    return any(p.requires_grad for p in module.parameters()) or any(t.requires_grad for t in inputs)

@@ -17,7 +17,7 @@ same starts as the reference.  t_init is unused, as in the reference (deepVCP.py
 import torch
 import torch.nn as nn
 
-from . import _lib, ops
+from . import _lib, autograd, ops
 from .cpg import cpg
 from .deep_feat_embedding import feat_embedding_layer
 from .deep_feat_extraction import feat_extraction_layer
@@ -44,6 +44,24 @@ class DeepVCP(nn.Module):
             cache[key] = torch.cuda.Stream(device=dev)
         return cache[key]
 
+    def _head_training(self):
+        """Whether this forward records autograd for the head (train.py:105-125 with the feature
+        extractor frozen).  The head (DFE, CPG) is differentiated when autograd is on and its
+        parameters require gradients; the feature extractor has no backward here, so it must be
+        frozen then (eval mode, requires_grad False), and a module left in training mode otherwise
+        raises instead of silently dropping gradients."""
+        head = [p for m in (self.DFE, self.cpg) for p in m.parameters()]
+        fe_frozen = not self.FE1.training and not any(p.requires_grad for p in self.FE1.parameters())
+        train_head = torch.is_grad_enabled() and any(p.requires_grad for p in head) and fe_frozen
+        if not train_head and self.training:
+            raise NotImplementedError(
+                "dvcp.DeepVCP: training mode needs a frozen feature extractor -- the FE backward "
+                "(batch-statistics BN, set-abstraction backward) is not implemented yet (SURVEY.md 8(f) rank 1). "
+                "Train the head with model.FE1.eval() and model.FE1.requires_grad_(False).")
+        if not train_head:
+            _inference_only(self)
+        return train_head
+
     def draw_starts(self, B, n_src, n_tgt):
         """The reference's seven torch.randint(0, n, (B,)) draws, in call order."""
         S1, S2, S3 = self.FE1.sa1.npoint, self.FE1.sa2.npoint, self.FE1.sa3.npoint
@@ -55,7 +73,7 @@ class DeepVCP(nn.Module):
         """``starts`` (7, B): FPS start indices (drawn like the reference when None).
         ``trace``: dict filled with the stage outputs.  ``keypoint_idx`` (B, K): stage override
         for parity testing -- use these FE-space key-point indices instead of the top-k."""
-        _inference_only(self)
+        train_head = self._head_training()
         _lib.require_gpu(src_pts, tgt_pts)   # no CPU fallback
         B = src_pts.shape[0]
         K, r, s = self.K, self.r, self.s
@@ -79,7 +97,7 @@ class DeepVCP(nn.Module):
             tgt_xyz, tgt_feat, _ = self.FE1.run(tgt_pts, starts[4:7], side_stream=side)
         top = ops.topk(score, K) if keypoint_idx is None else keypoint_idx.to(dev, torch.int64).contiguous()
         keypts, src_cat, moved = ops.src_keypoints(src_xyz, src_feat, top, starts[3], R_init, radius=1.0, nsample=32)
-        src_dfe = ops.dfe(src_cat, self.DFE.packed_params())
+        src_dfe = autograd.dfe_rows(src_cat, self.DFE) if train_head else ops.dfe(src_cat, self.DFE.packed_params())
 
         G = int((2 * r) / s + 1)                    # cpg.py:29
         if grid_side(r, s) != G:
@@ -88,9 +106,13 @@ class DeepVCP(nn.Module):
         C = G * G * G
         qry = cand.view(B, K * C, 3)
         dist, idx, _ = ops.knn(tgt_xyz, qry, 32, ref_pdim=2, qry_pdim=1, want_idx64=False)
-        tgt_dfe = ops.dfe_tgt(tgt_xyz, tgt_feat, qry, dist, idx, self.DFE.packed_params(), ref_pdim=2)
-        tgt_dfe = tgt_dfe.view(B, K, C, 32)
-        vcp = ops.cpg(src_dfe, tgt_dfe.permute(0, 1, 3, 2), cand, G, self.cpg.packed_params())
+        if train_head:
+            tgt_dfe = autograd.dfe_tgt(tgt_xyz, tgt_feat, qry, dist, idx, self.DFE).view(B, K, C, 32)
+            vcp = autograd.cpg(src_dfe, tgt_dfe.permute(0, 1, 3, 2), cand, G, self.cpg)
+        else:
+            tgt_dfe = ops.dfe_tgt(tgt_xyz, tgt_feat, qry, dist, idx, self.DFE.packed_params(), ref_pdim=2)
+            tgt_dfe = tgt_dfe.view(B, K, C, 32)
+            vcp = ops.cpg(src_dfe, tgt_dfe.permute(0, 1, 3, 2), cand, G, self.cpg.packed_params())
         if trace is not None:
             trace.update(src_xyz=src_xyz, src_feat=src_feat, score=score, topk=top, keypts=keypts,
                          src_cat=src_cat, moved=moved, src_dfe=src_dfe, tgt_xyz=tgt_xyz, tgt_feat=tgt_feat,

@@ -8,7 +8,7 @@ reference's loss_vis.py scrapes; it forces a host sync, so it is off by default.
 """
 import torch
 
-from . import ops
+from . import autograd, ops
 
 PRINT_LOSS = False
 
@@ -27,6 +27,12 @@ def deepVCP_loss(x, y_pred, R_true, t_true, alpha):
     """x, y_pred (B, K, 3); R_true (B, 3, 3); t_true (B, 3, 1) -> (loss, R (B,3,3), t (B,3,1))."""
     x = x.permute(0, 2, 1).double()
     y_pred = y_pred.permute(0, 2, 1).double()
+    if torch.is_grad_enabled() and y_pred.requires_grad:
+        # train.py:121 loss.backward(): both Kabsch solves differentiated on the GPU
+        loss, R, t = autograd.pose_loss(x, y_pred, R_true, t_true, alpha)
+        if PRINT_LOSS:
+            print(f"Loss: {loss}")
+        return loss, R, t
     R, t, x1, _, partial = ops.svd_optimization(x, y_pred, R_true, t_true)
     denom = float(x1.numel())
     loss = alpha * (partial[:, 0].sum() / denom) + (1 - alpha) * torch.abs(partial[:, 1].sum() / denom)

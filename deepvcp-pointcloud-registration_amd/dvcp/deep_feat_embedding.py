@@ -5,11 +5,12 @@ max over the 32 neighbours.  ``forward(X, src)`` takes the materialised (B, K, 3
 (B, K, C, 32, 35) input like the reference; DeepVCP.forward instead uses the fused target
 kernel (dvcp_dfe_tgt) that never materialises the target input.
 """
+import torch
 import torch.nn as nn
 
-from . import ops
+from . import autograd, ops
 from ._params import cached_pack, linear_pack, linear_tensors
-from .pointnet2_utils import _inference_only
+from .cpg import _wants_grad
 
 
 class feat_embedding_layer(nn.Module):
@@ -26,8 +27,12 @@ class feat_embedding_layer(nn.Module):
         return cached_pack(self, "dfe", linear_tensors(*lins), lambda: linear_pack(*lins))
 
     def forward(self, X, src=True):
-        _inference_only(self)
         expect = 4 if src else 5
         if X.dim() != expect:
             raise RuntimeError(f"feat_embedding_layer(src={src}) expects a {expect}-D input, got {tuple(X.shape)}")
+        if X.requires_grad and torch.is_grad_enabled():
+            raise NotImplementedError("feat_embedding_layer: the gradient with respect to the input rows is not "
+                                      "implemented (the feature extractor is frozen when training the head)")
+        if _wants_grad(self):
+            return autograd.dfe_rows(X, self)
         return ops.dfe(X, self.packed_params())

@@ -271,16 +271,8 @@ def rigid_transform(x, y):
 def svd_optimization(x, y_pred, R_true, t_true):
     """deepVCP_loss.py:57-90 (+ the per-pair loss sums of :110-119)."""
     _lib.require_gpu(x, y_pred, R_true, t_true)
-    x = x.double().contiguous()
-    y_pred = y_pred.double().contiguous()
+    x, y_pred, Rt, tt = pose_inputs(x, y_pred, R_true, t_true)
     B, _, n = x.shape
-    Rt = R_true.double().expand(B, 3, 3).contiguous()
-    tt = t_true.double()
-    if tt.dim() == 2:
-        tt = tt.unsqueeze(0)
-    if tt.shape[-1] != 1:
-        raise RuntimeError("t_true must broadcast as (B, 3, 1)")
-    tt = tt.expand(B, 3, 1).contiguous()
     n_in = int(n * 0.8)
     dev = x.device
     R2 = torch.empty(B, 3, 3, dtype=torch.float64, device=dev)
@@ -324,3 +316,90 @@ def rigid_apply(pts, R, t=None, pdim=2):
     call("dvcp_rigid_apply", dtype_code(pts), ptr(pts), sb, sc, sn, B, N, C, ptr(Rc), ptr(tc),
          0 if tc is None or tc.shape[0] == 1 else 3, ptr(out), stream())
     return out
+
+
+# ---- backward entry points (training; see dvcp/autograd.py) -----------------------------------
+
+DFE_NPARAMS = 3264   # fc1-3 weights and biases, packed
+CPG_NPARAMS = 15681  # conv1-3 weights and biases, packed
+
+
+def dfe_backward(X, params, grad_out):
+    """Parameter gradient of ``dfe`` (deep_feat_embedding.py:23-61) for rows X (..., 32, 35)."""
+    _lib.require_gpu(X, params, grad_out)
+    Xc = X.contiguous()
+    R = Xc.numel() // (32 * 35)
+    g = grad_out.reshape(R, 32).float().contiguous()
+    ws = torch.empty(max(1, int(_lib.load().dvcp_dfe_backward_workspace_bytes(R)) // 4), dtype=torch.float32,
+                     device=X.device)
+    gp = torch.empty(DFE_NPARAMS, dtype=torch.float32, device=X.device)
+    call("dvcp_dfe_backward", dtype_code(Xc), ptr(Xc), R, ptr(params), ptr(g), ptr(ws), ptr(gp), stream())
+    return gp
+
+
+def dfe_tgt_backward(ref_xyz, ref_feat, cand, dist, idx, params, grad_out, ref_pdim=2):
+    """Parameter gradient of ``dfe_tgt`` (get_cat_feat_tgt.py:54-96 + deep_feat_embedding.py:47-60)."""
+    _lib.require_gpu(ref_xyz, ref_feat, cand, dist, idx, params, grad_out)
+    B = ref_xyz.shape[0]
+    M, rb, rc, rn = _pts(ref_xyz, ref_pdim)
+    Q = cand.shape[1]
+    feat_c, cand_c, dist_c, idx_c = ref_feat.contiguous(), cand.contiguous(), dist.contiguous(), idx.contiguous()
+    g = grad_out.reshape(B, Q, 32).float().contiguous()
+    ws = torch.empty(max(1, int(_lib.load().dvcp_dfe_backward_workspace_bytes(B * Q)) // 4), dtype=torch.float32,
+                     device=ref_xyz.device)
+    gp = torch.empty(DFE_NPARAMS, dtype=torch.float32, device=ref_xyz.device)
+    call("dvcp_dfe_tgt_backward", dtype_code(ref_xyz), ptr(ref_xyz), rb, rc, rn, M, ptr(feat_c), ptr(cand_c),
+         ptr(dist_c), ptr(idx_c), B, Q, ptr(params), ptr(g), ptr(ws), ptr(gp), stream(),
+         work=(2.0 * 3168 * 32 * B * Q, B * (M * (12 + 128) + Q * (12 + 32 * 8 + 128))))
+    return gp
+
+
+def cpg_backward(src, tgt, cand, G, params, grad_vcp):
+    """Gradients of ``cpg`` (cpg.py:27-60): (d src (B,K,32), d tgt (B,K,32,C), d params)."""
+    _lib.require_gpu(src, tgt, cand, params, grad_vcp)
+    B, K, C, _ = cand.shape
+    if tgt.dim() != 4 or tuple(tgt.shape) != (B, K, 32, C):
+        raise RuntimeError(f"cpg_backward: tgt_dfe_feat must be (B, K, 32, C), got {tuple(tgt.shape)}")
+    if tgt.stride(0) != K * tgt.stride(1):
+        tgt = tgt.contiguous()
+    P = B * K
+    srcc = src.reshape(P, 32).contiguous().float()
+    candc = cand.contiguous()
+    gv = grad_vcp.reshape(P, 3).float().contiguous()
+    dev = cand.device
+    gsrc = torch.empty(B, K, 32, dtype=torch.float32, device=dev)
+    gtgt = torch.empty(B, K, 32, C, dtype=torch.float32, device=dev)
+    ws = torch.empty(max(1, int(_lib.load().dvcp_cpg_backward_workspace_bytes(P)) // 4), dtype=torch.float32,
+                     device=dev)
+    gp = torch.empty(CPG_NPARAMS, dtype=torch.float32, device=dev)
+    call("dvcp_cpg_backward", ptr(srcc), ptr(tgt), tgt.stride(1), tgt.stride(2), tgt.stride(3), ptr(candc), P, int(G),
+         ptr(params), ptr(gv), ptr(gsrc), ptr(gtgt), ptr(ws), ptr(gp), stream(),
+         work=(3 * 2.0 * 27 * (32 * 16 + 16 * 4 + 4) * P * C, P * (128 + C * (128 + 12 + 128) + 12)))
+    return gsrc, gtgt, gp
+
+
+def pose_inputs(x, y_pred, R_true, t_true):
+    """deepVCP_loss.py's operands as the pose kernels take them: x, y_pred (B, 3, n) fp64
+    contiguous; R_true (B, 3, 3), t_true (B, 3, 1) broadcast and contiguous."""
+    x = x.double().contiguous()
+    y_pred = y_pred.double().contiguous()
+    B = x.shape[0]
+    Rt = R_true.double().expand(B, 3, 3).contiguous()
+    tt = t_true.double()
+    if tt.dim() == 2:
+        tt = tt.unsqueeze(0)
+    if tt.shape[-1] != 1:
+        raise RuntimeError("t_true must broadcast as (B, 3, 1)")
+    return x, y_pred, Rt, tt.expand(B, 3, 1).contiguous()
+
+
+def svd_optimization_backward(x, y_pred, R_true, t_true, partial, grad_loss, alpha):
+    """dL/dy_pred (B, 3, n) fp64 of deepVCP_loss (deepVCP_loss.py:57-121); operands as
+    ``pose_inputs`` returns them, ``partial`` from ``svd_optimization``."""
+    _lib.require_gpu(x, y_pred, R_true, t_true, partial, grad_loss)
+    B, _, n = x.shape
+    g = torch.empty(B, 3, n, dtype=torch.float64, device=x.device)
+    gl = grad_loss.double().reshape(1).contiguous()
+    call("dvcp_svd_optimization_backward", ptr(x), ptr(y_pred), ptr(R_true), ptr(t_true), B, n,
+         ptr(partial.contiguous()), ptr(gl), float(alpha), ptr(g), stream())
+    return g

@@ -243,6 +243,42 @@ int dvcp_registration_error(const double* R_pred, const double* t_pred, const do
 int dvcp_rigid_apply(int dtype, const void* in, int64_t ib, int64_t ic, int64_t in_n, int B, int N, int C,
                      const double* R, const double* t, int64_t t_b, double* out, void* stream);
 
+/* ---- Backward (training: train.py:105-125 loss.backward()).  Gradients of the parameters come
+ * back packed in the forward's params layout, summed over the batch in a fixed order. ---- */
+
+/* deepVCP_loss backward.  Replaces autograd through deepVCP_loss.py:57-121 (torch.svd backward of
+ * :29 twice, the gathers of :81-82): dL/dy_pred (B x 3 x n fp64) for
+ * loss = alpha*mean|y_true1 - y2| + (1-alpha)*|mean(y2 - y_true1)|.  partial: the forward's
+ * (B x 2) per-pair sums; grad_loss: device scalar dL/dloss. */
+int dvcp_svd_optimization_backward(const double* x, const double* y_pred, const double* R_true,
+                                   const double* t_true, int B, int n, const double* partial,
+                                   const double* grad_loss, double alpha, double* grad_y_pred,
+                                   void* stream);
+
+/* Feature-embedding backward.  Replaces autograd through deep_feat_embedding.py:23-61 (fc1-3,
+ * MaxPool1d) for the materialised rows X (R x 32 x 35, fp32|fp64): grad_out R x 32 fp32 ->
+ * grad_params (3264 fp32: W1, b1, W2, b2, W3, b3).  ws: dvcp_dfe_backward_workspace_bytes(R). */
+int64_t dvcp_dfe_backward_workspace_bytes(int64_t R);
+int dvcp_dfe_backward(int x_dtype, const void* X, int64_t R, const float* params, const float* grad_out,
+                      float* ws, float* grad_params, void* stream);
+
+/* Target-side backward.  Replaces autograd through get_cat_feat_tgt.py:54-96 +
+ * deep_feat_embedding.py:47-60; same arguments as dvcp_dfe_tgt plus grad_out (B x Q x 32 fp32),
+ * ws (dvcp_dfe_backward_workspace_bytes(B*Q)) and grad_params (3264 fp32).  The target features
+ * are frozen inputs (no gradient). */
+int dvcp_dfe_tgt_backward(int dtype, const void* ref_xyz, int64_t rb, int64_t rc, int64_t rn, int M,
+                          const float* ref_feat, const float* cand, const float* dist, const int32_t* idx,
+                          int B, int Q, const float* params, const float* grad_out, float* ws,
+                          float* grad_params, void* stream);
+
+/* CPG backward.  Replaces autograd through cpg.py:27-60: dvcp_cpg's arguments plus grad_vcp
+ * (P x 3) -> grad_src (P x 32), grad_tgt (P x 32 x C contiguous, the (B,K,32,C) tensor's
+ * logical order), grad_params (15681 fp32).  ws: dvcp_cpg_backward_workspace_bytes(P). */
+int64_t dvcp_cpg_backward_workspace_bytes(int P);
+int dvcp_cpg_backward(const float* src, const float* tgt, int64_t t_p, int64_t t_f, int64_t t_c,
+                      const float* cand, int P, int G, const float* params, const float* grad_vcp,
+                      float* grad_src, float* grad_tgt, float* ws, float* grad_params, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

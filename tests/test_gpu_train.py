@@ -1,0 +1,187 @@
+"""Training parity (the head): HIP backward kernels vs torch autograd through
+the oracle's restatement of the reference modules (REF-R, oracle/ref_r.py).
+
+Gradients are compared as max |got - want| <= tol * max |want| per tensor: the GPU runs fp32
+arithmetic in its own summation order, the oracle runs the same graph in fp64 (module .double())
+(the DFE tests run the oracle in fp32 as the reference does: its forward casts X.float()).  Max-pool arg-max routing in the DFE makes a gradient row jump when two rows are
+within rounding of each other; random inputs keep such near-ties out of these sizes.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(got, want, tol, what, floor=1e-30):
+    """max |got - want| <= tol * max(max |want|, floor).  ``floor`` is for gradients that vanish
+    analytically: conv3's bias shifts every logit alike, and softmax is shift-invariant."""
+    got, want = got.detach().double().cpu(), want.detach().double().cpu()
+    scale = max(float(want.abs().max()), floor)
+    err = float((got - want).abs().max())
+    assert err <= tol * scale, f"{what}: max err {err:.3e} vs scale {scale:.3e} (tol {tol})"
+    return err / scale
+
+
+@pytest.mark.parametrize("B,K,r,s", [(2, 3, 1.0, 0.4), (1, 2, 2.0, 0.4)])
+def test_cpg_backward_vs_oracle(cuda, B, K, r, s):
+    """cpg.py:27-60 backward: d src, d tgt (the (B,K,32,C) view), d conv weights."""
+    import oracle as O
+    import dvcp
+    G = int(2 * r / s + 1)
+    C = G ** 3
+    torch.manual_seed(3)
+    ref = O.cpg().double()
+    mine = dvcp.cpg().to(cuda)
+    mine.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    src = torch.randn(B, K, 1, 32, dtype=torch.float64)
+    tgt_base = torch.randn(B, K, C, 32, dtype=torch.float64) * 0.5 + 0.3
+    cand = torch.randn(B, K, C, 3, dtype=torch.float64)
+    gv = torch.randn(B, K, 3, dtype=torch.float64)
+
+    s_o = src.clone().requires_grad_()
+    t_o = tgt_base.clone().requires_grad_()
+    vcp_o = ref(s_o, t_o.permute(0, 1, 3, 2), cand, r, s)
+    (vcp_o * gv).sum().backward()
+
+    s_g = src.float().to(cuda).requires_grad_()
+    t_g = tgt_base.float().to(cuda).requires_grad_()
+    vcp = mine(s_g, t_g.permute(0, 1, 3, 2), cand.float().to(cuda), r, s)
+    (vcp * gv.float().to(cuda)).sum().backward()
+
+    _close(vcp, vcp_o, 1e-5, "vcp")
+    _close(s_g.grad, s_o.grad, 2e-4, "d src")
+    _close(t_g.grad, t_o.grad, 2e-4, "d tgt")
+    for name in ("conv1", "conv2", "conv3"):
+        for p in ("weight", "bias"):
+            _close(getattr(getattr(mine, name), p).grad, getattr(getattr(ref, name), p).grad, 2e-4, f"{name}.{p}",
+                   floor=1e-3 if (name, p) == ("conv3", "bias") else 1e-30)
+
+
+def test_dfe_rows_backward_vs_oracle(cuda):
+    """deep_feat_embedding.py backward on materialised source rows (B, K, 32, 35)."""
+    import oracle as O
+    import dvcp
+    torch.manual_seed(4)
+    ref = O.feat_embedding_layer()   # the reference's own fp32 (X.float(), deep_feat_embedding.py:25)
+    mine = dvcp.feat_embedding_layer().to(cuda)
+    mine.load_state_dict(ref.state_dict())
+    X = torch.randn(2, 64, 32, 35)
+    g = torch.randn(2, 64, 32)
+    (ref(X, src=True) * g).sum().backward()
+    out = mine(X.to(cuda), src=True)
+    (out * g.float().to(cuda)).sum().backward()
+    for name in ("fc1", "fc2", "fc3"):
+        for p in ("weight", "bias"):
+            _close(getattr(getattr(mine, name), p).grad, getattr(getattr(ref, name), p).grad, 1e-4, f"{name}.{p}")
+
+
+def test_dfe_tgt_backward_vs_oracle(cuda):
+    """Fused target rows (get_cat_feat_tgt.py:54-96 + deep_feat_embedding.py:47-60) backward vs
+    the oracle's materialised rows through the same DFE."""
+    import oracle as O
+    import dvcp
+    from dvcp import autograd, ops
+    torch.manual_seed(5)
+    B, M, K, C = 2, 700, 3, 27
+    xyz = torch.rand(B, M, 3) * 2 - 1
+    feat = torch.rand(B, M, 32)
+    cand = (torch.rand(B, K, C, 3) * 2 - 1).double()
+    ref = O.feat_embedding_layer()   # fp32, as the reference
+    rows = O.Get_Cat_Feat_Tgt()(cand, torch.zeros(B, K, 3), xyz, feat)
+    g = torch.randn(B, K, C, 32)
+    (ref(rows, src=False) * g).sum().backward()
+
+    mine = dvcp.feat_embedding_layer().to(cuda)
+    mine.load_state_dict(ref.state_dict())
+    ref_xyz = xyz.to(cuda).permute(0, 2, 1)
+    qry = cand.float().to(cuda).view(B, K * C, 3)
+    dist, idx, _ = ops.knn(ref_xyz, qry, 32, ref_pdim=2, qry_pdim=1, want_idx64=False)
+    out = autograd.dfe_tgt(ref_xyz, feat.to(cuda), qry, dist, idx, mine)
+    (out * g.float().to(cuda).view(B, K * C, 32)).sum().backward()
+    for name in ("fc1", "fc2", "fc3"):
+        for p in ("weight", "bias"):
+            _close(getattr(getattr(mine, name), p).grad, getattr(getattr(ref, name), p).grad, 1e-4, f"{name}.{p}")
+
+
+def test_pose_loss_backward_vs_oracle(cuda):
+    """deepVCP_loss.py:105-121: d loss / d y_pred through both Kabsch solves and the inlier gather."""
+    import oracle as O
+    import dvcp
+    from dvcp.synthetic import make_pairs
+    torch.manual_seed(6)
+    B, n = 3, 64
+    _, _, R_gt, t_gt = make_pairs(B, 8, seed=6)
+    x = torch.rand(B, n, 3) * 2 - 1
+    y = (torch.matmul(R_gt, x.double().transpose(1, 2)) + t_gt).transpose(1, 2)
+    y = (y + 0.05 * torch.randn(B, n, 3, dtype=torch.float64)).float()
+
+    y_o = y.clone().requires_grad_()
+    loss_o, R_o, t_o = O.deepVCP_loss(x, y_o, R_gt, t_gt, 0.5)
+    loss_o.backward()
+
+    y_g = y.to(cuda).requires_grad_()
+    loss, R, t = dvcp.deepVCP_loss(x.to(cuda), y_g, R_gt.to(cuda), t_gt.to(cuda), 0.5)
+    loss.backward()
+    torch.testing.assert_close(loss.detach().cpu(), loss_o.detach(), rtol=1e-10, atol=1e-12)
+    torch.testing.assert_close(R.cpu(), R_o, rtol=0, atol=1e-10)
+    _close(y_g.grad, y_o.grad, 1e-6, "d y_pred")
+
+
+def test_head_train_step_vs_oracle(cuda):
+    """train.py:105-125 with the feature extractor frozen: model(...) -> deepVCP_loss -> backward.
+    The DFE and CPG parameter gradients match the oracle's autograd (fp32 both sides, the GPU
+    run from the oracle's key points), and one Adam step runs on them."""
+    import oracle as O
+    import dvcp
+    from dvcp.synthetic import condition_weights, make_pairs, randomize_bn
+    src, tgt, R_gt, t_gt = make_pairs(1, 1024, seed=91)
+    torch.manual_seed(0)
+    ref = O.DeepVCP(use_normal=False, K=32, r=1.0, s=0.4, fe_npoint=512)
+    randomize_bn(ref)
+    ref.FE1.eval()
+    with torch.no_grad():
+        _, calib = ref.FE1(src)
+    condition_weights(ref, feats=calib)
+    ref.FE1.requires_grad_(False)
+    mine = dvcp.DeepVCP(use_normal=False, K=32, r=1.0, s=0.4, fe_npoint=512)
+    mine.load_state_dict(ref.state_dict())
+    mine.to(cuda)
+    mine.FE1.eval()
+    mine.FE1.requires_grad_(False)
+
+    torch.manual_seed(1)
+    with O.tracing() as trace:
+        kp_o, vcp_o = ref(src, tgt, R_gt, torch.zeros(1, 3))
+    loss_o, _, _ = O.deepVCP_loss(kp_o, vcp_o, R_gt, t_gt, 0.5)
+    loss_o.backward()
+    top = dict(trace)["topk_idx"]
+
+    torch.manual_seed(1)
+    kp, vcp = mine(src.to(cuda), tgt.to(cuda), R_gt.to(cuda), torch.zeros(1, 3), keypoint_idx=top)
+    assert vcp.requires_grad and not kp.requires_grad
+    loss, _, _ = dvcp.deepVCP_loss(kp, vcp, R_gt.to(cuda), t_gt.to(cuda), 0.5)
+    loss.backward()
+    torch.testing.assert_close(loss.detach().cpu(), loss_o.detach(), rtol=1e-4, atol=1e-6)
+    errs = {}
+    for mod in ("DFE.fc1", "DFE.fc2", "DFE.fc3", "cpg.conv1", "cpg.conv2", "cpg.conv3"):
+        a, b = mod.split(".")
+        for p in ("weight", "bias"):
+            got = getattr(getattr(getattr(mine, a), b), p).grad
+            want = getattr(getattr(getattr(ref, a), b), p).grad
+            errs[f"{mod}.{p}"] = _close(got, want, 1e-3, f"{mod}.{p}",
+                                        floor=1e-3 if (mod, p) == ("cpg.conv3", "bias") else 1e-30)
+    assert all(p.grad is None for p in mine.FE1.parameters())
+    opt = torch.optim.Adam([p for p in mine.parameters() if p.requires_grad], lr=1e-3)
+    before = mine.cpg.conv1.weight.detach().clone()
+    opt.step()
+    assert not torch.equal(before, mine.cpg.conv1.weight.detach())
+    print("relative gradient errors:", {k: f"{v:.1e}" for k, v in errs.items()})
+
+
+def test_training_mode_needs_frozen_fe(cuda):
+    import dvcp
+    m = dvcp.DeepVCP(use_normal=False, K=8, fe_npoint=64).to(cuda)
+    m.FE1.eval()     # eval BN, but its parameters still require gradients
+    x = torch.rand(1, 3, 128, device=cuda)
+    with pytest.raises(NotImplementedError, match="requires_grad_"):
+        m(x, x, torch.eye(3, dtype=torch.float64, device=cuda)[None], torch.zeros(1, 3))
