@@ -13,8 +13,10 @@
 //   dL/dsrc[f'] = sum_v 2 (src[f'] - T) dL/dcost[f'][v];  dL/dT[l] = -2 (src[f'] - T) dL/dcost.
 // The workgroup recomputes the forward activations (conv1 from the cost volume, one input
 // channel at a time) and keeps them in LDS:
-//   A (16 x C): h1, later dL/dh1;    W (13824): conv1 weights [ci][tap][co], in the middle phases
-//   dL/dlg and reduction scratch;    D (4 x C): the cost channel being processed, or h2 / dL/dh2.
+//   A (16 x C): h1, later dL/dh1;    W: dL/dlg and reduction scratch;
+//   D (4 x C): the cost channel being processed, or h2 / dL/dh2.
+// Convolution weights are read as wave-uniform scalar loads (SGPR operands), so the LDS traffic
+// is one activation read per 16 (conv1 forward) or 32 (conv1 data backward) fmas.
 // Parameter gradients are written per key point (fixed order, no atomics) and summed over key
 // points by cpg_bwd_reduce_kernel in fp64.
 #include "common.h"
@@ -112,11 +114,7 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
     return T[static_cast<int64_t>(f) * t_f + static_cast<int64_t>(l - static_cast<int>(f) * C) * t_c];
   };
 
-  // ---- forward: conv1 (one cost channel at a time) -------------------------------------------
-  for (int i = tid; i < kCbW; i += kCbThreads) {  // torch (co, ci, kd, kh, kw) -> [ci][t][co]
-    const int co = i / (32 * 27), r = i % (32 * 27);
-    Wr[r * 16 + co] = P1[i];
-  }
+  // ---- forward: conv1 (one cost channel at a time; weights are wave-uniform scalar loads) ------
   float h1[kCbV][16];
 #pragma unroll
   for (int k = 0; k < kCbV; ++k)
@@ -137,9 +135,8 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
       for (int t = 0; t < 27; ++t) {
         if (!((msk[k] >> t) & 1u)) continue;
         const float c = D[vv[k] + tap_off(t, G, GG)];
-        const float* w = Wr + (ci * 27 + t) * 16;
 #pragma unroll
-        for (int co = 0; co < 16; ++co) h1[k][co] = __fmaf_rn(w[co], c, h1[k][co]);
+        for (int co = 0; co < 16; ++co) h1[k][co] = __fmaf_rn(P1[co * 864 + ci * 27 + t], c, h1[k][co]);
       }
     }
     __syncthreads();
@@ -227,7 +224,7 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
     dot += w[k] * gw[k];
   }
   dot = block_sum(dot, red);
-  float* gl = Wr;  // conv1 weights are reloaded before the last phase
+  float* gl = Wr;
   float gls = 0.f;
 #pragma unroll
   for (int k = 0; k < kCbV; ++k)
@@ -318,13 +315,52 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
     if (tid == 0) gp[kCbOffB1 + ci] = s;
   }
 
-  // ---- conv1 backward (one cost channel at a time): dW1, dL/dcost -> dsrc, dtgt --------------
-  for (int i = tid; i < kCbW; i += kCbThreads) {
-    const int co = i / (32 * 27), r = i % (32 * 27);
-    Wr[r * 16 + co] = P1[i];
-  }
-  float* scr1 = D + kCbMaxC + 16;
+  // ---- conv1 backward, data side: dL/dcost for all 32 channels of this thread's voxels -------
+  // (transposed conv over dL/dh1 in A; weights are scalar loads), then the cost volume's own
+  // derivative: dL/dsrc[f'] = sum 2 (src - T) dL/dcost, dL/dT = -2 (src - T) dL/dcost.
   float* gT = gtgt + static_cast<int64_t>(p) * 32 * C;
+  {
+    float gc[kCbV][32];
+#pragma unroll
+    for (int k = 0; k < kCbV; ++k)
+#pragma unroll
+      for (int ci = 0; ci < 32; ++ci) gc[k][ci] = 0.f;
+#pragma unroll 1
+    for (int co = 0; co < 16; ++co)
+#pragma unroll 1
+      for (int t = 0; t < 27; ++t) {
+        float g[kCbV];
+#pragma unroll
+        for (int k = 0; k < kCbV; ++k) {
+          const bool ok = vok[k] && ((msk[k] >> (26 - t)) & 1u);
+          g[k] = ok ? A[co * C + (ok ? vv[k] - tap_off(t, G, GG) : 0)] : 0.f;
+        }
+#pragma unroll
+        for (int ci = 0; ci < 32; ++ci) {
+          const float w = P1[co * 864 + ci * 27 + t];
+#pragma unroll
+          for (int k = 0; k < kCbV; ++k) gc[k][ci] = __fmaf_rn(w, g[k], gc[k][ci]);
+        }
+      }
+#pragma unroll
+    for (int ci = 0; ci < 32; ++ci) {
+      float gs = 0.f;
+#pragma unroll
+      for (int k = 0; k < kCbV; ++k) {
+        if (!vok[k]) continue;
+        const int l = vv[k] * 32 + ci;
+        const float d = sv[ci] - tval(l);
+        const float gd = 2.0f * d * gc[k][ci];
+        gs += gd;
+        gT[l] = -gd;
+      }
+      gs = block_sum(gs, red);
+      if (tid == 0) gsrc[static_cast<int64_t>(p) * 32 + ci] = gs;
+    }
+  }
+
+  // ---- conv1 backward, weight side: dW1 one cost channel at a time --------------------------
+  float* scr1 = D + kCbMaxC + 16;
 #pragma unroll 1
   for (int ci = 0; ci < 32; ++ci) {
     __syncthreads();  // previous channel's readers of D are done
@@ -338,27 +374,7 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
       const int co = o / 27, t = o % 27;
       scr1[tid] = wgrad_sum(A + co * C, D, G, GG, t, zc ? G / 2 : 0, zc ? G : G / 2);
     }
-    float gs = 0.f;
-#pragma unroll
-    for (int k = 0; k < kCbV; ++k) {
-      if (!vok[k]) continue;
-      float gc = 0.f;
-#pragma unroll 1
-      for (int t = 0; t < 27; ++t) {
-        if (!((msk[k] >> (26 - t)) & 1u)) continue;
-        const int u = vv[k] - tap_off(t, G, GG);
-        const float* w = Wr + (ci * 27 + t) * 16;
-#pragma unroll
-        for (int co = 0; co < 16; ++co) gc = __fmaf_rn(w[co], A[co * C + u], gc);
-      }
-      const int l = vv[k] * 32 + ci;
-      const float d = sv[ci] - tval(l);
-      const float gd = 2.0f * d * gc;
-      gs += gd;
-      gT[l] = -gd;
-    }
-    gs = block_sum(gs, red);  // (its barriers also order scr1)
-    if (tid == 0) gsrc[static_cast<int64_t>(p) * 32 + ci] = gs;
+    __syncthreads();
     if (tid < 432) {
       const int co = tid / 27, t = tid % 27;
       gp[(co * 32 + ci) * 27 + t] = scr1[tid] + scr1[tid + 432];

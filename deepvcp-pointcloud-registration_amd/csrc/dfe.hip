@@ -146,11 +146,59 @@ __global__ __launch_bounds__(kDfeThreads) void dfe_tgt_kernel(PointsView<T> ref,
 //   Gx[f][c] = sum_q g[q,f] x[q, j*(q,f), c]   (32 x 35),     gs[f] = sum_q g[q,f]
 //   Gh1 = Gx W1^T + gs b1^T,  Gh2 = Gh1 W2^T + gs b2^T
 //   dW3 = Gh2, db3 = gs;  dW2 = W3^T Gh1, db2 = W3^T gs;  dW1 = W2^T W3^T Gx, db1 = W2^T W3^T gs.
-// dfe_bwd_kernel re-runs the forward rows layer by layer (the reference's fp32 arithmetic) to find
-// j*, and accumulates Gx, gs per workgroup (fixed grid, fixed order: deterministic);
-// dfe_bwd_finish_kernel sums the workgroup partials in fp64 and applies the map.
+// dfe_bwd_kernel re-runs the forward rows to find j*, as the forward kernel evaluates them: the
+// collapsed map y = E x + e (dfe_collapse_kernel forms E, e in fp64 and rounds them once to fp32,
+// exactly like dfe_tgt_mfma1_kernel's prologue; 1120 fma per row instead of 3168), and
+// accumulates Gx, gs per workgroup (fixed grid, fixed order: deterministic); dfe_bwd_sum_kernel
+// sums the workgroup partials in fp64 and dfe_bwd_finish_kernel applies the map.
+// Workspace: [nblk][32][36] fp32 partials | [32][36] fp64 sums | [32][36] fp32 (E | e).
 constexpr int kDfeGPart = 32 * 36;  // per workgroup: [f][35 Gx + gs]
 constexpr int kDfeBwdMaxGrid = 2048;
+
+// E = W3 W2 W1 and e = W3 (W2 b1 + b2) + b3 in fp64, rounded once to fp32 ([f][36]: E | e).
+__global__ __launch_bounds__(1024) void dfe_collapse_kernel(const float* __restrict__ params, float* __restrict__ Ee) {
+  __shared__ double p[32][36];
+  const int tid = threadIdx.x;
+  const float* W1 = params;
+  const float* b1 = W1 + 32 * 35;
+  const float* W2 = b1 + 32;
+  const float* b2 = W2 + 32 * 32;
+  const float* W3 = b2 + 32;
+  const float* b3 = W3 + 32 * 32;
+  for (int i = tid; i < 32 * 36; i += 1024) {  // P = W2 W1 | W2 b1 + b2
+    const int o = i / 36, c = i % 36;
+    double acc = 0.0;
+    for (int a = 0; a < 32; ++a)
+      acc = __fma_rn(static_cast<double>(W2[o * 32 + a]), static_cast<double>(c < 35 ? W1[a * 35 + c] : b1[a]), acc);
+    p[o][c] = c < 35 ? acc : acc + static_cast<double>(b2[o]);
+  }
+  __syncthreads();
+  for (int i = tid; i < 32 * 36; i += 1024) {
+    const int o = i / 36, c = i % 36;
+    double acc = 0.0;
+    for (int a = 0; a < 32; ++a) acc = __fma_rn(static_cast<double>(W3[o * 32 + a]), p[a][c], acc);
+    Ee[i] = static_cast<float>(c < 35 ? acc : acc + static_cast<double>(b3[o]));
+  }
+}
+
+// Gs[e] = sum over workgroups of part[k][e] in fp64: 64 elements x 16 slices per workgroup,
+// slices summed in order.
+__global__ __launch_bounds__(1024) void dfe_bwd_sum_kernel(const float* __restrict__ part, int nblk,
+                                                           double* __restrict__ Gs) {
+  __shared__ double sl[16][64];
+  const int tid = threadIdx.x, c = tid & 63, slice = tid >> 6;
+  const int e = blockIdx.x * 64 + c;
+  double s = 0.0;
+  if (e < kDfeGPart)
+    for (int k = slice; k < nblk; k += 16) s += static_cast<double>(part[static_cast<int64_t>(k) * kDfeGPart + e]);
+  sl[slice][c] = s;
+  __syncthreads();
+  if (tid < 64 && e < kDfeGPart) {
+    double t = 0.0;
+    for (int k = 0; k < 16; ++k) t += sl[k][c];
+    Gs[e] = t;
+  }
+}
 
 template <int MODE, typename T>  // MODE 0: materialised rows X (R, 32, 35); 1: fused target rows
 __global__ __launch_bounds__(kDfeThreads) void dfe_bwd_kernel(const T* __restrict__ X, PointsView<T> ref,
@@ -158,7 +206,7 @@ __global__ __launch_bounds__(kDfeThreads) void dfe_bwd_kernel(const T* __restric
                                                               const float* __restrict__ cand,
                                                               const float* __restrict__ dist,
                                                               const int32_t* __restrict__ idx, int Q, int64_t R,
-                                                              const float* __restrict__ params,
+                                                              const float* __restrict__ Ee,
                                                               const float* __restrict__ gout, float* __restrict__ part) {
   __shared__ float ys[kDfeThreads][33];
   __shared__ float xs[kDfeThreads][37];
@@ -183,7 +231,13 @@ __global__ __launch_bounds__(kDfeThreads) void dfe_bwd_kernel(const T* __restric
       dfe_tgt_row(ref, feat, M, cand, dist, idx, Q, b, qq, live, dsh, wq, x);
     }
     float y[32];
-    dfe_mlp(x, y, params);
+#pragma unroll
+    for (int o = 0; o < 32; ++o) {  // E, e: wave-uniform addresses -> scalar operands
+      float a = 0.f;
+#pragma unroll
+      for (int c = 0; c < 35; ++c) a = __fmaf_rn(Ee[o * 36 + c], x[c], a);
+      y[o] = a + Ee[o * 36 + 35];
+    }
     __syncthreads();  // the previous group's readers are done
 #pragma unroll
     for (int c = 0; c < 32; ++c) ys[tid][c] = y[c];
@@ -218,7 +272,7 @@ __global__ __launch_bounds__(kDfeThreads) void dfe_bwd_kernel(const T* __restric
 }
 
 // One 1024-thread workgroup: partials -> packed parameter gradients (W1, b1, W2, b2, W3, b3).
-__global__ __launch_bounds__(1024) void dfe_bwd_finish_kernel(const float* __restrict__ part, int nblk,
+__global__ __launch_bounds__(1024) void dfe_bwd_finish_kernel(const double* __restrict__ Gsum,
                                                               const float* __restrict__ params,
                                                               float* __restrict__ grad) {
   __shared__ double Gs[kDfeGPart];
@@ -236,11 +290,7 @@ __global__ __launch_bounds__(1024) void dfe_bwd_finish_kernel(const float* __res
   float* gb2 = gW2 + 32 * 32;
   float* gW3 = gb2 + 32;
   float* gb3 = gW3 + 32 * 32;
-  for (int e = tid; e < kDfeGPart; e += 1024) {
-    double s = 0.0;
-    for (int k = 0; k < nblk; ++k) s += static_cast<double>(part[static_cast<int64_t>(k) * kDfeGPart + e]);
-    Gs[e] = s;
-  }
+  for (int e = tid; e < kDfeGPart; e += 1024) Gs[e] = Gsum ? Gsum[e] : 0.0;
   __syncthreads();
   {  // Gh1[f][k] = sum_c Gx[f][c] W1[k][c] + gs[f] b1[k]
     const int ff = tid / 32, k = tid % 32;
@@ -330,9 +380,13 @@ extern "C" int dvcp_dfe_tgt(int dtype, const void* ref_xyz, int64_t rb, int64_t 
   return dvcp::launch_status("dvcp_dfe_tgt");
 }
 
+static int64_t dfe_bwd_blocks(int64_t R) {
+  return R <= 0 ? 1 : std::min<int64_t>(dvcp::kDfeBwdMaxGrid, (R + dvcp::kDfeQPerBlock - 1) / dvcp::kDfeQPerBlock);
+}
+
 extern "C" int64_t dvcp_dfe_backward_workspace_bytes(int64_t R) {
-  const int64_t nblk = R <= 0 ? 1 : std::min<int64_t>(dvcp::kDfeBwdMaxGrid, (R + dvcp::kDfeQPerBlock - 1) / dvcp::kDfeQPerBlock);
-  return nblk * dvcp::kDfeGPart * static_cast<int64_t>(sizeof(float));
+  return dfe_bwd_blocks(R) * dvcp::kDfeGPart * static_cast<int64_t>(sizeof(float)) +
+         dvcp::kDfeGPart * static_cast<int64_t>(sizeof(double) + sizeof(float));
 }
 
 // mode 0: X (R, 32, 35) rows (x_dtype); mode 1: fused target rows (the dvcp_dfe_tgt arguments, R = B*Q).
@@ -341,32 +395,37 @@ static int dfe_backward_launch(int mode, int dtype, const void* X, const void* r
                                const int32_t* idx, int Q, int64_t R, const float* params, const float* grad_out,
                                float* ws, float* grad_params, hipStream_t st) {
   if (R <= 0) {  // no rows: zero gradients
-    hipLaunchKernelGGL(dvcp::dfe_bwd_finish_kernel, dim3(1), dim3(1024), 0, st, ws, 0, params, grad_params);
+    hipLaunchKernelGGL(dvcp::dfe_bwd_finish_kernel, dim3(1), dim3(1024), 0, st, nullptr, params, grad_params);
     return dvcp::launch_status("dvcp_dfe_backward");
   }
-  const int nblk = static_cast<int>(dvcp_dfe_backward_workspace_bytes(R) / (dvcp::kDfeGPart * sizeof(float)));
+  const int nblk = static_cast<int>(dfe_bwd_blocks(R));
+  double* Gs = reinterpret_cast<double*>(ws + static_cast<int64_t>(nblk) * dvcp::kDfeGPart);
+  float* Ee = reinterpret_cast<float*>(Gs + dvcp::kDfeGPart);
+  hipLaunchKernelGGL(dvcp::dfe_collapse_kernel, dim3(1), dim3(1024), 0, st, params, Ee);
   const dim3 grid(nblk), block(dvcp::kDfeThreads);
   if (mode == 0 && dtype == DVCP_F32)
     hipLaunchKernelGGL((dvcp::dfe_bwd_kernel<0, float>), grid, block, 0, st, static_cast<const float*>(X),
-                       dvcp::PointsView<float>{nullptr, 0, 0, 0}, nullptr, 0, nullptr, nullptr, nullptr, 1, R, params,
+                       dvcp::PointsView<float>{nullptr, 0, 0, 0}, nullptr, 0, nullptr, nullptr, nullptr, 1, R, Ee,
                        grad_out, ws);
   else if (mode == 0 && dtype == DVCP_F64)
     hipLaunchKernelGGL((dvcp::dfe_bwd_kernel<0, double>), grid, block, 0, st, static_cast<const double*>(X),
-                       dvcp::PointsView<double>{nullptr, 0, 0, 0}, nullptr, 0, nullptr, nullptr, nullptr, 1, R, params,
+                       dvcp::PointsView<double>{nullptr, 0, 0, 0}, nullptr, 0, nullptr, nullptr, nullptr, 1, R, Ee,
                        grad_out, ws);
   else if (mode == 1 && dtype == DVCP_F32)
     hipLaunchKernelGGL((dvcp::dfe_bwd_kernel<1, float>), grid, block, 0, st, nullptr,
                        dvcp::PointsView<float>{static_cast<const float*>(ref_xyz), rb, rc, rn}, ref_feat, M, cand, dist,
-                       idx, Q, R, params, grad_out, ws);
+                       idx, Q, R, Ee, grad_out, ws);
   else if (mode == 1 && dtype == DVCP_F64)
     hipLaunchKernelGGL((dvcp::dfe_bwd_kernel<1, double>), grid, block, 0, st, nullptr,
                        dvcp::PointsView<double>{static_cast<const double*>(ref_xyz), rb, rc, rn}, ref_feat, M, cand,
-                       dist, idx, Q, R, params, grad_out, ws);
+                       dist, idx, Q, R, Ee, grad_out, ws);
   else {
     dvcp::set_error("dvcp_dfe_backward: bad dtype %d", dtype);
     return DVCP_EINVAL;
   }
-  hipLaunchKernelGGL(dvcp::dfe_bwd_finish_kernel, dim3(1), dim3(1024), 0, st, ws, nblk, params, grad_params);
+  hipLaunchKernelGGL(dvcp::dfe_bwd_sum_kernel, dim3(dvcp::ceil_div(dvcp::kDfeGPart, 64)), dim3(1024), 0, st, ws, nblk,
+                     Gs);
+  hipLaunchKernelGGL(dvcp::dfe_bwd_finish_kernel, dim3(1), dim3(1024), 0, st, Gs, params, grad_params);
   return dvcp::launch_status("dvcp_dfe_backward");
 }
 

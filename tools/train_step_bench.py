@@ -1,0 +1,78 @@
+"""Head-training step throughput at C3 (train.py:96-125 with the feature extractor frozen).
+
+One step = model(src, tgt, R_gt, t_init) with autograd on the head -> deepVCP_loss -> backward
+-> Adam step, on one batch of synthetic KITTI-like pairs (8 x 16384 points, K=64, r=2.0, s=0.4).
+Prints one JSON line: pairs/s, ms/step and the per-entry-point HIP-event times of the backward
+kernels (and the forward's) over the timed steps.
+
+    python tools/train_step_bench.py [--steps 10 --warmup 2]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "deepvcp-pointcloud-registration_amd"))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--npoints", type=int, default=16384)
+    args = ap.parse_args()
+    import dvcp
+    from dvcp import _lib
+    from dvcp.synthetic import condition_weights, make_pairs, randomize_bn
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = dvcp.DeepVCP(use_normal=False, K=64, r=2.0, s=0.4).to(dev)
+    src, tgt, R_gt, t_gt = [t.to(dev) for t in make_pairs(args.batch, args.npoints, seed=1234)]
+    randomize_bn(model)
+    model.FE1.eval()
+    with torch.no_grad():
+        _, calib, _ = model.FE1.run(src)
+    condition_weights(model, feats=calib)
+    model.FE1.requires_grad_(False)
+    opt = torch.optim.Adam([p for p in model.parameters() if p.requires_grad], lr=1e-4)
+    t_init = torch.zeros(1, 3)
+
+    def step():
+        kp, vcp = model(src, tgt, R_gt, t_init)
+        opt.zero_grad()
+        loss, R, t = dvcp.deepVCP_loss(kp, vcp, R_gt, t_gt, 0.5)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    _lib.EVENT_LOG = []
+    t0 = time.perf_counter()
+    losses = [step() for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    log, _lib.EVENT_LOG = _lib.EVENT_LOG, None
+    per = {}
+    for name, e0, e1, _ in log:
+        per.setdefault(name, []).append(e0.elapsed_time(e1))
+    stages = {k: {"launches": len(v), "avg_ms": round(sum(v) / len(v), 4),
+                  "total_ms_per_step": round(sum(v) / args.steps, 4)}
+              for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1]))}
+    print(json.dumps({
+        "metric": "head-training steps (forward + deepVCP_loss + backward + Adam), FE frozen",
+        "value": round(args.batch * args.steps / dt, 3), "unit": "pairs/s",
+        "ms_per_step": round(1e3 * dt / args.steps, 3), "steps": args.steps, "warmup": args.warmup,
+        "config": {"pairs": args.batch, "n_points": args.npoints, "K": 64, "r": 2.0, "s": 0.4},
+        "loss_first_last": [float(losses[0].detach()), float(losses[-1].detach())],
+        "stages": stages}))
+
+
+if __name__ == "__main__":
+    main()
