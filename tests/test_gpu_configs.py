@@ -1,0 +1,110 @@
+"""BASELINE.json's other configurations at their full sizes (C3 is bench.py's and
+test_gpu_e2e.py's):
+
+* C2 -- ModelNet40-like, 32 pairs x 2048 points with normals (C_in = 6, fp64), K = 32: the whole
+  batch in one forward; every pair equals its own single-pair run (pairs are independent in
+  eval mode), and pair 0 matches the oracle (key points exact, R, t within 1e-4).
+* C5 -- synthetic 65536-point clouds, K = 256: the first FPS (65536 -> 10000, the dense kernel
+  above the register-resident limit) is bit-exact against the oracle, and the full forward +
+  pose solve runs with its structural properties intact.  C5's "fp16 features" is a stress
+  variant; the path keeps fp32 features (parity with the reference's fp32 FE), so it is run here
+  in fp32.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _calibrated_pair(use_normal, K, r, s, src0, fe_npoint=10000):
+    import oracle as O
+    import dvcp
+    from dvcp.synthetic import condition_weights, randomize_bn
+    torch.manual_seed(0)
+    ref = O.DeepVCP(use_normal=use_normal, K=K, r=r, s=s, fe_npoint=fe_npoint).eval()
+    randomize_bn(ref)
+    with torch.no_grad():
+        _, calib = ref.FE1(src0)
+    condition_weights(ref, feats=calib)
+    mine = dvcp.DeepVCP(use_normal=use_normal, K=K, r=r, s=s, fe_npoint=fe_npoint).eval()
+    mine.load_state_dict(ref.state_dict())
+    return ref, mine
+
+
+def test_c2_modelnet_batch32(cuda):
+    import oracle as O
+    import dvcp
+    from dvcp.synthetic import make_pairs
+    B, N, K, r, s = 32, 2048, 32, 1.0, 0.4
+    src, tgt, R_gt, t_gt = make_pairs(B, N, normals=True, seed=202)   # fp64, C_in = 6
+    ref, mine = _calibrated_pair(True, K, r, s, src[:1])
+    mine.to(cuda)
+    starts = mine.draw_starts(B, N, N)
+    with torch.no_grad():
+        kp, vcp = mine(src.to(cuda), tgt.to(cuda), R_gt.to(cuda), torch.zeros(1, 3), starts=starts)
+        loss, R, t = dvcp.deepVCP_loss(kp, vcp, R_gt.to(cuda), t_gt.to(cuda), 0.5)
+    assert kp.shape == (B, K, 3) and vcp.shape == (B, K, 3)
+    # pairs are independent: each equals its own single-pair run (same FPS starts)
+    for b in (0, 13, 31):
+        with torch.no_grad():
+            kp1, vcp1 = mine(src[b:b + 1].to(cuda), tgt[b:b + 1].to(cuda), R_gt[b:b + 1].to(cuda),
+                             torch.zeros(1, 3), starts=starts[:, b:b + 1])
+            _, R1, t1 = dvcp.deepVCP_loss(kp1, vcp1, R_gt[b:b + 1].to(cuda), t_gt[b:b + 1].to(cuda), 0.5)
+        assert torch.equal(kp1[0], kp[b]), b
+        torch.testing.assert_close(vcp1[0], vcp[b], rtol=0, atol=1e-6)
+        torch.testing.assert_close(R1[0], R[b], rtol=0, atol=1e-9)
+        torch.testing.assert_close(t1[0], t[b], rtol=0, atol=1e-9)
+    # pair 0 against the oracle
+    with torch.no_grad(), O.fps_starts(list(starts[:, :1])), O.tracing() as trace:
+        kp_o, vcp_o = ref(src[:1], tgt[:1], R_gt[:1], torch.zeros(1, 3))
+        _, R_o, t_o = O.deepVCP_loss(kp_o, vcp_o, R_gt[:1], t_gt[:1], 0.5)
+    score = dict(trace)["wl_score"][..., 0]
+    top = torch.sort(score[0].double(), descending=True).values[: K + 1]
+    gaps = (top[:-1] - top[1:]) / top[1:].abs().clamp_min(1e-30)
+    if bool((gaps[gaps > 0] < 1e-4).any()):
+        pytest.skip("oracle top-k of pair 0 not determined at fp32 feature precision")
+    assert torch.equal(kp[:1].cpu(), kp_o.to(kp.dtype))
+    torch.testing.assert_close(R[:1].cpu(), R_o, rtol=0, atol=1e-4)
+    torch.testing.assert_close(t[:1].cpu(), t_o, rtol=0, atol=1e-4)
+    assert torch.isfinite(loss)
+
+
+def test_c5_first_fps_full_size_vs_oracle(cuda):
+    """65536 -> 10000 (sa1 of C5): the dense FPS kernel, bit-exact against the oracle's FPS."""
+    import oracle as O
+    from dvcp import ops
+    g = torch.Generator().manual_seed(505)
+    xyz = torch.rand(1, 65536, 3, generator=g) * 2 - 1
+    start = torch.tensor([40000])
+    want = O.farthest_point_sample(xyz, 10000, start)
+    got, _ = ops.fps(xyz.to(cuda), 10000, start.to(cuda), pdim=1)
+    assert torch.equal(got.cpu(), want)
+
+
+def test_c5_forward_properties(cuda):
+    """C5 shape end to end (N = 65536, K = 256, r = 2.0, s = 0.4): key points are rows of the
+    source cloud, the virtual corresponding points are finite and inside the candidate grids'
+    hull, R is a rotation (R_init = R_gt, Q13's reflection aside) and the loss is finite."""
+    import dvcp
+    from dvcp.synthetic import make_pairs
+    B, N, K, r, s = 1, 65536, 256, 2.0, 0.4
+    src, tgt, R_gt, t_gt = make_pairs(B, N, seed=555)
+    torch.manual_seed(0)
+    mine = dvcp.DeepVCP(use_normal=False, K=K, r=r, s=s).eval().to(cuda)
+    tr = {}
+    with torch.no_grad():
+        kp, vcp = mine(src.to(cuda), tgt.to(cuda), R_gt.to(cuda), torch.zeros(1, 3), trace=tr)
+        loss, R, t = dvcp.deepVCP_loss(kp, vcp, R_gt.to(cuda), t_gt.to(cuda), 0.5)
+    assert kp.shape == (B, K, 3) and vcp.shape == (B, K, 3)
+    pts = src[0].t().to(cuda)                                     # (N, 3)
+    member = (kp[0][:, None, :] == pts[None, :, :]).all(-1).any(-1)
+    assert bool(member.all())                                     # every key point is a source point
+    assert torch.isfinite(vcp).all()
+    lo = tr["cand"].amin(dim=2)
+    hi = tr["cand"].amax(dim=2)
+    assert bool(((vcp >= lo - 1e-5) & (vcp <= hi + 1e-5)).all())  # convex combination of candidates
+    det = torch.linalg.det(R)
+    assert torch.isfinite(loss) and bool(torch.isfinite(R).all())
+    torch.testing.assert_close(R @ R.transpose(1, 2), torch.eye(3, dtype=R.dtype, device=cuda).expand_as(R),
+                               rtol=0, atol=1e-9)
+    assert float(det.abs().min()) == pytest.approx(1.0, abs=1e-9)
