@@ -840,6 +840,117 @@ __global__ __launch_bounds__(kFpsThreads) void fps_dense_kernel(PointsView<T> pt
   }
 }
 
+// Split FPS for clouds above one CU's register budget (C5: 65536 points): S workgroups per cloud,
+// each holding a contiguous chunk of up to P * 512 points (coordinates and running minima in
+// VGPRs).  Every step each workgroup updates its minima with the current centre and publishes
+// its best (value, index) as one key -- float bits of the fp32 minimum (monotonic for values >= 0)
+// over the complemented index, so the maximum key is the largest minimum with the lowest index,
+// the dense kernel's and the reference's argmax rule -- then waits for the cloud's S keys of that
+// step (release/acquire atomics at agent scope, keys double-buffered by step parity: a workgroup
+// can only reach step + 2 after every peer has arrived at step + 1, i.e. after it read step's
+// keys).  Every workgroup reduces the same S keys, so all agree on the next centre.  The wait is
+// bounded: after kFpsSpinCap polls a workgroup gives up and marks its remaining output -1 (the
+// launcher keeps the grid small enough to be co-resident, so this is a guard, not a path).
+constexpr int kFpsSplitMax = 16;
+constexpr int kFpsSplitMaxGrid = 128;
+constexpr uint32_t kFpsSpinCap = 1u << 22;
+
+template <typename T, int P>
+__global__ __launch_bounds__(kFpsThreads) void fps_split_kernel(PointsView<T> pts, int N, int npoint, int S,
+                                                                int b0, const int64_t* __restrict__ start,
+                                                                int64_t* __restrict__ out_idx,
+                                                                T* __restrict__ out_xyz,
+                                                                uint64_t* __restrict__ keys,
+                                                                uint32_t* __restrict__ arrived) {
+  constexpr int kW = kFpsThreads / kWave;
+  constexpr int chunk = P * kFpsThreads;
+  __shared__ uint64_t wbest[kW];
+  __shared__ uint64_t gbest;
+  __shared__ int timed_out;
+  const int b = b0 + static_cast<int>(blockIdx.x) / S, s = static_cast<int>(blockIdx.x) % S;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = s * chunk, n1 = min(N, n0 + chunk);
+  T px[P], py[P], pz[P];
+  float dm[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int n = n0 + p * kFpsThreads + tid;
+    const bool ok = n < n1;
+    px[p] = ok ? pts.at(b, 0, n) : static_cast<T>(0);
+    py[p] = ok ? pts.at(b, 1, n) : static_cast<T>(0);
+    pz[p] = ok ? pts.at(b, 2, n) : static_cast<T>(0);
+    dm[p] = 1e10f;
+  }
+  if (tid == 0) timed_out = 0;
+  int64_t cur = start[b];
+  if (cur < 0 || cur >= N) cur = 0;
+  T cx = pts.at(b, 0, cur), cy = pts.at(b, 1, cur), cz = pts.at(b, 2, cur);
+  uint64_t* kb = keys + static_cast<int64_t>(blockIdx.x / S) * 2 * S;
+  uint32_t* cnt = arrived + blockIdx.x / S;
+  int step = 0;
+  for (; step < npoint; ++step) {
+    if (s == 0 && tid == 0) {
+      out_idx[static_cast<int64_t>(b) * npoint + step] = cur;
+      if (out_xyz) {
+        T* ox = out_xyz + static_cast<int64_t>(b) * 3 * npoint;
+        ox[step] = cx;
+        ox[npoint + step] = cy;
+        ox[2 * npoint + step] = cz;
+      }
+    }
+    uint64_t best = 0;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const int n = n0 + p * kFpsThreads + tid;
+      const T dx = px[p] - cx, dy = py[p] - cy, dz = pz[p] - cz;
+      const T d = (dx * dx + dy * dy) + dz * dz;
+      float m = dm[p];
+      if (d < static_cast<T>(m)) m = static_cast<float>(d);
+      dm[p] = m;
+      const uint64_t key = (static_cast<uint64_t>(__float_as_uint(m)) << 32) | (0xFFFFFFFFu - static_cast<uint32_t>(n));
+      best = (n < n1 && key > best) ? key : best;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint64_t o = __shfl_xor(best, off, kWave);
+      best = o > best ? o : best;
+    }
+    if (lane == 0) wbest[wave] = best;
+    __syncthreads();
+    if (tid == 0) {
+      uint64_t wb = wbest[0];
+      for (int w = 1; w < kW; ++w) wb = wbest[w] > wb ? wbest[w] : wb;
+      uint64_t* slot = kb + (step & 1) * S;
+      __hip_atomic_store(slot + s, wb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t target = static_cast<uint32_t>(step + 1) * static_cast<uint32_t>(S);
+      uint32_t polls = 0;
+      while (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++polls > kFpsSpinCap) {
+          timed_out = 1;
+          break;
+        }
+      }
+      uint64_t g = 0;
+      for (int k = 0; k < S; ++k) {
+        const uint64_t v = __hip_atomic_load(slot + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        g = v > g ? v : g;
+      }
+      gbest = g;
+    }
+    __syncthreads();
+    if (timed_out) break;
+    cur = static_cast<int64_t>(0xFFFFFFFFu - static_cast<uint32_t>(gbest & 0xFFFFFFFFull));
+    cx = pts.at(b, 0, cur);
+    cy = pts.at(b, 1, cur);
+    cz = pts.at(b, 2, cur);
+    __syncthreads();  // gbest / wbest are rewritten next step
+  }
+  if (s == 0 && step < npoint)  // timed out: mark the rest invalid
+    for (int k = step + 1 + tid; k < npoint; k += kFpsThreads) out_idx[static_cast<int64_t>(b) * npoint + k] = -1;
+  if (s == 0 && step < npoint && tid == 0) out_idx[static_cast<int64_t>(b) * npoint + step] = -1;
+}
+
 template <typename T>
 static int launch_fps(const T* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N, int npoint,
                       const int64_t* start, int64_t* out_idx, T* out_xyz, float* ws, hipStream_t st) {
@@ -893,8 +1004,30 @@ static int launch_fps(const T* xyz, int64_t sb, int64_t sc, int64_t sn, int B, i
   }
 #undef DVCP_FPS_CASE
   if (!ws) {
-    set_error("dvcp_fps: N=%d needs the dense path and its B x N fp32 workspace (dvcp_fps_ws)", N);
+    set_error("dvcp_fps: N=%d needs the split/dense path and its B x N fp32 workspace (dvcp_fps_ws)", N);
     return DVCP_EINVAL;
+  }
+  {  // split across workgroups: S per cloud, clouds launched in groups that stay co-resident
+    constexpr int P = sizeof(T) == 4 ? 32 : 16;
+    const int S = ceil_div(N, P * kFpsThreads);
+    static const bool dense_forced = [] {
+      const char* e = getenv("DVCP_FPS_DENSE");
+      return e && e[0] == '1';
+    }();
+    // the workspace (B x N fp32, >= 64 KiB per cloud here) holds keys [B][2][S] and counters [B]
+    if (!dense_forced && S <= kFpsSplitMax) {
+      uint64_t* keys = reinterpret_cast<uint64_t*>(ws);
+      uint32_t* arrived = reinterpret_cast<uint32_t*>(keys + static_cast<int64_t>(B) * 2 * S);
+      hipError_t e = hipMemsetAsync(arrived, 0, sizeof(uint32_t) * B, st);
+      if (e != hipSuccess) return launch_status("dvcp_fps(split memset)");
+      const int per = kFpsSplitMaxGrid / S;
+      for (int b0 = 0; b0 < B; b0 += per) {
+        const int nb = min(per, B - b0);
+        hipLaunchKernelGGL((fps_split_kernel<T, P>), dim3(nb * S), block, 0, st, v, N, npoint, S, b0, start, out_idx,
+                           out_xyz, keys + static_cast<int64_t>(b0) * 2 * S, arrived + b0);
+      }
+      return launch_status("dvcp_fps(split)");
+    }
   }
   hipLaunchKernelGGL((fps_dense_kernel<T>), grid, block, 0, st, v, N, npoint, start, out_idx, out_xyz, ws);
   return launch_status("dvcp_fps(dense)");

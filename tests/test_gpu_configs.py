@@ -108,3 +108,18 @@ def test_c5_forward_properties(cuda):
     torch.testing.assert_close(R @ R.transpose(1, 2), torch.eye(3, dtype=R.dtype, device=cuda).expand_as(R),
                                rtol=0, atol=1e-9)
     assert float(det.abs().min()) == pytest.approx(1.0, abs=1e-9)
+
+
+@pytest.mark.parametrize("dtype,N,npoint,B", [(torch.float32, 40000, 3000, 3), (torch.float64, 20000, 2000, 2)])
+def test_split_fps_vs_oracle(cuda, dtype, N, npoint, B):
+    """The split FPS (S workgroups per cloud, ragged last chunk, several clouds per launch) is
+    bit-exact against the oracle's FPS."""
+    import oracle as O
+    from dvcp import ops
+    g = torch.Generator().manual_seed(N + B)
+    xyz = (torch.rand(B, N, 3, generator=g) * 2 - 1).to(dtype)
+    start = torch.randint(0, N, (B,), generator=g)
+    want = O.farthest_point_sample(xyz, npoint, start)
+    got, ctr = ops.fps(xyz.to(cuda), npoint, start.to(cuda), pdim=1)
+    assert torch.equal(got.cpu(), want)
+    assert torch.equal(ctr.cpu(), torch.gather(xyz, 1, want[..., None].expand(B, npoint, 3)).transpose(1, 2))
