@@ -69,6 +69,29 @@ def test_no_cpu_fallback():
         m(torch.rand(1, 3, 64), torch.rand(1, 3, 64), torch.eye(3, dtype=torch.float64)[None], torch.zeros(1, 3))
 
 
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU behaviour")
+def test_training_guards_and_no_cpu_fallback():
+    """Training mode: an unfrozen feature extractor is refused (its backward does not exist);
+    a frozen one takes the head-autograd path, which has no CPU fallback either."""
+    import dvcp
+    m = dvcp.DeepVCP(use_normal=False, fe_npoint=16)
+    args = (torch.rand(1, 3, 64), torch.rand(1, 3, 64), torch.eye(3, dtype=torch.float64)[None], torch.zeros(1, 3))
+    with pytest.raises(NotImplementedError, match="requires_grad_"):
+        m(*args)
+    m.FE1.eval()
+    with pytest.raises(NotImplementedError, match="requires_grad_"):
+        m(*args)                                   # eval BN, but trainable FE weights
+    m.FE1.requires_grad_(False)
+    assert m._head_training()
+    with pytest.raises(RuntimeError, match="no GPU"):
+        m(*args)
+    with pytest.raises(RuntimeError, match="no GPU"):
+        dvcp.deepVCP_loss(torch.rand(1, 8, 3), torch.rand(1, 8, 3, requires_grad=True),
+                          torch.eye(3, dtype=torch.float64)[None], torch.zeros(1, 3, 1, dtype=torch.float64), 0.5)
+    with pytest.raises(NotImplementedError):
+        dvcp.feat_embedding_layer()(torch.rand(1, 2, 32, 35, requires_grad=True))
+
+
 def test_product_never_imports_oracle():
     for dirpath, _, files in os.walk(os.path.join(PKG, "dvcp")):
         for f in files:
