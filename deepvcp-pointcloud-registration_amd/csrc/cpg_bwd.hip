@@ -26,6 +26,7 @@ namespace dvcp {
 
 constexpr int kCbThreads = 1024;
 constexpr int kCbMaxC = 1331;
+constexpr int kCbMaxG = 11;
 constexpr int kCbA = 16 * kCbMaxC;
 constexpr int kCbW = 16 * 32 * 27;
 constexpr int kCbD = 4 * kCbMaxC;
@@ -360,24 +361,60 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
   }
 
   // ---- conv1 backward, weight side: dW1 one cost channel at a time --------------------------
-  float* scr1 = D + kCbMaxC + 16;
+  // Register-blocked: a thread owns 4 output channels x the 3 x-taps of one (dz, dy) and a slice
+  // of the G^2 grid rows; per row it loads the shifted cost row once (zero-padded at both ends)
+  // and 4 rows of dL/dh1, then does 12 fmas per voxel.  Slices are summed in order afterwards.
+  constexpr int kRowSlices = 24;  // 36 (co quad, dz, dy) items x 24 = 864 threads
+  float* scr1 = Wr;               // [slice][item][12]; dL/dlg is dead by now
 #pragma unroll 1
   for (int ci = 0; ci < 32; ++ci) {
-    __syncthreads();  // previous channel's readers of D are done
+    __syncthreads();  // previous channel's readers of D / scr1 are done
     for (int v = tid; v < C; v += kCbThreads) {
       const float d = sv[ci] - tval(v * 32 + ci);
       D[v] = d * d;
     }
     __syncthreads();
-    if (tid < 2 * 432) {  // (co, t) x two z-halves
-      const int o = tid % 432, zc = tid / 432;
-      const int co = o / 27, t = o % 27;
-      scr1[tid] = wgrad_sum(A + co * C, D, G, GG, t, zc ? G / 2 : 0, zc ? G : G / 2);
+    if (tid < 36 * kRowSlices) {
+      const int item = tid % 36, slice = tid / 36;
+      const int q4 = item / 9, dz = (item / 3) % 3 - 1, dy = item % 3 - 1;
+      const int r0 = (slice * GG) / kRowSlices, r1 = ((slice + 1) * GG) / kRowSlices;
+      float acc[4][3];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) acc[i][k] = 0.f;
+      for (int r = r0; r < r1; ++r) {
+        const int z = static_cast<int>(dG.div(static_cast<uint32_t>(r))), y = r - z * G;
+        const int zz = z + dz, yy = y + dy;
+        if (zz < 0 || zz >= G || yy < 0 || yy >= G) continue;
+        float row[kCbMaxG + 2];  // cost row (zz, yy, x - 1), zero outside the grid
+        row[0] = 0.f;
+#pragma unroll
+        for (int x = 0; x < kCbMaxG + 1; ++x) row[x + 1] = x < G ? D[(zz * G + yy) * G + x] : 0.f;
+        const int base = (z * G + y) * G;
+#pragma unroll
+        for (int x = 0; x < kCbMaxG; ++x) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float g = x < G ? A[(q4 * 4 + i) * C + base + (x < G ? x : 0)] : 0.f;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) acc[i][k] = __fmaf_rn(g, row[x + k], acc[i][k]);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) scr1[(slice * 36 + item) * 12 + i * 3 + k] = acc[i][k];
     }
     __syncthreads();
-    if (tid < 432) {
-      const int co = tid / 27, t = tid % 27;
-      gp[(co * 32 + ci) * 27 + t] = scr1[tid] + scr1[tid + 432];
+    if (tid < 432) {  // (item, i, k) -> (co, t)
+      const int item = tid / 12, i = (tid % 12) / 3, k = tid % 3;
+      const int q4 = item / 9, dz = (item / 3) % 3 - 1, dy = item % 3 - 1;
+      float sum = 0.f;
+      for (int sl = 0; sl < kRowSlices; ++sl) sum += scr1[(sl * 36 + item) * 12 + i * 3 + k];
+      const int co = q4 * 4 + i, t = (dz + 1) * 9 + (dy + 1) * 3 + k;
+      gp[(co * 32 + ci) * 27 + t] = sum;
     }
   }
 }
