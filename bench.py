@@ -28,7 +28,8 @@ sys.path.insert(0, os.path.join(ROOT, "deepvcp-pointcloud-registration_amd"))
 # Hardware queues per process (read when HIP initialises, so set before torch touches the GPU).
 # Each in-flight batch drives two streams (the FPS chain and its side stream); with HIP's default
 # of 4 queues, streams that share a queue serialise behind each other's multi-millisecond FPS
-# launches.  8 measured +13% over 4 (profiles/README.md).  --hw-queues overrides.
+# launches.  8 measured +13% over 4; 16 (8 batches in flight x 2 streams) is the default, and
+# 24 queues or 12-16 batches measured no better (profiles/README.md).  --hw-queues overrides.
 def _hw_queues(argv):
     for i, a in enumerate(argv):
         if a == "--hw-queues" and i + 1 < len(argv):

@@ -446,9 +446,9 @@ extern "C" int dvcp_registration_error(const double* R_pred, const double* t_pre
 }
 
 extern "C" int dvcp_rigid_transform(const double* x, const double* y, int B, int n, double* R, double* t, void* stream) {
+  DVCP_REQUIRE(n > 0 && B >= 0, "dvcp_rigid_transform: n=%d B=%d", n, B);
+  if (B == 0) return DVCP_OK;  // empty tensors may carry null pointers
   DVCP_REQUIRE(x && y && R && t, "dvcp_rigid_transform: null pointer");
-  DVCP_REQUIRE(n > 0, "dvcp_rigid_transform: n=%d", n);
-  if (B == 0) return DVCP_OK;
   hipLaunchKernelGGL(dvcp::rigid_transform_kernel, dim3(B), dim3(dvcp::kRgThreads), 0, static_cast<hipStream_t>(stream), x,
                      y, n, R, t);
   return dvcp::launch_status("dvcp_rigid_transform");
@@ -457,11 +457,11 @@ extern "C" int dvcp_rigid_transform(const double* x, const double* y, int B, int
 extern "C" int dvcp_svd_optimization(const double* x, const double* y_pred, const double* R_true, const double* t_true,
                                      int B, int n, double* R2, double* t2, double* x1, double* y2, double* partial,
                                      void* stream) {
-  DVCP_REQUIRE(x && y_pred && R_true && t_true && R2 && t2, "dvcp_svd_optimization: null pointer");
   DVCP_REQUIRE(n > 0 && n <= dvcp::kRgMaxN, "dvcp_svd_optimization: n=%d unsupported (1..1024)", n);
   const int n_in = static_cast<int>(n * 0.8);  // deepVCP_loss.py:76 int(N*0.8)
   DVCP_REQUIRE(n_in > 0, "dvcp_svd_optimization: int(0.8 n) == 0");
-  if (B == 0) return DVCP_OK;
+  if (B == 0) return DVCP_OK;  // empty tensors may carry null pointers
+  DVCP_REQUIRE(x && y_pred && R_true && t_true && R2 && t2, "dvcp_svd_optimization: null pointer");
   hipLaunchKernelGGL(dvcp::svd_opt_kernel, dim3(B), dim3(dvcp::kRgThreads), 0, static_cast<hipStream_t>(stream), x,
                      y_pred, R_true, t_true, n, n_in, R2, t2, x1, y2, partial);
   return dvcp::launch_status("dvcp_svd_optimization");
@@ -471,12 +471,12 @@ extern "C" int dvcp_svd_optimization_backward(const double* x, const double* y_p
                                               const double* t_true, int B, int n, const double* partial,
                                               const double* grad_loss, double alpha, double* grad_y_pred,
                                               void* stream) {
-  DVCP_REQUIRE(x && y_pred && R_true && t_true && partial && grad_loss && grad_y_pred,
-               "dvcp_svd_optimization_backward: null pointer");
   DVCP_REQUIRE(n > 0 && n <= dvcp::kRgMaxN, "dvcp_svd_optimization_backward: n=%d unsupported (1..1024)", n);
   const int n_in = static_cast<int>(n * 0.8);
   DVCP_REQUIRE(n_in > 0, "dvcp_svd_optimization_backward: int(0.8 n) == 0");
-  if (B == 0) return DVCP_OK;
+  if (B == 0) return DVCP_OK;  // empty tensors may carry null pointers
+  DVCP_REQUIRE(x && y_pred && R_true && t_true && partial && grad_loss && grad_y_pred,
+               "dvcp_svd_optimization_backward: null pointer");
   const double inv_count = 1.0 / (static_cast<double>(B) * 3.0 * n_in);
   hipLaunchKernelGGL(dvcp::svd_opt_bwd_kernel, dim3(B), dim3(dvcp::kRgThreads), 0, static_cast<hipStream_t>(stream), x,
                      y_pred, R_true, t_true, n, n_in, B, partial, grad_loss, alpha, inv_count, grad_y_pred);

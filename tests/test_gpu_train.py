@@ -185,3 +185,33 @@ def test_training_mode_needs_frozen_fe(cuda):
     x = torch.rand(1, 3, 128, device=cuda)
     with pytest.raises(NotImplementedError, match="requires_grad_"):
         m(x, x, torch.eye(3, dtype=torch.float64, device=cuda)[None], torch.zeros(1, 3))
+
+
+def test_backward_entry_points_empty_inputs(cuda):
+    """Zero key points / rows / pairs: the backward entry points return zero gradients."""
+    from dvcp import ops
+    dev = cuda
+    params = torch.randn(ops.DFE_NPARAMS, device=dev)
+    gp = ops.dfe_backward(torch.zeros(0, 32, 35, device=dev), params, torch.zeros(0, 32, device=dev))
+    assert gp.shape == (ops.DFE_NPARAMS,) and not gp.any()
+    cparams = torch.randn(ops.CPG_NPARAMS, device=dev)
+    C = 216
+    gsrc, gtgt, gpc = ops.cpg_backward(torch.zeros(0, 2, 32, device=dev), torch.zeros(0, 2, 32, C, device=dev),
+                                       torch.zeros(0, 2, C, 3, device=dev), 6, cparams,
+                                       torch.zeros(0, 2, 3, device=dev))
+    assert gsrc.numel() == 0 and gtgt.numel() == 0 and not gpc.any()
+    x = torch.zeros(0, 3, 64, dtype=torch.float64, device=dev)
+    g = ops.svd_optimization_backward(x, x, torch.zeros(0, 3, 3, dtype=torch.float64, device=dev),
+                                      torch.zeros(0, 3, 1, dtype=torch.float64, device=dev),
+                                      torch.zeros(0, 2, dtype=torch.float64, device=dev),
+                                      torch.ones((), dtype=torch.float64, device=dev), 0.5)
+    assert g.shape == (0, 3, 64)
+
+
+def test_cpg_backward_rejects_bad_grid(cuda):
+    from dvcp import ops
+    C = 1
+    with pytest.raises(RuntimeError, match="grid side"):
+        ops.cpg_backward(torch.zeros(1, 1, 32, device=cuda), torch.zeros(1, 1, 32, C, device=cuda),
+                         torch.zeros(1, 1, C, 3, device=cuda), 1, torch.zeros(ops.CPG_NPARAMS, device=cuda),
+                         torch.zeros(1, 1, 3, device=cuda))
