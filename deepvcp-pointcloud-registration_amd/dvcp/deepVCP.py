@@ -69,19 +69,20 @@ class DeepVCP(nn.Module):
         del S3
         return torch.stack([torch.randint(0, n, (B,), dtype=torch.long) for n in sizes])
 
-    def forward(self, src_pts, tgt_pts, R_init, t_init, starts=None, trace=None, keypoint_idx=None):
-        """``starts`` (7, B): FPS start indices (drawn like the reference when None).
-        ``trace``: dict filled with the stage outputs.  ``keypoint_idx`` (B, K): stage override
-        for parity testing -- use these FE-space key-point indices instead of the top-k."""
-        train_head = self._head_training()
+    def extract_features(self, src_pts, tgt_pts, starts=None):
+        """The feature-extractor half of forward (deepVCP.py:29,72 -- FE1 on both clouds, the
+        weighting layer's scores): a dict the head half (``forward_head``) consumes.  It depends on
+        no trainable head parameter, so with the extractor frozen a training loop can run it for
+        upcoming batches on other streams while the current batch's head trains
+        (tools/train_step_bench.py --prefetch)."""
+        if self.FE1.training:
+            _inference_only(self.FE1)
         _lib.require_gpu(src_pts, tgt_pts)   # no CPU fallback
         B = src_pts.shape[0]
-        K, r, s = self.K, self.r, self.s
         dev = src_pts.device
         if starts is None:
             starts = self.draw_starts(B, src_pts.shape[2], tgt_pts.shape[2])
         starts = starts.to(dev, non_blocking=True)
-
         side = self._side_stream(dev)
         if src_pts.shape == tgt_pts.shape and src_pts.dtype == tgt_pts.dtype:
             # src and tgt share FE1's weights and eval-mode FE is per cloud: one 2B-cloud pass
@@ -95,6 +96,27 @@ class DeepVCP(nn.Module):
         else:
             src_xyz, src_feat, score = self.FE1.run(src_pts, starts[0:3], wl=self.WL, side_stream=side)
             tgt_xyz, tgt_feat, _ = self.FE1.run(tgt_pts, starts[4:7], side_stream=side)
+        return dict(src_xyz=src_xyz, src_feat=src_feat, score=score, tgt_xyz=tgt_xyz, tgt_feat=tgt_feat,
+                    starts=starts)
+
+    def forward_head(self, feats, R_init, t_init=None, trace=None, keypoint_idx=None):
+        """The head half of forward (deepVCP.py:39-110 after FE1): key points, DFE, candidates,
+        kNN, CPG.  Differentiable in DFE/CPG when training the head (see ``_head_training``)."""
+        return self._head(feats, R_init, self._head_training(), trace, keypoint_idx)
+
+    def forward(self, src_pts, tgt_pts, R_init, t_init, starts=None, trace=None, keypoint_idx=None):
+        """``starts`` (7, B): FPS start indices (drawn like the reference when None).
+        ``trace``: dict filled with the stage outputs.  ``keypoint_idx`` (B, K): stage override
+        for parity testing -- use these FE-space key-point indices instead of the top-k."""
+        train_head = self._head_training()
+        return self._head(self.extract_features(src_pts, tgt_pts, starts), R_init, train_head, trace, keypoint_idx)
+
+    def _head(self, f, R_init, train_head, trace, keypoint_idx):
+        src_xyz, src_feat, score, tgt_xyz, tgt_feat, starts = (f["src_xyz"], f["src_feat"], f["score"], f["tgt_xyz"],
+                                                               f["tgt_feat"], f["starts"])
+        B = src_xyz.shape[0]
+        K, r, s = self.K, self.r, self.s
+        dev = src_xyz.device
         top = ops.topk(score, K) if keypoint_idx is None else keypoint_idx.to(dev, torch.int64).contiguous()
         keypts, src_cat, moved = ops.src_keypoints(src_xyz, src_feat, top, starts[3], R_init, radius=1.0, nsample=32)
         src_dfe = autograd.dfe_rows(src_cat, self.DFE) if train_head else ops.dfe(src_cat, self.DFE.packed_params())

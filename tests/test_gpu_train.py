@@ -215,3 +215,18 @@ def test_cpg_backward_rejects_bad_grid(cuda):
         ops.cpg_backward(torch.zeros(1, 1, 32, device=cuda), torch.zeros(1, 1, 32, C, device=cuda),
                          torch.zeros(1, 1, C, 3, device=cuda), 1, torch.zeros(ops.CPG_NPARAMS, device=cuda),
                          torch.zeros(1, 1, 3, device=cuda))
+
+
+def test_extract_features_plus_head_equals_forward(cuda):
+    """forward == forward_head(extract_features(...)) (the split the prefetching trainer uses)."""
+    import dvcp
+    from dvcp.synthetic import make_pairs
+    src, tgt, R_gt, _ = make_pairs(2, 2048, seed=71)
+    torch.manual_seed(0)
+    m = dvcp.DeepVCP(use_normal=False, K=32, r=1.0, s=0.4, fe_npoint=512).eval().to(cuda)
+    starts = m.draw_starts(2, 2048, 2048)
+    with torch.no_grad():
+        kp, vcp = m(src.to(cuda), tgt.to(cuda), R_gt.to(cuda), torch.zeros(1, 3), starts=starts)
+        f = m.extract_features(src.to(cuda), tgt.to(cuda), starts=starts)
+        kp2, vcp2 = m.forward_head(f, R_gt.to(cuda))
+    assert torch.equal(kp, kp2) and torch.equal(vcp, vcp2)

@@ -5,8 +5,13 @@ One step = model(src, tgt, R_gt, t_init) with autograd on the head -> deepVCP_lo
 Prints one JSON line: pairs/s, ms/step and the per-entry-point HIP-event times of the backward
 kernels (and the forward's) over the timed steps.
 
-    python tools/train_step_bench.py [--steps 10 --warmup 2]
+    python tools/train_step_bench.py [--steps 10 --warmup 2] [--prefetch P]
+
+--prefetch P: the frozen feature extractor of the next P batches runs ahead on P streams
+(DeepVCP.extract_features) while the current batch's head trains (DeepVCP.forward_head); the
+head steps themselves stay in order on the default stream, as the optimizer requires.
 """
+import collections
 import argparse
 import json
 import os
@@ -25,6 +30,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--npoints", type=int, default=16384)
+    ap.add_argument("--prefetch", type=int, default=0)
     args = ap.parse_args()
     import dvcp
     from dvcp import _lib
@@ -42,12 +48,45 @@ def main():
     opt = torch.optim.Adam([p for p in model.parameters() if p.requires_grad], lr=1e-4)
     t_init = torch.zeros(1, 3)
 
+    P = args.prefetch
+    lanes = [torch.cuda.Stream(device=dev) for _ in range(max(P, 1))]
+    batches = [(src, tgt, R_gt, t_gt)]
+    for i in range(1, max(P, 1)):
+        batches.append(tuple(t.to(dev) for t in make_pairs(args.batch, args.npoints, seed=1234 + 7919 * i)))
+    main = torch.cuda.current_stream(dev)
+    pending = collections.deque()
+    issued = [0]
+
+    def issue():
+        i = issued[0]
+        issued[0] += 1
+        lane = lanes[i % len(lanes)]
+        lane.wait_stream(main)
+        b = batches[i % len(batches)]
+        with torch.no_grad(), torch.cuda.stream(lane):
+            f = model.extract_features(b[0], b[1])
+            ev = torch.cuda.Event()
+            ev.record(lane)
+        pending.append((f, ev, b))
+
     def step():
-        kp, vcp = model(src, tgt, R_gt, t_init)
+        if P == 0:
+            kp, vcp = model(src, tgt, R_gt, t_init)
+            Rg, tg = R_gt, t_gt
+        else:
+            while len(pending) < P:
+                issue()
+            f, ev, (_, _, Rg, tg) = pending.popleft()
+            main.wait_event(ev)
+            for t in f.values():
+                t.record_stream(main)
+            kp, vcp = model.forward_head(f, Rg)
         opt.zero_grad()
-        loss, R, t = dvcp.deepVCP_loss(kp, vcp, R_gt, t_gt, 0.5)
+        loss, R, t = dvcp.deepVCP_loss(kp, vcp, Rg, tg, 0.5)
         loss.backward()
         opt.step()
+        if P:
+            issue()
         return loss
 
     for _ in range(args.warmup):
@@ -67,6 +106,7 @@ def main():
               for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1]))}
     print(json.dumps({
         "metric": "head-training steps (forward + deepVCP_loss + backward + Adam), FE frozen",
+        "prefetch": P,
         "value": round(args.batch * args.steps / dt, 3), "unit": "pairs/s",
         "ms_per_step": round(1e3 * dt / args.steps, 3), "steps": args.steps, "warmup": args.warmup,
         "config": {"pairs": args.batch, "n_points": args.npoints, "K": 64, "r": 2.0, "s": 0.4},
