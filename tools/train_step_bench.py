@@ -19,6 +19,9 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# prefetch lanes each drive two streams (bench.py's reasoning): 16 hardware queues, read when HIP
+# initialises (P=3: 496 pairs/s at HIP's default of 4, 512 at 16)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 sys.path.insert(0, os.path.join(ROOT, "deepvcp-pointcloud-registration_amd"))
 
 import torch  # noqa: E402
