@@ -207,7 +207,8 @@ __global__ __launch_bounds__(kDfeThreads) void dfe_bwd_kernel(const T* __restric
                                                               const float* __restrict__ dist,
                                                               const int32_t* __restrict__ idx, int Q, int64_t R,
                                                               const float* __restrict__ Ee,
-                                                              const float* __restrict__ gout, float* __restrict__ part) {
+                                                              const float* __restrict__ gout, float* __restrict__ part,
+                                                              float* __restrict__ gX, float* __restrict__ gF) {
   __shared__ float ys[kDfeThreads][33];
   __shared__ float xs[kDfeThreads][37];
   __shared__ double wq[kDfeQPerBlock][32];
@@ -258,6 +259,31 @@ __global__ __launch_bounds__(kDfeThreads) void dfe_bwd_kernel(const T* __restric
 #pragma unroll
     for (int i = 0; i < 35; ++i) acc[i] = __fmaf_rn(g, xs[ql * 32 + bj][i], acc[i]);
     acc[35] += g;
+    if (gX || gF) {  // block-uniform: the input rows' gradient, dL/dx_j = sum_{f: j*(f) = j} g_f E[f]
+      __syncthreads();  // the Gx reads of xs are done
+#pragma unroll
+      for (int i = 0; i < 35; ++i) xs[tid][i] = 0.f;
+      __syncthreads();
+      for (int i = 0; i < 35; ++i) atomicAdd(&xs[ql * 32 + bj][i], g * Ee[f * 36 + i]);
+      __syncthreads();
+      const int j = f;  // this thread's own row
+      if constexpr (MODE == 0) {
+        if (live)
+          for (int i = 0; i < 35; ++i) gX[(q * 32 + j) * 35 + i] = xs[tid][i];
+      } else {
+        // get_cat_feat_tgt.py:85,95: x[3 + c] = F[idx_j, c] * w[c] (fp64 weight) -> dF[idx_j, c] += dx * w[c]
+        if (live) {
+          const int b = static_cast<int>(q / Q);
+          int n = idx[q * 32 + j];
+          n = n < 0 ? 0 : (n >= M ? M - 1 : n);
+          float* dst = gF + (static_cast<int64_t>(b) * M + n) * 32;
+          for (int c = 0; c < 32; ++c) {
+            const float d = xs[tid][3 + c];
+            if (d != 0.f) atomicAdd(dst + c, static_cast<float>(static_cast<double>(d) * wq[ql][c]));
+          }
+        }
+      }
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -384,7 +410,7 @@ static int64_t dfe_bwd_blocks(int64_t R) {
   return R <= 0 ? 1 : std::min<int64_t>(dvcp::kDfeBwdMaxGrid, (R + dvcp::kDfeQPerBlock - 1) / dvcp::kDfeQPerBlock);
 }
 
-extern "C" int64_t dvcp_dfe_backward_workspace_bytes(int64_t R) {
+extern "C" int64_t dvcp_dfe_backward_workspace_bytes(int64_t R) {  // (same for the target entry)
   return dfe_bwd_blocks(R) * dvcp::kDfeGPart * static_cast<int64_t>(sizeof(float)) +
          dvcp::kDfeGPart * static_cast<int64_t>(sizeof(double) + sizeof(float));
 }
@@ -393,7 +419,7 @@ extern "C" int64_t dvcp_dfe_backward_workspace_bytes(int64_t R) {
 static int dfe_backward_launch(int mode, int dtype, const void* X, const void* ref_xyz, int64_t rb, int64_t rc,
                                int64_t rn, int M, const float* ref_feat, const float* cand, const float* dist,
                                const int32_t* idx, int Q, int64_t R, const float* params, const float* grad_out,
-                               float* ws, float* grad_params, hipStream_t st) {
+                               float* ws, float* grad_params, float* gX, float* gF, hipStream_t st) {
   if (R <= 0) {  // no rows: zero gradients
     hipLaunchKernelGGL(dvcp::dfe_bwd_finish_kernel, dim3(1), dim3(1024), 0, st, nullptr, params, grad_params);
     return dvcp::launch_status("dvcp_dfe_backward");
@@ -406,19 +432,19 @@ static int dfe_backward_launch(int mode, int dtype, const void* X, const void* r
   if (mode == 0 && dtype == DVCP_F32)
     hipLaunchKernelGGL((dvcp::dfe_bwd_kernel<0, float>), grid, block, 0, st, static_cast<const float*>(X),
                        dvcp::PointsView<float>{nullptr, 0, 0, 0}, nullptr, 0, nullptr, nullptr, nullptr, 1, R, Ee,
-                       grad_out, ws);
+                       grad_out, ws, gX, gF);
   else if (mode == 0 && dtype == DVCP_F64)
     hipLaunchKernelGGL((dvcp::dfe_bwd_kernel<0, double>), grid, block, 0, st, static_cast<const double*>(X),
                        dvcp::PointsView<double>{nullptr, 0, 0, 0}, nullptr, 0, nullptr, nullptr, nullptr, 1, R, Ee,
-                       grad_out, ws);
+                       grad_out, ws, gX, gF);
   else if (mode == 1 && dtype == DVCP_F32)
     hipLaunchKernelGGL((dvcp::dfe_bwd_kernel<1, float>), grid, block, 0, st, nullptr,
                        dvcp::PointsView<float>{static_cast<const float*>(ref_xyz), rb, rc, rn}, ref_feat, M, cand, dist,
-                       idx, Q, R, Ee, grad_out, ws);
+                       idx, Q, R, Ee, grad_out, ws, gX, gF);
   else if (mode == 1 && dtype == DVCP_F64)
     hipLaunchKernelGGL((dvcp::dfe_bwd_kernel<1, double>), grid, block, 0, st, nullptr,
                        dvcp::PointsView<double>{static_cast<const double*>(ref_xyz), rb, rc, rn}, ref_feat, M, cand,
-                       dist, idx, Q, R, Ee, grad_out, ws);
+                       dist, idx, Q, R, Ee, grad_out, ws, gX, gF);
   else {
     dvcp::set_error("dvcp_dfe_backward: bad dtype %d", dtype);
     return DVCP_EINVAL;
@@ -430,21 +456,21 @@ static int dfe_backward_launch(int mode, int dtype, const void* X, const void* r
 }
 
 extern "C" int dvcp_dfe_backward(int x_dtype, const void* X, int64_t R, const float* params, const float* grad_out,
-                                 float* ws, float* grad_params, void* stream) {
+                                 float* ws, float* grad_params, float* grad_X, void* stream) {
   DVCP_REQUIRE(params && grad_params && (R <= 0 || (X && grad_out && ws)), "dvcp_dfe_backward: null pointer");
   return dfe_backward_launch(0, x_dtype, X, nullptr, 0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, 1, R, params,
-                             grad_out, ws, grad_params, static_cast<hipStream_t>(stream));
+                             grad_out, ws, grad_params, grad_X, nullptr, static_cast<hipStream_t>(stream));
 }
 
 extern "C" int dvcp_dfe_tgt_backward(int dtype, const void* ref_xyz, int64_t rb, int64_t rc, int64_t rn, int M,
                                      const float* ref_feat, const float* cand, const float* dist, const int32_t* idx,
                                      int B, int Q, const float* params, const float* grad_out, float* ws,
-                                     float* grad_params, void* stream) {
+                                     float* grad_params, float* grad_ref_feat, void* stream) {
   DVCP_REQUIRE(params && grad_params, "dvcp_dfe_tgt_backward: null pointer");
   DVCP_REQUIRE(B == 0 || Q == 0 || (ref_xyz && ref_feat && cand && dist && idx && grad_out && ws),
                "dvcp_dfe_tgt_backward: null pointer");
   DVCP_REQUIRE(M > 0 && B >= 0 && Q >= 0, "dvcp_dfe_tgt_backward: bad sizes");
   return dfe_backward_launch(1, dtype, nullptr, ref_xyz, rb, rc, rn, M, ref_feat, cand, dist, idx, Q > 0 ? Q : 1,
-                             static_cast<int64_t>(B) * Q, params, grad_out, ws, grad_params,
+                             static_cast<int64_t>(B) * Q, params, grad_out, ws, grad_params, nullptr, grad_ref_feat,
                              static_cast<hipStream_t>(stream));
 }

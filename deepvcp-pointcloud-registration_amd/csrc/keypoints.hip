@@ -22,7 +22,8 @@ template <typename T>
 __global__ __launch_bounds__(kKpThreads) void src_keypoints_kernel(
     const T* __restrict__ fe_xyz, const float* __restrict__ fe_feat, int S, const int64_t* __restrict__ topk, int K,
     const int64_t* __restrict__ kstart, T r2, int ns, const double* __restrict__ R_init, int64_t r_b,
-    T* __restrict__ keypts, float* __restrict__ src_cat, double* __restrict__ moved) {
+    T* __restrict__ keypts, float* __restrict__ src_cat, double* __restrict__ moved,
+    const float* __restrict__ grad_cat, float* __restrict__ grad_feat) {  // backward: grad_cat -> grad_feat
   __shared__ T kx[kKpMaxK], ky[kKpMaxK], kz[kKpMaxK], kss[kKpMaxK];
   __shared__ int fidx[kKpMaxK];
   __shared__ int pidx[kKpMaxK * kKpMaxNs];
@@ -42,6 +43,9 @@ __global__ __launch_bounds__(kKpThreads) void src_keypoints_kernel(
     ky[tid] = y;
     kz[tid] = z;
     kss[tid] = sumsq3(x, y, z);
+  }
+  if (tid < K && !grad_cat) {
+    const T x = kx[tid], y = ky[tid], z = kz[tid];
     T* o = keypts + (static_cast<int64_t>(b) * K + tid) * 3;
     o[0] = x;
     o[1] = y;
@@ -111,6 +115,17 @@ __global__ __launch_bounds__(kKpThreads) void src_keypoints_kernel(
   }
   __syncthreads();
 
+  if (grad_cat) {  // backward of step 5's feature product (pointnet2_utils.py:59 gather, get_cat_feat_src.py:50)
+    float* dF = grad_feat + static_cast<int64_t>(b) * S * 32;
+    for (int e = tid; e < K * ns; e += kKpThreads) {
+      const int i = e / ns, p = pidx[e];
+      const T w = dist[e] / dsum[i];
+      const float* g = grad_cat + (static_cast<int64_t>(b) * K * ns + e) * 35 + 3;
+      for (int q = 0; q < 32; ++q)
+        if (g[q] != 0.f) atomicAdd(dF + static_cast<int64_t>(p) * 32 + q, static_cast<float>(static_cast<T>(g[q]) * w));
+    }
+    return;
+  }
   // 5. rows of the DFE input: [grouped - keypt (3), feat * w (32)] -> fp32
   const float* F = fe_feat + static_cast<int64_t>(b) * S * 32;
   for (int e = tid; e < K * ns; e += kKpThreads) {
@@ -133,7 +148,8 @@ static int launch_kp(const void* fe_xyz, const float* fe_feat, int S, const int6
                      float* src_cat, double* moved, hipStream_t st) {
   const T r2 = static_cast<T>(radius * radius);
   hipLaunchKernelGGL((src_keypoints_kernel<T>), dim3(B), dim3(kKpThreads), 0, st, static_cast<const T*>(fe_xyz),
-                     fe_feat, S, topk, K, kstart, r2, ns, R, r_b, static_cast<T*>(keypts), src_cat, moved);
+                     fe_feat, S, topk, K, kstart, r2, ns, R, r_b, static_cast<T*>(keypts), src_cat, moved, nullptr,
+                     nullptr);
   return launch_status("dvcp_src_keypoints");
 }
 
@@ -160,4 +176,33 @@ extern "C" int dvcp_src_keypoints(int dtype, const void* fe_xyz, const float* fe
                                    src_cat, moved, st);
   dvcp::set_error("dvcp_src_keypoints: bad dtype %d", dtype);
   return DVCP_EINVAL;
+}
+
+// Backward of the key-point stage's feature rows: grad_cat (B x K x ns x 35, the src_cat gradient)
+// -> grad_feat (B x S x 32 fp32, accumulated: zero it first).  Re-runs steps 1-4 (key-point FPS,
+// ball query, distance weights) exactly as the forward; only the 32 feature columns carry a
+// gradient (the coordinates come from index ops).
+extern "C" int dvcp_src_keypoints_backward(int dtype, const void* fe_xyz, int S, const int64_t* topk, int B, int K,
+                                           const int64_t* kstart, double radius, int nsample, const float* grad_cat,
+                                           float* grad_feat, void* stream) {
+  DVCP_REQUIRE(K > 0 && K <= dvcp::kKpMaxK && K <= S && nsample > 0 && nsample <= dvcp::kKpMaxNs && K >= nsample,
+               "dvcp_src_keypoints_backward: K=%d nsample=%d unsupported", K, nsample);
+  if (B == 0) return DVCP_OK;
+  DVCP_REQUIRE(fe_xyz && topk && kstart && grad_cat && grad_feat, "dvcp_src_keypoints_backward: null pointer");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (dtype == DVCP_F32) {
+    const float r2 = static_cast<float>(radius * radius);
+    hipLaunchKernelGGL((dvcp::src_keypoints_kernel<float>), dim3(B), dim3(dvcp::kKpThreads), 0, st,
+                       static_cast<const float*>(fe_xyz), nullptr, S, topk, K, kstart, r2, nsample, nullptr, 0,
+                       nullptr, nullptr, nullptr, grad_cat, grad_feat);
+  } else if (dtype == DVCP_F64) {
+    const double r2 = radius * radius;
+    hipLaunchKernelGGL((dvcp::src_keypoints_kernel<double>), dim3(B), dim3(dvcp::kKpThreads), 0, st,
+                       static_cast<const double*>(fe_xyz), nullptr, S, topk, K, kstart, r2, nsample, nullptr, 0,
+                       nullptr, nullptr, nullptr, grad_cat, grad_feat);
+  } else {
+    dvcp::set_error("dvcp_src_keypoints_backward: bad dtype %d", dtype);
+    return DVCP_EINVAL;
+  }
+  return dvcp::launch_status("dvcp_src_keypoints_backward");
 }

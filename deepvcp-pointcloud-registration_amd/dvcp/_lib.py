@@ -46,8 +46,9 @@ SIGNATURES = {
     "dvcp_registration_error": [_P, _P, _P, _L, _P, _L, _I, _P, _P, _P],
     "dvcp_rigid_apply": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _L, _P, _P],
     "dvcp_svd_optimization_backward": [_P, _P, _P, _P, _I, _I, _P, _P, _D, _P, _P],
-    "dvcp_dfe_backward": [_I, _P, _L, _P, _P, _P, _P, _P],
-    "dvcp_dfe_tgt_backward": [_I, _P, _L, _L, _L, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P],
+    "dvcp_dfe_backward": [_I, _P, _L, _P, _P, _P, _P, _P, _P],
+    "dvcp_dfe_tgt_backward": [_I, _P, _L, _L, _L, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P],
+    "dvcp_src_keypoints_backward": [_I, _P, _I, _P, _I, _I, _P, _D, _I, _P, _P, _P],
     "dvcp_cpg_backward": [_P, _P, _L, _L, _L, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P],
 }
 

@@ -9,7 +9,10 @@ feature extractor.  Here the head's backward runs in hand-written HIP kernels:
   * ``cpg``        -- cpg.py:27-60 (dvcp_cpg / dvcp_cpg_backward): gradients for the conv
                       weights and for both DFE outputs;
   * ``dfe_rows``   -- deep_feat_embedding.py on the source rows (dvcp_dfe / dvcp_dfe_backward);
-  * ``dfe_tgt``    -- the fused target rows (dvcp_dfe_tgt / dvcp_dfe_tgt_backward).
+  * ``dfe_tgt``    -- the fused target rows (dvcp_dfe_tgt / dvcp_dfe_tgt_backward), also
+                      differentiable in the target features (the get_cat_feat_tgt.py:85 gather);
+  * ``src_keypoints`` -- the key-point stage, differentiable in the source features (the
+                      pointnet2_utils.py:59 gather, dvcp_src_keypoints_backward).
 
 The key points, candidates and kNN indices carry no gradient in the reference either (index
 ops, knn_cuda under no_grad); the weighting layer gets none (only its top-k indices are used).
@@ -48,6 +51,9 @@ class _DfeRows(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         X, params = ctx.saved_tensors
+        if ctx.needs_input_grad[0]:
+            gp, gX = ops.dfe_backward(X, params, g, want_input_grad=True)
+            return (gX.to(X.dtype), *_split(gp, ctx.weights))
         return (None, *_split(ops.dfe_backward(X, params, g), ctx.weights))
 
 
@@ -62,6 +68,10 @@ class _DfeTgt(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         ref_xyz, ref_feat, cand, dist, idx, params = ctx.saved_tensors
+        if ctx.needs_input_grad[1]:  # the get_cat_feat_tgt.py:85 gather's backward
+            gp, gF = ops.dfe_tgt_backward(ref_xyz, ref_feat, cand, dist, idx, params, g, ref_pdim=2,
+                                          want_feat_grad=True)
+            return (None, gF.to(ref_feat.dtype), None, None, None, *_split(gp, ctx.weights))
         gp = ops.dfe_tgt_backward(ref_xyz, ref_feat, cand, dist, idx, params, g, ref_pdim=2)
         return (None, None, None, None, None, *_split(gp, ctx.weights))
 
@@ -82,6 +92,26 @@ class _Cpg(torch.autograd.Function):
         gsrc = gsrc.view(src.shape).to(src.dtype) if ctx.needs_input_grad[0] else None
         gtgt = gtgt.to(tgt.dtype) if ctx.needs_input_grad[1] else None
         return (gsrc, gtgt, None, None, *_split(gp, ctx.weights))
+
+
+class _SrcKeypoints(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, fe_xyz, fe_feat, topk_idx, kstart, R_init, radius, nsample):
+        keypts, src_cat, moved = ops.src_keypoints(fe_xyz, fe_feat, topk_idx, kstart, R_init, radius=radius,
+                                                   nsample=nsample)
+        ctx.save_for_backward(fe_xyz, topk_idx, kstart)
+        ctx.radius, ctx.nsample, ctx.feat_dtype = radius, nsample, fe_feat.dtype
+        ctx.mark_non_differentiable(keypts, moved)
+        return keypts, src_cat, moved
+
+    @staticmethod
+    def backward(ctx, g_kp, g_cat, g_moved):
+        fe_xyz, topk_idx, kstart = ctx.saved_tensors
+        gF = None
+        if ctx.needs_input_grad[1] and g_cat is not None:
+            gF = ops.src_keypoints_backward(fe_xyz, topk_idx, kstart, g_cat, radius=ctx.radius,
+                                            nsample=ctx.nsample).to(ctx.feat_dtype)
+        return None, gF, None, None, None, None, None
 
 
 class _PoseLoss(torch.autograd.Function):
@@ -118,6 +148,12 @@ def cpg(src, tgt, cand, G, cpg_module):
     """cpg.py:27-60, differentiable in src, tgt and the conv weights."""
     convs = [cpg_module.conv1, cpg_module.conv2, cpg_module.conv3]
     return _Cpg.apply(src, tgt, cand, G, *[t for c in convs for t in (c.weight, c.bias)])
+
+
+def src_keypoints(fe_xyz, fe_feat, topk_idx, kstart, R_init, radius=1.0, nsample=32):
+    """The key-point stage (deepVCP.py:39-68 + get_cat_feat_src.py), differentiable in fe_feat
+    through the index_points gather (pointnet2_utils.py:59) and the distance weighting."""
+    return _SrcKeypoints.apply(fe_xyz, fe_feat, topk_idx, kstart, R_init, radius, nsample)
 
 
 def pose_loss(x, y_pred, R_true, t_true, alpha):

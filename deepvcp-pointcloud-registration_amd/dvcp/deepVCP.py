@@ -118,7 +118,11 @@ class DeepVCP(nn.Module):
         K, r, s = self.K, self.r, self.s
         dev = src_xyz.device
         top = ops.topk(score, K) if keypoint_idx is None else keypoint_idx.to(dev, torch.int64).contiguous()
-        keypts, src_cat, moved = ops.src_keypoints(src_xyz, src_feat, top, starts[3], R_init, radius=1.0, nsample=32)
+        if train_head and src_feat.requires_grad:
+            keypts, src_cat, moved = autograd.src_keypoints(src_xyz, src_feat, top, starts[3], R_init)
+        else:
+            keypts, src_cat, moved = ops.src_keypoints(src_xyz, src_feat, top, starts[3], R_init, radius=1.0,
+                                                       nsample=32)
         src_dfe = autograd.dfe_rows(src_cat, self.DFE) if train_head else ops.dfe(src_cat, self.DFE.packed_params())
 
         G = int((2 * r) / s + 1)                    # cpg.py:29

@@ -30,9 +30,6 @@ class feat_embedding_layer(nn.Module):
         expect = 4 if src else 5
         if X.dim() != expect:
             raise RuntimeError(f"feat_embedding_layer(src={src}) expects a {expect}-D input, got {tuple(X.shape)}")
-        if X.requires_grad and torch.is_grad_enabled():
-            raise NotImplementedError("feat_embedding_layer: the gradient with respect to the input rows is not "
-                                      "implemented (the feature extractor is frozen when training the head)")
-        if _wants_grad(self):
+        if _wants_grad(self, X):
             return autograd.dfe_rows(X, self)
         return ops.dfe(X, self.packed_params())

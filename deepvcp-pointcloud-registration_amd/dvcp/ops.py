@@ -324,8 +324,9 @@ DFE_NPARAMS = 3264   # fc1-3 weights and biases, packed
 CPG_NPARAMS = 15681  # conv1-3 weights and biases, packed
 
 
-def dfe_backward(X, params, grad_out):
-    """Parameter gradient of ``dfe`` (deep_feat_embedding.py:23-61) for rows X (..., 32, 35)."""
+def dfe_backward(X, params, grad_out, want_input_grad=False):
+    """Parameter gradient of ``dfe`` (deep_feat_embedding.py:23-61) for rows X (..., 32, 35),
+    and (``want_input_grad``) the rows' own gradient, shaped like X, fp32."""
     _lib.require_gpu(X, params, grad_out)
     Xc = X.contiguous()
     R = Xc.numel() // (32 * 35)
@@ -333,12 +334,14 @@ def dfe_backward(X, params, grad_out):
     ws = torch.empty(max(1, int(_lib.load().dvcp_dfe_backward_workspace_bytes(R)) // 4), dtype=torch.float32,
                      device=X.device)
     gp = torch.empty(DFE_NPARAMS, dtype=torch.float32, device=X.device)
-    call("dvcp_dfe_backward", dtype_code(Xc), ptr(Xc), R, ptr(params), ptr(g), ptr(ws), ptr(gp), stream())
-    return gp
+    gX = torch.empty(X.shape, dtype=torch.float32, device=X.device) if want_input_grad else None
+    call("dvcp_dfe_backward", dtype_code(Xc), ptr(Xc), R, ptr(params), ptr(g), ptr(ws), ptr(gp), ptr(gX), stream())
+    return (gp, gX) if want_input_grad else gp
 
 
-def dfe_tgt_backward(ref_xyz, ref_feat, cand, dist, idx, params, grad_out, ref_pdim=2):
-    """Parameter gradient of ``dfe_tgt`` (get_cat_feat_tgt.py:54-96 + deep_feat_embedding.py:47-60)."""
+def dfe_tgt_backward(ref_xyz, ref_feat, cand, dist, idx, params, grad_out, ref_pdim=2, want_feat_grad=False):
+    """Parameter gradient of ``dfe_tgt`` (get_cat_feat_tgt.py:54-96 + deep_feat_embedding.py:47-60),
+    and (``want_feat_grad``) the gradient of ``ref_feat`` (B, M, 32) through the :85 gather."""
     _lib.require_gpu(ref_xyz, ref_feat, cand, dist, idx, params, grad_out)
     B = ref_xyz.shape[0]
     M, rb, rc, rn = _pts(ref_xyz, ref_pdim)
@@ -348,10 +351,28 @@ def dfe_tgt_backward(ref_xyz, ref_feat, cand, dist, idx, params, grad_out, ref_p
     ws = torch.empty(max(1, int(_lib.load().dvcp_dfe_backward_workspace_bytes(B * Q)) // 4), dtype=torch.float32,
                      device=ref_xyz.device)
     gp = torch.empty(DFE_NPARAMS, dtype=torch.float32, device=ref_xyz.device)
+    gF = torch.zeros(B, M, 32, dtype=torch.float32, device=ref_xyz.device) if want_feat_grad else None
     call("dvcp_dfe_tgt_backward", dtype_code(ref_xyz), ptr(ref_xyz), rb, rc, rn, M, ptr(feat_c), ptr(cand_c),
-         ptr(dist_c), ptr(idx_c), B, Q, ptr(params), ptr(g), ptr(ws), ptr(gp), stream(),
+         ptr(dist_c), ptr(idx_c), B, Q, ptr(params), ptr(g), ptr(ws), ptr(gp), ptr(gF), stream(),
          work=(2.0 * 3168 * 32 * B * Q, B * (M * (12 + 128) + Q * (12 + 32 * 8 + 128))))
-    return gp
+    return (gp, gF) if want_feat_grad else gp
+
+
+def src_keypoints_backward(fe_xyz, topk_idx, kstart, grad_cat, radius=1.0, nsample=32):
+    """Gradient of FE features (B, S, 32) through the key-point stage's feature rows
+    (pointnet2_utils.py:59 gather + get_cat_feat_src.py:50 weighting); ``grad_cat`` is the
+    src_cat gradient (B, K, nsample, 35)."""
+    _lib.require_gpu(fe_xyz, topk_idx, grad_cat)
+    B, _, S_ = fe_xyz.shape
+    K = topk_idx.shape[1]
+    dev = fe_xyz.device
+    xyz_c, top_c = fe_xyz.contiguous(), topk_idx.contiguous()
+    ks_c = kstart.to(device=dev, dtype=torch.int64).contiguous()
+    g = grad_cat.float().contiguous()
+    gF = torch.zeros(B, S_, 32, dtype=torch.float32, device=dev)
+    call("dvcp_src_keypoints_backward", dtype_code(fe_xyz), ptr(xyz_c), S_, ptr(top_c), B, K, ptr(ks_c),
+         float(radius), int(nsample), ptr(g), ptr(gF), stream())
+    return gF
 
 
 def cpg_backward(src, tgt, cand, G, params, grad_vcp):

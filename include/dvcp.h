@@ -257,19 +257,29 @@ int dvcp_svd_optimization_backward(const double* x, const double* y_pred, const 
 
 /* Feature-embedding backward.  Replaces autograd through deep_feat_embedding.py:23-61 (fc1-3,
  * MaxPool1d) for the materialised rows X (R x 32 x 35, fp32|fp64): grad_out R x 32 fp32 ->
- * grad_params (3264 fp32: W1, b1, W2, b2, W3, b3).  ws: dvcp_dfe_backward_workspace_bytes(R). */
+ * grad_params (3264 fp32: W1, b1, W2, b2, W3, b3) and, optionally, grad_X (R x 32 x 35 fp32).
+ * ws: dvcp_dfe_backward_workspace_bytes(R). */
 int64_t dvcp_dfe_backward_workspace_bytes(int64_t R);
 int dvcp_dfe_backward(int x_dtype, const void* X, int64_t R, const float* params, const float* grad_out,
-                      float* ws, float* grad_params, void* stream);
+                      float* ws, float* grad_params, float* grad_X, void* stream);
 
 /* Target-side backward.  Replaces autograd through get_cat_feat_tgt.py:54-96 +
  * deep_feat_embedding.py:47-60; same arguments as dvcp_dfe_tgt plus grad_out (B x Q x 32 fp32),
- * ws (dvcp_dfe_backward_workspace_bytes(B*Q)) and grad_params (3264 fp32).  The target features
- * are frozen inputs (no gradient). */
+ * ws (dvcp_dfe_backward_workspace_bytes(B*Q)) and grad_params (3264 fp32).  grad_ref_feat
+ * (optional, B x M x 32 fp32, accumulated: zero it first) receives the gradient of the gathered
+ * target features (the get_cat_feat_tgt.py:85 gather, weighted as :95). */
 int dvcp_dfe_tgt_backward(int dtype, const void* ref_xyz, int64_t rb, int64_t rc, int64_t rn, int M,
                           const float* ref_feat, const float* cand, const float* dist, const int32_t* idx,
                           int B, int Q, const float* params, const float* grad_out, float* ws,
-                          float* grad_params, void* stream);
+                          float* grad_params, float* grad_ref_feat, void* stream);
+
+/* Key-point stage backward.  Replaces autograd through the source feature gather
+ * (pointnet2_utils.py:59 index_points, deepVCP.py:62) and its weighting (get_cat_feat_src.py:50):
+ * dvcp_src_keypoints' inputs plus grad_cat (B x K x nsample x 35, the src_cat gradient) ->
+ * grad_feat (B x S x 32 fp32, accumulated: zero it first). */
+int dvcp_src_keypoints_backward(int dtype, const void* fe_xyz, int S, const int64_t* topk, int B, int K,
+                                const int64_t* kstart, double radius, int nsample, const float* grad_cat,
+                                float* grad_feat, void* stream);
 
 /* CPG backward.  Replaces autograd through cpg.py:27-60: dvcp_cpg's arguments plus grad_vcp
  * (P x 3) -> grad_src (P x 32), grad_tgt (P x 32 x C contiguous, the (B,K,32,C) tensor's

@@ -88,7 +88,7 @@ def test_training_guards_and_no_cpu_fallback():
     with pytest.raises(RuntimeError, match="no GPU"):
         dvcp.deepVCP_loss(torch.rand(1, 8, 3), torch.rand(1, 8, 3, requires_grad=True),
                           torch.eye(3, dtype=torch.float64)[None], torch.zeros(1, 3, 1, dtype=torch.float64), 0.5)
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(RuntimeError, match="no GPU"):
         dvcp.feat_embedding_layer()(torch.rand(1, 2, 32, 35, requires_grad=True))
 
 

@@ -230,3 +230,72 @@ def test_extract_features_plus_head_equals_forward(cuda):
         f = m.extract_features(src.to(cuda), tgt.to(cuda), starts=starts)
         kp2, vcp2 = m.forward_head(f, R_gt.to(cuda))
     assert torch.equal(kp, kp2) and torch.equal(vcp, vcp2)
+
+
+def test_dfe_rows_input_grad_vs_oracle(cuda):
+    """dL/dX of the DFE on materialised rows (the source side's input rows)."""
+    import oracle as O
+    import dvcp
+    torch.manual_seed(8)
+    ref = O.feat_embedding_layer()
+    mine = dvcp.feat_embedding_layer().to(cuda)
+    mine.load_state_dict(ref.state_dict())
+    X = torch.randn(2, 16, 32, 35)
+    g = torch.randn(2, 16, 32)
+    Xo = X.clone().requires_grad_()
+    (ref(Xo, src=True) * g).sum().backward()
+    Xg = X.to(cuda).requires_grad_()
+    (mine(Xg, src=True) * g.to(cuda)).sum().backward()
+    _close(Xg.grad, Xo.grad, 1e-5, "d X")
+
+
+def test_dfe_tgt_feature_grad_vs_oracle(cuda):
+    """The get_cat_feat_tgt.py:85 gather's backward: dL/d(target features) through the fused rows."""
+    import oracle as O
+    import dvcp
+    from dvcp import autograd, ops
+    torch.manual_seed(9)
+    B, M, K, C = 2, 500, 3, 27
+    xyz = torch.rand(B, M, 3) * 2 - 1
+    feat = torch.rand(B, M, 32)
+    cand = (torch.rand(B, K, C, 3) * 2 - 1).double()
+    ref = O.feat_embedding_layer()
+    fo = feat.clone().requires_grad_()
+    rows = O.Get_Cat_Feat_Tgt()(cand, torch.zeros(B, K, 3), xyz, fo)
+    g = torch.randn(B, K, C, 32)
+    (ref(rows, src=False) * g).sum().backward()
+    mine = dvcp.feat_embedding_layer().to(cuda)
+    mine.load_state_dict(ref.state_dict())
+    ref_xyz = xyz.to(cuda).permute(0, 2, 1)
+    qry = cand.float().to(cuda).view(B, K * C, 3)
+    dist, idx, _ = ops.knn(ref_xyz, qry, 32, ref_pdim=2, qry_pdim=1, want_idx64=False)
+    fg = feat.to(cuda).requires_grad_()
+    out = autograd.dfe_tgt(ref_xyz, fg, qry, dist, idx, mine)
+    (out * g.to(cuda).view(B, K * C, 32)).sum().backward()
+    _close(fg.grad, fo.grad, 1e-5, "d target features")
+
+
+def test_src_keypoints_feature_grad_vs_oracle(cuda):
+    """The key-point stage's gather (pointnet2_utils.py:59) + weighting (get_cat_feat_src.py:50)
+    backward: dL/d(source FE features)."""
+    import oracle as O
+    from dvcp import autograd
+    torch.manual_seed(10)
+    B, S, K, ns = 2, 200, 48, 32
+    xyz = torch.rand(B, S, 3) * 2 - 1
+    feat = torch.rand(B, S, 32)
+    top = torch.stack([torch.randperm(S)[:K] for _ in range(B)])
+    kstart = torch.randint(0, K, (B,))
+    G = torch.randn(B, K, ns, 35)
+    fo = feat.clone().requires_grad_()
+    kp = O.index_points(xyz, top)
+    with O.fps_starts([kstart]):
+        _, g_local, picked = O.sample_and_group(npoint=K, radius=1, nsample=ns, xyz=kp, points=None, returnidx=True)
+    cat_o = O.Get_Cat_Feat_Src()(kp, g_local, O.index_points(fo, picked))
+    (cat_o * G).sum().backward()
+    fg = feat.to(cuda).requires_grad_()
+    R = torch.eye(3, dtype=torch.float64, device=cuda)[None]
+    _, cat, _ = autograd.src_keypoints(xyz.to(cuda).transpose(1, 2).contiguous(), fg, top.to(cuda), kstart.to(cuda), R)
+    torch.testing.assert_close(cat.cpu(), cat_o.float(), rtol=1e-5, atol=1e-6)
+    (cat * G.to(cuda)).sum().backward()
+    _close(fg.grad, fo.grad, 1e-5, "d source features")
