@@ -80,7 +80,8 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
                                                              const float* __restrict__ cand, int G,
                                                              const float* __restrict__ params,
                                                              const float* __restrict__ gvcp, float* __restrict__ gsrc,
-                                                             float* __restrict__ gtgt, float* __restrict__ gpart) {
+                                                             float* __restrict__ gtgt, float* __restrict__ gpart,
+                                                             const float* __restrict__ wt) {
   __shared__ __attribute__((aligned(16))) float lds[kCbA + kCbW + kCbD];
   __shared__ float red[32];
   __shared__ float sv[32];
@@ -90,9 +91,13 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
   const int p = blockIdx.x, tid = threadIdx.x;
   const int C = G * G * G, GG = G * G;
   const FastDiv dG(G), dGG(GG), dC(C);
-  const float* P1 = params;
-  const float* P2 = params + kCbOffW2;
   const float* P3 = params + kCbOffW3;
+  // weight tables with the inner loop's index contiguous, so a tap's weights are one wide scalar
+  // load (s_load_dwordx16) instead of 16-32 single ones (cpg_bwd_prep_kernel)
+  const float* W1a = wt;                      // [ci][t][co]
+  const float* W1b = W1a + kCbW;              // [co][t][ci]
+  const float* W2a = W1b + kCbW;              // [ci][t][co4]
+  const float* W2b = W2a + 4 * 16 * 27;       // [co4][t][ci]
   float* gp = gpart + static_cast<int64_t>(p) * kCbParams;
   const float* T = tgt + static_cast<int64_t>(p) * t_p;
   if (tid < 32) sv[tid] = src[static_cast<int64_t>(p) * 32 + tid];
@@ -137,7 +142,7 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
         if (!((msk[k] >> t) & 1u)) continue;
         const float c = D[vv[k] + tap_off(t, G, GG)];
 #pragma unroll
-        for (int co = 0; co < 16; ++co) h1[k][co] = __fmaf_rn(P1[co * 864 + ci * 27 + t], c, h1[k][co]);
+        for (int co = 0; co < 16; ++co) h1[k][co] = __fmaf_rn(W1a[(ci * 27 + t) * 16 + co], c, h1[k][co]);
       }
     }
     __syncthreads();
@@ -163,7 +168,7 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
         if (!((msk[k] >> t) & 1u)) continue;
         const float c = A[ci * C + vv[k] + tap_off(t, G, GG)];
 #pragma unroll
-        for (int co = 0; co < 4; ++co) h2[k][co] = __fmaf_rn(P2[(co * 16 + ci) * 27 + t], c, h2[k][co]);
+        for (int co = 0; co < 4; ++co) h2[k][co] = __fmaf_rn(W2a[(ci * 27 + t) * 4 + co], c, h2[k][co]);
       }
   }
 #pragma unroll
@@ -298,7 +303,7 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
         if (!((msk[k] >> (26 - t)) & 1u)) continue;
         const float g = D[co * C + vv[k] - tap_off(t, G, GG)];
 #pragma unroll
-        for (int ci = 0; ci < 16; ++ci) gh1[k][ci] = __fmaf_rn(P2[(co * 16 + ci) * 27 + t], g, gh1[k][ci]);
+        for (int ci = 0; ci < 16; ++ci) gh1[k][ci] = __fmaf_rn(W2b[(co * 27 + t) * 16 + ci], g, gh1[k][ci]);
       }
   }
   __syncthreads();  // h1 readers done
@@ -338,7 +343,7 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
         }
 #pragma unroll
         for (int ci = 0; ci < 32; ++ci) {
-          const float w = P1[co * 864 + ci * 27 + t];
+          const float w = W1b[(co * 27 + t) * 32 + ci];
 #pragma unroll
           for (int k = 0; k < kCbV; ++k) gc[k][ci] = __fmaf_rn(w, g[k], gc[k][ci]);
         }
@@ -419,6 +424,21 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
   }
 }
 
+__global__ void cpg_bwd_prep_kernel(const float* __restrict__ params, float* __restrict__ wt) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < kCbW) {  // torch (co, ci, t)
+    const int co = i / 864, ci = (i / 27) % 32, t = i % 27;
+    wt[(ci * 27 + t) * 16 + co] = params[i];
+    wt[kCbW + (co * 27 + t) * 32 + ci] = params[i];
+  }
+  if (i < 4 * 16 * 27) {
+    const int co = i / 432, ci = (i / 27) % 16, t = i % 27;
+    wt[2 * kCbW + (ci * 27 + t) * 4 + co] = params[kCbOffW2 + i];
+    wt[2 * kCbW + 4 * 16 * 27 + (co * 27 + t) * 16 + ci] = params[kCbOffW2 + i];
+  }
+}
+constexpr int kCbWt = 2 * kCbW + 2 * 4 * 16 * 27;
+
 // grad[i] = sum over key points of part[p][i], in fp64, key-point order
 __global__ void cpg_bwd_reduce_kernel(const float* __restrict__ part, int P, float* __restrict__ grad) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -431,7 +451,7 @@ __global__ void cpg_bwd_reduce_kernel(const float* __restrict__ part, int P, flo
 }  // namespace dvcp
 
 extern "C" int64_t dvcp_cpg_backward_workspace_bytes(int P) {
-  return static_cast<int64_t>(P > 0 ? P : 0) * dvcp::kCbParams * static_cast<int64_t>(sizeof(float));
+  return (static_cast<int64_t>(P > 0 ? P : 0) * dvcp::kCbParams + dvcp::kCbWt) * static_cast<int64_t>(sizeof(float));
 }
 
 extern "C" int dvcp_cpg_backward(const float* src, const float* tgt, int64_t t_p, int64_t t_f, int64_t t_c,
@@ -442,9 +462,12 @@ extern "C" int dvcp_cpg_backward(const float* src, const float* tgt, int64_t t_p
                "dvcp_cpg_backward: null pointer");
   DVCP_REQUIRE(G >= 2 && G * G * G <= dvcp::kCbMaxC, "dvcp_cpg_backward: grid side G=%d unsupported (2..11)", G);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (P > 0)
+  if (P > 0) {
+    float* wt = ws + static_cast<int64_t>(P) * dvcp::kCbParams;  // after the per-key-point partials
+    hipLaunchKernelGGL(dvcp::cpg_bwd_prep_kernel, dim3(dvcp::ceil_div(dvcp::kCbW, 256)), dim3(256), 0, st, params, wt);
     hipLaunchKernelGGL(dvcp::cpg_bwd_kernel, dim3(P), dim3(dvcp::kCbThreads), 0, st, src, tgt, t_p, t_f, t_c, cand, G,
-                       params, grad_vcp, grad_src, grad_tgt, ws);
+                       params, grad_vcp, grad_src, grad_tgt, ws, wt);
+  }
   hipLaunchKernelGGL(dvcp::cpg_bwd_reduce_kernel, dim3(dvcp::ceil_div(dvcp::kCbParams, 256)), dim3(256), 0, st, ws,
                      P > 0 ? P : 0, grad_params);
   return dvcp::launch_status("dvcp_cpg_backward");
