@@ -127,11 +127,18 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
 #pragma unroll
     for (int co = 0; co < 16; ++co) h1[k][co] = params[kCbOffB1 + co];
   __syncthreads();
+  // the scrambled target gather is latency-bound: channel ci + 1's values are loaded while
+  // channel ci is convolved (thread voxels vv[k] are exactly the staging loop's v)
+  float tpre[kCbV];
+#pragma unroll
+  for (int k = 0; k < kCbV; ++k) tpre[k] = vok[k] ? tval(vv[k] * 32) : 0.f;
 #pragma unroll 1
   for (int ci = 0; ci < 32; ++ci) {
-    for (int v = tid; v < C; v += kCbThreads) {
-      const float d = sv[ci] - tval(v * 32 + ci);
-      D[v] = d * d;
+#pragma unroll
+    for (int k = 0; k < kCbV; ++k) {
+      const float d = sv[ci] - tpre[k];
+      if (vok[k]) D[vv[k]] = d * d;
+      if (ci + 1 < 32) tpre[k] = vok[k] ? tval(vv[k] * 32 + ci + 1) : 0.f;
     }
     __syncthreads();
 #pragma unroll
@@ -371,12 +378,16 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
   // and 4 rows of dL/dh1, then does 12 fmas per voxel.  Slices are summed in order afterwards.
   constexpr int kRowSlices = 24;  // 36 (co quad, dz, dy) items x 24 = 864 threads
   float* scr1 = Wr;               // [slice][item][12]; dL/dlg is dead by now
+#pragma unroll
+  for (int k = 0; k < kCbV; ++k) tpre[k] = vok[k] ? tval(vv[k] * 32) : 0.f;
 #pragma unroll 1
   for (int ci = 0; ci < 32; ++ci) {
     __syncthreads();  // previous channel's readers of D / scr1 are done
-    for (int v = tid; v < C; v += kCbThreads) {
-      const float d = sv[ci] - tval(v * 32 + ci);
-      D[v] = d * d;
+#pragma unroll
+    for (int k = 0; k < kCbV; ++k) {
+      const float d = sv[ci] - tpre[k];
+      if (vok[k]) D[vv[k]] = d * d;
+      if (ci + 1 < 32) tpre[k] = vok[k] ? tval(vv[k] * 32 + ci + 1) : 0.f;
     }
     __syncthreads();
     if (tid < 36 * kRowSlices) {
