@@ -17,6 +17,8 @@
 
 namespace dvcp {
 
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
 // dfe_mfma.hip: the target side on fp32 MFMA (default; DVCP_DFE_VALU=1 selects the kernel below)
 template <typename T>
 int launch_dfe_tgt_mfma(PointsView<T> ref, const float* feat, int M, const float* cand, const float* dist,
@@ -209,11 +211,12 @@ __global__ __launch_bounds__(kDfeThreads) void dfe_bwd_kernel(const T* __restric
                                                               const float* __restrict__ Ee,
                                                               const float* __restrict__ gout, float* __restrict__ part,
                                                               float* __restrict__ gX, float* __restrict__ gF) {
-  __shared__ float ys[kDfeThreads][33];
   __shared__ float xs[kDfeThreads][37];
+  __shared__ float Es[32][37];  // E (the bias e shifts a channel's rows alike: not needed for the arg-max)
   __shared__ double wq[kDfeQPerBlock][32];
   __shared__ double dsh[kDfeThreads];
-  const int tid = threadIdx.x, ql = tid / 32, f = tid % 32;
+  const int tid = threadIdx.x, ql = tid / 32, f = tid % 32, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < 32 * 36; i += kDfeThreads) Es[i / 36][i % 36] = Ee[i];
   float acc[36];
 #pragma unroll
   for (int i = 0; i < 36; ++i) acc[i] = 0.f;
@@ -231,29 +234,46 @@ __global__ __launch_bounds__(kDfeThreads) void dfe_bwd_kernel(const T* __restric
       const int64_t qq = (live ? q : 0) - static_cast<int64_t>(b) * Q;
       dfe_tgt_row(ref, feat, M, cand, dist, idx, Q, b, qq, live, dsh, wq, x);
     }
-    float y[32];
-#pragma unroll
-    for (int o = 0; o < 32; ++o) {  // E, e: wave-uniform addresses -> scalar operands
-      float a = 0.f;
-#pragma unroll
-      for (int c = 0; c < 35; ++c) a = __fmaf_rn(Ee[o * 36 + c], x[c], a);
-      y[o] = a + Ee[o * 36 + 35];
-    }
     __syncthreads();  // the previous group's readers are done
-#pragma unroll
-    for (int c = 0; c < 32; ++c) ys[tid][c] = y[c];
 #pragma unroll
     for (int i = 0; i < 35; ++i) xs[tid][i] = x[i];
     __syncthreads();
-    // thread (ql, f): the row the max-pool picked for channel f
-    float best = ys[ql * 32][f];
+    // Y = X E^T for this wave's two queries on v_mfma_f32_32x32x2_f32 (18 k-steps over the 35
+    // inputs): lane l supplies A = X[row l&31][k], B = E^T[k][channel l&31]; the result holds
+    // channel l&31, rows (r&3) + 8(r>>2) + 4(l>>5) in register r.
     int bj = 0;
-    for (int r = 1; r < 32; ++r) {
-      const float v = ys[ql * 32 + r][f];
-      if (v > best) {
-        best = v;
-        bj = r;
+    {
+      const int h = lane >> 5, c32 = lane & 31;
+      f32x16 y0 = {}, y1 = {};
+#pragma unroll
+      for (int s2 = 0; s2 < 18; ++s2) {
+        const int k = 2 * s2 + h;
+        const float bk = k < 35 ? Es[c32][k] : 0.f;
+        const float a0 = k < 35 ? xs[(2 * wave) * 32 + c32][k] : 0.f;
+        const float a1 = k < 35 ? xs[(2 * wave + 1) * 32 + c32][k] : 0.f;
+        y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bk, y0, 0, 0, 0);
+        y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bk, y1, 0, 0, 0);
       }
+      // per lane: the best of its 16 rows, then against lane ^ 32's (MaxPool1d: first index)
+      float b0 = -__builtin_huge_valf(), bb1 = -__builtin_huge_valf();
+      int j0 = 64, j1 = 64;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (y0[r] > b0 || (y0[r] == b0 && row < j0)) {
+          b0 = y0[r];
+          j0 = row;
+        }
+        if (y1[r] > bb1 || (y1[r] == bb1 && row < j1)) {
+          bb1 = y1[r];
+          j1 = row;
+        }
+      }
+      const float ob0 = __shfl_xor(b0, 32, kWave), ob1 = __shfl_xor(bb1, 32, kWave);
+      const int oj0 = __shfl_xor(j0, 32, kWave), oj1 = __shfl_xor(j1, 32, kWave);
+      if (ob0 > b0 || (ob0 == b0 && oj0 < j0)) j0 = oj0;
+      if (ob1 > bb1 || (ob1 == bb1 && oj1 < j1)) j1 = oj1;
+      bj = h == 0 ? j0 : j1;  // thread (ql = 2 wave + h, f = lane & 31)
     }
     const float g = live ? gout[q * 32 + f] : 0.f;
 #pragma unroll
