@@ -24,6 +24,8 @@
 
 namespace dvcp {
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 constexpr int kCbThreads = 1024;
 constexpr int kCbMaxC = 1331;
 constexpr int kCbMaxG = 11;
@@ -39,6 +41,7 @@ constexpr int kCbOffW3 = kCbOffB2 + 4;
 constexpr int kCbOffB3 = kCbOffW3 + 4 * 27;
 constexpr int kCbParams = kCbOffB3 + 1;
 static_assert(kCbA + kCbW + kCbD + 64 <= 160 * 1024 / 4, "LDS budget");
+static_assert(kCbW + kCbD >= 8 * 13 * 13 * 13 && kCbA >= kCbW, "conv1 MFMA staging: quarter volume in Wr..D, W1 in A");
 
 // tap t of a 3x3x3 kernel: (dz, dy, dx) = (t / 9 - 1, (t / 3) % 3 - 1, t % 3 - 1)
 __device__ __forceinline__ int tap_off(int t, int G, int GG) {
@@ -120,46 +123,67 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
     return T[static_cast<int64_t>(f) * t_f + static_cast<int64_t>(l - static_cast<int>(f) * C) * t_c];
   };
 
-  // ---- forward: conv1 (one cost channel at a time; weights are wave-uniform scalar loads) ------
-  float h1[kCbV][16];
-#pragma unroll
-  for (int k = 0; k < kCbV; ++k)
-#pragma unroll
-    for (int co = 0; co < 16; ++co) h1[k][co] = params[kCbOffB1 + co];
-  __syncthreads();
-  // the scrambled target gather is latency-bound: channel ci + 1's values are loaded while
-  // channel ci is convolved (thread voxels vv[k] are exactly the staging loop's v)
+  // ---- forward: conv1 on the matrix cores, as cpg_kernel: an implicit GEMM on
+  // v_mfma_f32_16x16x4_f32 over 8-channel haloed quarters of the cost volume (rows = 16-voxel
+  // tiles, k = 4 input channels at one tap, columns = the 16 output channels).  LDS during this
+  // phase: W1 [ci][t][co] in A, the haloed quarter from Wr on (8 x 13^3 floats, into D).
   float tpre[kCbV];
+  {
+    const int PG = G + 2, PGG = PG * PG, PV = PG * PGG;
+    float* w1s = A;
+    float* vol = Wr;
+    for (int i = tid; i < kCbW; i += kCbThreads) w1s[i] = W1a[i];
+    constexpr int kT = (kCbMaxC + 15) / 16, kW = kCbThreads / 64, kTW = (kT + kW - 1) / kW;
+    const int lane = tid & 63, wave = tid >> 6, kg = lane >> 4, l16 = lane & 15;
+    const int NT = (C + 15) / 16;
+    int vx[kTW];
 #pragma unroll
-  for (int k = 0; k < kCbV; ++k) tpre[k] = vok[k] ? tval(vv[k] * 32) : 0.f;
-#pragma unroll 1
-  for (int ci = 0; ci < 32; ++ci) {
-#pragma unroll
-    for (int k = 0; k < kCbV; ++k) {
-      const float d = sv[ci] - tpre[k];
-      if (vok[k]) D[vv[k]] = d * d;
-      if (ci + 1 < 32) tpre[k] = vok[k] ? tval(vv[k] * 32 + ci + 1) : 0.f;
+    for (int i = 0; i < kTW; ++i) {
+      const int g = 16 * (wave + kW * i) + l16;
+      vx[i] = g < C ? cpg_halo(g, dG, dGG, PG, PGG) : 0;
     }
-    __syncthreads();
+    f32x4 acc[kTW];
 #pragma unroll
-    for (int k = 0; k < kCbV; ++k) {
-      if (!vok[k]) continue;
+    for (int i = 0; i < kTW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int q = 0; q < 4; ++q) {
+      __syncthreads();
+      for (int h = tid; h < 8 * PV; h += kCbThreads) vol[h] = 0.f;
+      __syncthreads();
+      for (int e = tid; e < 8 * C; e += kCbThreads) {
+        const int c8 = static_cast<int>(dC.div(static_cast<uint32_t>(e))), v = e - c8 * C;
+        const int ci = 8 * q + c8;
+        const float d = sv[ci] - tval(v * 32 + ci);
+        vol[c8 * PV + cpg_halo(v, dG, dGG, PG, PGG)] = d * d;
+      }
+      __syncthreads();
 #pragma unroll 1
       for (int t = 0; t < 27; ++t) {
-        if (!((msk[k] >> t) & 1u)) continue;
-        const float c = D[vv[k] + tap_off(t, G, GG)];
+        const int off = (t / 9 - 1) * PGG + ((t / 3) % 3 - 1) * PG + (t % 3 - 1);
 #pragma unroll
-        for (int co = 0; co < 16; ++co) h1[k][co] = __fmaf_rn(W1a[(ci * 27 + t) * 16 + co], c, h1[k][co]);
+        for (int cg = 0; cg < 2; ++cg) {
+          const int ci = 4 * cg + kg;
+          const float bw = w1s[((8 * q + ci) * 27 + t) * 16 + l16];
+          const float* vin = vol + ci * PV + off;
+#pragma unroll
+          for (int i = 0; i < kTW; ++i)
+            if (wave + kW * i < NT) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(vin[vx[i]], bw, acc[i], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();  // W1 readers are done: h1 replaces it in A
+    // register r of lane l: voxel 16 t + 4 (l >> 4) + r, output channel l & 15
+#pragma unroll
+    for (int i = 0; i < kTW; ++i) {
+      const int t = wave + kW * i;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int g = 16 * t + 4 * kg + r;
+        if (t < NT && g < C) A[l16 * C + g] = acc[i][r] + params[kCbOffB1 + l16];
       }
     }
     __syncthreads();
   }
-#pragma unroll
-  for (int k = 0; k < kCbV; ++k)
-    if (vok[k])
-#pragma unroll
-      for (int co = 0; co < 16; ++co) A[co * C + vv[k]] = h1[k][co];
-  __syncthreads();
 
   // ---- forward: conv2 -> D, conv3 -> logits ------------------------------------------------
   float h2[kCbV][4];
