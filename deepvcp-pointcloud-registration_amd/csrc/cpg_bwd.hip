@@ -41,7 +41,8 @@ constexpr int kCbOffW3 = kCbOffB2 + 4;
 constexpr int kCbOffB3 = kCbOffW3 + 4 * 27;
 constexpr int kCbParams = kCbOffB3 + 1;
 static_assert(kCbA + kCbW + kCbD + 64 <= 160 * 1024 / 4, "LDS budget");
-static_assert(kCbW + kCbD >= 8 * 13 * 13 * 13 && kCbA >= kCbW, "conv1 MFMA staging: quarter volume in Wr..D, W1 in A");
+static_assert(kCbW + kCbD >= 8 * 13 * 13 * 13 + 1024 && kCbA >= kCbW,
+              "conv1 MFMA staging: haloed 8-channel volume (+ partial sums) in Wr..D, W1 in A");
 
 // tap t of a 3x3x3 kernel: (dz, dy, dx) = (t / 9 - 1, (t / 3) % 3 - 1, t % 3 - 1)
 __device__ __forceinline__ int tap_off(int t, int G, int GG) {
@@ -352,47 +353,79 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
     if (tid == 0) gp[kCbOffB1 + ci] = s;
   }
 
-  // ---- conv1 backward, data side: dL/dcost for all 32 channels of this thread's voxels -------
-  // (transposed conv over dL/dh1 in A; weights are scalar loads), then the cost volume's own
-  // derivative: dL/dsrc[f'] = sum 2 (src - T) dL/dcost, dL/dT = -2 (src - T) dL/dcost.
+  // ---- conv1 backward, data side, on the matrix cores: dL/dcost[ci][u] = sum_co sum_t
+  // W1[co][ci][t] dL/dh1[co][u - off_t], an implicit GEMM over haloed 8-channel halves of dL/dh1
+  // (rows = 16-voxel tiles, k = 4 dL/dh1 channels at one tap, columns = 16 cost channels), then
+  // the cost volume's own derivative: dL/dsrc[f'] = sum 2 (src - T) dL/dcost, dL/dT = -2 (src - T)
+  // dL/dcost.  LDS: the haloed half from Wr on (into D), then 1024 partial sums of dL/dsrc.
   float* gT = gtgt + static_cast<int64_t>(p) * 32 * C;
   {
-    float gc[kCbV][32];
+    const int PG = G + 2, PGG = PG * PG, PV = PG * PGG;
+    float* vol = Wr;
+    float* gpart_s = Wr + 8 * 13 * 13 * 13;  // [wave][kg][16]
+    constexpr int kT = (kCbMaxC + 15) / 16, kW = kCbThreads / 64, kTW = (kT + kW - 1) / kW;
+    const int lane = tid & 63, wave = tid >> 6, kg = lane >> 4, l16 = lane & 15;
+    const int NT = (C + 15) / 16;
+    int vx[kTW];
 #pragma unroll
-    for (int k = 0; k < kCbV; ++k)
-#pragma unroll
-      for (int ci = 0; ci < 32; ++ci) gc[k][ci] = 0.f;
+    for (int i = 0; i < kTW; ++i) {
+      const int g = 16 * (wave + kW * i) + l16;
+      vx[i] = g < C ? cpg_halo(g, dG, dGG, PG, PGG) : 0;
+    }
 #pragma unroll 1
-    for (int co = 0; co < 16; ++co)
-#pragma unroll 1
-      for (int t = 0; t < 27; ++t) {
-        float g[kCbV];
+    for (int cb = 0; cb < 2; ++cb) {
+      f32x4 acc[kTW];
 #pragma unroll
-        for (int k = 0; k < kCbV; ++k) {
-          const bool ok = vok[k] && ((msk[k] >> (26 - t)) & 1u);
-          g[k] = ok ? A[co * C + (ok ? vv[k] - tap_off(t, G, GG) : 0)] : 0.f;
+      for (int i = 0; i < kTW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+      for (int hc = 0; hc < 2; ++hc) {
+        __syncthreads();
+        for (int h = tid; h < 8 * PV; h += kCbThreads) vol[h] = 0.f;
+        __syncthreads();
+        for (int e = tid; e < 8 * C; e += kCbThreads) {
+          const int c8 = static_cast<int>(dC.div(static_cast<uint32_t>(e))), v = e - c8 * C;
+          vol[c8 * PV + cpg_halo(v, dG, dGG, PG, PGG)] = A[(8 * hc + c8) * C + v];
         }
+        __syncthreads();
+#pragma unroll 1
+        for (int t = 0; t < 27; ++t) {
+          const int off = (t / 9 - 1) * PGG + ((t / 3) % 3 - 1) * PG + (t % 3 - 1);
 #pragma unroll
-        for (int ci = 0; ci < 32; ++ci) {
-          const float w = W1b[(co * 27 + t) * 32 + ci];
+          for (int cg = 0; cg < 2; ++cg) {
+            const int col = 4 * cg + kg;  // dL/dh1 channel within the half
+            const float bw = W1b[((8 * hc + col) * 27 + t) * 32 + 16 * cb + l16];
+            const float* vin = vol + col * PV - off;
 #pragma unroll
-          for (int k = 0; k < kCbV; ++k) gc[k][ci] = __fmaf_rn(w, g[k], gc[k][ci]);
+            for (int i = 0; i < kTW; ++i)
+              if (wave + kW * i < NT) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(vin[vx[i]], bw, acc[i], 0, 0, 0);
+          }
         }
       }
+      // register r of lane l: voxel 16 t + 4 (l >> 4) + r, cost channel 16 cb + (l & 15)
+      const int ci = 16 * cb + l16;
+      float gsl = 0.f;
 #pragma unroll
-    for (int ci = 0; ci < 32; ++ci) {
-      float gs = 0.f;
+      for (int i = 0; i < kTW; ++i) {
+        const int t = wave + kW * i;
 #pragma unroll
-      for (int k = 0; k < kCbV; ++k) {
-        if (!vok[k]) continue;
-        const int l = vv[k] * 32 + ci;
-        const float d = sv[ci] - tval(l);
-        const float gd = 2.0f * d * gc[k][ci];
-        gs += gd;
-        gT[l] = -gd;
+        for (int r = 0; r < 4; ++r) {
+          const int u = 16 * t + 4 * kg + r;
+          if (t < NT && u < C) {
+            const int l = u * 32 + ci;
+            const float d = sv[ci] - tval(l);
+            const float gd = 2.0f * d * acc[i][r];
+            gsl += gd;
+            gT[l] = -gd;
+          }
+        }
       }
-      gs = block_sum(gs, red);
-      if (tid == 0) gsrc[static_cast<int64_t>(p) * 32 + ci] = gs;
+      gpart_s[(wave * 4 + kg) * 16 + l16] = gsl;
+      __syncthreads();
+      if (tid < 16) {  // fixed order over (wave, kg)
+        float sum = 0.f;
+        for (int w = 0; w < kW * 4; ++w) sum += gpart_s[w * 16 + tid];
+        gsrc[static_cast<int64_t>(p) * 32 + 16 * cb + tid] = sum;
+      }
     }
   }
 
