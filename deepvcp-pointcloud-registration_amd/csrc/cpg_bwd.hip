@@ -28,7 +28,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kCbThreads = 1024;
 constexpr int kCbMaxC = 1331;
-constexpr int kCbMaxG = 11;
 constexpr int kCbA = 16 * kCbMaxC;
 constexpr int kCbW = 16 * 32 * 27;
 constexpr int kCbD = 4 * kCbMaxC;
@@ -41,7 +40,7 @@ constexpr int kCbOffW3 = kCbOffB2 + 4;
 constexpr int kCbOffB3 = kCbOffW3 + 4 * 27;
 constexpr int kCbParams = kCbOffB3 + 1;
 static_assert(kCbA + kCbW + kCbD + 64 <= 160 * 1024 / 4, "LDS budget");
-static_assert(kCbW + kCbD >= 8 * 13 * 13 * 13 + 1024 && kCbA >= kCbW,
+static_assert(kCbW + kCbD >= 8 * 13 * 13 * 13 + 1024 && kCbA >= kCbW && kCbW >= 2304 + 16 * 2 * 256,
               "conv1 MFMA staging: haloed 8-channel volume (+ partial sums) in Wr..D, W1 in A");
 
 // tap t of a 3x3x3 kernel: (dz, dy, dx) = (t / 9 - 1, (t / 3) % 3 - 1, t % 3 - 1)
@@ -429,65 +428,65 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
     }
   }
 
-  // ---- conv1 backward, weight side: dW1 one cost channel at a time --------------------------
-  // Register-blocked: a thread owns 4 output channels x the 3 x-taps of one (dz, dy) and a slice
-  // of the G^2 grid rows; per row it loads the shifted cost row once (zero-padded at both ends)
-  // and 4 rows of dL/dh1, then does 12 fmas per voxel.  Slices are summed in order afterwards.
-  constexpr int kRowSlices = 24;  // 36 (co quad, dz, dy) items x 24 = 864 threads
-  float* scr1 = Wr;               // [slice][item][12]; dL/dlg is dead by now
+  // ---- conv1 backward, weight side, on the matrix cores: for each cost channel ci,
+  // dW1[co][ci][t] = sum_v dL/dh1[co][v] cost[ci][v + off_t] is a 16 x 27 (x voxels) GEMM:
+  // rows = the 16 output channels, k = 4 voxels, columns = 16 taps (two blocks, 27 padded to 32).
+  // The voxels are split over the 16 waves; their partial products are summed in wave order.
+  // LDS: the haloed cost channel from Wr on, the partials after it.
+  {
+    const int PG = G + 2, PGG = PG * PG, PV = PG * PGG;
+    float* ch = Wr;                  // haloed cost[ci] (<= 13^3)
+    float* wpart = Wr + 2304;        // [wave][block][lane][4]: 16 x 2 x 256
+    constexpr int kW = kCbThreads / 64;
+    const int lane = tid & 63, wave = tid >> 6, kg = lane >> 4, l16 = lane & 15;
+    // this wave's voxel range, 4-aligned
+    const int nstep = (C + 3) / 4;
+    const int s0 = (wave * nstep) / kW, s1 = ((wave + 1) * nstep) / kW;
+    int toff[2];
 #pragma unroll
-  for (int k = 0; k < kCbV; ++k) tpre[k] = vok[k] ? tval(vv[k] * 32) : 0.f;
+    for (int tb = 0; tb < 2; ++tb) {
+      const int t = 16 * tb + l16;
+      toff[tb] = t < 27 ? (t / 9 - 1) * PGG + ((t / 3) % 3 - 1) * PG + (t % 3 - 1) : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kCbV; ++k) tpre[k] = vok[k] ? tval(vv[k] * 32) : 0.f;
 #pragma unroll 1
-  for (int ci = 0; ci < 32; ++ci) {
-    __syncthreads();  // previous channel's readers of D / scr1 are done
+    for (int ci = 0; ci < 32; ++ci) {
+      __syncthreads();  // previous channel's readers of ch / wpart are done
+      for (int h = tid; h < PV; h += kCbThreads) ch[h] = 0.f;
+      __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kCbV; ++k) {
-      const float d = sv[ci] - tpre[k];
-      if (vok[k]) D[vv[k]] = d * d;
-      if (ci + 1 < 32) tpre[k] = vok[k] ? tval(vv[k] * 32 + ci + 1) : 0.f;
-    }
-    __syncthreads();
-    if (tid < 36 * kRowSlices) {
-      const int item = tid % 36, slice = tid / 36;
-      const int q4 = item / 9, dz = (item / 3) % 3 - 1, dy = item % 3 - 1;
-      const int r0 = (slice * GG) / kRowSlices, r1 = ((slice + 1) * GG) / kRowSlices;
-      float acc[4][3];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) acc[i][k] = 0.f;
-      for (int r = r0; r < r1; ++r) {
-        const int z = static_cast<int>(dG.div(static_cast<uint32_t>(r))), y = r - z * G;
-        const int zz = z + dz, yy = y + dy;
-        if (zz < 0 || zz >= G || yy < 0 || yy >= G) continue;
-        float row[kCbMaxG + 2];  // cost row (zz, yy, x - 1), zero outside the grid
-        row[0] = 0.f;
-#pragma unroll
-        for (int x = 0; x < kCbMaxG + 1; ++x) row[x + 1] = x < G ? D[(zz * G + yy) * G + x] : 0.f;
-        const int base = (z * G + y) * G;
-#pragma unroll
-        for (int x = 0; x < kCbMaxG; ++x) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float g = x < G ? A[(q4 * 4 + i) * C + base + (x < G ? x : 0)] : 0.f;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) acc[i][k] = __fmaf_rn(g, row[x + k], acc[i][k]);
-          }
-        }
+      for (int k = 0; k < kCbV; ++k) {
+        const float d = sv[ci] - tpre[k];
+        if (vok[k]) ch[cpg_halo(vv[k], dG, dGG, PG, PGG)] = d * d;
+        if (ci + 1 < 32) tpre[k] = vok[k] ? tval(vv[k] * 32 + ci + 1) : 0.f;
       }
+      __syncthreads();
+      f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int st = s0; st < s1; ++st) {
+        const int v = 4 * st + kg;  // this lane's voxel of the k-step
+        const bool okv = v < C;
+        const float a = okv ? A[l16 * C + v] : 0.f;  // dL/dh1[co = l16][v]
+        const int hv = okv ? cpg_halo(v, dG, dGG, PG, PGG) : 0;
+        const float b0 = okv ? ch[hv + toff[0]] : 0.f;
+        const float b1 = (okv && l16 + 16 < 27) ? ch[hv + toff[1]] : 0.f;
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b1, acc1, 0, 0, 0);
+      }
+      // register r of lane l: row co = 4 (l >> 4) + r, column tap 16 tb + (l & 15)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) scr1[(slice * 36 + item) * 12 + i * 3 + k] = acc[i][k];
-    }
-    __syncthreads();
-    if (tid < 432) {  // (item, i, k) -> (co, t)
-      const int item = tid / 12, i = (tid % 12) / 3, k = tid % 3;
-      const int q4 = item / 9, dz = (item / 3) % 3 - 1, dy = item % 3 - 1;
-      float sum = 0.f;
-      for (int sl = 0; sl < kRowSlices; ++sl) sum += scr1[(sl * 36 + item) * 12 + i * 3 + k];
-      const int co = q4 * 4 + i, t = (dz + 1) * 9 + (dy + 1) * 3 + k;
-      gp[(co * 32 + ci) * 27 + t] = sum;
+      for (int r = 0; r < 4; ++r) {
+        wpart[((wave * 2 + 0) * 64 + lane) * 4 + r] = acc0[r];
+        wpart[((wave * 2 + 1) * 64 + lane) * 4 + r] = acc1[r];
+      }
+      __syncthreads();
+      if (tid < 432) {  // (co, t), summed over the waves in order
+        const int co = tid / 27, t = tid % 27;
+        const int tb = t >> 4, l = ((co >> 2) << 4) | (t & 15), r = co & 3;
+        float sum = 0.f;
+        for (int w = 0; w < kW; ++w) sum += wpart[((w * 2 + tb) * 64 + l) * 4 + r];
+        gp[(co * 32 + ci) * 27 + t] = sum;
+      }
     }
   }
 }
