@@ -450,11 +450,11 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
     }
 #pragma unroll
     for (int k = 0; k < kCbV; ++k) tpre[k] = vok[k] ? tval(vv[k] * 32) : 0.f;
+    __syncthreads();
+    for (int h = tid; h < PV; h += kCbThreads) ch[h] = 0.f;  // the zero border stays; interiors are rewritten
 #pragma unroll 1
     for (int ci = 0; ci < 32; ++ci) {
-      __syncthreads();  // previous channel's readers of ch / wpart are done
-      for (int h = tid; h < PV; h += kCbThreads) ch[h] = 0.f;
-      __syncthreads();
+      __syncthreads();  // previous channel's readers of ch / wpart are done (and the zeroing)
 #pragma unroll
       for (int k = 0; k < kCbV; ++k) {
         const float d = sv[ci] - tpre[k];
