@@ -10,25 +10,9 @@ import numpy as np
 import pytest
 import torch
 
-from tests_helpers import golden, golden_state_dict
+from tests_helpers import golden, golden_state_dict, topk_parity
 
 pytestmark = pytest.mark.gpu
-
-
-def _near_tie(score, K, rel):
-    """True if two distinct values among the oracle's top K+1 scores are closer than `rel`
-    (relative): the top-k order/set is then not determined at the precision both sides agree
-    to.  Exactly equal scores come from duplicated FE points (N < npoint, Q1) and are
-    value-identical, so they are not counted."""
-    for row in score.double():
-        s = torch.unique(torch.sort(row, descending=True).values[: K + 1])
-        if s.numel() > 1 and bool(((s[1:] - s[:-1]) / s[1:].abs().clamp_min(1e-30) < rel).any()):
-            return True
-    return False
-
-
-def _score_noise(got, want):
-    return float(((got.double() - want.double()).abs() / want.double().abs().clamp_min(1e-30)).max())
 
 
 def _load_model(cuda, z):
@@ -67,11 +51,16 @@ def test_e2e_fixture_front(cuda, name):
     # noise by mean/std of the raw logit (~100x); scores agree to 1e-3 relative
     want = torch.from_numpy(z["score"])
     torch.testing.assert_close(tr["score"].cpu(), want, rtol=1e-3, atol=1e-5)
-    noise = _score_noise(tr["score"].cpu(), want)
-    if _near_tie(want, K, rel=max(1e-5, 10 * noise)):
-        pytest.skip(f"oracle top-{K} not determined at the agreed precision ({noise:.1e}); the back half is "
-                    "checked with the oracle's top-k in test_e2e_fixture_back")
-    torch.testing.assert_close(kp.cpu(), torch.from_numpy(z["keypts_out"]), rtol=0, atol=0)
+    exact, n_amb = topk_parity(tr["topk"], tr["score"], torch.from_numpy(z["topk"]), want, K)
+    print(f"{name}: GPU top-k == oracle top-k: {exact} ({n_amb} near-tie rank boundaries)")
+    if exact or torch.equal(kp.cpu(), torch.from_numpy(z["keypts_out"])):
+        # the GPU's own top-k drives the back half: the whole forward against the fixture
+        torch.testing.assert_close(kp.cpu(), torch.from_numpy(z["keypts_out"]), rtol=0, atol=0)
+        torch.testing.assert_close(vcp.cpu(), torch.from_numpy(z["vcp"]), rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(R.cpu(), torch.from_numpy(z["R"]), rtol=0, atol=1e-4)
+        torch.testing.assert_close(t.cpu(), torch.from_numpy(z["t"]), rtol=0, atol=1e-4)
+    # otherwise the order differs only inside near-tie blocks (asserted above) and the back
+    # half is checked from the oracle's top-k in test_e2e_fixture_back
 
 
 @pytest.mark.parametrize("name", ["e2e_c3small", "e2e_c1"])
@@ -96,45 +85,98 @@ def test_e2e_fixture_back(cuda, name):
     torch.testing.assert_close(loss.cpu(), torch.from_numpy(z["loss"]), rtol=1e-4, atol=1e-6)
 
 
-def test_e2e_live_full_size_pair(cuda):
-    """One C3 pair at full size (N=16384, K=64, r=2.0, npoint 10000) against the live oracle,
-    end to end with the GPU's own top-k (R, t within the north_star's 1e-4)."""
+def _oracle_threads():
+    """The oracle's CPU threads: the cores this process may use, capped at the GPU box's CPU
+    share (16 per GPU)."""
+    import os
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(n, 16))
+
+
+def test_e2e_c3_batch8_lanes(cuda):
+    """BASELINE C3 as bench.py runs it: B = 8 pairs, N = 16384, K = 64, r = 2.0, s = 0.4, FE
+    npoint 10000, with two more 8-pair batches in flight on their own streams.  Checked:
+    * the lane-0 batch run concurrently equals the same batch run alone (bit for bit);
+    * pairs 0 and 7 against the live oracle, each end to end with the GPU's OWN top-k: FE
+      geometry exact, top-k per rank (tests_helpers.topk_parity), key points exact, candidates
+      exact, vcp within 1e-5 and R, t within the north_star's 1e-4.  Should a near-tie block
+      reorder the top-k, the pair is re-run from the oracle's top-k at full size and R, t
+      must still be within 1e-4 (asserted, never skipped)."""
     import oracle as O
     import dvcp
     from dvcp.synthetic import condition_weights, make_pairs, randomize_bn
-    src, tgt, R_gt, t_gt = make_pairs(1, 16384, seed=777)
+    B, N, K, r, s = 8, 16384, 64, 2.0, 0.4
+    lanes_data = [make_pairs(B, N, seed=777 + 101 * lane) for lane in range(3)]
     torch.manual_seed(0)
-    ref = O.DeepVCP(use_normal=False, K=64, r=2.0, s=0.4).eval()
+    ref = O.DeepVCP(use_normal=False, K=K, r=r, s=s).eval()
     randomize_bn(ref)
-    with torch.no_grad():
-        _, calib = ref.FE1(src)
-    condition_weights(ref, feats=calib)
-    mine = dvcp.DeepVCP(use_normal=False, K=64, r=2.0, s=0.4).eval()
+    mine = dvcp.DeepVCP(use_normal=False, K=K, r=r, s=s).eval().to(cuda)
     mine.load_state_dict(ref.state_dict())
-    mine.to(cuda)
+    src, tgt, R_gt, t_gt = lanes_data[0]
+    with torch.no_grad():
+        _, calib, _ = mine.FE1.run(src[:1].to(cuda))
+    condition_weights(ref, feats=calib)     # separated key-point scores (dvcp/synthetic.py)
+    mine.load_state_dict(ref.state_dict())
     torch.manual_seed(1)
-    with torch.no_grad(), O.tracing() as trace:
-        kp_o, vcp_o = ref(src, tgt, R_gt, torch.zeros(1, 3))
-        loss_o, R_o, t_o = O.deepVCP_loss(kp_o, vcp_o, R_gt, t_gt, 0.5)
-    torch.manual_seed(1)
+    starts = [mine.draw_starts(B, N, N) for _ in lanes_data]
+    dev_data = [tuple(x.to(cuda) for x in d) for d in lanes_data]
+
+    def run(lane, trace=None):
+        s_, g_, R_, t_ = dev_data[lane]
+        kp, vcp = mine(s_, g_, R_, torch.zeros(1, 3), starts=starts[lane], trace=trace)
+        loss, R, t = dvcp.deepVCP_loss(kp, vcp, R_, t_, 0.5)
+        return kp, vcp, loss, R, t
+
+    streams = [torch.cuda.Stream(device=cuda) for _ in lanes_data]
     tr = {}
     with torch.no_grad():
-        kp, vcp = mine(src.to(cuda), tgt.to(cuda), R_gt.to(cuda), torch.zeros(1, 3), trace=tr)
-        loss, R, t = dvcp.deepVCP_loss(kp, vcp, R_gt.to(cuda), t_gt.to(cuda), 0.5)
-    d = dict(trace)
-    fe_x = [v for n, v in trace if n == "fe_xyz"]
-    assert torch.equal(tr["src_xyz"].transpose(1, 2).cpu(), fe_x[0])
-    assert torch.equal(tr["tgt_xyz"].transpose(1, 2).cpu(), fe_x[1])
-    want = d["wl_score"][..., 0]
-    noise = _score_noise(tr["score"].cpu(), want)
-    if _near_tie(want, 64, rel=max(1e-5, 10 * noise)):
-        pytest.skip(f"top-k not determined at the agreed precision ({noise:.1e})")
-    torch.testing.assert_close(kp.cpu(), kp_o, rtol=0, atol=0)
-    assert torch.equal(tr["cand"].cpu(), d["candidates"])
-    torch.testing.assert_close(vcp.cpu(), vcp_o, rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(R.cpu(), R_o, rtol=0, atol=1e-4)
-    torch.testing.assert_close(t.cpu(), t_o, rtol=0, atol=1e-4)
-    torch.testing.assert_close(loss.cpu(), loss_o, rtol=1e-4, atol=1e-6)
+        outs = []
+        for lane, st in enumerate(streams):
+            with torch.cuda.stream(st):
+                outs.append(run(lane, trace=tr if lane == 0 else None))
+        torch.cuda.synchronize()
+        alone = run(0)
+        torch.cuda.synchronize()
+    for a, b in zip(outs[0], alone):
+        assert torch.equal(a, b), "a batch run alongside others differs from the same batch run alone"
+    kp, vcp, loss, R, t = (x.cpu() for x in outs[0])
+
+    torch.set_num_threads(_oracle_threads())
+    for b in (0, B - 1):
+        with torch.no_grad(), O.fps_starts([x[b:b + 1] for x in starts[0]]), O.tracing() as trace:
+            kp_o, vcp_o = ref(src[b:b + 1], tgt[b:b + 1], R_gt[b:b + 1], torch.zeros(1, 3))
+            loss_o, R_o, t_o = O.deepVCP_loss(kp_o, vcp_o, R_gt[b:b + 1], t_gt[b:b + 1], 0.5)
+        d = dict(trace)
+        fe_x = [v for n, v in trace if n == "fe_xyz"]
+        assert torch.equal(tr["src_xyz"][b:b + 1].transpose(1, 2).cpu(), fe_x[0])
+        assert torch.equal(tr["tgt_xyz"][b:b + 1].transpose(1, 2).cpu(), fe_x[1])
+        want = d["wl_score"][..., 0]
+        torch.testing.assert_close(tr["score"][b:b + 1].cpu(), want, rtol=1e-3, atol=1e-5)
+        exact, n_amb = topk_parity(tr["topk"][b:b + 1], tr["score"][b:b + 1], d["topk_idx"], want, K)
+        print(f"C3 pair {b}: GPU top-k == oracle top-k: {exact} ({n_amb} near-tie rank boundaries), "
+              f"max|dR| {float((R[b] - R_o[0]).abs().max()):.2e}, max|dt| {float((t[b] - t_o[0]).abs().max()):.2e}")
+        if exact:
+            assert torch.equal(kp[b:b + 1], kp_o)
+            assert torch.equal(tr["cand"][b:b + 1].cpu(), d["candidates"])
+            torch.testing.assert_close(vcp[b:b + 1], vcp_o, rtol=1e-5, atol=1e-5)
+            torch.testing.assert_close(R[b:b + 1], R_o, rtol=0, atol=1e-4)
+            torch.testing.assert_close(t[b:b + 1], t_o, rtol=0, atol=1e-4)
+        else:
+            one = tuple(x[b:b + 1].to(cuda) for x in lanes_data[0])
+            with torch.no_grad():
+                kp1, vcp1, _, R1, t1 = _run_pair(mine, one, [x[b:b + 1] for x in starts[0]], d["topk_idx"])
+            assert torch.equal(kp1.cpu(), kp_o)
+            torch.testing.assert_close(vcp1.cpu(), vcp_o, rtol=1e-5, atol=1e-5)
+            torch.testing.assert_close(R1.cpu(), R_o, rtol=0, atol=1e-4)
+            torch.testing.assert_close(t1.cpu(), t_o, rtol=0, atol=1e-4)
+
+
+def _run_pair(model, data, starts, keypoint_idx):
+    import dvcp
+    s_, g_, R_, t_ = data
+    kp, vcp = model(s_, g_, R_, torch.zeros(1, 3), starts=torch.stack(starts), keypoint_idx=keypoint_idx)
+    loss, R, t = dvcp.deepVCP_loss(kp, vcp, R_, t_, 0.5)
+    return kp, vcp, loss, R, t
 
 
 def test_module_surface_errors(cuda):
