@@ -10,8 +10,13 @@ r=2.0 / s=0.4 -> C=1331), inputs resident in HBM, eval mode, random-init weights
 (torch.manual_seed(0)).  Pairs are independent, so ranks shard the pairs with no data-path
 collective ("weak" scaling); the per-pair (R, t) are all-gathered over RCCL once at the end of
 the timed region.  Rank 0 prints one JSON line.  At N=1 the CPU oracle (REF-R restated in
-torch CPU ops) is timed on one of the same pairs with the same weights and FPS starts, and
-its R, t are compared with the GPU's.
+torch CPU ops) is timed on the same pairs with the same weights and FPS starts (median of
+--cpu-pairs), and its R, t are compared with the GPU's.
+
+Roofline fields: ``roofline`` is the FPS chain's latency roofline (us per
+dependent step against the measured step floor); ``step_roofline`` and ``stages`` are SURVEY.md
+8(d)'s per-stage ceilings from one batch in flight; ``live_launch_ms`` are per-launch durations
+over the timed region (batches in flight contend, so they exceed the isolated ones).
 """
 import argparse
 import json
@@ -47,6 +52,7 @@ import torch.distributed as dist  # noqa: E402
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
 PEAK_FP32_TFLOPS = 157.3   # fp32 vector = fp32 MFMA dense rate
 PEAK_HBM_GBS = 8000.0
+N_CU = 256
 
 
 def parse():
@@ -65,7 +71,10 @@ def parse():
     p.add_argument("--hw-queues", type=int, default=16, help="GPU_MAX_HW_QUEUES for this process (<= 32)")
     p.add_argument("--stage-report", action="store_true", help="print the per-kernel table to stderr")
     p.add_argument("--no-kernel-events", action="store_true",
-                   help="diagnostic: no per-launch HIP events in the timed region (no roofline/stages)")
+                   help="diagnostic: no per-launch HIP events in the timed region")
+    p.add_argument("--iso-steps", type=int, default=3,
+                   help="steps timed per kernel with one batch in flight (stage roofline)")
+    p.add_argument("--cpu-pairs", type=int, default=3, help="C3 pairs timed for the CPU baseline (median)")
     return p.parse_args()
 
 
@@ -151,44 +160,22 @@ def main():
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         elapsed = float(tmax.item())
 
-    # per-kernel live HIP-event timing over the timed region (events on the launching stream)
+    # ---- per-kernel HIP-event timing (events on the stream each kernel is launched on) --------
+    # (1) live over the timed region, 8 batches in flight: per-launch durations under contention
+    live = _per_kernel(log)
+    # (2) isolated: the same step with one batch in flight (a few steps on lane 0, after the timed
+    #     region), for the per-stage roofline; (3) the FPS step floor probe
+    _lib.EVENT_LOG = []
+    for _ in range(args.iso_steps):
+        step(0)
+        torch.cuda.synchronize()
+    iso, _lib.EVENT_LOG = _per_kernel(_lib.EVENT_LOG), None
+    floor_us = fps_step_floor_us(dev)
+    ms_step = elapsed / args.steps * 1e3
     S = model.FE1.sa1.npoint
     C = int((2 * r) / s + 1) ** 3
-    per, work = {}, {}
-    for name, e0, e1, w in log:
-        per.setdefault(name, []).append(e0.elapsed_time(e1))
-        if w is not None:
-            acc = work.setdefault(name, [0.0, 0.0])
-            acc[0] += w[0]
-            acc[1] += w[1]
-    if not per:  # --no-kernel-events
-        per = {"(no kernel events)": [float("nan")]}
-    tot = {k: sum(v) for k, v in per.items()}
-    dom = max(tot, key=tot.get)
-    n_launch = len(per[dom])
-    avg_ms = tot[dom] / n_launch
-    flops = work.get(dom, [0.0, 0.0])[0] / n_launch
-    nbytes = work.get(dom, [0.0, 0.0])[1] / n_launch
-    achieved = flops / (avg_ms * 1e-3) / 1e12
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    if os.path.exists(pmc):
-        try:
-            traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    roofline = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 4), "peak": PEAK_FP32_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 6), "traffic": traffic,
-                "avg_launch_ms": round(avg_ms, 4), "algorithmic_flops_per_launch": flops,
-                "algorithmic_bytes_per_launch": nbytes,
-                "hbm_GBs_algorithmic": round(nbytes / (avg_ms * 1e-3) / 1e9, 2),
-                "note": "fp32 arithmetic (VALU and MFMA share the 157.3 TF fp32 peak); algorithmic flops per "
-                        "launch as defined in DESIGN.md (reference op graph)"}
-    stages = {k: {"launches": len(v), "total_ms_per_step": round(sum(v) / args.steps, 3),
-                  "avg_ms": round(sum(v) / len(v), 4),
-                  "tflops": round(work.get(k, [0, 0])[0] / (sum(v) * 1e-3) / 1e12, 3) if k in work else None}
-              for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1]))}
-
+    stages, step_roof = stage_roofline(iso, args.iso_steps, floor_us, ms_step)
+    roofline = fps_roofline(live, iso, floor_us)
     res_cpu = res.cpu()
     reg_err = {"rot_deg_mean": float(res_cpu[:, 12].mean()), "rot_deg_max": float(res_cpu[:, 12].max()),
                "trans_mean": float(res_cpu[:, 13].mean()), "trans_max": float(res_cpu[:, 13].max()),
@@ -209,61 +196,204 @@ def main():
         "host_issue_ms_per_step": round(t_issue / args.steps * 1e3, 3),
         "registration_error_vs_gt": reg_err,
         "roofline": roofline,
+        "step_roofline": step_roof,
         "stages": stages,
+        "live_launch_ms": {k: round(v["ms"] / v["n"], 4) for k, v in sorted(live.items(), key=lambda kv: -kv[1]["ms"])},
     }
     # HBM fraction of the whole step (north_star asks for it; the path is compute/latency bound)
     out["hbm_fraction_step"] = round(177e6 * B / (elapsed / args.steps) / (PEAK_HBM_GBS * 1e9), 6)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"], out["parity"] = cpu_baseline(model, src, tgt, R_gt, t_gt, dev)
+        out["cpu_baseline"], out["parity"] = cpu_baseline(model, src, tgt, R_gt, t_gt, dev, args.cpu_pairs)
     if rank == 0:
         if args.stage_report:
             for k, v in stages.items():
                 print(f"{k:28s} {v}", file=sys.stderr)
+            print(json.dumps(step_roof), file=sys.stderr)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def cpu_baseline(model, src, tgt, R_gt, t_gt, dev):
-    """Time the CPU oracle (REF-R in torch CPU ops) on pair 0, same weights and FPS starts."""
+def _per_kernel(log):
+    """EVENT_LOG -> {entry point: {n, ms, flops, bytes, exec_flops, wgs, steps}} (sums)."""
+    out = {}
+    for name, e0, e1, w in log:
+        d = out.setdefault(name, {"n": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0, "exec_flops": 0.0,
+                                  "exec_known": True, "wgs": None, "steps": 0})
+        d["n"] += 1
+        d["ms"] += e0.elapsed_time(e1)
+        w = tuple(w or ()) + (None,) * 5
+        d["flops"] += w[0] or 0.0
+        d["bytes"] += w[1] or 0.0
+        if w[2] is None:
+            d["exec_known"] = False
+        else:
+            d["exec_flops"] += w[2]
+        if w[3] is not None:
+            d["wgs"] = w[3]
+            d["steps"] += w[4]
+    return out
+
+
+def fps_step_floor_us(dev, steps=20000):
+    """Measured floor of one FPS step: dvcp_fps_step_floor (a 512-thread workgroup running the
+    chain's per-step DPP argmax + LDS slot + barrier + slot reduction with no point work)."""
+    from dvcp import _lib
+    out = torch.empty(16, dtype=torch.float32, device=dev)
+    st = _lib.stream()
+    _lib.call("dvcp_fps_step_floor", 1000, 16, _lib.ptr(out), st)   # warm-up
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    _lib.call("dvcp_fps_step_floor", steps, 16, _lib.ptr(out), st)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / steps
+
+
+def stage_roofline(iso, iso_steps, floor_us, ms_step):
+    """per stage, its ceiling time max(bytes/BW, flops/peak) (FPS: the latency
+    floor x its dependent steps) against the isolated measured time; the step roofline is the
+    sum of the ceilings in device-time over the measured step time.  Device time of a kernel
+    whose grid covers only part of the GPU (the FPS chain: one workgroup per cloud) is its
+    duration x its share of the 256 CUs, so the per-step device times add up like the work does."""
+    stages, ideal_dev, meas_dev = {}, 0.0, 0.0
+    for k, v in sorted(iso.items(), key=lambda kv: -kv[1]["ms"]):
+        ms = v["ms"] / iso_steps
+        share = min(1.0, v["wgs"] / N_CU) if v["wgs"] else 1.0
+        t_flop = v["flops"] / iso_steps / (PEAK_FP32_TFLOPS * 1e12) * 1e3
+        t_byte = v["bytes"] / iso_steps / (PEAK_HBM_GBS * 1e9) * 1e3
+        ideal, bound = (t_flop, "fp32") if t_flop >= t_byte else (t_byte, "hbm")
+        if v["wgs"]:
+            # one dependent step per sampled centre; a step's FPS launches run back to back
+            t_lat = v["steps"] / iso_steps * floor_us * 1e-3
+            if t_lat > ideal:
+                ideal, bound = t_lat, "latency"
+        dev_ms, dev_ideal = ms * share, ideal * share
+        ideal_dev += dev_ideal
+        meas_dev += dev_ms
+        stages[k] = {"launches_per_step": round(v["n"] / iso_steps, 2), "isolated_ms_per_step": round(ms, 4),
+                     "cu_share": round(share, 4), "device_ms_per_step": round(dev_ms, 4),
+                     "ceiling_ms_per_step": round(ideal, 4), "bound": bound,
+                     "frac_of_ceiling": round(ideal / ms, 4) if ms > 0 else None,
+                     "ref_graph_gflop": round(v["flops"] / iso_steps / 1e9, 3),
+                     "executed_gflop": round(v["exec_flops"] / iso_steps / 1e9, 3) if v["exec_known"] else None,
+                     "tflops_ref_graph": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 3) if v["flops"] else None,
+                     "tflops_executed": (round(v["exec_flops"] / (v["ms"] * 1e-3) / 1e12, 3)
+                                         if v["exec_known"] and v["exec_flops"] else None),
+                     # the kernel against its own work: executed flops (upper bound) at the fp32 peak
+                     "frac_of_executed_ceiling": (round(max(v["exec_flops"] / iso_steps / (PEAK_FP32_TFLOPS * 1e12) * 1e3,
+                                                            t_byte) / ms, 4)
+                                                  if v["exec_known"] and v["exec_flops"] and ms > 0 else None)}
+    roof = {"formula": "sum_s max(bytes_s/BW, flops_s/peak_s [, FPS: steps x floor]) x cu_share_s / ms_per_step",
+            "ceiling_device_ms_per_step": round(ideal_dev, 4), "measured_device_ms_per_step_isolated": round(meas_dev, 4),
+            "ms_per_step": round(ms_step, 4), "achieved_frac": round(ideal_dev / ms_step, 4),
+            "isolated_frac": round(ideal_dev / meas_dev, 4) if meas_dev else None,
+            "note": "stage times from one batch in flight (bench --iso-steps); ms_per_step with the default "
+                    "batches in flight; flops on the reference's op graph (executed flops listed per stage)"}
+    return stages, roof
+
+
+def fps_roofline(live, iso, floor_us):
+    """FPS is a serial chain of npoint dependent argmax steps per cloud: latency-bound, so its
+    roofline is microseconds per step against the measured step floor (dvcp_fps_step_floor)."""
+    name = "dvcp_fps_ws"
+    if name not in iso:
+        return None
+    v, w = iso[name], live.get(name)
+    us_iso = v["ms"] * 1e3 / v["steps"]
+    us_live = w["ms"] * 1e3 / w["steps"] if w and w["steps"] else None
+    return {"bound": "latency", "kernel": name, "unit": "us/step", "achieved": round(us_iso, 4),
+            "peak": round(floor_us, 4), "frac": round(floor_us / us_iso, 4),
+            "traffic": _pmc_traffic(name), "avg_launch_ms_isolated": round(v["ms"] / v["n"], 4),
+            "avg_launch_ms_live": round(w["ms"] / w["n"], 4) if w else None,
+            "us_per_step_live": round(us_live, 4) if us_live else None,
+            "algorithmic_bytes_per_launch": v["bytes"] / v["n"],
+            "note": "achieved = isolated launch time / sampled centres (one batch in flight); peak = the measured "
+                    "per-step floor of the chain's synchronisation (DPP argmax + LDS slot + barrier + slot "
+                    "reduction, no point work); the batched kernel accepts several centres per round, so frac > 1 "
+                    "is possible; live = with the default batches in flight"}
+
+
+def _pmc_traffic(kernel):
+    pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        return json.load(open(pmc)).get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def _cpu_topology():
+    """(model name, physical cores, logical CPUs) from lscpu."""
+    info = {}
+    try:
+        for line in subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout.splitlines():
+            k, _, v = line.partition(":")
+            info[k.strip()] = v.strip()
+    except Exception:
+        pass
+    try:
+        phys = int(info["Core(s) per socket"]) * int(info["Socket(s)"])
+    except Exception:
+        phys = None
+    return info.get("Model name", platform.processor() or ""), phys, os.cpu_count()
+
+
+def cpu_baseline(model, src, tgt, R_gt, t_gt, dev, n_pairs):
+    """Time the CPU oracle (REF-R in torch CPU ops) on the bench's C3 pairs, same
+    weights and FPS starts: one warm-up forward on a small pair (oneDNN / allocator warm-up), then
+    the median of ``n_pairs`` full-size pairs, one pair per forward (B = 1, eval, no_grad).
+    Threads: the physical cores this process may use, capped by the box's CPU share per GPU
+    (OMP_NUM_THREADS, 16 on the GPU pool), stated in the result."""
     import oracle as O
     import dvcp
-    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = max(1, min(threads, 16))
+    from dvcp.synthetic import make_pairs
+    cpu_model, phys, logical = _cpu_topology()
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (logical or 1)
+    share = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    threads = max(1, min(avail, phys or avail, share))
     torch.set_num_threads(threads)
     ref = O.DeepVCP(use_normal=False, K=model.K, r=model.r, s=model.s).eval()
     ref.load_state_dict({k: v.cpu() for k, v in model.state_dict().items()})
     N = src.shape[2]
-    starts = model.draw_starts(1, N, N)
-    with torch.no_grad():
-        kp, vcp = model(src[:1], tgt[:1], R_gt[:1], torch.zeros(1, 3), starts=starts)
-        _, Rg, tg = dvcp.deepVCP_loss(kp, vcp, R_gt[:1], t_gt[:1], 0.5)
-    s0, g0, R0, t0 = src[:1].cpu(), tgt[:1].cpu(), R_gt[:1].cpu(), t_gt[:1].cpu()
-    t_start = time.perf_counter()
-    with torch.no_grad(), O.fps_starts(list(starts)):
-        kpo, vcpo = ref(s0, g0, R0, torch.zeros(1, 3))
-        _, Ro, to = O.deepVCP_loss(kpo, vcpo, R0, t0, 0.5)
-    secs = time.perf_counter() - t_start
-    cpu_model = platform.processor() or ""
-    try:
-        for line in subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout.splitlines():
-            if line.startswith("Model name"):
-                cpu_model = line.split(":", 1)[1].strip()
-    except Exception:
-        pass
-    base = {"value": round(1.0 / secs, 5), "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"1 C3 pair (N=16384, K=64, r=2.0), oracle/ref_r.py torch CPU ops, {secs:.1f} s",
-            "cpu_model": cpu_model, "os_cpu_count": os.cpu_count()}
-    rot_vs_ref, trans_vs_ref = dvcp.registration_errors(Rg, tg, Ro.to(dev), to.to(dev))
-    parity = {"R_maxabs_vs_ref": float((Rg.cpu() - Ro).abs().max()), "t_maxabs_vs_ref": float((tg.cpu() - to).abs().max()),
-              "rot_err_deg_vs_ref": float(rot_vs_ref.max()), "trans_err_vs_ref": float(trans_vs_ref.max()),
-              "rot_trans_err_note": "train.py:112-120 metric between the GPU pose and the oracle pose; "
-                                    "PairwiseDistance's eps contributes sqrt(3)*1e-6 at exact agreement",
-              "vcp_maxabs_vs_ref": float((vcp.cpu() - vcpo).abs().max()),
-              "keypts_equal": bool(torch.equal(kp.cpu(), kpo)),
-              "keypts_same_set": bool(torch.equal(torch.sort(kp.cpu().reshape(-1, 3), 0).values,
-                                                  torch.sort(kpo.reshape(-1, 3), 0).values))}
+    n_pairs = max(1, min(n_pairs, src.shape[0]))
+    with torch.no_grad():   # warm-up: a small pair through the same ops
+        ws, wt, wR, _ = make_pairs(1, 2048, seed=4321)
+        small = O.DeepVCP(use_normal=False, K=model.K, r=model.r, s=model.s, fe_npoint=512).eval()
+        small.load_state_dict(ref.state_dict())
+        small(ws, wt, wR, torch.zeros(1, 3))
+    secs, parity = [], None
+    for b in range(n_pairs):
+        starts = model.draw_starts(1, N, N)
+        sl = slice(b, b + 1)
+        s0, g0, R0, t0 = src[sl].cpu(), tgt[sl].cpu(), R_gt[sl].cpu(), t_gt[sl].cpu()
+        t_start = time.perf_counter()
+        with torch.no_grad(), O.fps_starts(list(starts)):
+            kpo, vcpo = ref(s0, g0, R0, torch.zeros(1, 3))
+            _, Ro, to = O.deepVCP_loss(kpo, vcpo, R0, t0, 0.5)
+        secs.append(time.perf_counter() - t_start)
+        if b == 0:   # the GPU's result for the same pair and starts
+            with torch.no_grad():
+                kp, vcp = model(src[sl], tgt[sl], R_gt[sl], torch.zeros(1, 3), starts=starts)
+                _, Rg, tg = dvcp.deepVCP_loss(kp, vcp, R_gt[sl], t_gt[sl], 0.5)
+            rot_vs_ref, trans_vs_ref = dvcp.registration_errors(Rg, tg, Ro.to(dev), to.to(dev))
+            parity = {"R_maxabs_vs_ref": float((Rg.cpu() - Ro).abs().max()),
+                      "t_maxabs_vs_ref": float((tg.cpu() - to).abs().max()),
+                      "rot_err_deg_vs_ref": float(rot_vs_ref.max()), "trans_err_vs_ref": float(trans_vs_ref.max()),
+                      "rot_trans_err_note": "train.py:112-120 metric between the GPU pose and the oracle pose; "
+                                            "PairwiseDistance's eps contributes sqrt(3)*1e-6 at exact agreement",
+                      "vcp_maxabs_vs_ref": float((vcp.cpu() - vcpo).abs().max()),
+                      "keypts_equal": bool(torch.equal(kp.cpu(), kpo)),
+                      "keypts_same_set": bool(torch.equal(torch.sort(kp.cpu().reshape(-1, 3), 0).values,
+                                                          torch.sort(kpo.reshape(-1, 3), 0).values))}
+    med = sorted(secs)[len(secs) // 2]
+    base = {"value": round(1.0 / med, 5), "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"median of {len(secs)} C3 pairs (N=16384, K=64, r=2.0, one pair per forward) after a "
+                      f"small warm-up pair; oracle/ref_r.py torch CPU ops; per pair "
+                      f"{', '.join(f'{x:.1f}' for x in secs)} s",
+            "cpu_model": cpu_model, "physical_cores": phys, "os_cpu_count": logical,
+            "threads_note": "physical cores available to the process, capped at the box's CPU share per GPU "
+                            "(OMP_NUM_THREADS)"}
     return base, parity
 
 

@@ -12,7 +12,6 @@
 #include "common.h"
 #include "morton.h"
 
-#include <cstdlib>
 
 namespace dvcp {
 
@@ -427,15 +426,6 @@ __global__ void square_distance_kernel(PointsView<T> src, int S, PointsView<T> d
       expansion_d2(dot3_blas(sx, sy, sz, dx, dy, dz), sumsq3(sx, sy, sz), sumsq3(dx, dy, dz));
 }
 
-// DVCP_BQ_SCAN=1 forces the index-order scan (A/B measurements); read once.
-static bool bq_scan_forced() {
-  static const bool v = [] {
-    const char* e = getenv("DVCP_BQ_SCAN");
-    return e && *e && *e != '0';
-  }();
-  return v;
-}
-
 template <typename T>
 static int launch_bq(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, const void* c, int64_t cb,
                      int64_t cc, int64_t cn, int S, int B, double radius, int nsample, int32_t* count,
@@ -447,7 +437,7 @@ static int launch_bq(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
   if constexpr (sizeof(T) == 4) {
     if (workspace) {
       const BqLayout L = bq_layout(workspace, B, N, S);
-      const int tiled = N <= kBqMaxTiles * kBqTile && !bq_scan_forced();
+      const int tiled = N <= kBqMaxTiles * kBqTile;
       hipLaunchKernelGGL(bq_build_kernel, dim3(B), dim3(kBuildThreads), 0, st, pv, N, cv, S, L, tiled);
       if (int e = launch_status("dvcp_ball_query(build)")) return e;
       if (tiled)

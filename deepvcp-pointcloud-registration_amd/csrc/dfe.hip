@@ -13,24 +13,17 @@
 #include "common.h"
 
 #include <algorithm>
-#include <cstdlib>
 
 namespace dvcp {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// dfe_mfma.hip: the target side on fp32 MFMA (default; DVCP_DFE_VALU=1 selects the kernel below)
+// dfe_mfma.hip: the target side on fp32 MFMA.  literal = false: the three linear layers collapsed
+// into one map (default); true: fc1, fc2, fc3 evaluated one after the other.
 template <typename T>
 int launch_dfe_tgt_mfma(PointsView<T> ref, const float* feat, int M, const float* cand, const float* dist,
-                        const int32_t* idx, int B, int Q, const float* params, float* out, hipStream_t st);
-
-static bool dfe_valu_forced() {
-  static const bool v = [] {
-    const char* e = getenv("DVCP_DFE_VALU");
-    return e && *e && *e != '0';
-  }();
-  return v;
-}
+                        const int32_t* idx, int B, int Q, const float* params, float* out, bool literal,
+                        hipStream_t st);
 
 constexpr int kDfeRowsPerQ = 32;
 constexpr int kDfeThreads = 256;
@@ -117,27 +110,6 @@ __device__ __forceinline__ void dfe_tgt_row(PointsView<T> ref, const float* __re
     x[3 + 4 * f4 + 2] = static_cast<float>(static_cast<double>(v.z) * wq[ql][4 * f4 + 2]);
     x[3 + 4 * f4 + 3] = static_cast<float>(static_cast<double>(v.w) * wq[ql][4 * f4 + 3]);
   }
-}
-
-template <typename T>
-__global__ __launch_bounds__(kDfeThreads) void dfe_tgt_kernel(PointsView<T> ref, const float* __restrict__ feat, int M,
-                                                              const float* __restrict__ cand,
-                                                              const float* __restrict__ dist,
-                                                              const int32_t* __restrict__ idx, int Q,
-                                                              const float* __restrict__ params,
-                                                              float* __restrict__ out) {
-  __shared__ float red[kDfeThreads][33];
-  __shared__ double wq[kDfeQPerBlock][32];
-  __shared__ double dsh[kDfeThreads];
-  const int b = blockIdx.y;
-  const int64_t q0 = static_cast<int64_t>(blockIdx.x) * kDfeQPerBlock;
-  const int64_t q = q0 + threadIdx.x / 32;
-  float x[35];
-  dfe_tgt_row(ref, feat, M, cand, dist, idx, Q, b, q, q < Q, dsh, wq, x);
-  float y[32];
-  dfe_mlp(x, y, params);
-  dfe_pool_store(y, red, static_cast<int64_t>(b) * Q + q0,
-                 static_cast<int64_t>(b) * Q + min(static_cast<int64_t>(Q), q0 + kDfeQPerBlock), out);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -394,36 +366,35 @@ extern "C" int dvcp_dfe(int x_dtype, const void* X, int64_t R, const float* para
   return dvcp::launch_status("dvcp_dfe");
 }
 
+static int dfe_tgt_entry(const char* name, bool literal, int dtype, const void* ref_xyz, int64_t rb, int64_t rc,
+                         int64_t rn, int M, const float* ref_feat, const float* cand, const float* dist,
+                         const int32_t* idx, int B, int Q, const float* params, float* out, void* stream) {
+  DVCP_REQUIRE(ref_xyz && ref_feat && cand && dist && idx && params && out, "%s: null pointer", name);
+  DVCP_REQUIRE(M > 0 && B >= 0 && B <= 65535 && Q >= 0, "%s: bad sizes", name);
+  if (B == 0 || Q == 0) return DVCP_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (dtype == DVCP_F32)
+    return dvcp::launch_dfe_tgt_mfma<float>(dvcp::PointsView<float>{static_cast<const float*>(ref_xyz), rb, rc, rn},
+                                            ref_feat, M, cand, dist, idx, B, Q, params, out, literal, st);
+  if (dtype == DVCP_F64)
+    return dvcp::launch_dfe_tgt_mfma<double>(dvcp::PointsView<double>{static_cast<const double*>(ref_xyz), rb, rc, rn},
+                                             ref_feat, M, cand, dist, idx, B, Q, params, out, literal, st);
+  dvcp::set_error("%s: bad dtype %d", name, dtype);
+  return DVCP_EINVAL;
+}
+
 extern "C" int dvcp_dfe_tgt(int dtype, const void* ref_xyz, int64_t rb, int64_t rc, int64_t rn, int M,
                             const float* ref_feat, const float* cand, const float* dist, const int32_t* idx, int B, int Q,
                             const float* params, float* out, void* stream) {
-  DVCP_REQUIRE(ref_xyz && ref_feat && cand && dist && idx && params && out, "dvcp_dfe_tgt: null pointer");
-  DVCP_REQUIRE(M > 0 && B <= 65535, "dvcp_dfe_tgt: bad sizes");
-  if (B == 0 || Q == 0) return DVCP_OK;
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  if (!dvcp::dfe_valu_forced()) {
-    if (dtype == DVCP_F32)
-      return dvcp::launch_dfe_tgt_mfma<float>(dvcp::PointsView<float>{static_cast<const float*>(ref_xyz), rb, rc, rn},
-                                              ref_feat, M, cand, dist, idx, B, Q, params, out, st);
-    if (dtype == DVCP_F64)
-      return dvcp::launch_dfe_tgt_mfma<double>(
-          dvcp::PointsView<double>{static_cast<const double*>(ref_xyz), rb, rc, rn}, ref_feat, M, cand, dist, idx, B,
-          Q, params, out, st);
-  }
-  dim3 grid(dvcp::ceil_div(Q, dvcp::kDfeQPerBlock), B);
-  if (dtype == DVCP_F32)
-    hipLaunchKernelGGL((dvcp::dfe_tgt_kernel<float>), grid, dim3(dvcp::kDfeThreads), 0, st,
-                       dvcp::PointsView<float>{static_cast<const float*>(ref_xyz), rb, rc, rn}, ref_feat, M, cand, dist,
-                       idx, Q, params, out);
-  else if (dtype == DVCP_F64)
-    hipLaunchKernelGGL((dvcp::dfe_tgt_kernel<double>), grid, dim3(dvcp::kDfeThreads), 0, st,
-                       dvcp::PointsView<double>{static_cast<const double*>(ref_xyz), rb, rc, rn}, ref_feat, M, cand,
-                       dist, idx, Q, params, out);
-  else {
-    dvcp::set_error("dvcp_dfe_tgt: bad dtype %d", dtype);
-    return DVCP_EINVAL;
-  }
-  return dvcp::launch_status("dvcp_dfe_tgt");
+  return dfe_tgt_entry("dvcp_dfe_tgt", false, dtype, ref_xyz, rb, rc, rn, M, ref_feat, cand, dist, idx, B, Q, params,
+                       out, stream);
+}
+
+extern "C" int dvcp_dfe_tgt_literal(int dtype, const void* ref_xyz, int64_t rb, int64_t rc, int64_t rn, int M,
+                                    const float* ref_feat, const float* cand, const float* dist, const int32_t* idx,
+                                    int B, int Q, const float* params, float* out, void* stream) {
+  return dfe_tgt_entry("dvcp_dfe_tgt_literal", true, dtype, ref_xyz, rb, rc, rn, M, ref_feat, cand, dist, idx, B, Q,
+                       params, out, stream);
 }
 
 static int64_t dfe_bwd_blocks(int64_t R) {

@@ -20,7 +20,6 @@
 // chain; only the summation order differs from the row-per-thread kernel.
 #include "common.h"
 
-#include <cstdlib>
 
 namespace dvcp {
 
@@ -303,18 +302,15 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
 
 template <typename T>
 int launch_dfe_tgt_mfma(PointsView<T> ref, const float* feat, int M, const float* cand, const float* dist,
-                        const int32_t* idx, int B, int Q, const float* params, float* out, hipStream_t st) {
+                        const int32_t* idx, int B, int Q, const float* params, float* out, bool literal,
+                        hipStream_t st) {
   const int64_t total = static_cast<int64_t>(B) * Q;
   if (total >= (int64_t(1) << 31) / 32) {
     set_error("dvcp_dfe_tgt: B*Q=%lld too large", static_cast<long long>(total));
     return DVCP_EINVAL;
   }
   const int64_t need = (total + kDfeMfmaWaves - 1) / kDfeMfmaWaves;
-  static const bool layerwise = [] {
-    const char* e = getenv("DVCP_DFE_LAYERWISE");
-    return e && *e && *e != '0';
-  }();
-  if (layerwise) {
+  if (literal) {
     const int grid = static_cast<int>(need < 4096 ? need : 4096);
     hipLaunchKernelGGL((dfe_tgt_mfma_kernel<T>), dim3(grid), dim3(kDfeMfmaWaves * kWave), 0, st, ref, feat, M, cand,
                        dist, idx, Q, B, params, out);
@@ -328,8 +324,8 @@ int launch_dfe_tgt_mfma(PointsView<T> ref, const float* feat, int M, const float
 }
 
 template int launch_dfe_tgt_mfma<float>(PointsView<float>, const float*, int, const float*, const float*,
-                                        const int32_t*, int, int, const float*, float*, hipStream_t);
+                                        const int32_t*, int, int, const float*, float*, bool, hipStream_t);
 template int launch_dfe_tgt_mfma<double>(PointsView<double>, const float*, int, const float*, const float*,
-                                         const int32_t*, int, int, const float*, float*, hipStream_t);
+                                         const int32_t*, int, int, const float*, float*, bool, hipStream_t);
 
 }  // namespace dvcp

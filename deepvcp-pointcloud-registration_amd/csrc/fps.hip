@@ -18,8 +18,6 @@
 //     wave publishes {value, index, x, y, z} to a double-buffered LDS slot, and every wave
 //     reduces the 16 slots with a 16-lane DPP max.  No global memory in the loop except the
 //     output stores.
-#include <cstdlib>
-
 #include "common.h"
 
 namespace dvcp {
@@ -777,6 +775,37 @@ __global__ __launch_bounds__(THREADS) void fps_batched_kernel(PointsView<T> pts,
   }
 }
 
+// Step floor of the FPS chain (bench.py's latency roofline): fps_kernel's per-step
+// synchronisation with no point work -- each wave's 64-lane DPP argmax + ballot, one LDS slot per
+// wave, one barrier, the W-slot DPP reduction and readlanes -- each step's value depending on the
+// previous step's winner, so the steps form one dependent chain as in FPS.
+template <int W>
+__global__ __launch_bounds__(W * kWave) void fps_floor_kernel(int steps, float* __restrict__ out) {
+  __shared__ FpsSlot<float> slots[2][W];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float base = static_cast<float>(lane * 7 % 64) + 64.0f * static_cast<float>(wave * 3 % W);
+  int cur = 0;
+  for (int step = 0; step < steps; ++step) {
+    const float bv = base + static_cast<float>(cur & 1) * 0.5f;
+    const float wv = wave_maxf_dpp(bv);
+    const uint64_t tied = __ballot(bv == wv);
+    const int wl = __ffsll(static_cast<long long>(tied)) - 1;
+    FpsSlot<float>* buf = slots[step & 1];
+    if (lane == 0) buf[wave] = FpsSlot<float>{wv, wave * kWave + wl, 0.f, 0.f, 0.f};
+    lds_barrier();
+    const FpsSlot<float> mine = buf[lane & (W - 1)];
+    float v = mine.v;
+    if constexpr (W > 1) v = dpp_maxf<0x111, 0x1>(v);
+    if constexpr (W > 2) v = dpp_maxf<0x112, 0x1>(v);
+    if constexpr (W > 4) v = dpp_maxf<0x114, 0x1>(v);
+    if constexpr (W > 8) v = dpp_maxf<0x118, 0x1>(v);
+    const float gv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), W - 1));
+    const int ws = __ffsll(static_cast<long long>(__ballot((lane < W) & (mine.v == gv)))) - 1;
+    cur = __builtin_amdgcn_readlane(mine.i, ws) + step;
+  }
+  if (tid == 0) out[blockIdx.x] = static_cast<float>(cur);
+}
+
 // Dense fallback (no sort, no pruning) for clouds larger than the sorted kernel's VGPR budget.
 template <typename T>
 __global__ __launch_bounds__(kFpsThreads) void fps_dense_kernel(PointsView<T> pts, int N, int npoint,
@@ -848,27 +877,41 @@ __global__ __launch_bounds__(kFpsThreads) void fps_dense_kernel(PointsView<T> pt
 // the dense kernel's and the reference's argmax rule -- then waits for the cloud's S keys of that
 // step (release/acquire atomics at agent scope, keys double-buffered by step parity: a workgroup
 // can only reach step + 2 after every peer has arrived at step + 1, i.e. after it read step's
-// keys).  Every workgroup reduces the same S keys, so all agree on the next centre.  The wait is
-// bounded: after kFpsSpinCap polls a workgroup gives up and marks its remaining output -1 (the
-// launcher keeps the grid small enough to be co-resident, so this is a guard, not a path).
+// keys).  Every workgroup reduces the same S keys, so all agree on the next centre.
+//
+// Progress does not rest on the whole grid being co-resident.  A workgroup takes its (cloud,
+// chunk) from a ticket counter when it starts running, not from blockIdx, so the tickets handed
+// out so far cover whole clouds plus at most one partly started cloud per launch: a waiting
+// workgroup only ever waits for peers of that one cloud, which take the next free slots on the
+// device (S - 1 slots per concurrent launch).  The wait is still bounded (spin_cap polls) as a
+// guard: a workgroup that gives up raises the launch's error word, which the host checks
+// (dvcp/_lib.py check_device_flags), and writes in-range indices (the start point) for the
+// steps it could not finish, so nothing downstream reads out of bounds.
 constexpr int kFpsSplitMax = 16;
-constexpr int kFpsSplitMaxGrid = 128;
 constexpr uint32_t kFpsSpinCap = 1u << 22;
 
 template <typename T, int P>
 __global__ __launch_bounds__(kFpsThreads) void fps_split_kernel(PointsView<T> pts, int N, int npoint, int S,
-                                                                int b0, const int64_t* __restrict__ start,
+                                                                const int64_t* __restrict__ start,
                                                                 int64_t* __restrict__ out_idx,
                                                                 T* __restrict__ out_xyz,
                                                                 uint64_t* __restrict__ keys,
-                                                                uint32_t* __restrict__ arrived) {
+                                                                uint32_t* __restrict__ arrived,
+                                                                uint32_t* __restrict__ ticket,
+                                                                int32_t* __restrict__ err, uint32_t spin_cap) {
   constexpr int kW = kFpsThreads / kWave;
   constexpr int chunk = P * kFpsThreads;
   __shared__ uint64_t wbest[kW];
   __shared__ uint64_t gbest;
   __shared__ int timed_out;
-  const int b = b0 + static_cast<int>(blockIdx.x) / S, s = static_cast<int>(blockIdx.x) % S;
+  __shared__ uint32_t my_ticket;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) {
+    my_ticket = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    timed_out = 0;
+  }
+  __syncthreads();
+  const int b = static_cast<int>(my_ticket) / S, s = static_cast<int>(my_ticket) % S;
   const int n0 = s * chunk, n1 = min(N, n0 + chunk);
   T px[P], py[P], pz[P];
   float dm[P];
@@ -881,12 +924,12 @@ __global__ __launch_bounds__(kFpsThreads) void fps_split_kernel(PointsView<T> pt
     pz[p] = ok ? pts.at(b, 2, n) : static_cast<T>(0);
     dm[p] = 1e10f;
   }
-  if (tid == 0) timed_out = 0;
-  int64_t cur = start[b];
-  if (cur < 0 || cur >= N) cur = 0;
+  int64_t first = start[b];
+  if (first < 0 || first >= N) first = 0;
+  int64_t cur = first;
   T cx = pts.at(b, 0, cur), cy = pts.at(b, 1, cur), cz = pts.at(b, 2, cur);
-  uint64_t* kb = keys + static_cast<int64_t>(blockIdx.x / S) * 2 * S;
-  uint32_t* cnt = arrived + blockIdx.x / S;
+  uint64_t* kb = keys + static_cast<int64_t>(b) * 2 * S;
+  uint32_t* cnt = arrived + b;
   int step = 0;
   for (; step < npoint; ++step) {
     if (s == 0 && tid == 0) {
@@ -926,7 +969,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_split_kernel(PointsView<T> pt
       uint32_t polls = 0;
       while (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(1);
-        if (++polls > kFpsSpinCap) {
+        if (++polls > spin_cap) {
           timed_out = 1;
           break;
         }
@@ -946,50 +989,62 @@ __global__ __launch_bounds__(kFpsThreads) void fps_split_kernel(PointsView<T> pt
     cz = pts.at(b, 2, cur);
     __syncthreads();  // gbest / wbest are rewritten next step
   }
-  if (s == 0 && step < npoint)  // timed out: mark the rest invalid
-    for (int k = step + 1 + tid; k < npoint; k += kFpsThreads) out_idx[static_cast<int64_t>(b) * npoint + k] = -1;
-  if (s == 0 && step < npoint && tid == 0) out_idx[static_cast<int64_t>(b) * npoint + step] = -1;
+  if (step < npoint) {  // gave up waiting: flag the launch, keep every index in range
+    if (tid == 0) __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (s == 0)
+      for (int k = step + tid; k < npoint; k += kFpsThreads) out_idx[static_cast<int64_t>(b) * npoint + k] = first;
+  }
+}
+
+// Workspace of the split kernel, carved from the caller's B x N fp32 buffer (>= 64 KiB per cloud):
+// keys [B][2][S] u64 | arrived [B] u32 | ticket u32 | err i32 (err is the caller's when given).
+struct FpsSplitWs {
+  uint64_t* keys;
+  uint32_t* arrived;
+  uint32_t* ticket;
+  int32_t* err;
+};
+static FpsSplitWs fps_split_ws(float* ws, int B, int S) {
+  FpsSplitWs w;
+  w.keys = reinterpret_cast<uint64_t*>(ws);
+  w.arrived = reinterpret_cast<uint32_t*>(w.keys + static_cast<int64_t>(B) * 2 * S);
+  w.ticket = w.arrived + B;
+  w.err = reinterpret_cast<int32_t*>(w.ticket + 1);
+  return w;
+}
+
+// Launch the split kernel over B clouds; `withhold` > 0 (tests only) launches that many fewer
+// workgroups, so the last cloud never completes and its workgroups must give up.
+template <typename T>
+static int launch_fps_split(PointsView<T> v, int B, int N, int npoint, const int64_t* start, int64_t* out_idx,
+                            T* out_xyz, float* ws, int32_t* err, uint32_t spin_cap, int withhold, hipStream_t st) {
+  constexpr int P = sizeof(T) == 4 ? 32 : 16;
+  const int S = ceil_div(N, P * kFpsThreads);
+  FpsSplitWs w = fps_split_ws(ws, B, S);
+  hipError_t e = hipMemsetAsync(w.arrived, 0, sizeof(uint32_t) * (B + 2), st);
+  if (e != hipSuccess) return launch_status("dvcp_fps(split memset)");
+  if (!err) err = w.err;
+  const int grid = B * S - withhold;
+  if (grid > 0)
+    hipLaunchKernelGGL((fps_split_kernel<T, P>), dim3(grid), dim3(kFpsThreads), 0, st, v, N, npoint, S, start, out_idx,
+                       out_xyz, w.keys, w.arrived, w.ticket, err, spin_cap);
+  return launch_status("dvcp_fps(split)");
 }
 
 template <typename T>
 static int launch_fps(const T* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N, int npoint,
-                      const int64_t* start, int64_t* out_idx, T* out_xyz, float* ws, hipStream_t st) {
+                      const int64_t* start, int64_t* out_idx, T* out_xyz, float* ws, int32_t* err, hipStream_t st) {
   PointsView<T> v{xyz, sb, sc, sn};
   const int ppt = ceil_div(N, kFpsThreads);
   dim3 grid(B), block(kFpsThreads);
-  // diagnostics only (identical results): DVCP_FPS_SERIAL=1 runs the one-centre-per-step kernel,
-  // DVCP_FPS_SERIAL=2 that kernel without box pruning
-  static const int mode = [] {
-    const char* e = getenv("DVCP_FPS_SERIAL");
-    return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
-  }();
-  // 16 waves for the batched kernel: half the points per lane in the update/regroup phase
-  static const bool wide = [] {
-    const char* e = getenv("DVCP_FPS_WIDE");
-    return e && e[0] == '1';
-  }();
-  if (wide && sizeof(T) == 4 && mode == 0 && N >= kFpsBatchedMinN) {
-    const int pw = ceil_div(N, 1024);
-#define DVCP_FPS_WIDE(P)                                                                                   \
-    if (pw <= P) {                                                                                         \
-      hipLaunchKernelGGL((fps_batched_kernel<T, P, false, 1024>), grid, dim3(1024), 0, st, v, N, npoint, start, \
-                         out_idx, out_xyz, nullptr);                                                       \
-      return launch_status("dvcp_fps(wide)");                                                              \
-    }
-    DVCP_FPS_WIDE(8)
-    DVCP_FPS_WIDE(16)
-#undef DVCP_FPS_WIDE
-  }
+  // batched kernel from 2048 points; below, the one-centre-per-step kernel (box-pruned)
 #define DVCP_FPS_CASE(P)                                                                                   \
   if (ppt <= P) {                                                                                          \
-    if (mode == 0 && N >= kFpsBatchedMinN)                                                                 \
+    if (N >= kFpsBatchedMinN)                                                                              \
       hipLaunchKernelGGL((fps_batched_kernel<T, P>), grid, block, 0, st, v, N, npoint, start, out_idx, out_xyz, \
                          nullptr);                                                                         \
-    else if (mode <= 1)                                                                                    \
-      hipLaunchKernelGGL((fps_kernel<T, kFpsThreads, P, true>), grid, block, 0, st, v, N, npoint, start,        \
-                         out_idx, out_xyz, nullptr);                                                       \
     else                                                                                                   \
-      hipLaunchKernelGGL((fps_kernel<T, kFpsThreads, P, false>), grid, block, 0, st, v, N, npoint, start,       \
+      hipLaunchKernelGGL((fps_kernel<T, kFpsThreads, P, true>), grid, block, 0, st, v, N, npoint, start,        \
                          out_idx, out_xyz, nullptr);                                                       \
     return launch_status("dvcp_fps");                                                                      \
   }
@@ -1007,28 +1062,9 @@ static int launch_fps(const T* xyz, int64_t sb, int64_t sc, int64_t sn, int B, i
     set_error("dvcp_fps: N=%d needs the split/dense path and its B x N fp32 workspace (dvcp_fps_ws)", N);
     return DVCP_EINVAL;
   }
-  {  // split across workgroups: S per cloud, clouds launched in groups that stay co-resident
-    constexpr int P = sizeof(T) == 4 ? 32 : 16;
-    const int S = ceil_div(N, P * kFpsThreads);
-    static const bool dense_forced = [] {
-      const char* e = getenv("DVCP_FPS_DENSE");
-      return e && e[0] == '1';
-    }();
-    // the workspace (B x N fp32, >= 64 KiB per cloud here) holds keys [B][2][S] and counters [B]
-    if (!dense_forced && S <= kFpsSplitMax) {
-      uint64_t* keys = reinterpret_cast<uint64_t*>(ws);
-      uint32_t* arrived = reinterpret_cast<uint32_t*>(keys + static_cast<int64_t>(B) * 2 * S);
-      hipError_t e = hipMemsetAsync(arrived, 0, sizeof(uint32_t) * B, st);
-      if (e != hipSuccess) return launch_status("dvcp_fps(split memset)");
-      const int per = kFpsSplitMaxGrid / S;
-      for (int b0 = 0; b0 < B; b0 += per) {
-        const int nb = min(per, B - b0);
-        hipLaunchKernelGGL((fps_split_kernel<T, P>), dim3(nb * S), block, 0, st, v, N, npoint, S, b0, start, out_idx,
-                           out_xyz, keys + static_cast<int64_t>(b0) * 2 * S, arrived + b0);
-      }
-      return launch_status("dvcp_fps(split)");
-    }
-  }
+  constexpr int P = sizeof(T) == 4 ? 32 : 16;
+  if (ceil_div(N, P * kFpsThreads) <= kFpsSplitMax)
+    return launch_fps_split<T>(v, B, N, npoint, start, out_idx, out_xyz, ws, err, kFpsSpinCap, 0, st);
   hipLaunchKernelGGL((fps_dense_kernel<T>), grid, block, 0, st, v, N, npoint, start, out_idx, out_xyz, ws);
   return launch_status("dvcp_fps(dense)");
 }
@@ -1036,7 +1072,8 @@ static int launch_fps(const T* xyz, int64_t sb, int64_t sc, int64_t sn, int B, i
 }  // namespace dvcp
 
 extern "C" int dvcp_fps_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N, int npoint,
-                           const int64_t* start, int64_t* out_idx, void* out_xyz, float* ws, void* stream) {
+                           const int64_t* start, int64_t* out_idx, void* out_xyz, float* ws, int32_t* err,
+                           void* stream) {
   DVCP_REQUIRE(xyz && start && out_idx, "dvcp_fps: null pointer");
   DVCP_REQUIRE(B >= 0 && N > 0 && npoint >= 0, "dvcp_fps: bad sizes B=%d N=%d npoint=%d", B, N, npoint);
   DVCP_REQUIRE(N <= 65535 || ws, "dvcp_fps: N=%d needs a workspace", N);
@@ -1044,15 +1081,44 @@ extern "C" int dvcp_fps_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, i
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (dtype == DVCP_F32)
     return dvcp::launch_fps<float>(static_cast<const float*>(xyz), sb, sc, sn, B, N, npoint, start, out_idx,
-                                   static_cast<float*>(out_xyz), ws, st);
+                                   static_cast<float*>(out_xyz), ws, err, st);
   if (dtype == DVCP_F64)
     return dvcp::launch_fps<double>(static_cast<const double*>(xyz), sb, sc, sn, B, N, npoint, start, out_idx,
-                                    static_cast<double*>(out_xyz), ws, st);
+                                    static_cast<double*>(out_xyz), ws, err, st);
   dvcp::set_error("dvcp_fps: bad dtype %d", dtype);
   return DVCP_EINVAL;
 }
 
 extern "C" int dvcp_fps(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N, int npoint,
                         const int64_t* start, int64_t* out_idx, void* out_xyz, void* stream) {
-  return dvcp_fps_ws(dtype, xyz, sb, sc, sn, B, N, npoint, start, out_idx, out_xyz, nullptr, stream);
+  return dvcp_fps_ws(dtype, xyz, sb, sc, sn, B, N, npoint, start, out_idx, out_xyz, nullptr, nullptr, stream);
+}
+
+// bench.py: `blocks` workgroups of 512 threads each run the FPS step floor chain for `steps` steps.
+extern "C" int dvcp_fps_step_floor(int steps, int blocks, float* out, void* stream) {
+  DVCP_REQUIRE(out && steps >= 0 && blocks > 0 && blocks <= 65535, "dvcp_fps_step_floor: bad arguments");
+  hipLaunchKernelGGL((dvcp::fps_floor_kernel<dvcp::kFpsThreads / dvcp::kWave>), dim3(blocks), dim3(dvcp::kFpsThreads),
+                     0, static_cast<hipStream_t>(stream), steps, out);
+  return dvcp::launch_status("dvcp_fps_step_floor");
+}
+
+// Test hook for the split kernel's guard: runs the split path with the given poll cap and
+// `withhold` workgroups left out of the grid (so the last cloud cannot complete).
+extern "C" int dvcp_fps_split_probe(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N,
+                                    int npoint, const int64_t* start, int64_t* out_idx, float* ws, int32_t* err,
+                                    uint32_t spin_cap, int withhold, void* stream) {
+  DVCP_REQUIRE(xyz && start && out_idx && ws && err, "dvcp_fps_split_probe: null pointer");
+  DVCP_REQUIRE(B > 0 && N > 0 && npoint > 0 && withhold >= 0, "dvcp_fps_split_probe: bad sizes");
+  const int P = dtype == DVCP_F32 ? 32 : 16;
+  const int S = dvcp::ceil_div(N, P * dvcp::kFpsThreads);
+  DVCP_REQUIRE(S >= 2 && S <= dvcp::kFpsSplitMax && withhold < S, "dvcp_fps_split_probe: N=%d is not a split size", N);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (dtype == DVCP_F32)
+    return dvcp::launch_fps_split<float>(dvcp::PointsView<float>{static_cast<const float*>(xyz), sb, sc, sn}, B, N,
+                                         npoint, start, out_idx, nullptr, ws, err, spin_cap, withhold, st);
+  if (dtype == DVCP_F64)
+    return dvcp::launch_fps_split<double>(dvcp::PointsView<double>{static_cast<const double*>(xyz), sb, sc, sn}, B,
+                                          N, npoint, start, out_idx, nullptr, ws, err, spin_cap, withhold, st);
+  dvcp::set_error("dvcp_fps_split_probe: bad dtype %d", dtype);
+  return DVCP_EINVAL;
 }

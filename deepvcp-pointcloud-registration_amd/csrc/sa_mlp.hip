@@ -12,7 +12,6 @@
 // the layer weights read as wave-uniform scalar loads (SGPR operands) and activations in VGPRs.
 // The max over a centre's rows is an LDS atomic max on the fp32 bit pattern (outputs are
 // post-ReLU, hence >= +0, so unsigned order is float order).
-#include <cstdlib>
 
 #include "common.h"
 
@@ -146,15 +145,6 @@ static int launch_sa(const void* xyz, int64_t sb, int64_t sc, int64_t sn, const 
 
 }  // namespace dvcp
 
-// diagnostics only: DVCP_SA_VALU=1 keeps the two-layer tables on the row-per-thread kernel
-static bool dvcp_sa_force_valu() {
-  static const bool v = [] {
-    const char* e = getenv("DVCP_SA_VALU");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-
 // Workspace of the two-layer MFMA path: U = W1f f + b1 per input point (B x N x C1 fp32), then
 // the centres' curve order (B x S int32).
 static bool sa_mfma_table(int nlayer, const int* chans) {
@@ -206,7 +196,7 @@ static int sa_group_mlp_impl(int dtype, const void* xyz, int64_t sb, int64_t sc,
   }
   // two-layer tables: fp32 MFMA when each point's features are a contiguous, 16-B aligned fp32 run
   const bool mfma_ok = !ff64 && fd == 1 && fb % 4 == 0 && fn % 4 == 0 &&
-                       (reinterpret_cast<uintptr_t>(feat) & 15) == 0 && !dvcp_sa_force_valu();
+                       (reinterpret_cast<uintptr_t>(feat) & 15) == 0;
 #define DVCP_SA_M(DD, A, Bc)                                                                                     \
   return f64 ? dvcp::launch_sa_mfma<double, DD, A, Bc>(xyz, sb, sc, sn, N, ctr, cb, cc, cn, S, B,               \
                                                      static_cast<const float*>(feat), fb, fn, count, list,      \

@@ -3,7 +3,7 @@
 Drop-in for the reference's module surface (deepVCP.py, cpg.py, deep_feat_embedding.py,
 deepVCP_loss.py, pointnet2_utils.py, voxelize.py, knn_cuda.KNN); see INTEGRATION.md.
 """
-from ._lib import load as load_library  # noqa: F401
+from ._lib import check_device_flags, load as load_library  # noqa: F401
 from .cpg import cpg  # noqa: F401
 from .deepVCP import DeepVCP  # noqa: F401
 from .deepVCP_loss import deepVCP_loss, get_rigid_transform, svd_optimization  # noqa: F401

@@ -22,7 +22,9 @@ _D = ctypes.c_double
 # name -> argtypes (every entry point returns int, 0 on success)
 SIGNATURES = {
     "dvcp_fps": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P],
-    "dvcp_fps_ws": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P],
+    "dvcp_fps_ws": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P, _P],
+    "dvcp_fps_step_floor": [_I, _I, _P, _P],
+    "dvcp_fps_split_probe": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, ctypes.c_uint32, _I, _P],
     "dvcp_ball_query": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _D, _I, _P, _P, _P, _P],
     "dvcp_ball_query_ws": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _D, _I, _P, _P, _P, _P, _P],
     "dvcp_square_distance": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _P, _P],
@@ -40,6 +42,7 @@ SIGNATURES = {
     "dvcp_knn_tiled": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P],
     "dvcp_dfe": [_I, _P, _L, _P, _P, _P],
     "dvcp_dfe_tgt": [_I, _P, _L, _L, _L, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P],
+    "dvcp_dfe_tgt_literal": [_I, _P, _L, _L, _L, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P],
     "dvcp_cpg": [_P, _P, _L, _L, _L, _P, _I, _I, _P, _P, _P, _P],
     "dvcp_rigid_transform": [_P, _P, _I, _I, _P, _P, _P],
     "dvcp_svd_optimization": [_P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P],
@@ -99,8 +102,10 @@ def exported_symbols():
 
 # When a list, every entry-point call appends (name, start_event, end_event, work) recorded on
 # torch's current stream (the stream the kernel is launched on) -- bench.py's live per-kernel
-# HIP-event timing.  `work` = (algorithmic flops, algorithmic bytes) of that launch, as defined
-# in DESIGN.md "Roofline accounting".  None (the default) costs nothing.
+# HIP-event timing.  `work` = (algorithmic flops, algorithmic bytes[, executed flops[, workgroups,
+# serial steps]]) of that launch: flops and bytes on the reference's op graph (DESIGN.md section
+# 6), the flops the kernel actually executes where they differ (None: not counted), and for the
+# latency-bound FPS chain its workgroup count and dependent steps.  None (the default) costs nothing.
 EVENT_LOG = None
 
 
@@ -125,6 +130,37 @@ def call(name, *args, work=None):
         rc = getattr(lib, name)(*args)
     if rc != 0:
         raise RuntimeError(f"{name} failed ({rc}): {lib.dvcp_last_error().decode()}")
+
+
+# Device error words (split-FPS guard, voxel grid length) checked without stalling the stream:
+# each is copied to pinned host memory behind an event; ``check_device_flags`` raises for any
+# whose event has completed with a nonzero word (block=True waits for all of them).
+_PENDING_FLAGS = []
+
+
+def defer_flag_check(what, flag):
+    host = torch.empty(flag.shape, dtype=flag.dtype, pin_memory=True)
+    host.copy_(flag, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    _PENDING_FLAGS.append((what, ev, host))
+
+
+def check_device_flags(block=False):
+    """Raise RuntimeError for a completed launch whose error word is set (see defer_flag_check)."""
+    global _PENDING_FLAGS
+    keep, failed = [], None
+    for what, ev, host in _PENDING_FLAGS:
+        if block:
+            ev.synchronize()
+        if block or ev.query():
+            if failed is None and bool((host != 0).any()):
+                failed = what
+        else:
+            keep.append((what, ev, host))
+    _PENDING_FLAGS = keep
+    if failed is not None:
+        raise RuntimeError(f"dvcp: {failed}")
 
 
 def ptr(t):

@@ -117,6 +117,7 @@ class DeepVCP(nn.Module):
         B = src_xyz.shape[0]
         K, r, s = self.K, self.r, self.s
         dev = src_xyz.device
+        _lib.check_device_flags()   # guards of earlier launches (non-blocking)
         top = ops.topk(score, K) if keypoint_idx is None else keypoint_idx.to(dev, torch.int64).contiguous()
         if train_head and src_feat.requires_grad:
             keypts, src_cat, moved = autograd.src_keypoints(src_xyz, src_feat, top, starts[3], R_init)
@@ -128,7 +129,10 @@ class DeepVCP(nn.Module):
         G = int((2 * r) / s + 1)                    # cpg.py:29
         if grid_side(r, s) != G:
             raise AssertionError("cpg.py:30: candidate count != grid_size^3")
-        cand, _ = ops.voxelize(moved, r, s, G, pdim=1)
+        cand, verr = ops.voxelize(moved, r, s, G, pdim=1)
+        # the reference's per-point aranges would not stack if a length differed from G (checked
+        # without a stall: raised by a later dvcp call once this launch has completed)
+        _lib.defer_flag_check("voxelize: a key point's per-axis grid length differs from the others", verr)
         C = G * G * G
         qry = cand.view(B, K * C, 3)
         dist, idx, _ = ops.knn(tgt_xyz, qry, 32, ref_pdim=2, qry_pdim=1, want_idx64=False)

@@ -31,10 +31,16 @@ def fps(xyz, npoint, start, pdim=1):
     idx = torch.empty(B, npoint, dtype=torch.int64, device=xyz.device)
     ctr = torch.empty(B, 3, npoint, dtype=xyz.dtype, device=xyz.device)
     limit = FPS_REG_LIMIT[xyz.dtype]
-    ws = torch.empty(B, N, dtype=torch.float32, device=xyz.device) if N > limit else None
+    _lib.check_device_flags()   # earlier launches' guards (non-blocking)
+    split = N > limit
+    ws = torch.empty(B, N, dtype=torch.float32, device=xyz.device) if split else None
+    err = torch.zeros(1, dtype=torch.int32, device=xyz.device) if split else None
     es = xyz.element_size()
     call("dvcp_fps_ws", dtype_code(xyz), ptr(xyz), sb, sc, sn, B, N, npoint, ptr(start), ptr(idx), ptr(ctr), ptr(ws),
-         stream(), work=(9.0 * B * npoint * N, B * (3 * N * es + npoint * (8 + 3 * es))))
+         ptr(err), stream(), work=(9.0 * B * npoint * N, B * (3 * N * es + npoint * (8 + 3 * es)), None,
+                                   B * (-(-N // 16384) if split else 1), npoint))
+    if split:
+        _lib.defer_flag_check(f"dvcp_fps: split FPS workgroups gave up waiting for their peers (N={N})", err)
     return idx, ctr
 
 
@@ -98,8 +104,19 @@ def sa_group_mlp(xyz, ctr, feat, count, lst, nsample, chans, params, xyz_pdim=2,
     call("dvcp_sa_group_mlp_ws", dtype_code(xyz), ptr(xyz), sb, sc, sn, N, ptr(ctr), cb, cc, cn, S, B, fdt,
          ptr(feat), fb, fd, fn, D, ptr(count), ptr(lst), int(nsample), len(chans) - 1, ptr(ch), ptr(params), ptr(out),
          ptr(ws), stream(),
-         work=(2.0 * macs * B * S * nsample, B * S * (4 * nsample + 4 * chans[-1]) + B * N * 4 * (3 + D)))
+         work=(2.0 * macs * B * S * nsample, B * S * (4 * nsample + 4 * chans[-1]) + B * N * 4 * (3 + D),
+               _sa_exec_flops(chans, B, N, S, nsample)))
     return out
+
+
+def _sa_exec_flops(chans, B, N, S, nsample):
+    """Flops the kernels execute (upper bound: padded rows counted): the two-layer MFMA tables
+    split layer 1 into a per-point part (D x C1 per input point) and a per-row part (3 x C1), and
+    the layer-2 ReLU + max fold (csrc/sa_mlp_mfma.hip); other tables run the reference graph."""
+    if len(chans) == 3 and chans[0] - 3 in (32, 64):
+        D, C1, C2 = chans[0] - 3, chans[1], chans[2]
+        return 2.0 * B * (N * D * C1 + S * nsample * (3 * C1 + C1 * C2))
+    return 2.0 * B * S * nsample * sum(a * b for a, b in zip(chans[:-1], chans[1:]))
 
 
 def fe_head(x, params, with_score):
@@ -223,17 +240,20 @@ def dfe(X, params):
     return out.view(*lead, 32)
 
 
-def dfe_tgt(ref_xyz, ref_feat, cand, dist, idx, params, ref_pdim=2):
-    """get_cat_feat_tgt.py:54-96 fused with deep_feat_embedding.py:47-60.  cand (B, Q, 3)."""
+def dfe_tgt(ref_xyz, ref_feat, cand, dist, idx, params, ref_pdim=2, literal=False):
+    """get_cat_feat_tgt.py:54-96 fused with deep_feat_embedding.py:47-60.  cand (B, Q, 3).
+    ``literal``: fc1-fc3 chained as written instead of collapsed into one map (Q14)."""
     _lib.require_gpu(ref_xyz, ref_feat, cand, dist, idx, params)
     B = ref_xyz.shape[0]
     M, rb, rc, rn = _pts(ref_xyz, ref_pdim)
     Q = cand.shape[1]
     feat_c, cand_c, dist_c, idx_c = ref_feat.contiguous(), cand.contiguous(), dist.contiguous(), idx.contiguous()
     out = torch.empty(B, Q, 32, dtype=torch.float32, device=ref_xyz.device)
-    call("dvcp_dfe_tgt", dtype_code(ref_xyz), ptr(ref_xyz), rb, rc, rn, M, ptr(feat_c), ptr(cand_c), ptr(dist_c),
+    call("dvcp_dfe_tgt_literal" if literal else "dvcp_dfe_tgt", dtype_code(ref_xyz), ptr(ref_xyz), rb, rc, rn, M,
+         ptr(feat_c), ptr(cand_c), ptr(dist_c),
          ptr(idx_c), B, Q, ptr(params), ptr(out), stream(),
-         work=(2.0 * 3168 * 32 * B * Q, B * (M * (12 + 128) + Q * (12 + 32 * 8 + 128))))
+         work=(2.0 * 3168 * 32 * B * Q, B * (M * (12 + 128) + Q * (12 + 32 * 8 + 128)),
+               2.0 * (3168 if literal else 35 * 32) * 32 * B * Q))
     return out
 
 
@@ -252,7 +272,8 @@ def cpg(src, tgt, cand, G, params, want_weight=False):
     w = torch.empty(B, K, C, dtype=torch.float32, device=cand.device) if want_weight else None
     call("dvcp_cpg", ptr(srcc), ptr(tgt), tgt.stride(1), tgt.stride(2), tgt.stride(3), ptr(candc), B * K, int(G),
          ptr(params), ptr(vcp), ptr(w), stream(),
-         work=(2.0 * 27 * (32 * 16 + 16 * 4 + 4) * B * K * C, B * K * (128 + C * (128 + 12) + 12)))
+         work=(2.0 * 27 * (32 * 16 + 16 * 4 + 4) * B * K * C, B * K * (128 + C * (128 + 12) + 12),
+               2.0 * 27 * (32 * 16 + 16 * 4 + 4) * B * K * C))
     return (vcp, w) if want_weight else vcp
 
 

@@ -48,10 +48,26 @@ int dvcp_fps(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int
              int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz, void* stream);
 
 /* dvcp_fps with a B x N fp32 workspace, required when N exceeds the register-resident limit
- * (16384 fp32 / 8192 fp64 points per cloud); smaller clouds ignore it. */
+ * (16384 fp32 / 8192 fp64 points per cloud); smaller clouds ignore it.  Such clouds are split
+ * over ceil(N / 16384) workgroups (8192 fp64) that exchange one argmax key per step through
+ * device-scope atomics.  err (optional int32, zeroed by the caller): set to 1 if a workgroup
+ * gave up waiting for its peers (a guard; the indices then stay in range but are not FPS). */
 int dvcp_fps_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N,
                 int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz, float* ws,
-                void* stream);
+                int32_t* err, void* stream);
+
+/* Measurement probe (no reference counterpart): `blocks` workgroups each run `steps` steps of
+ * the FPS chain's per-step synchronisation with no point work (wave DPP argmax, LDS slot, one
+ * barrier, slot reduction); out: blocks floats.  bench.py times it as the latency floor. */
+int dvcp_fps_step_floor(int steps, int blocks, float* out, void* stream);
+
+/* Test hook of the split FPS guard (no reference counterpart): the split path of dvcp_fps_ws
+ * for N in (16384, 262144] fp32 / (8192, 131072] fp64, with at most spin_cap polls per wait and
+ * `withhold` workgroups left out of the grid, so that the last cloud cannot complete and must
+ * raise *err. */
+int dvcp_fps_split_probe(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B,
+                         int N, int npoint, const int64_t* start, int64_t* out_idx, float* ws,
+                         int32_t* err, uint32_t spin_cap, int withhold, void* stream);
 
 /* Ball query.  Replaces pointnet2_utils.py:87-107 query_ball_point (and the
  * square_distance expansion it uses, :19-40): the first `nsample` ascending point indices
@@ -197,6 +213,15 @@ int dvcp_dfe(int x_dtype, const void* X, int64_t R, const float* params, float* 
 int dvcp_dfe_tgt(int dtype, const void* ref_xyz, int64_t rb, int64_t rc, int64_t rn, int M,
                  const float* ref_feat, const float* cand, const float* dist, const int32_t* idx,
                  int B, int Q, const float* params, float* out, void* stream);
+
+/* dvcp_dfe_tgt evaluating fc1, fc2, fc3 one after the other exactly as deep_feat_embedding.py:
+ * 48-50 chains them.  dvcp_dfe_tgt instead collapses the three linear
+ * layers into one 32 x 35 map (formed in fp64, rounded once to fp32); both agree within fp32
+ * rounding (tests/test_gpu_kernels.py). */
+int dvcp_dfe_tgt_literal(int dtype, const void* ref_xyz, int64_t rb, int64_t rc, int64_t rn, int M,
+                         const float* ref_feat, const float* cand, const float* dist,
+                         const int32_t* idx, int B, int Q, const float* params, float* out,
+                         void* stream);
 
 /* Corresponding point generation.  Replaces cpg.py:27-60: cost volume
  * (src - scrambled tgt)^2 (Q11), Conv3d 32-16-4-1 (k3, p1, no activations), softmax over C,

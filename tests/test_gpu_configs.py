@@ -123,3 +123,61 @@ def test_split_fps_vs_oracle(cuda, dtype, N, npoint, B):
     got, ctr = ops.fps(xyz.to(cuda), npoint, start.to(cuda), pdim=1)
     assert torch.equal(got.cpu(), want)
     assert torch.equal(ctr.cpu(), torch.gather(xyz, 1, want[..., None].expand(B, npoint, 3)).transpose(1, 2))
+
+
+def test_dense_fps_vs_oracle(cuda):
+    """Clouds beyond the split kernel's 16 workgroups (here fp64, 140000 points > 16 x 8192) take
+    the one-workgroup dense kernel: bit-exact against the oracle."""
+    import oracle as O
+    from dvcp import ops
+    g = torch.Generator().manual_seed(77)
+    B, N, npoint = 1, 140000, 300
+    xyz = torch.rand(B, N, 3, generator=g, dtype=torch.float64) * 2 - 1
+    start = torch.randint(0, N, (B,), generator=g)
+    got, _ = ops.fps(xyz.to(cuda), npoint, start.to(cuda), pdim=1)
+    assert torch.equal(got.cpu(), O.farthest_point_sample(xyz, npoint, start))
+
+
+def test_split_fps_guard_raises(cuda):
+    """The split FPS's bounded wait: with one workgroup of the last cloud withheld from the grid,
+    that cloud's other workgroups give up after spin_cap polls and raise the error word; their
+    indices stay in range (never -1) and the complete clouds are still exact."""
+    import ctypes
+
+    import oracle as O
+    from dvcp import _lib
+    g = torch.Generator().manual_seed(78)
+    B, N, npoint = 3, 40000, 200                       # S = 3 workgroups per fp32 cloud
+    xyz = torch.rand(B, N, 3, generator=g) * 2 - 1
+    start = torch.randint(0, N, (B,), generator=g)
+    x, st = xyz.to(cuda), start.to(cuda)
+    idx = torch.full((B, npoint), -7, dtype=torch.int64, device=cuda)
+    ws = torch.empty(B, N, dtype=torch.float32, device=cuda)
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    _lib.call("dvcp_fps_split_probe", _lib.F32, _lib.ptr(x), N * 3, 1, 3, B, N, npoint, _lib.ptr(st), _lib.ptr(idx),
+              _lib.ptr(ws), _lib.ptr(err), ctypes.c_uint32(2000), 1, _lib.stream())
+    torch.cuda.synchronize()
+    assert int(err.item()) == 1
+    got = idx.cpu()
+    assert bool(((got >= 0) & (got < N)).all())
+    want = O.farthest_point_sample(xyz[:B - 1], npoint, start[:B - 1])
+    assert torch.equal(got[:B - 1], want)
+    # the same launch with the full grid completes and leaves the word clear
+    err.zero_()
+    _lib.call("dvcp_fps_split_probe", _lib.F32, _lib.ptr(x), N * 3, 1, 3, B, N, npoint, _lib.ptr(st), _lib.ptr(idx),
+              _lib.ptr(ws), _lib.ptr(err), ctypes.c_uint32(1 << 22), 0, _lib.stream())
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    assert torch.equal(idx.cpu(), O.farthest_point_sample(xyz, npoint, start))
+
+
+def test_device_flag_check_raises(cuda):
+    """A set error word surfaces as RuntimeError from dvcp.check_device_flags (the path the split
+    FPS guard and the voxel-grid length check take)."""
+    import dvcp
+    from dvcp import _lib
+    dvcp.check_device_flags(block=True)
+    _lib.defer_flag_check("probe flag", torch.ones(1, dtype=torch.int32, device=cuda))
+    with pytest.raises(RuntimeError, match="probe flag"):
+        dvcp.check_device_flags(block=True)
+    dvcp.check_device_flags(block=True)   # reported once

@@ -186,24 +186,28 @@ def _bq_case(case, g):
         ctr[0, 5, 2] = float("nan")
         ctr[1, 600, 0] = float("-inf")
         return xyz, ctr, [(0.25, 64), (0.5, 16)]
+    if case == "untiled":
+        # above the tiled path's 16384 points: the index-order streaming kernel (C5's sa1)
+        xyz = torch.randint(-32, 33, (1, 20000, 3), generator=g).float() / 32
+        return xyz, xyz[:, :900].contiguous(), [(0.125, 64), (0.25, 256)]
     raise ValueError(case)
 
 
-@pytest.mark.parametrize("case", ["kitti", "clusters", "ragged", "boundary", "nonfinite"])
+@pytest.mark.parametrize("case", ["kitti", "clusters", "ragged", "boundary", "nonfinite", "untiled"])
 def test_ball_query_pruned_vs_oracle(cuda, case):
     """The spatially pruned fp32 ball query (tiles + per-wave candidate bitmap) against the
     oracle (pointnet2_utils.py:87-107 restated); exact where every d2 is exact (dyadic inputs),
     else only radius-boundary rounding may differ."""
     import oracle as O
     from dvcp import ops
-    g = torch.Generator().manual_seed(["kitti", "clusters", "ragged", "boundary", "nonfinite"].index(case) + 140)
+    g = torch.Generator().manual_seed(["kitti", "clusters", "ragged", "boundary", "nonfinite", "untiled"].index(case) + 140)
     xyz, ctr, radii = _bq_case(case, g)
     for r, ns in radii:
         ns = min(ns, xyz.shape[1])
         want = O.query_ball_point(r, ns, xyz, ctr)
         cnt, lst, pad = ops.ball_query(xyz.to(cuda), ctr.to(cuda), r, ns, padded=True)
         got = pad.cpu()
-        if case in ("boundary", "nonfinite"):
+        if case in ("boundary", "nonfinite", "untiled"):
             assert torch.equal(got, want), (case, r, ns)
         else:
             assert ball_mismatch_ok(xyz, ctr, got, want, r), (case, r, ns)
@@ -424,8 +428,13 @@ def test_dfe_vs_oracle(cuda):
         torch.testing.assert_close(mine(Xt.to(cuda), src=False).cpu(), ref(Xt, src=False), rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("literal", [False, True], ids=["collapsed", "literal"])
 @pytest.mark.parametrize("f64", [False, True])
-def test_dfe_tgt_fused_vs_oracle(cuda, f64):
+def test_dfe_tgt_fused_vs_oracle(cuda, f64, literal):
+    """The fused target DFE against the oracle's materialised Get_Cat_Feat_Tgt + feat_embedding_layer:
+    the default kernel collapses fc3 fc2 fc1 into one map (SURVEY App. A.3 Q14 deviation, formed in
+    fp64 and rounded once), dvcp_dfe_tgt_literal chains the three layers as written; both within
+    1e-5, the same bar."""
     import oracle as O
     import dvcp
     from dvcp import ops
@@ -446,7 +455,9 @@ def test_dfe_tgt_fused_vs_oracle(cuda, f64):
         want = dfe_ref(cat, src=False)
     qry = cand.view(B, K * C, 3).to(cuda)
     dist, idx, _ = ops.knn(ref_xyz.to(cuda), qry, 32, ref_pdim=1, qry_pdim=1)
-    got = ops.dfe_tgt(ref_xyz.to(cuda), ref_feat.to(cuda), qry, dist, idx, mine.packed_params(), ref_pdim=1)
+    got = ops.dfe_tgt(ref_xyz.to(cuda), ref_feat.to(cuda), qry, dist, idx, mine.packed_params(), ref_pdim=1,
+                      literal=literal)
+    print(f"dfe_tgt literal={literal} f64={f64}: max|err| {float((got.view(B, K, C, 32).cpu() - want).abs().max()):.2e}")
     torch.testing.assert_close(got.view(B, K, C, 32).cpu(), want, rtol=1e-5, atol=1e-5)
 
 
