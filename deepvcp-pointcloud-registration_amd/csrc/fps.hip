@@ -4,20 +4,15 @@
 // dtypes (:74, :82), distance ((dx*dx + dy*dy) + dz*dz) in the coordinate dtype (:80), strict
 // '<' update (:81), argmax = largest running minimum, ties to the LOWEST original index (:83).
 //
-// FPS is a serial chain of `npoint` dependent argmax steps per cloud, so the kernel is built
-// around the latency of one step.  One 1024-thread workgroup per cloud (16 waves):
-//   * Setup: the cloud is counting-sorted in LDS by a 12-bit Morton cell (16^3 cells), and wave
-//     w takes sorted positions [w*64*PPT, (w+1)*64*PPT): every wave owns a compact region and
-//     keeps its points, running minima and original indices in VGPRs for the whole launch.
-//   * Exact pruning: a wave skips a step when lb2(centre, wave box) >= its current max running
-//     minimum.  lb2 is computed with the same ops as a point distance on box-face coordinates,
-//     and round-to-nearest is monotone, so every point of the box then has d >= lb2 >= its
-//     running minimum: the reference's strict '<' would not update any of them.  A skipped wave
-//     re-publishes its cached best.  Late in the chain only waves near the new centre work.
-//   * One barrier per step: wave argmax by DPP (row_shr / row_bcast) + ballot tie-break, each
-//     wave publishes {value, index, x, y, z} to a double-buffered LDS slot, and every wave
-//     reduces the 16 slots with a 16-lane DPP max.  No global memory in the loop except the
-//     output stores.
+// FPS is a serial chain of `npoint` dependent argmax steps per cloud.  Kernels by cloud size:
+//   * N < 2048: fps_kernel, one centre per step (one workgroup, per-step DPP argmax + one barrier,
+//     wave-box pruning);
+//   * 2048 <= N <= 16384 (8192 fp64): fps_select_kernel, which certifies a whole prefix of the
+//     serial chain per round (~27 centres on C3 clouds) from a threshold-selected candidate list;
+//   * larger: fps_split_kernel (S workgroups per cloud exchanging one key per step), then
+//     fps_dense_kernel.
+// Every kernel keeps each cloud's coordinates and running minima in VGPRs (Morton-sorted for the
+// first two), so the loop touches no global memory except the output stores.
 #include "common.h"
 
 namespace dvcp {
@@ -91,7 +86,7 @@ struct alignas(16) FpsSlot {
 
 constexpr int kFpsThreads = 512;  // 8 waves: 2 per SIMD, up to 256 VGPRs each
 constexpr int kMortonBins = 4096;
-constexpr int kFpsProf = 8;       // timing probe words per wave (fps_kernel<..., TIMING=true>)
+constexpr int kFpsProf = 12;      // timing probe words per wave (fps_kernel<..., TIMING=true>)
 
 __device__ __forceinline__ uint32_t spread4(uint32_t v) {  // 4 bits -> every third bit
   v &= 0xF;
@@ -394,43 +389,9 @@ __global__ __launch_bounds__(THREADS) void fps_kernel(PointsView<T> pts, int N, 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Exact batched FPS (numpy model: tools/fps_lab/batched_fps_proto.py).
-//
-// Groups: 64 Morton-consecutive points (a compact box); wave w holds groups w*PPT .. w*PPT+PPT-1
-// (a compact region, so a centre's update usually concerns one or two waves).  Each group publishes
-// its best point (value desc, index asc), the second largest running minimum (an upper bound on
-// the rest of the group) and keeps its box.  Per round, wave 0 ("the walker") lists the best group
-// of each of its lanes (groups l, l+64, ...) and bounds every unlisted group by the largest
-// unlisted candidate value T.  It then accepts centres one by one:
-//   next = argmax over listed candidates of (value desc, index asc), values updated exactly by
-//          every centre accepted so far (same float formula as the point update);
-//   accept if it is the first of the round, or if its value is strictly above
-//          UB = max(T, bounds of the listed groups), each bound lowered by every accepted centre to
-//          the rounding-safe max distance from the centre to the group box.
-// A strictly larger value than every possibly-unlisted running minimum, and the argmax of the
-// listed ones, is exactly the serial FPS's next centre.  Then every wave applies the round's
-// centres to its points (wave- and group-box pruning), re-reduces the groups it touched, and
-// republishes.  Two barriers per round; rounds ~ npoint / 9 on C3 clouds.  Ties and clouds with
-// fewer points than npoint degrade to one centre per round, still exact.
-template <typename T>
-struct alignas(16) FpsGroup {
-  float cv;  // group max running minimum
-  int pid;   // its original index (lowest among equal maxima)
-  float ub;  // second largest running minimum of the group
-  float pad;
-  T x, y, z;
-};
-
-template <typename T>
-struct alignas(16) FpsCentre {
-  int pid;
-  int pad;
-  T x, y, z;
-};
-
-constexpr int kFpsMaxBatch = 64;
+// Helpers of the threshold-select kernel below.
 // Below this cloud size the one-centre-per-step kernel is faster (few groups, short steps; and
-// npoint > N tails, where every running minimum is 0, give batches of one) -- tools/fps_lab.
+// npoint > N tails, where every running minimum is 0, give rounds of one) -- tools/fps_lab.
 constexpr int kFpsBatchedMinN = 2048;
 
 template <int CTRL, int ROWS>
@@ -504,40 +465,85 @@ __device__ __forceinline__ float fps_update(float m, T px, T py, T pz, T cx, T c
   }
 }
 
-template <typename T, int PPT, bool TIMING = false, int THREADS = kFpsThreads>
-__global__ __launch_bounds__(THREADS) void fps_batched_kernel(PointsView<T> pts, int N, int npoint,
-                                                                  const int64_t* __restrict__ start,
-                                                                  int64_t* __restrict__ out_idx,
-                                                                  T* __restrict__ out_xyz,
-                                                                  unsigned long long* __restrict__ prof) {
-  constexpr int W = THREADS / kWave;
-  constexpr int G = W * PPT;               // groups
-  constexpr int GPL = (G + kWave - 1) / kWave;  // groups per walker lane
-  static_assert(PPT <= 32, "group masks are 32-bit");
-  __shared__ uint32_t bins[kMortonBins];
-  __shared__ uint16_t perm[THREADS * PPT];
+// ---------------------------------------------------------------------------------------------
+// Threshold-select FPS (the default for 2048 <= N <= 16384 fp32 / 8192 fp64 points per cloud).
+//
+// Same point layout as the batched kernel (Morton-sorted 64-point groups, slot p of wave w holds
+// sorted positions (w*PPT + p)*64 + lane, coordinates and running minima in VGPRs), but a round
+// is decided without a serial walk:
+//   1. scan: every point above a floor f is appended to an LDS list (value, position, xyz) and
+//      counted in a 256-bin histogram of its float bits over (f, vmax]; T_f = the largest
+//      running minimum at or below f (the floor adapts: raised from the histogram when more than
+//      kSelCap points lie above it, lowered when fewer than kSelMin do);
+//   2. the histogram gives a bin edge with about kSelTarget points above it: those are the
+//      listed candidates (at most kSelMax), every other point's running minimum is <= T, the
+//      largest unlisted value (exact: T_f and the list entries below the edge);
+//   3. candidates are ranked by (value desc, original index asc) -- the reference's argmax
+//      order (:83) -- and the longest prefix c_0..c_{k-1} is accepted such that for every j >= 1
+//      v_j > T and no c_i (i < j) lowers c_j's running minimum (every d(c_i, c_j) >= v_j, the
+//      same float formula as the point update).  Then c_j keeps v_j while c_0..c_{j-1} are
+//      applied, every other listed value can only have dropped (to at most v_j, ties ordered
+//      by index) and every unlisted one stays <= T < v_j, so c_j is exactly the serial FPS's
+//      j-th next centre;
+//   4. all waves apply the k accepted centres to their points (wave- and group-box pruning
+//      against each group's exact maximum, re-reduced for the groups whose minima dropped).
+// Ties beyond kSelMax points at one value (dyadic grids, npoint > N tails) fall back to one exact
+// block argmax per round.  On uniform C3 clouds a round accepts ~27 centres (~370 rounds for
+// 10000; tools/fps_lab), against ~9 for the batched walker.
+constexpr int kSelCap = 1024;    // list capacity
+constexpr int kSelBins = 256;
+constexpr int kSelTarget = 64;
+constexpr int kSelMax = 128;
+constexpr int kSelMin = 16;
+constexpr int kSelMaxScans = 8;  // rescans per round before the fallback (a guard)
+constexpr int kSelAccept = 64;   // centres accepted per round at most
+
+__device__ __forceinline__ int sel_shift(uint32_t range) {  // smallest s with (range >> s) < kSelBins
+  return range < kSelBins ? 0 : (32 - __clz(range)) - 8;
+}
+__device__ __forceinline__ float prev_float(float v) {  // largest float below v (v > 0)
+  return __uint_as_float(__float_as_uint(v) - 1u);
+}
+// wave-wide max / min of non-negative floats (as ordered bits)
+__device__ __forceinline__ float wave_fmax_nn(float v) { return float_unorder_fps(wave_umax(float_order(v))); }
+
+template <typename T, int PPT, bool TIMING = false>
+__global__ __launch_bounds__(kFpsThreads) void fps_select_kernel(PointsView<T> pts, int N, int npoint,
+                                                                 const int64_t* __restrict__ start,
+                                                                 int64_t* __restrict__ out_idx,
+                                                                 T* __restrict__ out_xyz,
+                                                                 unsigned long long* __restrict__ prof) {
+  constexpr int W = kFpsThreads / kWave;
+  static_assert(PPT <= 32 && kSelMax == 128 && kFpsThreads == 512, "layout");
+  __shared__ uint32_t bins[kMortonBins];  // setup; then the list's values [0, kSelCap) and positions
+  __shared__ uint16_t perm[kFpsThreads * PPT];
   __shared__ T red[2][3][W];
   __shared__ uint32_t wsum[W];
-  __shared__ FpsGroup<T> groups[G];
-  __shared__ T gbox[G][6];
-  __shared__ FpsCentre<T> centres[kFpsMaxBatch];
-  __shared__ int ncentre;
+  __shared__ T lx[kSelCap], ly[kSelCap], lz[kSelCap];
+  __shared__ uint32_t hist[kSelBins];
+  __shared__ __attribute__((aligned(16))) float cvv[kSelMax];
+  __shared__ __attribute__((aligned(16))) int cpid[kSelMax];
+  __shared__ __attribute__((aligned(16))) T cxx[kSelMax];
+  __shared__ __attribute__((aligned(16))) T cyy[kSelMax];
+  __shared__ __attribute__((aligned(16))) T czz[kSelMax];
+  __shared__ int prank[4][kSelMax];  // per quarter: count of preceding candidates | touched << 16
+  __shared__ float wtf[W], wT[W];
+  __shared__ uint32_t wpid[W];
+  __shared__ uint32_t na_cnt, cand_fill;
+  float* lv = reinterpret_cast<float*>(bins);
+  uint32_t* lpos = bins + kSelCap;
 
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  fps_morton_sort<T, THREADS>(pts, b, N, bins, perm, red, wsum);
+  fps_morton_sort<T, kFpsThreads>(pts, b, N, bins, perm, red, wsum);
 
-  // ---- this lane's points: slot p = sorted position (wave*PPT + p)*64 + lane -----------------
   T px[PPT], py[PPT], pz[PPT];
   float dmin[PPT];
-  T gb[6];  // lane p < PPT: box of group (wave, p)
-  T wb[6];  // the wave's box (uniform)
+  T gb[6], wb[6];  // lane p < PPT: box of group (wave, p); the wave's box (uniform)
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     gb[a] = wb[a] = static_cast<T>(__builtin_huge_val());
     gb[3 + a] = wb[3 + a] = -static_cast<T>(__builtin_huge_val());
   }
-  // Setup runs one slot at a time (uniform dynamic register indexing, s_set_gpr_idx): unrolled,
-  // every slot's loads and box reductions would be in flight together and set the VGPR peak.
 #pragma unroll 1
   for (int p = 0; p < PPT; ++p) {
     const int pos = (wave * PPT + p) * kWave + lane;
@@ -547,7 +553,7 @@ __global__ __launch_bounds__(THREADS) void fps_batched_kernel(PointsView<T> pts,
     px[p] = real ? x : static_cast<T>(0);
     py[p] = real ? y : static_cast<T>(0);
     pz[p] = real ? z : static_cast<T>(0);
-    dmin[p] = real ? 1e10f : -1.0f;  // torch.ones(B, N) * 1e10 (fp32), :74; padding: never selected
+    dmin[p] = real ? 1e10f : -1.0f;  // torch.ones(B, N) * 1e10 (fp32), :74; padding: never listed
     const T inf = static_cast<T>(__builtin_huge_val());
     T l[3] = {real ? x : inf, real ? y : inf, real ? z : inf};
     T h[3] = {real ? x : -inf, real ? y : -inf, real ? z : -inf};
@@ -563,23 +569,16 @@ __global__ __launch_bounds__(THREADS) void fps_batched_kernel(PointsView<T> pts,
       gb[a] = lane == p ? l[a] : gb[a];
       gb[3 + a] = lane == p ? h[a] : gb[3 + a];
     }
-    if (lane == 0) {
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        gbox[wave * PPT + p][a] = l[a];
-        gbox[wave * PPT + p][3 + a] = h[a];
-      }
-    }
   }
 #pragma unroll
   for (int a = 0; a < 6; ++a) wb[a] = readfirstlane_t(wb[a]);
+  const bool grp = lane < PPT && (wave * PPT + lane) * kWave < N;  // lane p: a non-empty group
 
   int64_t* oi = out_idx + static_cast<int64_t>(b) * npoint;
   T* ox = out_xyz ? out_xyz + static_cast<int64_t>(b) * 3 * npoint : nullptr;
-
-  // ---- step 0: the start point --------------------------------------------------------------
   int64_t cur = start[b];
   if (cur < 0 || cur >= N) cur = 0;  // host validates; keep the kernel in bounds regardless
+  float gub, wub, vmax;
   {
     const T cx = pts.at(b, 0, cur), cy = pts.at(b, 1, cur), cz = pts.at(b, 2, cur);
     if (tid == 0) {
@@ -590,187 +589,418 @@ __global__ __launch_bounds__(THREADS) void fps_batched_kernel(PointsView<T> pts,
         ox[2 * npoint] = cz;
       }
     }
+    float m = -1.0f;
 #pragma unroll
-    for (int p = 0; p < PPT; ++p) dmin[p] = fps_update<T>(dmin[p], px[p], py[p], pz[p], cx, cy, cz);
+    for (int p = 0; p < PPT; ++p) {
+      dmin[p] = fps_update<T>(dmin[p], px[p], py[p], pz[p], cx, cy, cz);
+      m = fmaxf(m, dmin[p]);
+    }
+    // exact group maxima (kept exact: groups whose minima drop are re-reduced after each update)
+    gub = -1.0f;
+#pragma unroll 1
+    for (int p = 0; p < PPT; ++p) {
+      const float gm = wave_fmax_nn(fmaxf(dmin[p], 0.f));
+      gub = lane == p ? gm : gub;
+    }
+    gub = grp ? gub : -1.0f;
+    wub = wave_fmax_nn(fmaxf(gub, 0.f));
+    m = wave_fmax_nn(fmaxf(m, 0.f));
+    if (lane == 0) wtf[wave] = m;
   }
-  // Groups whose candidate's running minimum changed ("dirty") are re-reduced.  A group whose
-  // candidate kept its value keeps its record: no other point can have risen above it, and its
-  // old second maximum still bounds the rest.
-  uint32_t dirty = (PPT >= 32) ? 0xFFFFFFFFu : ((1u << (PPT & 31)) - 1u);
-  float gcv = -2.0f;    // lane p < PPT: max of group (wave, p) = its candidate's running minimum
-  T gcx = 0, gcy = 0, gcz = 0;  // lane p < PPT: that candidate's coordinates
-  float wgmax = -2.0f;  // max over the wave's groups (uniform)
+  for (int i = tid; i < kSelBins; i += kFpsThreads) hist[i] = 0u;
+  if (tid == 0) {
+    na_cnt = 0u;
+    cand_fill = 0u;
+  }
+  lds_barrier();
+  vmax = wtf[0];
+#pragma unroll
+  for (int w = 1; w < W; ++w) vmax = fmaxf(vmax, wtf[w]);
+  lds_barrier();  // wtf is rewritten by the first scan
+
+  float f = 0.0f;  // floor: the first scan lists every positive value and re-derives f
   int step = 1;
-  uint64_t rounds = 0, t_walk = 0, t_update = 0, t_regroup = 0, t_barrier = 0, n_regroup = 0;
-
-  while (true) {
-    // ---- re-reduce the groups whose candidate changed and republish them ---------------------
-    uint64_t tr0 = 0;
-    if constexpr (TIMING) tr0 = fps_clock();
-    if (dirty) {
-      uint32_t dm = dirty;
-      while (dm) {  // p is wave-uniform -> indexed register access
-        const int p = __ffs(dm) - 1;
-        dm &= dm - 1;
-        {
-          const uint32_t vk = float_order(dmin[p]);
-          const uint32_t m1 = wave_umax(vk);
-          const uint64_t tied = __ballot(vk == m1);
-          int L;
-          if ((tied & (tied - 1)) == 0) {
-            L = __ffsll(static_cast<long long>(tied)) - 1;
-          } else {  // equal maxima: the lowest original index (sorted position -> index in LDS)
-            const uint32_t mypid = perm[(wave * PPT + p) * kWave + lane];
-            const uint32_t mi = wave_umin(vk == m1 ? mypid : 0xFFFFFFFFu);
-            L = __ffsll(static_cast<long long>(__ballot((vk == m1) & (mypid == mi)))) - 1;
+  unsigned long long n_round = 0, n_scan = 0, n_fallback = 0;
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};  // TIMING: scan, decide+list, rank, prefix+k, update, outputs
+  unsigned long long why[4] = {0, 0, 0, 0};       // TIMING: rescans for none above f, > cap, < kSelMin, crowded bin
+  uint64_t tp = 0;
+  auto tick = [&](int k) {
+    if constexpr (TIMING) {
+      const uint64_t t = fps_clock();
+      if (k >= 0) ph[k] += t - tp;
+      tp = t;
+    }
+  };
+  while (step < npoint) {
+    ++n_round;
+    int kstar = 0;
+    uint64_t acc0 = 0, acc1 = 0;  // accepted candidates (slots 0-63, 64-127)
+    bool raised = false;
+    for (int scan = 0;; ++scan) {
+      ++n_scan;
+      tick(-1);
+      // ---- 1. scan: list the points above f, histogram their float bits over (f, vmax] ----------
+      const uint32_t kf = __float_as_uint(f);
+      const uint32_t kv = max(__float_as_uint(vmax), kf + 1u);
+      const int shift = sel_shift(kv - kf);
+      float tf = 0.0f;
+      uint32_t nh = 0;
+#pragma unroll
+      for (int p = 0; p < PPT; ++p) {
+        const float v = dmin[p];
+        const bool hit = v > f;
+        tf = hit ? tf : fmaxf(tf, v);
+        nh += hit ? 1u : 0u;
+      }
+      // this lane's list offset: one wave scan and one LDS atomic per wave
+      uint32_t incl = nh;
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t u = __shfl_up(incl, off, kWave);
+        incl += lane >= off ? u : 0u;
+      }
+      const uint32_t wtot = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
+      uint32_t wbase = 0;
+      if (wtot) {
+        if (lane == 0) wbase = atomicAdd(&na_cnt, wtot);
+        wbase = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(wbase)));
+      }
+      uint32_t li = wbase + incl - nh;
+#pragma unroll
+      for (int p = 0; p < PPT; ++p) {
+        const float v = dmin[p];
+        const bool hit = v > f;
+        if (__ballot(hit)) {
+          if (hit) {
+            const uint32_t bin = min((__float_as_uint(v) - kf) >> shift, static_cast<uint32_t>(kSelBins - 1));
+            atomicAdd(&hist[bin], 1u);
+            if (li < kSelCap) {
+              lv[li] = v;
+              lpos[li] = static_cast<uint32_t>((wave * PPT + p) * kWave + lane);
+              lx[li] = px[p];
+              ly[li] = py[p];
+              lz[li] = pz[p];
+            }
+            ++li;
           }
-          const uint32_t m2 = wave_umax(lane == L ? 0u : vk);
-          const float cv = float_unorder_fps(m1);
-          FpsGroup<T> g;
-          g.cv = cv;
-          g.pid = perm[(wave * PPT + p) * kWave + L];
-          g.ub = float_unorder_fps(m2);
-          g.pad = 0.f;
-          g.x = readlane_t(px[p], L);
-          g.y = readlane_t(py[p], L);
-          g.z = readlane_t(pz[p], L);
-          if (lane == 0) groups[wave * PPT + p] = g;
-          gcv = lane == p ? cv : gcv;
-          gcx = lane == p ? g.x : gcx;
-          gcy = lane == p ? g.y : gcy;
-          gcz = lane == p ? g.z : gcz;
-          if constexpr (TIMING) ++n_regroup;
-          __builtin_amdgcn_sched_barrier(0);
         }
       }
-      wgmax = float_unorder_fps(wave_umax(lane < PPT ? float_order(gcv) : 0u));
-    }
-    uint64_t tr1 = 0;
-    if constexpr (TIMING) tr1 = fps_clock();
-    lds_barrier();
-    if constexpr (TIMING) {
-      const uint64_t tr2 = fps_clock();
-      t_regroup += tr1 - tr0;
-      t_barrier += tr2 - tr1;
-    }
-    if (step >= npoint) break;
-
-    // ---- the walk (wave 0) ---------------------------------------------------------------
-    uint64_t tw0 = 0;
-    if constexpr (TIMING) tw0 = fps_clock();
-    if (wave == 0) {
-      // this lane's listed group: its best of groups lane, lane+64, ... ; T over the others
-      int mg = -1;
-      uint32_t mk = 0, mpid = 0xFFFFFFFFu, tk = 0;
+      tf = wave_fmax_nn(tf);
+      if (lane == 0) wtf[wave] = tf;
+      lds_barrier();
+      tick(0);
+      // ---- 2. decide (every wave computes the same decision from LDS) -------------------------
+      const uint32_t na = na_cnt;
+      float Tf = wtf[0];
 #pragma unroll
-      for (int k = 0; k < GPL; ++k) {
-        const int g = k * kWave + lane;
-        if (g < G) {
-          const uint32_t key = float_order(groups[g].cv);
-          const uint32_t gp = static_cast<uint32_t>(groups[g].pid);
-          const bool better = (mg < 0) | (key > mk) | ((key == mk) & (gp < mpid));
-          const uint32_t loser = better ? mk : key;
-          tk = (mg >= 0) ? max(tk, loser) : tk;
-          mk = better ? key : mk;
-          mpid = better ? gp : mpid;
-          mg = better ? g : mg;
+      for (int w = 1; w < W; ++w) Tf = fmaxf(Tf, wtf[w]);
+      // suffix counts: lane l holds bins 4l .. 4l+3; suf(k) = hits in bins >= k
+      uint32_t h[4], hs[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) h[k] = hist[4 * lane + k];
+      hs[3] = h[3];
+      hs[2] = h[2] + hs[3];
+      hs[1] = h[1] + hs[2];
+      hs[0] = h[0] + hs[1];
+      uint32_t above = 0;  // hits in lanes > this lane
+      {
+        uint32_t incl = hs[0];
+        for (int off = 1; off < 64; off <<= 1) {
+          const uint32_t u = __shfl_down(incl, off, kWave);
+          incl += (lane + off < 64) ? u : 0u;
         }
+        above = incl - hs[0];
       }
-      const uint32_t T_all = wave_umax(tk);
-      bool alive = mg >= 0;
-      float cv = alive ? float_unorder_fps(mk) : -3.0f;
-      float ub = alive ? groups[mg].ub : -3.0f;
-      T gx = 0, gy = 0, gz = 0, bx[6];
+      // the largest bin k with suf(k) >= need (suf is non-increasing in k)
+      auto last_bin_at_least = [&](uint32_t need) -> int {
+        int best = -1;
 #pragma unroll
-      for (int a = 0; a < 6; ++a) bx[a] = alive ? gbox[mg][a] : static_cast<T>(0);
-      if (alive) {
-        gx = groups[mg].x;
-        gy = groups[mg].y;
-        gz = groups[mg].z;
-      }
-      const int listed_pid = static_cast<int>(mpid);
-      int acc = 0;
-      int a_pid = 0;
-      T a_x = 0, a_y = 0, a_z = 0;
-      while (step + acc < npoint && acc < kFpsMaxBatch) {
-        const uint32_t key = alive ? float_order(cv) : 0u;
-        uint32_t km, umax;
-        wave_umax2(key, mg >= 0 ? float_order(ub) : 0u, km, umax);
-        if (acc > 0 && !(km > max(T_all, umax))) break;
-        const uint64_t tied = __ballot(alive & (key == km));
-        int j;
-        if ((tied & (tied - 1)) == 0) {
-          j = __ffsll(static_cast<long long>(tied)) - 1;
+        for (int k = 0; k < 4; ++k) best = (hs[k] + above >= need) ? 4 * lane + k : best;
+        return static_cast<int>(wave_umax(static_cast<uint32_t>(best + 1))) - 1;
+      };
+      auto suf_of = [&](int bin) -> uint32_t {  // suf(bin), uniform bin
+        const int L = bin >> 2, k = bin & 3;
+        const uint32_t mine = (k == 0 ? hs[0] : k == 1 ? hs[1] : k == 2 ? hs[2] : hs[3]) + above;
+        return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(mine), L));
+      };
+      int mode = 0;  // 0: select, 1: rescan with the new f, 2: fallback (one exact argmax)
+      int bsel = 0;
+      if (scan >= kSelMaxScans) {
+        mode = 2;
+      } else if (na == 0) {
+        if (Tf > 0.0f) {
+          f = prev_float(Tf);
+          mode = 1;
+          ++why[0];
         } else {
-          const uint32_t mi = wave_umin((alive & (key == km)) ? static_cast<uint32_t>(listed_pid) : 0xFFFFFFFFu);
-          j = __ffsll(static_cast<long long>(__ballot(alive & (key == km) & (static_cast<uint32_t>(listed_pid) == mi)))) - 1;
+          mode = 2;
         }
-        const int cpid = __builtin_amdgcn_readlane(listed_pid, j);
-        const T cx = readlane_t(gx, j), cy = readlane_t(gy, j), cz = readlane_t(gz, j);
-        const bool mine = lane == acc;  // lane acc keeps the acc-th accepted centre (selects, no exec branch)
-        a_pid = mine ? cpid : a_pid;
-        a_x = mine ? cx : a_x;
-        a_y = mine ? cy : a_y;
-        a_z = mine ? cz : a_z;
-        alive = alive & (lane != j);
-        cv = fps_update<T>(cv, gx, gy, gz, cx, cy, cz);
-        const float u2 = static_cast<float>(box_ub2<T>(cx, cy, cz, bx));
-        ub = u2 < ub ? u2 : ub;
-        ++acc;
-      }
-      if (lane < acc) {
-        centres[lane] = FpsCentre<T>{a_pid, 0, a_x, a_y, a_z};
-        oi[step + lane] = a_pid;
-        if (ox) {
-          ox[step + lane] = a_x;
-          ox[npoint + step + lane] = a_y;
-          ox[2 * npoint + step + lane] = a_z;
+      } else {
+        // highest non-empty bin: values lie below its upper edge, a tighter vmax for a rescan
+        const int top = last_bin_at_least(1);
+        auto tighten = [&]() {
+          if (top < kSelBins - 1) vmax = fminf(vmax, __uint_as_float(kf + (static_cast<uint32_t>(top + 1) << shift)));
+        };
+        auto edge_below = [&](int bin) {  // the f that lists exactly bins >= bin
+          return __uint_as_float(kf + (static_cast<uint32_t>(bin) << shift) - 1u);
+        };
+        if (na > static_cast<uint32_t>(kSelCap)) {
+          int bb = max(0, last_bin_at_least(4 * kSelTarget));
+          while (bb + 1 < kSelBins && suf_of(bb) > static_cast<uint32_t>(kSelCap) && suf_of(bb + 1) > 0u) ++bb;
+          if (shift == 0 && suf_of(bb) > static_cast<uint32_t>(kSelCap)) {
+            mode = 2;  // more than kSelCap points share one value
+          } else {
+            if (bb > 0) f = edge_below(bb);
+            tighten();
+            mode = 1;
+            raised = true;
+            ++why[1];
+          }
+        } else if (na < static_cast<uint32_t>(kSelMin) && Tf > 0.0f && !raised) {
+          f = fminf(f * 0.5f, prev_float(Tf));
+          mode = 1;
+          ++why[2];
+        } else {
+          bsel = max(0, last_bin_at_least(min(static_cast<uint32_t>(kSelTarget), na)));
+          while (bsel + 1 < kSelBins && suf_of(bsel) > static_cast<uint32_t>(kSelMax) && suf_of(bsel + 1) > 0u) ++bsel;
+          if (suf_of(bsel) > static_cast<uint32_t>(kSelMax)) {  // a crowded top bin
+            if (shift == 0) {
+              mode = 2;
+            } else {
+              if (bsel > 0) f = edge_below(bsel);
+              tighten();
+              mode = 1;
+              raised = true;
+              ++why[3];
+            }
+          }
         }
       }
-      if (lane == 0) ncentre = acc;
+      if (mode == 1) {  // rescan: everyone has read hist / na / wtf; clear them
+        lds_barrier();
+        for (int i = tid; i < kSelBins; i += kFpsThreads) hist[i] = 0u;
+        if (tid == 0) na_cnt = 0u;
+        lds_barrier();
+        continue;
+      }
+      if (mode == 2) {
+        // ---- fallback: one exact argmax (value desc, original index asc) over every point ------
+        ++n_fallback;
+        float bv = -1.0f;
+#pragma unroll
+        for (int p = 0; p < PPT; ++p) bv = fmaxf(bv, dmin[p]);
+        bv = wave_fmax_nn(fmaxf(bv, 0.f));
+        lds_barrier();  // (wtf / hist reads above are done)
+        if (lane == 0) wtf[wave] = bv;
+        for (int i = tid; i < kSelBins; i += kFpsThreads) hist[i] = 0u;
+        if (tid == 0) na_cnt = 0u;
+        lds_barrier();
+        float gmax = wtf[0];
+#pragma unroll
+        for (int w = 1; w < W; ++w) gmax = fmaxf(gmax, wtf[w]);
+        uint32_t mp = 0xFFFFFFFFu;
+#pragma unroll
+        for (int p = 0; p < PPT; ++p) {
+          const int pos = (wave * PPT + p) * kWave + lane;
+          if (__ballot(dmin[p] == gmax)) {
+            if (dmin[p] == gmax) mp = min(mp, static_cast<uint32_t>(perm[pos]));
+          }
+        }
+        mp = wave_umin(mp);
+        if (lane == 0) wpid[wave] = mp;
+        lds_barrier();
+        uint32_t gp = wpid[0];
+#pragma unroll
+        for (int w = 1; w < W; ++w) gp = min(gp, wpid[w]);
+        if (tid == 0) {
+          const T gx = pts.at(b, 0, gp), gy = pts.at(b, 1, gp), gz = pts.at(b, 2, gp);
+          cxx[0] = gx;
+          cyy[0] = gy;
+          czz[0] = gz;
+          oi[step] = static_cast<int64_t>(gp);
+          if (ox) {
+            ox[step] = gx;
+            ox[npoint + step] = gy;
+            ox[2 * npoint + step] = gz;
+          }
+        }
+        lds_barrier();
+        kstar = 1;
+        acc0 = 1ull;
+        acc1 = 0ull;
+        vmax = gmax;  // every value is <= gmax; the new centre's drops to 0
+        break;
+      }
+      // ---- 3. list: entries in bins >= bsel are the candidates; T over the rest ---------------
+      const int cnt = static_cast<int>(suf_of(bsel));
+      float tl = Tf;
+      for (int i = wave * (kSelCap / W) + lane; i < (wave + 1) * (kSelCap / W); i += kWave) {
+        const bool live = i < static_cast<int>(na);
+        const float v = live ? lv[i] : 0.0f;
+        const bool in = live && static_cast<int>(min((__float_as_uint(v) - kf) >> shift,
+                                                     static_cast<uint32_t>(kSelBins - 1))) >= bsel;
+        tl = (live && !in) ? fmaxf(tl, v) : tl;
+        const uint64_t m = __ballot(in);
+        if (m) {
+          const int first = __ffsll(static_cast<long long>(m)) - 1;
+          uint32_t base = 0;
+          if (lane == first) base = atomicAdd(&cand_fill, static_cast<uint32_t>(__popcll(m)));
+          base = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(base), first));
+          const uint32_t o = base + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0));
+          if (in) {
+            cvv[o] = v;
+            cpid[o] = static_cast<int>(perm[lpos[i]]);
+            cxx[o] = lx[i];
+            cyy[o] = ly[i];
+            czz[o] = lz[i];
+          }
+        }
+      }
+      tl = wave_fmax_nn(tl);
+      if (lane == 0) wT[wave] = tl;
+      if (na < 4u * kSelTarget) f *= 0.85f;  // next round: keep a few hundred points above the floor
+      lds_barrier();
+      float Tb = wT[0];
+#pragma unroll
+      for (int w = 1; w < W; ++w) Tb = fmaxf(Tb, wT[w]);
+      if (tid == 0) {
+        na_cnt = 0u;
+        cand_fill = 0u;
+      }
+      for (int i = tid; i < kSelBins; i += kFpsThreads) hist[i] = 0u;
+      tick(1);
+      // ---- 4. rank and prefix test in one pass over candidate pairs ----------------------------
+      // c_i precedes c_j (value desc, index asc) iff beats(i, j); rank_j = #{i : beats(i, j)}; c_j
+      // is "touched" if some c_i preceding it lowers its running minimum (d(c_i, c_j) < v_j, the
+      // point update's formula).  Thread (j, q) covers i in [32q, 32q + 32), four candidates per
+      // 16-byte LDS read of each array.
+      const int j = tid & (kSelMax - 1), q = tid >> 7;
+      if (j < cnt) {
+        const float vj = cvv[j];
+        const int pj = cpid[j];
+        const T xj = cxx[j], yj = cyy[j], zj = czz[j];
+        int r = 0, touched = 0;
+#pragma unroll 2
+        for (int c4 = 0; c4 < 8; ++c4) {
+          const int i0 = q * 32 + 4 * c4;
+          const float4 v4 = *reinterpret_cast<const float4*>(&cvv[i0]);
+          const int4 p4 = *reinterpret_cast<const int4*>(&cpid[i0]);
+          const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
+          const int pp[4] = {p4.x, p4.y, p4.z, p4.w};
+          T xx[4], yy[4], zz[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            xx[k] = cxx[i0 + k];
+            yy[k] = cyy[i0 + k];
+            zz[k] = czz[i0 + k];
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const bool bt = (i0 + k < cnt) & ((vv[k] > vj) | ((vv[k] == vj) & (pp[k] < pj)));
+            const T dx = xj - xx[k], dy = yj - yy[k], dz = zj - zz[k];
+            const T d = (dx * dx + dy * dy) + dz * dz;
+            r += bt ? 1 : 0;
+            touched |= (bt & (d < static_cast<T>(vj))) ? 1 : 0;
+          }
+        }
+        prank[q][j] = r | (touched << 16);
+      }
+      lds_barrier();
+      tick(2);
+      // ---- 5. k = the smallest rank that fails; accepted = ranks < k (every wave, redundantly) ----
+      const int left = npoint - step;
+      int rk[2];
+      uint32_t failr = 0xFFFFFFFFu;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int jj = hh * 64 + lane;
+        rk[hh] = 0x7FFFFFFF;
+        if (jj < cnt) {
+          const int w0 = prank[0][jj], w1 = prank[1][jj], w2 = prank[2][jj], w3 = prank[3][jj];
+          const int r = (w0 & 0xFFFF) + (w1 & 0xFFFF) + (w2 & 0xFFFF) + (w3 & 0xFFFF);
+          const bool touched = ((w0 | w1 | w2 | w3) >> 16) != 0;
+          rk[hh] = r;
+          const bool fail = r >= left || (r > 0 && (touched || !(cvv[jj] > Tb)));
+          failr = fail ? min(failr, static_cast<uint32_t>(r)) : failr;
+        }
+      }
+      kstar = static_cast<int>(min(min(wave_umin(failr), static_cast<uint32_t>(cnt)),
+                                   static_cast<uint32_t>(kSelAccept)));
+      acc0 = __ballot(rk[0] < kstar);
+      acc1 = __ballot(rk[1] < kstar);
+      // upper bound of every running minimum after this round: T, and the listed not accepted
+      float vm = Tb;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int jj = hh * 64 + lane;
+        vm = (jj < cnt && rk[hh] >= kstar) ? fmaxf(vm, cvv[jj]) : vm;
+      }
+      if (wave == 0) {  // outputs in rank order
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int jj = hh * 64 + lane;
+          if (rk[hh] < kstar) {
+            oi[step + rk[hh]] = cpid[jj];
+            if (ox) {
+              ox[step + rk[hh]] = cxx[jj];
+              ox[npoint + step + rk[hh]] = cyy[jj];
+              ox[2 * npoint + step + rk[hh]] = czz[jj];
+            }
+          }
+        }
+      }
+      vmax = wave_fmax_nn(fmaxf(vm, 0.f));
+      tick(3);
+      break;
     }
-    lds_barrier();
-    uint64_t tw1 = 0;
-    if constexpr (TIMING) tw1 = fps_clock();
-
-    // ---- apply the round's centres ---------------------------------------------------------
-    const int nc = ncentre;
-    step += nc;
-    ++rounds;
-    const FpsCentre<T> mc = centres[lane < nc ? lane : 0];
-    dirty = 0u;
-    // centres that can lower some running minimum of this wave: one vector test, lane i = centre i
-    uint64_t rel = __ballot((lane < nc) & !(box_lb2(mc.x, mc.y, mc.z, wb) >= static_cast<T>(wgmax)));
-    while (rel) {
-      const int i = __ffsll(static_cast<long long>(rel)) - 1;
-      rel &= rel - 1;
-      const T cx = readlane_t(mc.x, i), cy = readlane_t(mc.y, i), cz = readlane_t(mc.z, i);
-      const bool grp = lane < PPT;
-      uint32_t m = static_cast<uint32_t>(__ballot(grp & !(box_lb2(cx, cy, cz, gb) >= static_cast<T>(gcv))));
-      // the candidate itself drops exactly when the point update would lower it (same formula)
-      dirty |= static_cast<uint32_t>(__ballot(grp & (fps_update<T>(gcv, gcx, gcy, gcz, cx, cy, cz) != gcv)));
-      while (m) {  // touched slots only; p is wave-uniform -> indexed register access
-        const int p = __ffs(m) - 1;
-        m &= m - 1;
-        dmin[p] = fps_update<T>(dmin[p], px[p], py[p], pz[p], cx, cy, cz);
+    // ---- the update: apply the accepted centres ----------------------------------------------
+    tick(-1);
+    uint32_t dirty = 0u;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const uint64_t am = hh ? acc1 : acc0;
+      if (!am) continue;
+      const int i = hh * 64 + lane;
+      const bool live = (am >> lane) & 1ull;
+      const T mx = live ? cxx[i] : static_cast<T>(0), my = live ? cyy[i] : static_cast<T>(0),
+              mz = live ? czz[i] : static_cast<T>(0);
+      uint64_t rel = __ballot(live && !(box_lb2(mx, my, mz, wb) >= static_cast<T>(wub)));
+      while (rel) {
+        const int k = __ffsll(static_cast<long long>(rel)) - 1;
+        rel &= rel - 1;
+        const T cx = readlane_t(mx, k), cy = readlane_t(my, k), cz = readlane_t(mz, k);
+        uint32_t m = static_cast<uint32_t>(__ballot(grp && !(box_lb2(cx, cy, cz, gb) >= static_cast<T>(gub))));
+        dirty |= m;
+        while (m) {  // touched slots only; p is wave-uniform -> indexed register access
+          const int p = __ffs(m) - 1;
+          m &= m - 1;
+          dmin[p] = fps_update<T>(dmin[p], px[p], py[p], pz[p], cx, cy, cz);
+        }
       }
     }
-    if constexpr (TIMING) {
-      t_walk += tw1 - tw0;
-      t_update += fps_clock() - tw1;
+    // re-reduce the touched groups whose maximum point dropped (values only drop: a group keeps
+    // its maximum while some point still holds it)
+    while (dirty) {
+      const int p = __ffs(dirty) - 1;
+      dirty &= dirty - 1;
+      const float gp = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gub), p));
+      if (!__ballot(dmin[p] == gp)) {
+        const float gm = wave_fmax_nn(fmaxf(dmin[p], 0.f));
+        gub = lane == p ? gm : gub;
+      }
     }
+    wub = wave_fmax_nn(fmaxf(gub, 0.f));
+    tick(4);
+    step += kstar;
   }
   if constexpr (TIMING) {
-    if (prof && lane == 0) {
+    if (prof && lane == 0) {  // per wave: [rounds, scans, fallbacks, clk: scan, decide+list, rank, prefix, update]
       unsigned long long* o = prof + (static_cast<int64_t>(b) * W + wave) * kFpsProf;
-      o[0] = t_walk;
-      o[1] = t_update;
-      o[2] = rounds;
-      o[3] = t_regroup;
-      o[4] = t_barrier;
-      o[5] = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
-      o[6] = n_regroup;
-      o[7] = 0;
+      o[0] = n_round;
+      o[1] = n_scan;
+      o[2] = n_fallback;
+      for (int k = 0; k < 5; ++k) o[3 + k] = ph[k];
+      for (int k = 0; k < 4; ++k) o[8 + k] = why[k];
     }
   }
 }
@@ -1037,11 +1267,11 @@ static int launch_fps(const T* xyz, int64_t sb, int64_t sc, int64_t sn, int B, i
   PointsView<T> v{xyz, sb, sc, sn};
   const int ppt = ceil_div(N, kFpsThreads);
   dim3 grid(B), block(kFpsThreads);
-  // batched kernel from 2048 points; below, the one-centre-per-step kernel (box-pruned)
+  // threshold-select kernel from 2048 points; below, the one-centre-per-step kernel (box-pruned)
 #define DVCP_FPS_CASE(P)                                                                                   \
   if (ppt <= P) {                                                                                          \
     if (N >= kFpsBatchedMinN)                                                                              \
-      hipLaunchKernelGGL((fps_batched_kernel<T, P>), grid, block, 0, st, v, N, npoint, start, out_idx, out_xyz, \
+      hipLaunchKernelGGL((fps_select_kernel<T, P>), grid, block, 0, st, v, N, npoint, start, out_idx, out_xyz, \
                          nullptr);                                                                         \
     else                                                                                                   \
       hipLaunchKernelGGL((fps_kernel<T, kFpsThreads, P, true>), grid, block, 0, st, v, N, npoint, start,        \

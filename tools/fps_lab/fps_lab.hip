@@ -60,8 +60,8 @@ struct Config {
 };
 
 #define CFG(T, P, PR, TM, NAME) Config{NAME, dvcp::fps_kernel<float, T, P, PR, TM>, T, P, TM}
-#define BAT(P, NAME) Config{NAME, dvcp::fps_batched_kernel<float, P, false>, 512, P, false}
-#define BATT(P, NAME) Config{NAME, dvcp::fps_batched_kernel<float, P, true>, 512, P, true}
+#define SEL(P, NAME) Config{NAME, dvcp::fps_select_kernel<float, P, false>, 512, P, false}
+#define SELT(P, NAME) Config{NAME, dvcp::fps_select_kernel<float, P, true>, 512, P, true}
 
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 16;
@@ -94,11 +94,10 @@ int main(int argc, char** argv) {
   const PointsView<float> view{dx, 3LL * N, N, 1};
 
   const std::vector<Config> cfgs = {
-      BAT(32, "batched 512x32"),
-      BATT(32, "batched 512x32 +timing"),
-      BAT(24, "batched 512x24"),
-      BAT(16, "batched 512x16"),
-      BAT(2, "batched 512x2"),
+      SEL(32, "select 512x32"),
+      SELT(32, "select 512x32 +stats"),
+      SEL(24, "select 512x24"),
+      SEL(20, "select 512x20"),
       CFG(512, 32, true, false, "v3 512x32 prune"),
       CFG(512, 32, true, true, "v3 512x32 prune +timing"),
       CFG(512, 32, false, false, "v3 512x32 noprune"),
@@ -130,17 +129,17 @@ int main(int argc, char** argv) {
       for (int s = 0; s < npoint; ++s) bad += got[static_cast<size_t>(b) * npoint + s] != want[b][s];
     printf("%-28s B %3d N %6d npoint %6d  %8.3f ms  %6.3f us/step  mismatches %d\n", c.name, B, N, npoint, best,
            1e3f * best / npoint, bad);
-    if (c.timing && c.fn == reinterpret_cast<KernelFn>(dvcp::fps_batched_kernel<float, 32, true>)) {
-      const unsigned long long* o = &pr_dummy[0];
-      (void)o;
+    if (c.timing && c.fn == reinterpret_cast<KernelFn>(dvcp::fps_select_kernel<float, 32, true>)) {
       std::vector<unsigned long long> pr(prof_words);
       CK(hipMemcpy(pr.data(), dprof, pr.size() * 8, hipMemcpyDeviceToHost));
+      printf("   cloud 0: rounds %llu  scans %llu  fallbacks %llu  centres/round %.1f  rescans: none-above %llu "
+             "over-cap %llu under-min %llu crowded %llu\n", pr[0], pr[1], pr[2],
+             pr[0] ? double(npoint - 1) / pr[0] : 0.0, pr[8], pr[9], pr[10], pr[11]);
       for (int w = 0; w < 8; ++w) {
-        const unsigned long long* q = &pr[static_cast<size_t>(w) * dvcp::kFpsProf];  // cloud 0
-        const double r = q[2] ? double(q[2]) : 1.0;
-        printf("   wave %d: rounds %llu  regroup %.0f  barrierA %.0f  walk+barrierB %.0f  update %.0f clk/round  "
-               "regroups/round %.2f\n",
-               w, q[2], q[3] / r, q[4] / r, q[0] / r, q[1] / r, q[6] / r);
+        const unsigned long long* q = &pr[static_cast<size_t>(w) * dvcp::kFpsProf];
+        const double r = q[0] ? double(q[0]) : 1.0;
+        printf("   wave %d clk/round: scan %.0f  decide+list %.0f  rank %.0f  prefix %.0f  update %.0f\n", w,
+               q[3] / r, q[4] / r, q[5] / r, q[6] / r, q[7] / r);
       }
     } else if (c.timing) {
       const int W = c.threads / 64;
