@@ -53,6 +53,9 @@ SIGNATURES = {
     "dvcp_dfe_tgt_backward": [_I, _P, _L, _L, _L, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P],
     "dvcp_src_keypoints_backward": [_I, _P, _I, _P, _I, _I, _P, _D, _I, _P, _P, _P],
     "dvcp_cpg_backward": [_P, _P, _L, _L, _L, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+    "dvcp_sa_group_mlp_backward": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _L, _L, _L, _I,
+                                   _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P],
+    "dvcp_fe_head_backward": [_P, _I, _P, _P, _P, _P, _P, _P],
 }
 
 _lib = None
@@ -85,6 +88,11 @@ def load():
     lib.dvcp_dfe_backward_workspace_bytes.argtypes = [ctypes.c_int64]
     lib.dvcp_cpg_backward_workspace_bytes.restype = ctypes.c_int64
     lib.dvcp_cpg_backward_workspace_bytes.argtypes = [ctypes.c_int]
+    lib.dvcp_sa_group_mlp_backward_workspace_bytes.restype = ctypes.c_int64
+    lib.dvcp_sa_group_mlp_backward_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                               ctypes.c_void_p]
+    lib.dvcp_fe_head_backward_workspace_bytes.restype = ctypes.c_int64
+    lib.dvcp_fe_head_backward_workspace_bytes.argtypes = [ctypes.c_int]
     for name, args in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = ctypes.c_int
@@ -97,7 +105,8 @@ def exported_symbols():
     return ["dvcp_last_error", "dvcp_abi_version", "dvcp_knn_grid_workspace_bytes",
             "dvcp_knn_tiled_workspace_bytes", "dvcp_ball_query_workspace_bytes",
             "dvcp_sa_group_mlp_workspace_bytes", "dvcp_dfe_backward_workspace_bytes",
-            "dvcp_cpg_backward_workspace_bytes"] + list(SIGNATURES)
+            "dvcp_cpg_backward_workspace_bytes", "dvcp_sa_group_mlp_backward_workspace_bytes",
+            "dvcp_fe_head_backward_workspace_bytes"] + list(SIGNATURES)
 
 
 # When a list, every entry-point call appends (name, start_event, end_event, work) recorded on

@@ -14,12 +14,17 @@ feature extractor.  Here the head's backward runs in hand-written HIP kernels:
   * ``src_keypoints`` -- the key-point stage, differentiable in the source features (the
                       pointnet2_utils.py:59 gather, dvcp_src_keypoints_backward).
 
+  * ``feat_extraction`` -- the feature extractor (deep_feat_extraction.py:18-32 + REF-R R1) with
+                      its BatchNorm layers in eval mode (frozen-BN training: FE1.eval() with trainable
+                      parameters): fc (dvcp_fe_head_backward) and the three set-abstraction MLPs
+                      (dvcp_sa_group_mlp_backward), chained through the FPS-order gathers and the
+                      ball-query groupings.
+
 The key points, candidates and kNN indices carry no gradient in the reference either (index
 ops, knn_cuda under no_grad); the weighting layer gets none (only its top-k indices are used).
-The feature extractor must be frozen (eval BN, requires_grad False): its backward (batch-
-statistics BN + set-abstraction backward) is not implemented, and DeepVCP.forward raises
-rather than silently dropping its gradient.  Parameter gradients come back summed over the
-batch in a fixed order (deterministic).
+A feature extractor in training mode (batch-statistics BN) is not implemented: DeepVCP.forward
+raises rather than silently computing something else.  Parameter gradients come back summed over
+the batch in a fixed order (deterministic); the feature scatters use float atomics.
 """
 import torch
 
@@ -132,6 +137,80 @@ class _PoseLoss(torch.autograd.Function):
         x, y, Rt, tt, partial = ctx.saved_tensors
         gy = ops.svd_optimization_backward(x, y, Rt, tt, partial, g_loss, ctx.alpha)
         return None, gy.to(ctx.y_dtype), None, None, None
+
+
+def _fe_params(fe):
+    """FE1's trainable tensors in a fixed order: per SA layer (conv.weight, conv.bias, bn.weight,
+    bn.bias) per MLP layer, then fc.weight, fc.bias."""
+    out = []
+    for sa in (fe.sa1, fe.sa2, fe.sa3):
+        for conv, bn in zip(sa.mlp_convs, sa.mlp_bns):
+            out += [conv.weight, conv.bias, bn.weight, bn.bias]
+    return out + [fe.fc.weight, fe.fc.bias]
+
+
+def _bn_stats(sa):
+    """Per MLP layer: running_mean | 1 / sqrt(running_var + eps) (fp32), the eval-mode BN's
+    normalisation for the gamma gradient."""
+    parts = []
+    for bn in sa.mlp_bns:
+        parts += [bn.running_mean.float(), torch.rsqrt(bn.running_var.double() + bn.eps).float()]
+    return torch.cat(parts).contiguous()
+
+
+def _scatter_rows(g, idx, n):
+    """The backward of gathering per-point rows by FPS indices: (B, S, C) -> (B, n, C)."""
+    out = torch.zeros(g.shape[0], n, g.shape[2], dtype=torch.float32, device=g.device)
+    return out.scatter_add_(1, idx.unsqueeze(-1).expand(-1, -1, g.shape[2]), g.float())
+
+
+class _FeatExtract(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, fe, pts, starts, wl, side_stream, *params):
+        saved = {}
+        xyz, feat, score = fe.run(pts, starts, wl=wl, side_stream=side_stream, saved=saved)
+        ctx.fe, ctx.saved = fe, saved
+        ctx.shapes = [(p.shape, p.dtype) for p in params]
+        ctx.mark_non_differentiable(xyz)
+        if score is not None:
+            ctx.mark_non_differentiable(score)
+        return xyz, feat, score
+
+    @staticmethod
+    def backward(ctx, g_xyz, g_feat, g_score):
+        fe, saved = ctx.fe, ctx.saved
+        grads = []
+        if g_feat is None:
+            return (None,) * 5 + tuple(None for _ in ctx.shapes)
+        B, S, _ = g_feat.shape
+        gp_fc, g = ops.fe_head_backward(saved["f3"], fe.fc_params(), g_feat.reshape(B * S, 32))
+        g = g.view(B, S, 64)
+        per_layer = []
+        for sa, lay in reversed(list(zip((fe.sa1, fe.sa2, fe.sa3), saved["layers"]))):
+            n_l = lay["pts"].shape[2]
+            g_out = _scatter_rows(g, lay["idx"], n_l) if lay["per_point"] else g
+            first = sa is fe.sa1
+            gp, g_in = ops.sa_group_mlp_backward(lay["pts"], lay["ctr"], lay["feat"], lay["count"], lay["lst"],
+                                                 lay["ns"], sa.chans, sa.packed_params(), _bn_stats(sa), g_out,
+                                                 want_feat_grad=not first)
+            per_layer.append((sa, gp))
+            g = g_in  # (B, n_l, D): the previous layer's outputs, in its centre order
+        for sa, gp in reversed(per_layer):
+            o = 0
+            for conv, bn in zip(sa.mlp_convs, sa.mlp_bns):
+                co, ci = conv.weight.shape[0], conv.weight.shape[1]
+                grads += [gp[o:o + co * ci].view(conv.weight.shape), gp[o + co * ci:o + co * ci + co],
+                          gp[o + co * ci + co:o + co * ci + 2 * co], gp[o + co * ci + 2 * co:o + co * ci + 3 * co]]
+                o += co * ci + 3 * co
+        grads += [gp_fc[:32 * 64].view(32, 64), gp_fc[32 * 64:]]
+        ctx.saved = None
+        out = [gr.to(dt) if ctx.needs_input_grad[5 + k] else None for k, (gr, (_, dt)) in enumerate(zip(grads, ctx.shapes))]
+        return (None, None, None, None, None, *out)
+
+
+def feat_extraction(fe, pts, starts, wl=None, side_stream=None):
+    """FE1.run differentiable in FE1's parameters (eval-mode BN): -> (xyz, feat, score)."""
+    return _FeatExtract.apply(fe, pts, starts, wl, side_stream, *_fe_params(fe))
 
 
 def dfe_rows(X, dfe_module):

@@ -44,23 +44,28 @@ class DeepVCP(nn.Module):
             cache[key] = torch.cuda.Stream(device=dev)
         return cache[key]
 
-    def _head_training(self):
-        """Whether this forward records autograd for the head (train.py:105-125 with the feature
-        extractor frozen).  The head (DFE, CPG) is differentiated when autograd is on and its
-        parameters require gradients; the feature extractor has no backward here, so it must be
-        frozen then (eval mode, requires_grad False), and a module left in training mode otherwise
-        raises instead of silently dropping gradients."""
+    def _training_mode(self):
+        """(train_head, train_fe) for this forward (train.py:105-125).  Autograd records through
+        the head (DFE, CPG) when it is enabled and any head or extractor parameter requires
+        gradients; through the feature extractor when its parameters require gradients.  The
+        extractor's BatchNorm must then be in eval mode (frozen-BN training, FE1.eval()): batch-
+        statistics BN is not implemented, and a module left in training mode raises instead of
+        silently computing something else."""
         head = [p for m in (self.DFE, self.cpg) for p in m.parameters()]
-        fe_frozen = not self.FE1.training and not any(p.requires_grad for p in self.FE1.parameters())
-        train_head = torch.is_grad_enabled() and any(p.requires_grad for p in head) and fe_frozen
-        if not train_head and self.training:
+        fe_grad = any(p.requires_grad for p in self.FE1.parameters())
+        grad = torch.is_grad_enabled()
+        train_fe = grad and fe_grad
+        train_head = grad and (any(p.requires_grad for p in head) or train_fe)
+        if self.FE1.training and (train_head or self.training):
             raise NotImplementedError(
-                "dvcp.DeepVCP: training mode needs a frozen feature extractor -- the FE backward "
-                "(batch-statistics BN, set-abstraction backward) is not implemented yet (SURVEY.md 8(f) rank 1). "
-                "Train the head with model.FE1.eval() and model.FE1.requires_grad_(False).")
+                "dvcp.DeepVCP: the feature extractor trains with frozen BatchNorm only -- batch-statistics BN "
+                "(FE1 in training mode) is not implemented.  Call model.FE1.eval(); its parameters may stay "
+                "trainable (frozen-BN fine-tuning) or be frozen with model.FE1.requires_grad_(False).")
+        if not train_head and self.training:
+            raise NotImplementedError("dvcp.DeepVCP: training mode with autograd disabled or no trainable parameter")
         if not train_head:
             _inference_only(self)
-        return train_head
+        return train_head, train_fe
 
     def draw_starts(self, B, n_src, n_tgt):
         """The reference's seven torch.randint(0, n, (B,)) draws, in call order."""
@@ -69,7 +74,7 @@ class DeepVCP(nn.Module):
         del S3
         return torch.stack([torch.randint(0, n, (B,), dtype=torch.long) for n in sizes])
 
-    def extract_features(self, src_pts, tgt_pts, starts=None):
+    def extract_features(self, src_pts, tgt_pts, starts=None, train_fe=False):
         """The feature-extractor half of forward (deepVCP.py:29,72 -- FE1 on both clouds, the
         weighting layer's scores): a dict the head half (``forward_head``) consumes.  It depends on
         no trainable head parameter, so with the extractor frozen a training loop can run it for
@@ -84,32 +89,43 @@ class DeepVCP(nn.Module):
             starts = self.draw_starts(B, src_pts.shape[2], tgt_pts.shape[2])
         starts = starts.to(dev, non_blocking=True)
         side = self._side_stream(dev)
+        if train_fe:  # differentiable in FE1's parameters (autograd.feat_extraction)
+            def run(pts, st, wl=None):
+                return autograd.feat_extraction(self.FE1, pts, st, wl=wl, side_stream=side)
+        else:
+            run = self.FE1.run
         if src_pts.shape == tgt_pts.shape and src_pts.dtype == tgt_pts.dtype:
             # src and tgt share FE1's weights and eval-mode FE is per cloud: one 2B-cloud pass
             # (the serial FPS chain then runs once for both clouds, on 2B workgroups)
             both = torch.cat([src_pts, tgt_pts], 0)
             fe_starts = [torch.cat([starts[i], starts[4 + i]]) for i in range(3)]
-            xyz2, feat2, score2 = self.FE1.run(both, fe_starts, wl=self.WL, side_stream=side)
+            xyz2, feat2, score2 = (run(both, fe_starts, wl=self.WL) if train_fe
+                                   else run(both, fe_starts, wl=self.WL, side_stream=side))
             src_xyz, tgt_xyz = xyz2[:B], xyz2[B:]
             src_feat, tgt_feat = feat2[:B], feat2[B:]
             score = score2[:B]
         else:
-            src_xyz, src_feat, score = self.FE1.run(src_pts, starts[0:3], wl=self.WL, side_stream=side)
-            tgt_xyz, tgt_feat, _ = self.FE1.run(tgt_pts, starts[4:7], side_stream=side)
+            if train_fe:
+                src_xyz, src_feat, score = run(src_pts, starts[0:3], wl=self.WL)
+                tgt_xyz, tgt_feat, _ = run(tgt_pts, starts[4:7])
+            else:
+                src_xyz, src_feat, score = run(src_pts, starts[0:3], wl=self.WL, side_stream=side)
+                tgt_xyz, tgt_feat, _ = run(tgt_pts, starts[4:7], side_stream=side)
         return dict(src_xyz=src_xyz, src_feat=src_feat, score=score, tgt_xyz=tgt_xyz, tgt_feat=tgt_feat,
                     starts=starts)
 
     def forward_head(self, feats, R_init, t_init=None, trace=None, keypoint_idx=None):
         """The head half of forward (deepVCP.py:39-110 after FE1): key points, DFE, candidates,
-        kNN, CPG.  Differentiable in DFE/CPG when training the head (see ``_head_training``)."""
-        return self._head(feats, R_init, self._head_training(), trace, keypoint_idx)
+        kNN, CPG.  Differentiable in DFE/CPG when training the head (see ``_training_mode``)."""
+        return self._head(feats, R_init, self._training_mode()[0], trace, keypoint_idx)
 
     def forward(self, src_pts, tgt_pts, R_init, t_init, starts=None, trace=None, keypoint_idx=None):
         """``starts`` (7, B): FPS start indices (drawn like the reference when None).
         ``trace``: dict filled with the stage outputs.  ``keypoint_idx`` (B, K): stage override
         for parity testing -- use these FE-space key-point indices instead of the top-k."""
-        train_head = self._head_training()
-        return self._head(self.extract_features(src_pts, tgt_pts, starts), R_init, train_head, trace, keypoint_idx)
+        train_head, train_fe = self._training_mode()
+        feats = self.extract_features(src_pts, tgt_pts, starts, train_fe=train_fe)
+        return self._head(feats, R_init, train_head, trace, keypoint_idx)
 
     def _head(self, f, R_init, train_head, trace, keypoint_idx):
         src_xyz, src_feat, score, tgt_xyz, tgt_feat, starts = (f["src_xyz"], f["src_feat"], f["score"], f["tgt_xyz"],

@@ -39,9 +39,12 @@ class feat_extraction_layer(nn.Module):
         return cached_pack(self, "head" if wl is None else "head_wl", linear_tensors(*lins),
                            lambda: linear_pack(*lins))
 
-    def run(self, pts, starts=None, wl=None, side_stream=None):
+    def run(self, pts, starts=None, wl=None, side_stream=None, saved=None):
         """Fused forward.  starts: (3, B) FPS start indices (drawn like the reference if None).
         Returns xyz (B, 3, S) contiguous, feat (B, S, 32), score (B, S) when ``wl`` is given.
+        ``saved`` (a dict): filled with what the backward needs (dvcp/autograd.py feat_extraction):
+        per layer its points, centres, input features, ball-query lists and FPS indices, and the
+        fc input rows.
 
         FPS of layer l+1 depends only on layer l's sampled centres, not on its features, so the
         three FPS launches (the serial critical path) run back to back on the current stream
@@ -88,19 +91,29 @@ class feat_extraction_layer(nn.Module):
                     side.wait_event(ev)
                     i.record_stream(side)
                     out = torch.gather(per_point, 1, i.unsqueeze(-1).expand(-1, -1, per_point.shape[2]))
+                    ctr_l = pts_l
                 else:
                     side.wait_event(ev)
                     count, lst, _ = ops.ball_query(pts_l, c, sa.radius, ns, pdim=2, cdim_pts=2)
                     out = ops.sa_group_mlp(pts_l, c, f, count, lst, ns, sa.chans, sa.packed_params(),
                                            xyz_pdim=2, feat_ddim=1, feat_pdim=2)
+                    ctr_l = c
+                if saved is not None:
+                    saved.setdefault("layers", []).append(dict(pts=pts_l, ctr=ctr_l, feat=f, count=count, lst=lst,
+                                                               ns=ns, idx=i, per_point=sa.npoint >= n_l))
                 c.record_stream(side)
                 pts_l, f = c, out.permute(0, 2, 1)
             S = pts_l.shape[2]
             f3 = f.permute(0, 2, 1).reshape(B * S, 64)  # sa output is (B, S, 64) in memory
             head, score = ops.fe_head(f3, self.fc_params(wl), with_score=wl is not None)
+        if saved is not None:
+            saved["f3"] = f3
         if side is not main:
             main.wait_stream(side)
-            for t in (head, score):
+            keep = [head, score]
+            if saved is not None:
+                keep += [saved["f3"]] + [t for lay in saved["layers"] for t in lay.values() if torch.is_tensor(t)]
+            for t in keep:
                 if t is not None:
                     t.record_stream(main)  # allocated on the side stream, consumed on main
         return pts_l, head.view(B, S, 32), (score.view(B, S) if score is not None else None)

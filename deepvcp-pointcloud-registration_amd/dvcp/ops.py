@@ -420,6 +420,52 @@ def cpg_backward(src, tgt, cand, G, params, grad_vcp):
     return gsrc, gtgt, gp
 
 
+def sa_group_mlp_backward(xyz, ctr, feat, count, lst, nsample, chans, params, bnstat, grad_out, want_feat_grad,
+                          xyz_pdim=2, feat_ddim=1, feat_pdim=2):
+    """Backward of ``sa_group_mlp`` with eval-mode BN (pointnet2_utils.py:176-202 + the :59 gather).
+    Returns (packed parameter gradient: per layer dW, db, dgamma, dbeta; dL/d feat (B, N, D) fp32
+    or None)."""
+    _lib.require_gpu(xyz, ctr, count, lst, params, bnstat, grad_out)
+    B = xyz.shape[0]
+    N, sb, sc, sn = _pts(xyz, xyz_pdim)
+    S, cb, cc, cn = _pts(ctr, 2)
+    if feat is not None:
+        st = feat.stride()
+        D = feat.shape[feat_ddim]
+        fb, fd, fn = st[0], st[feat_ddim], st[feat_pdim]
+        fdt = dtype_code(feat)
+    else:
+        D, fb, fd, fn, fdt = 0, 0, 0, 0, _lib.F32
+    ch = torch.tensor(list(chans), dtype=torch.int32)
+    nl = len(chans) - 1
+    npar = sum(a * b + 3 * b for a, b in zip(chans[:-1], chans[1:]))
+    dev = xyz.device
+    ws = torch.empty(max(1, int(_lib.load().dvcp_sa_group_mlp_backward_workspace_bytes(B, S, nl, ch.data_ptr())) // 4),
+                     dtype=torch.float32, device=dev)
+    gp = torch.empty(npar, dtype=torch.float32, device=dev)
+    gF = torch.zeros(B, N, D, dtype=torch.float32, device=dev) if (want_feat_grad and D > 0) else None
+    g = grad_out.float().contiguous()
+    call("dvcp_sa_group_mlp_backward", dtype_code(xyz), ptr(xyz), sb, sc, sn, N, ptr(ctr), cb, cc, cn, S, B, fdt,
+         ptr(feat), fb, fd, fn, D, ptr(count), ptr(lst), int(nsample), nl, ptr(ch), ptr(params), ptr(bnstat), ptr(g),
+         ptr(gF), ptr(ws), ptr(gp), stream())
+    return gp, gF
+
+
+def fe_head_backward(x, params, grad):
+    """Backward of the feature extractor's fc (deep_feat_extraction.py:15) on rows x (P, 64):
+    (packed dW | db, dL/dx (P, 64))."""
+    _lib.require_gpu(x, params, grad)
+    P = x.shape[0]
+    xc = x.float().contiguous()
+    g = grad.reshape(P, 32).float().contiguous()
+    ws = torch.empty(max(1, int(_lib.load().dvcp_fe_head_backward_workspace_bytes(P)) // 4), dtype=torch.float32,
+                     device=x.device)
+    gp = torch.empty(32 * 64 + 32, dtype=torch.float32, device=x.device)
+    gx = torch.empty(P, 64, dtype=torch.float32, device=x.device)
+    call("dvcp_fe_head_backward", ptr(xc), P, ptr(params), ptr(g), ptr(gx), ptr(ws), ptr(gp), stream())
+    return gp, gx
+
+
 def pose_inputs(x, y_pred, R_true, t_true):
     """deepVCP_loss.py's operands as the pose kernels take them: x, y_pred (B, 3, n) fp64
     contiguous; R_true (B, 3, 3), t_true (B, 3, 1) broadcast and contiguous."""

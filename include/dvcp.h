@@ -223,6 +223,32 @@ int dvcp_dfe_tgt_literal(int dtype, const void* ref_xyz, int64_t rb, int64_t rc,
                          const int32_t* idx, int B, int Q, const float* params, float* out,
                          void* stream);
 
+/* Backward of dvcp_sa_group_mlp with eval-mode BatchNorm (running statistics; the frozen-BN
+ * training mode), replacing autograd through pointnet2_utils.py:176-202 (+ the index_points gather
+ * of the grouped features, :59).  Same geometry arguments and folded `params` as the forward;
+ * bnstat: per layer running_mean (C_l) | 1/sqrt(running_var + eps) (C_l).
+ * grad_out: B x S x C_last fp32 (dL/d output).  grad_feat (optional): B x N x D fp32, ACCUMULATED
+ * (the caller zeroes it): dL/d feat through the grouping.  grad_params: per layer dW (C_{l+1} x C_l),
+ * db, dgamma, dbeta (fp32, packed in that order).  torch.max routes each channel's gradient to the
+ * first row holding the maximum.  Tables: sa1 (3[+3]-16-16-32), sa2 (35-32-64), sa3 (67-64-64).
+ * workspace: dvcp_sa_group_mlp_backward_workspace_bytes(B, S, nlayer, chans) bytes. */
+int64_t dvcp_sa_group_mlp_backward_workspace_bytes(int B, int S, int nlayer, const int* chans);
+int dvcp_sa_group_mlp_backward(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
+                               const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
+                               int feat_dtype, const void* feat, int64_t fb, int64_t fd, int64_t fn,
+                               int D, const int32_t* count, const int32_t* list, int nsample,
+                               int nlayer, const int* chans, const float* params,
+                               const float* bnstat, const float* grad_out, float* grad_feat,
+                               void* workspace, float* grad_params, void* stream);
+
+/* Backward of the feature extractor's fc (deep_feat_extraction.py:15, Linear 64 -> 32):
+ * x: P x 64 fp32 (its input rows), params: fc.W (32 x 64) | fc.b (32), grad: P x 32;
+ * grad_x (optional): P x 64; grad_params: dW (32 x 64) | db (32), summed in fixed order.
+ * workspace: dvcp_fe_head_backward_workspace_bytes(P) bytes. */
+int64_t dvcp_fe_head_backward_workspace_bytes(int P);
+int dvcp_fe_head_backward(const float* x, int P, const float* params, const float* grad,
+                          float* grad_x, void* workspace, float* grad_params, void* stream);
+
 /* Corresponding point generation.  Replaces cpg.py:27-60: cost volume
  * (src - scrambled tgt)^2 (Q11), Conv3d 32-16-4-1 (k3, p1, no activations), softmax over C,
  * vcp = sum(w*cand)/sum(w).

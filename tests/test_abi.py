@@ -71,18 +71,20 @@ def test_no_cpu_fallback():
 
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU behaviour")
 def test_training_guards_and_no_cpu_fallback():
-    """Training mode: an unfrozen feature extractor is refused (its backward does not exist);
-    a frozen one takes the head-autograd path, which has no CPU fallback either."""
+    """Training mode: a feature extractor with batch-statistics BN (FE1 in training mode) is refused
+    (not implemented); with FE1.eval() it trains in frozen-BN mode, frozen or not it takes the
+    autograd path, which has no CPU fallback either."""
     import dvcp
     m = dvcp.DeepVCP(use_normal=False, fe_npoint=16)
     args = (torch.rand(1, 3, 64), torch.rand(1, 3, 64), torch.eye(3, dtype=torch.float64)[None], torch.zeros(1, 3))
-    with pytest.raises(NotImplementedError, match="requires_grad_"):
+    with pytest.raises(NotImplementedError, match="FE1.eval"):
         m(*args)
     m.FE1.eval()
-    with pytest.raises(NotImplementedError, match="requires_grad_"):
-        m(*args)                                   # eval BN, but trainable FE weights
+    assert m._training_mode() == (True, True)      # frozen-BN training of the extractor and the head
+    with pytest.raises(RuntimeError, match="no GPU"):
+        m(*args)
     m.FE1.requires_grad_(False)
-    assert m._head_training()
+    assert m._training_mode() == (True, False)     # head only
     with pytest.raises(RuntimeError, match="no GPU"):
         m(*args)
     with pytest.raises(RuntimeError, match="no GPU"):

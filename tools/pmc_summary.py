@@ -14,7 +14,7 @@ import sys
 # entry point (bench stage key) -> (kernels one call launches once each: the call count,
 #                                  helper kernels the same call also launches)
 ENTRY = {
-    "dvcp_fps_ws": (["fps_batched_kernel", "fps_kernel"], []),
+    "dvcp_fps_ws": (["fps_select_kernel", "fps_kernel"], []),
     "dvcp_knn_tiled": (["knn_tiled_query_kernel"], ["knn_tiled_build_kernel"]),
     "dvcp_sa_group_mlp_ws": (["sa_mlp_mfma_kernel", "sa_mlp_kernel"], ["sa_pre_kernel", "sa_order_kernel"]),
     "dvcp_ball_query_ws": (["bq_tiled_kernel", "bq_wave_kernel", "ball_query_kernel"], ["bq_build_kernel"]),

@@ -1,4 +1,5 @@
-"""Head-training step throughput at C3 (train.py:96-125 with the feature extractor frozen).
+"""Training step throughput at C3 (train.py:96-125): the head with the feature extractor frozen,
+or (--train-fe) the whole model with the extractor trainable in frozen-BN mode (FE1.eval()).
 
 One step = model(src, tgt, R_gt, t_init) with autograd on the head -> deepVCP_loss -> backward
 -> Adam step, on one batch of synthetic KITTI-like pairs (8 x 16384 points, K=64, r=2.0, s=0.4).
@@ -34,7 +35,11 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--npoints", type=int, default=16384)
     ap.add_argument("--prefetch", type=int, default=0)
+    ap.add_argument("--train-fe", action="store_true",
+                    help="train FE1 too (frozen-BN: eval-mode BatchNorm, trainable parameters); no prefetch")
     args = ap.parse_args()
+    if args.train_fe and args.prefetch:
+        ap.error("--train-fe trains the extractor, so its forward cannot run ahead (--prefetch 0)")
     import dvcp
     from dvcp import _lib
     from dvcp.synthetic import condition_weights, make_pairs, randomize_bn
@@ -47,7 +52,7 @@ def main():
     with torch.no_grad():
         _, calib, _ = model.FE1.run(src)
     condition_weights(model, feats=calib)
-    model.FE1.requires_grad_(False)
+    model.FE1.requires_grad_(args.train_fe)
     opt = torch.optim.Adam([p for p in model.parameters() if p.requires_grad], lr=1e-4)
     t_init = torch.zeros(1, 3)
 
@@ -108,7 +113,8 @@ def main():
                   "total_ms_per_step": round(sum(v) / args.steps, 4)}
               for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1]))}
     print(json.dumps({
-        "metric": "head-training steps (forward + deepVCP_loss + backward + Adam), FE frozen",
+        "metric": ("training steps (forward + deepVCP_loss + backward + Adam), FE trainable with frozen BN"
+                   if args.train_fe else "head-training steps (forward + deepVCP_loss + backward + Adam), FE frozen"),
         "prefetch": P,
         "value": round(args.batch * args.steps / dt, 3), "unit": "pairs/s",
         "ms_per_step": round(1e3 * dt / args.steps, 3), "steps": args.steps, "warmup": args.warmup,
