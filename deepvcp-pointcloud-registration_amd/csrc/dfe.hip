@@ -187,6 +187,8 @@ __global__ __launch_bounds__(kDfeThreads) void dfe_bwd_kernel(const T* __restric
   __shared__ float Es[32][37];  // E (the bias e shifts a channel's rows alike: not needed for the arg-max)
   __shared__ double wq[kDfeQPerBlock][32];
   __shared__ double dsh[kDfeThreads];
+  __shared__ int rsel[kDfeThreads];   // input-row gradient: each channel's arg-max row ...
+  __shared__ float rg[kDfeThreads];   // ... and its output gradient
   const int tid = threadIdx.x, ql = tid / 32, f = tid % 32, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < 32 * 36; i += kDfeThreads) Es[i / 36][i % 36] = Ee[i];
   float acc[36];
@@ -252,29 +254,40 @@ __global__ __launch_bounds__(kDfeThreads) void dfe_bwd_kernel(const T* __restric
     for (int i = 0; i < 35; ++i) acc[i] = __fmaf_rn(g, xs[ql * 32 + bj][i], acc[i]);
     acc[35] += g;
     if (gX || gF) {  // block-uniform: the input rows' gradient, dL/dx_j = sum_{f: j*(f) = j} g_f E[f]
-      __syncthreads();  // the Gx reads of xs are done
-#pragma unroll
-      for (int i = 0; i < 35; ++i) xs[tid][i] = 0.f;
-      __syncthreads();
-      for (int i = 0; i < 35; ++i) atomicAdd(&xs[ql * 32 + bj][i], g * Ee[f * 36 + i]);
+      // each thread gathers the channels routed to its own row j (pulled from the per-candidate
+      // (j*, g) table; no LDS atomics), in channel order
+      rsel[tid] = bj;
+      rg[tid] = g;
       __syncthreads();
       const int j = f;  // this thread's own row
+      float dx[35];
+#pragma unroll
+      for (int i = 0; i < 35; ++i) dx[i] = 0.f;
+      bool any = false;
+      for (int ff = 0; ff < 32; ++ff) {
+        if (rsel[ql * 32 + ff] == j) {
+          const float gf = rg[ql * 32 + ff];
+          any = true;
+#pragma unroll
+          for (int i = 0; i < 35; ++i) dx[i] = __fmaf_rn(gf, Es[ff][i], dx[i]);
+        }
+      }
       if constexpr (MODE == 0) {
         if (live)
-          for (int i = 0; i < 35; ++i) gX[(q * 32 + j) * 35 + i] = xs[tid][i];
+          for (int i = 0; i < 35; ++i) gX[(q * 32 + j) * 35 + i] = dx[i];
       } else {
         // get_cat_feat_tgt.py:85,95: x[3 + c] = F[idx_j, c] * w[c] (fp64 weight) -> dF[idx_j, c] += dx * w[c]
-        if (live) {
+        if (live && any) {
           const int b = static_cast<int>(q / Q);
           int n = idx[q * 32 + j];
           n = n < 0 ? 0 : (n >= M ? M - 1 : n);
           float* dst = gF + (static_cast<int64_t>(b) * M + n) * 32;
-          for (int c = 0; c < 32; ++c) {
-            const float d = xs[tid][3 + c];
-            if (d != 0.f) atomicAdd(dst + c, static_cast<float>(static_cast<double>(d) * wq[ql][c]));
-          }
+#pragma unroll
+          for (int c = 0; c < 32; ++c)
+            if (dx[3 + c] != 0.f) atomicAdd(dst + c, static_cast<float>(static_cast<double>(dx[3 + c]) * wq[ql][c]));
         }
       }
+      __syncthreads();  // rsel / rg are rewritten by the next group
     }
   }
   __syncthreads();

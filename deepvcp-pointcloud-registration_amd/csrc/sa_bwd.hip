@@ -320,14 +320,23 @@ __global__ __launch_bounds__(kSbThreads) void sa_bwd_kernel(
   }
 }
 
-// out[e] = sum over the nw partial rows of part[k][e], in order, in fp64 (deterministic).
-__global__ __launch_bounds__(256) void sb_sum_kernel(const float* __restrict__ part, int nw, int P,
-                                                     float* __restrict__ out) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= P) return;
+// out[e] = sum over the nw partial rows of part[k][e] in fp64, in a fixed order (deterministic):
+// 64 parameters x 16 row slices per workgroup, the slices combined in order.
+__global__ __launch_bounds__(1024) void sb_sum_kernel(const float* __restrict__ part, int nw, int P,
+                                                      float* __restrict__ out) {
+  __shared__ double sl[16][64];
+  const int tid = threadIdx.x, c = tid & 63, slice = tid >> 6;
+  const int e = blockIdx.x * 64 + c;
   double acc = 0.0;
-  for (int k = 0; k < nw; ++k) acc += static_cast<double>(part[static_cast<int64_t>(k) * P + e]);
-  out[e] = static_cast<float>(acc);
+  if (e < P)
+    for (int k = slice; k < nw; k += 16) acc += static_cast<double>(part[static_cast<int64_t>(k) * P + e]);
+  sl[slice][c] = acc;
+  __syncthreads();
+  if (tid < 64 && e < P) {
+    double t = 0.0;
+    for (int k = 0; k < 16; ++k) t += sl[k][c];
+    out[e] = static_cast<float>(t);
+  }
 }
 
 // fc backward (deep_feat_extraction.py:15, y = W x + b, W 32 x 64): gx = W^T g per row, and the
@@ -389,7 +398,7 @@ static int launch_sa_bwd(const void* xyz, int64_t sb, int64_t sc, int64_t sn, co
   hipLaunchKernelGGL((sa_bwd_kernel<T, FT, D, C1, C2, C3>), dim3(grid), dim3(kSbThreads), 0, st, pv, cv, S, B, fv,
                      count, list, nsample, params, bnst, gout, gfeat, gfb, ws);
   if (int e = launch_status("dvcp_sa_group_mlp_backward")) return e;
-  hipLaunchKernelGGL(sb_sum_kernel, dim3(ceil_div(Tb::P, 256)), dim3(256), 0, st, ws, grid * kSbWaves, Tb::P, gparams);
+  hipLaunchKernelGGL(sb_sum_kernel, dim3(ceil_div(Tb::P, 64)), dim3(1024), 0, st, ws, grid * kSbWaves, Tb::P, gparams);
   return launch_status("dvcp_sa_group_mlp_backward(sum)");
 }
 
@@ -476,7 +485,7 @@ extern "C" int dvcp_fe_head_backward(const float* x, int P, const float* params,
   hipLaunchKernelGGL(dvcp::fc_bwd_kernel, dim3(grid), dim3(256), 0, st, x, P, params, grad, grad_x, ws);
   if (int e = dvcp::launch_status("dvcp_fe_head_backward")) return e;
   const int PP = dvcp::kFcOut * dvcp::kFcIn + dvcp::kFcOut;
-  hipLaunchKernelGGL(dvcp::sb_sum_kernel, dim3(dvcp::ceil_div(PP, 256)), dim3(256), 0, st, ws, grid * 4, PP,
+  hipLaunchKernelGGL(dvcp::sb_sum_kernel, dim3(dvcp::ceil_div(PP, 64)), dim3(1024), 0, st, ws, grid * 4, PP,
                      grad_params);
   return dvcp::launch_status("dvcp_fe_head_backward(sum)");
 }
