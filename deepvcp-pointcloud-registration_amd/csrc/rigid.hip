@@ -432,6 +432,103 @@ __global__ void registration_error_kernel(const double* __restrict__ Rp, const d
   trans[b] = sqrt(st);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Paper-faithful pose solve (DeepVCP paper, Sec. 3.4-3.5; SURVEY.md 8(f) rank 4 -- not reference
+// parity, the reference solves unweighted with no reflection fix): weighted Kabsch with the key
+// points' weights w_i, c_x = sum w x / sum w, H = sum w (x - c_x)(y - c_y)^T, and the det-sign
+// correction R = V diag(1, 1, d) U^T, d = sign(det(V U^T)).  With the ground truth it also forms
+// the paper's two loss terms per pair: sum |y_gt - y*| (the VCPs against the ground-truth
+// correspondences) and sum |y_gt - (R x + t)| (the solved pose applied to the key points).
+__global__ __launch_bounds__(kRgThreads) void paper_pose_kernel(const double* __restrict__ xg,
+                                                                const double* __restrict__ yg,
+                                                                const double* __restrict__ wg, int n, int reflection_fix,
+                                                                const double* __restrict__ Rtrue,
+                                                                const double* __restrict__ ttrue,
+                                                                double* __restrict__ Rout, double* __restrict__ tout,
+                                                                double* __restrict__ partial) {
+  __shared__ double scratch[16];
+  __shared__ double rt[12];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const double* x = xg + static_cast<int64_t>(b) * 3 * n;
+  const double* y = yg + static_cast<int64_t>(b) * 3 * n;
+  const double* w = wg ? wg + static_cast<int64_t>(b) * n : nullptr;
+  double c[7];
+  for (int a = 0; a < 7; ++a) c[a] = 0;
+  for (int j = tid; j < n; j += kRgThreads) {
+    const double wj = w ? w[j] : 1.0;
+    for (int a = 0; a < 3; ++a) {
+      c[a] = fma(wj, x[a * n + j], c[a]);
+      c[3 + a] = fma(wj, y[a * n + j], c[3 + a]);
+    }
+    c[6] += wj;
+  }
+  double cen[7];
+  for (int a = 0; a < 7; ++a) cen[a] = block_sum(c[a], scratch);
+  const double wsum = cen[6];
+  for (int a = 0; a < 6; ++a) cen[a] /= wsum;
+  double h[9];
+  for (int a = 0; a < 9; ++a) h[a] = 0;
+  for (int j = tid; j < n; j += kRgThreads) {
+    const double wj = w ? w[j] : 1.0;
+    double dx[3], dy[3];
+    for (int a = 0; a < 3; ++a) {
+      dx[a] = x[a * n + j] - cen[a];
+      dy[a] = y[a * n + j] - cen[3 + a];
+    }
+    for (int a = 0; a < 3; ++a)
+      for (int bb = 0; bb < 3; ++bb) h[a * 3 + bb] = fma(wj * dx[a], dy[bb], h[a * 3 + bb]);
+  }
+  double H[3][3];
+  for (int a = 0; a < 9; ++a) H[a / 3][a % 3] = block_sum(h[a], scratch);
+  if (tid == 0) {
+    double R[3][3], U[3][3], sig[3];
+    kabsch_svd(H, R, U, sig);
+    const double det = R[0][0] * (R[1][1] * R[2][2] - R[1][2] * R[2][1]) -
+                       R[0][1] * (R[1][0] * R[2][2] - R[1][2] * R[2][0]) +
+                       R[0][2] * (R[1][0] * R[2][1] - R[1][1] * R[2][0]);
+    if (reflection_fix && det < 0) {  // V diag(1,1,-1) U^T = R - 2 v_min u_min^T, v_min = R u_min
+      int k = 0;
+      for (int j = 1; j < 3; ++j) k = sig[j] < sig[k] ? j : k;
+      double v[3];
+      for (int a = 0; a < 3; ++a) v[a] = R[a][0] * U[0][k] + R[a][1] * U[1][k] + R[a][2] * U[2][k];
+      for (int a = 0; a < 3; ++a)
+        for (int bb = 0; bb < 3; ++bb) R[a][bb] -= 2.0 * v[a] * U[bb][k];
+    }
+    for (int a = 0; a < 3; ++a) {
+      for (int bb = 0; bb < 3; ++bb) rt[a * 3 + bb] = R[a][bb];
+      rt[9 + a] = cen[3 + a] - (R[a][0] * cen[0] + R[a][1] * cen[1] + R[a][2] * cen[2]);
+    }
+  }
+  __syncthreads();
+  double R[3][3], t[3];
+  for (int a = 0; a < 9; ++a) R[a / 3][a % 3] = rt[a];
+  for (int a = 0; a < 3; ++a) t[a] = rt[9 + a];
+  if (tid == 0) {
+    for (int a = 0; a < 9; ++a) Rout[b * 9 + a] = R[a / 3][a % 3];
+    for (int a = 0; a < 3; ++a) tout[b * 3 + a] = t[a];
+  }
+  if (partial) {
+    double Rg[3][3], tg[3];
+    for (int a = 0; a < 9; ++a) Rg[a / 3][a % 3] = Rtrue[b * 9 + a];
+    for (int a = 0; a < 3; ++a) tg[a] = ttrue[b * 3 + a];
+    double s1 = 0, s2 = 0;
+    for (int j = tid; j < n; j += kRgThreads) {
+      for (int a = 0; a < 3; ++a) {
+        const double ygt = Rg[a][0] * x[j] + Rg[a][1] * x[n + j] + Rg[a][2] * x[2 * n + j] + tg[a];
+        const double yp = R[a][0] * x[j] + R[a][1] * x[n + j] + R[a][2] * x[2 * n + j] + t[a];
+        s1 += fabs(ygt - y[a * n + j]);
+        s2 += fabs(ygt - yp);
+      }
+    }
+    s1 = block_sum(s1, scratch);
+    s2 = block_sum(s2, scratch);
+    if (tid == 0) {
+      partial[b * 2] = s1;
+      partial[b * 2 + 1] = s2;
+    }
+  }
+}
+
 }  // namespace dvcp
 
 extern "C" int dvcp_registration_error(const double* R_pred, const double* t_pred, const double* R_gt, int64_t rg_b,
@@ -481,4 +578,16 @@ extern "C" int dvcp_svd_optimization_backward(const double* x, const double* y_p
   hipLaunchKernelGGL(dvcp::svd_opt_bwd_kernel, dim3(B), dim3(dvcp::kRgThreads), 0, static_cast<hipStream_t>(stream), x,
                      y_pred, R_true, t_true, n, n_in, B, partial, grad_loss, alpha, inv_count, grad_y_pred);
   return dvcp::launch_status("dvcp_svd_optimization_backward");
+}
+
+extern "C" int dvcp_paper_pose(const double* x, const double* y, const double* w, int B, int n, int reflection_fix,
+                               const double* R_true, const double* t_true, double* R, double* t, double* partial,
+                               void* stream) {
+  DVCP_REQUIRE(x && y && R && t, "dvcp_paper_pose: null pointer");
+  DVCP_REQUIRE(!partial || (R_true && t_true), "dvcp_paper_pose: the loss terms need R_true and t_true");
+  DVCP_REQUIRE(B >= 0 && B <= 65535 && n > 0, "dvcp_paper_pose: bad sizes B=%d n=%d", B, n);
+  if (B == 0) return DVCP_OK;
+  hipLaunchKernelGGL(dvcp::paper_pose_kernel, dim3(B), dim3(dvcp::kRgThreads), 0, static_cast<hipStream_t>(stream), x,
+                     y, w, n, reflection_fix, R_true, t_true, R, t, partial);
+  return dvcp::launch_status("dvcp_paper_pose");
 }

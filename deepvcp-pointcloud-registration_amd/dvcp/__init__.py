@@ -12,6 +12,7 @@ from .deep_feat_extraction import feat_extraction_layer  # noqa: F401
 from .get_cat_feat_src import Get_Cat_Feat_Src  # noqa: F401
 from .get_cat_feat_tgt import Get_Cat_Feat_Tgt  # noqa: F401
 from .knn import KNN  # noqa: F401
+from . import paper  # noqa: F401
 from .metrics import registration_errors  # noqa: F401
 from .datasets import KITTIDataset, ModelNet40Dataset  # noqa: F401
 from .voxelize import voxelize, voxelize_point  # noqa: F401

@@ -119,13 +119,20 @@ class DeepVCP(nn.Module):
         kNN, CPG.  Differentiable in DFE/CPG when training the head (see ``_training_mode``)."""
         return self._head(feats, R_init, self._training_mode()[0], trace, keypoint_idx)
 
-    def forward(self, src_pts, tgt_pts, R_init, t_init, starts=None, trace=None, keypoint_idx=None):
+    def forward(self, src_pts, tgt_pts, R_init, t_init, starts=None, trace=None, keypoint_idx=None,
+                return_weights=False):
         """``starts`` (7, B): FPS start indices (drawn like the reference when None).
         ``trace``: dict filled with the stage outputs.  ``keypoint_idx`` (B, K): stage override
-        for parity testing -- use these FE-space key-point indices instead of the top-k."""
+        for parity testing -- use these FE-space key-point indices instead of the top-k.
+        ``return_weights``: also return the key points' weighting-layer scores (B, K), the
+        weights of the paper's weighted pose solve (dvcp.paper)."""
         train_head, train_fe = self._training_mode()
         feats = self.extract_features(src_pts, tgt_pts, starts, train_fe=train_fe)
-        return self._head(feats, R_init, train_head, trace, keypoint_idx)
+        tr = {} if (return_weights and trace is None) else trace
+        keypts, vcp = self._head(feats, R_init, train_head, tr, keypoint_idx)
+        if not return_weights:
+            return keypts, vcp
+        return keypts, vcp, torch.gather(feats["score"].detach(), 1, tr["topk"])
 
     def _head(self, f, R_init, train_head, trace, keypoint_idx):
         src_xyz, src_feat, score, tgt_xyz, tgt_feat, starts = (f["src_xyz"], f["src_feat"], f["score"], f["tgt_xyz"],

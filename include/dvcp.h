@@ -249,6 +249,17 @@ int64_t dvcp_fe_head_backward_workspace_bytes(int P);
 int dvcp_fe_head_backward(const float* x, int P, const float* params, const float* grad,
                           float* grad_x, void* workspace, float* grad_params, void* stream);
 
+/* Paper-faithful pose solve (DeepVCP paper Sec. 3.4-3.5; NOT reference
+ * parity -- the reference's get_rigid_transform, deepVCP_loss.py:13-44, is unweighted with no
+ * reflection fix): weighted Kabsch with per-point weights w (B x n fp64, NULL = uniform),
+ * centroids sum(w x) / sum(w), and with reflection_fix the det-sign correction
+ * R = V diag(1,1,sign det(V U^T)) U^T.  x, y: B x 3 x n fp64 -> R (B x 3 x 3), t (B x 3 x 1).
+ * partial (optional, B x 2 fp64, needs R_true (B x 3 x 3) and t_true (B x 3 x 1)): per pair
+ * sum |R_true x + t_true - y| and sum |R_true x + t_true - (R x + t)| (the paper's two L1 terms). */
+int dvcp_paper_pose(const double* x, const double* y, const double* w, int B, int n, int reflection_fix,
+                    const double* R_true, const double* t_true, double* R, double* t, double* partial,
+                    void* stream);
+
 /* Corresponding point generation.  Replaces cpg.py:27-60: cost volume
  * (src - scrambled tgt)^2 (Q11), Conv3d 32-16-4-1 (k3, p1, no activations), softmax over C,
  * vcp = sum(w*cand)/sum(w).

@@ -192,3 +192,28 @@ def test_module_surface_errors(cuda):
     with pytest.raises(AssertionError):
         c(torch.zeros(1, 1, 1, 32, device=cuda), torch.zeros(1, 1, 32, 100, device=cuda),
           torch.zeros(1, 1, 100, 3, device=cuda), 1.0, 0.4)
+
+
+def test_return_weights_and_paper_loss(cuda):
+    """forward(..., return_weights=True) also returns the key points' weighting-layer scores
+    (score[topk], descending like torch.topk), and the paper's weighted loss runs on them."""
+    import dvcp
+    from dvcp.synthetic import condition_weights, make_pairs, randomize_bn
+    src, tgt, R, t = make_pairs(2, 2048, seed=41)
+    torch.manual_seed(0)
+    m = dvcp.DeepVCP(use_normal=False, K=32, r=1.0, s=0.4, fe_npoint=512).eval().to(cuda)
+    randomize_bn(m)
+    with torch.no_grad():
+        _, calib, _ = m.FE1.run(src.to(cuda))
+    condition_weights(m, feats=calib)
+    starts = m.draw_starts(2, 2048, 2048)
+    tr = {}
+    with torch.no_grad():
+        kp, vcp, w = m(src.to(cuda), tgt.to(cuda), R.to(cuda), torch.zeros(1, 3), starts=starts, trace=tr,
+                       return_weights=True)
+        kp2, vcp2 = m(src.to(cuda), tgt.to(cuda), R.to(cuda), torch.zeros(1, 3), starts=starts)
+        loss, Rp, tp = dvcp.paper.deepVCP_loss_paper(kp, vcp, w, R.to(cuda), t.to(cuda), 0.5)
+    assert torch.equal(kp, kp2) and torch.equal(vcp, vcp2)
+    assert torch.equal(w, torch.gather(tr["score"], 1, tr["topk"]))
+    assert (w[:, 1:] <= w[:, :-1]).all() and (w > 0).all()
+    assert torch.isfinite(loss) and (torch.linalg.det(Rp) > 0).all()

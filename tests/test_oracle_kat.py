@@ -197,3 +197,30 @@ def test_registration_error_kat():
     refl = torch.diag(torch.tensor([1.0, 1.0, -1.0], dtype=torch.float64))[None]
     rot, _ = O.registration_errors(refl, z, I, z)
     assert math.isnan(rot.item())
+
+
+def test_paper_pose_checker_kats():
+    """oracle/paper.py (the checker of the paper-faithful pose solve): an exact rotation is
+    recovered with any positive weights; zero weights drop points; a reflected point set gives
+    det(R) = -1 without the fix and a proper rotation with it."""
+    import numpy as np
+    from oracle import paper as OP
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal((3, 20))
+    th = 0.7
+    Rz = np.array([[np.cos(th), -np.sin(th), 0], [np.sin(th), np.cos(th), 0], [0, 0, 1.0]])
+    t = np.array([0.3, -1.2, 2.0])
+    y = Rz @ x + t[:, None]
+    w = rng.random(20) + 0.1
+    R, tt = OP.weighted_rigid_transform(x, y, w)
+    assert np.allclose(R, Rz, atol=1e-12) and np.allclose(tt, t, atol=1e-12)
+    y_bad = y.copy()
+    y_bad[:, :5] += 10.0                              # corrupted points with zero weight
+    w0 = w.copy()
+    w0[:5] = 0.0
+    R, tt = OP.weighted_rigid_transform(x, y_bad, w0)
+    assert np.allclose(R, Rz, atol=1e-12) and np.allclose(tt, t, atol=1e-12)
+    M = np.diag([1.0, 1.0, -1.0])                     # a mirror image: the unconstrained fit reflects
+    R0, _ = OP.weighted_rigid_transform(x, M @ x, None, reflection_fix=False)
+    R1, _ = OP.weighted_rigid_transform(x, M @ x, None, reflection_fix=True)
+    assert np.isclose(np.linalg.det(R0), -1.0) and np.isclose(np.linalg.det(R1), 1.0)
