@@ -881,7 +881,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_select_kernel(PointsView<T> p
         const T xj = cxx[j], yj = cyy[j], zj = czz[j];
         int r = 0, touched = 0;
 #pragma unroll 2
-        for (int c4 = 0; c4 < 8; ++c4) {
+        for (int c4 = 0; c4 < 8 && q * 32 + 4 * c4 < cnt; ++c4) {  // (bound uniform per wave)
           const int i0 = q * 32 + 4 * c4;
           const float4 v4 = *reinterpret_cast<const float4*>(&cvv[i0]);
           const int4 p4 = *reinterpret_cast<const int4*>(&cpid[i0]);
