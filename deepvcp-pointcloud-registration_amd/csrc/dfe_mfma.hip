@@ -162,7 +162,7 @@ template <typename T>
 __global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
     PointsView<T> ref, const float* __restrict__ feat, int M, const float* __restrict__ cand,
     const float* __restrict__ dist, const int32_t* __restrict__ idx, int Q, int B, const float* __restrict__ params,
-    float* __restrict__ out) {
+    float* __restrict__ out, int xcd) {
   __shared__ Dfe1Lds L;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
   const float* W1 = params;
@@ -208,12 +208,29 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
   // Loads are unconditional (indices clamped to the last candidate) and a loaded index is only
   // clamped in the iteration that gathers with it.  Candidate indices are wave-uniform int32
   // (B * Q < 2^31 is checked by the launcher).
-  const int total = B * Q;
-  const int stride = static_cast<int>(gridDim.x) * kDfe1Waves;
-  int g = static_cast<int>(blockIdx.x) * kDfe1Waves + __builtin_amdgcn_readfirstlane(wave);
+  // Candidate order.  xcd == 0: one index space over all B*Q candidates.  xcd != 0 (B >= 8, grid a
+  // multiple of 8): workgroups are dispatched to the 8 XCDs round robin (blockIdx % 8), so the
+  // workgroups of XCD x take the candidates of pairs x, x+8, ...; each pair's gathered feature
+  // table then lives in one XCD's L2 instead of being fetched into all eight.
+  int total, stride, g, xo = 0;
+  if (xcd) {
+    xo = static_cast<int>(blockIdx.x) & 7;
+    total = ((B - xo + 7) / 8) * Q;
+    stride = static_cast<int>(gridDim.x >> 3) * kDfe1Waves;
+    g = static_cast<int>(blockIdx.x >> 3) * kDfe1Waves + __builtin_amdgcn_readfirstlane(wave);
+  } else {
+    total = B * Q;
+    stride = static_cast<int>(gridDim.x) * kDfe1Waves;
+    g = static_cast<int>(blockIdx.x) * kDfe1Waves + __builtin_amdgcn_readfirstlane(wave);
+  }
   if (g >= total) return;
+  auto glob = [&](int li) -> int {  // local candidate index -> global (b * Q + q)
+    if (!xcd) return li;
+    const int pl = li / Q;
+    return (xo + 8 * pl) * Q + (li - pl * Q);
+  };
   auto load_row = [&](int gg, float& dj, int& n) {
-    const int gc = gg < total ? gg : total - 1;
+    const int gc = glob(gg < total ? gg : total - 1);
     dj = dist[static_cast<int64_t>(gc) * 32 + r32];
     n = idx[static_cast<int64_t>(gc) * 32 + r32];
   };
@@ -223,7 +240,7 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
     float cx, cy, cz;
   };
   auto gather = [&](int gg, int nraw, Gathered& G) {
-    const int gc = gg < total ? gg : total - 1;
+    const int gc = glob(gg < total ? gg : total - 1);
     const int bb = gc / Q;
     const int n = nraw < 0 ? 0 : (nraw >= M ? M - 1 : nraw);
     const float4* fr = reinterpret_cast<const float4*>(feat + (static_cast<int64_t>(bb) * M + n) * 32 + 16 * h);
@@ -274,7 +291,7 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
 #pragma unroll
     for (int r = 1; r < 16; ++r) m = fmaxf(m, a[r]);
     m = fmaxf(m, __shfl_xor(m, 32, kWave));
-    if (h == 0) out[static_cast<int64_t>(gg) * 32 + r32] = m;
+    if (h == 0) out[static_cast<int64_t>(glob(gg)) * 32 + r32] = m;
     __builtin_amdgcn_wave_barrier();  // the w row is rewritten for the next candidate
   };
   float djA, djB;
@@ -316,9 +333,10 @@ int launch_dfe_tgt_mfma(PointsView<T> ref, const float* feat, int M, const float
                        dist, idx, Q, B, params, out);
   } else {
     // a few resident workgroups per CU amortise the fp64 prologue over many candidates
+    const int xcd = B % 8 == 0 && need >= 2048 ? 1 : 0;  // equal pairs per XCD
     const int grid = static_cast<int>(need < 2048 ? need : 2048);
     hipLaunchKernelGGL((dfe_tgt_mfma1_kernel<T>), dim3(grid), dim3(kDfe1Waves * kWave), 0, st, ref, feat, M, cand,
-                       dist, idx, Q, B, params, out);
+                       dist, idx, Q, B, params, out, xcd);
   }
   return launch_status("dvcp_dfe_tgt(mfma)");
 }
