@@ -60,9 +60,12 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=32)
     p.add_argument("--warmup", type=int, default=4)
-    p.add_argument("--batch", type=int, default=8, help="pairs per GPU")
-    p.add_argument("--npoints", type=int, default=16384)
-    p.add_argument("--K", type=int, default=64)
+    p.add_argument("--config", choices=["c3", "c5"], default="c3",
+                   help="c3: BASELINE's headline (8 pairs x 16384 points, K=64); c5: the stress config "
+                        "(65536 points, K=256, 2 pairs per batch, fp32 features, no CPU baseline)")
+    p.add_argument("--batch", type=int, default=None, help="pairs per GPU (c3: 8, c5: 2)")
+    p.add_argument("--npoints", type=int, default=None)
+    p.add_argument("--K", type=int, default=None)
     p.add_argument("--r", type=float, default=2.0)
     p.add_argument("--s", type=float, default=0.4)
     p.add_argument("--inflight", type=int, default=8,
@@ -75,7 +78,14 @@ def parse():
     p.add_argument("--iso-steps", type=int, default=3,
                    help="steps timed per kernel with one batch in flight (stage roofline)")
     p.add_argument("--cpu-pairs", type=int, default=3, help="C3 pairs timed for the CPU baseline (median)")
-    return p.parse_args()
+    a = p.parse_args()
+    c5 = a.config == "c5"
+    a.batch = a.batch if a.batch is not None else (2 if c5 else 8)
+    a.npoints = a.npoints if a.npoints is not None else (65536 if c5 else 16384)
+    a.K = a.K if a.K is not None else (256 if c5 else 64)
+    if c5:
+        a.no_cpu_baseline = True   # minutes per pair on the host: not a bounded sample
+    return a
 
 
 def main():
@@ -183,12 +193,16 @@ def main():
                "note": "vs ground truth (train.py:112-120 metric), random-init weights, R_init = R_gt as train.py:105 passes it"}
     pairs = B * world * args.steps
     value = pairs / elapsed
+    c5 = args.config == "c5"
     out = {
-        "metric": "pairs/sec (full DeepVCP forward) at N=16384, K=64; rot/trans error vs ref",
+        "metric": ("pairs/sec (full DeepVCP forward) at N=65536, K=256 (C5 stress, fp32 features)" if c5 else
+                   "pairs/sec (full DeepVCP forward) at N=16384, K=64; rot/trans error vs ref"),
         "value": round(value, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": "C3: KITTI-like synthetic pairs, DeepVCP.forward + deepVCP_loss (eval)",
+        "config": {"workload": ("C5: synthetic 65536-point pairs, K=256, DeepVCP.forward + deepVCP_loss (eval), fp32 "
+                                "features (the fp16-feature variant is not built)" if c5 else
+                                "C3: KITTI-like synthetic pairs, DeepVCP.forward + deepVCP_loss (eval)"),
                    "pairs_per_gpu": B, "global_batch": B * world, "n_points": N, "K": K, "r": r, "s": s,
                    "candidates": C, "fe_npoint": S, "parallelism": f"pairs sharded x{world}, all_gather(R,t)",
                    "inflight_batches": P, "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
@@ -201,7 +215,10 @@ def main():
         "live_launch_ms": {k: round(v["ms"] / v["n"], 4) for k, v in sorted(live.items(), key=lambda kv: -kv[1]["ms"])},
     }
     # HBM fraction of the whole step (north_star asks for it; the path is compute/latency bound)
-    out["hbm_fraction_step"] = round(177e6 * B / (elapsed / args.steps) / (PEAK_HBM_GBS * 1e9), 6)
+    out["hbm_fraction_step"] = round(sum(v["bytes"] for v in iso.values()) / args.iso_steps /
+                                     (elapsed / args.steps) / (PEAK_HBM_GBS * 1e9), 6)
+    out["hbm_fraction_note"] = ("algorithmic bytes of every stage (one batch in flight) over ms_per_step x 8 TB/s; "
+                                "the path is compute/latency bound, so this is structurally small")
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], out["parity"] = cpu_baseline(model, src, tgt, R_gt, t_gt, dev, args.cpu_pairs)

@@ -529,6 +529,19 @@ __global__ __launch_bounds__(kRgThreads) void paper_pose_kernel(const double* __
   }
 }
 
+// deepVCP_loss.py:110-119 from the per-pair partial sums: alpha * sum|.| / numel +
+// (1 - alpha) * |sum(.) / numel|, summed over pairs in order (one thread; B is small).
+__global__ void loss_finish_kernel(const double* __restrict__ partial, int B, double denom, double alpha,
+                                   double* __restrict__ loss) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double sabs = 0.0, sdif = 0.0;
+  for (int b = 0; b < B; ++b) {
+    sabs += partial[b * 2];
+    sdif += partial[b * 2 + 1];
+  }
+  loss[0] = alpha * (sabs / denom) + (1.0 - alpha) * fabs(sdif / denom);
+}
+
 }  // namespace dvcp
 
 extern "C" int dvcp_registration_error(const double* R_pred, const double* t_pred, const double* R_gt, int64_t rg_b,
@@ -590,4 +603,15 @@ extern "C" int dvcp_paper_pose(const double* x, const double* y, const double* w
   hipLaunchKernelGGL(dvcp::paper_pose_kernel, dim3(B), dim3(dvcp::kRgThreads), 0, static_cast<hipStream_t>(stream), x,
                      y, w, n, reflection_fix, R_true, t_true, R, t, partial);
   return dvcp::launch_status("dvcp_paper_pose");
+}
+
+extern "C" int dvcp_deepvcp_loss(const double* x, const double* y_pred, const double* R_true, const double* t_true,
+                                 int B, int n, double alpha, double* R2, double* t2, double* partial, double* loss,
+                                 void* stream) {
+  DVCP_REQUIRE(partial && loss, "dvcp_deepvcp_loss: null pointer");
+  const int n_in = static_cast<int>(n * 0.8);
+  if (int e = dvcp_svd_optimization(x, y_pred, R_true, t_true, B, n, R2, t2, nullptr, nullptr, partial, stream)) return e;
+  hipLaunchKernelGGL(dvcp::loss_finish_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), partial, B,
+                     static_cast<double>(B) * 3.0 * n_in, alpha, loss);
+  return dvcp::launch_status("dvcp_deepvcp_loss");
 }

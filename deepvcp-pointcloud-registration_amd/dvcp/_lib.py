@@ -47,6 +47,7 @@ SIGNATURES = {
     "dvcp_rigid_transform": [_P, _P, _I, _I, _P, _P, _P],
     "dvcp_paper_pose": [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P],
     "dvcp_svd_optimization": [_P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P],
+    "dvcp_deepvcp_loss": [_P, _P, _P, _P, _I, _I, _D, _P, _P, _P, _P, _P],
     "dvcp_registration_error": [_P, _P, _P, _L, _P, _L, _I, _P, _P, _P],
     "dvcp_rigid_apply": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _L, _P, _P],
     "dvcp_svd_optimization_backward": [_P, _P, _P, _P, _I, _I, _P, _P, _D, _P, _P],

@@ -33,9 +33,7 @@ def deepVCP_loss(x, y_pred, R_true, t_true, alpha):
         if PRINT_LOSS:
             print(f"Loss: {loss}")
         return loss, R, t
-    R, t, x1, _, partial = ops.svd_optimization(x, y_pred, R_true, t_true)
-    denom = float(x1.numel())
-    loss = alpha * (partial[:, 0].sum() / denom) + (1 - alpha) * torch.abs(partial[:, 1].sum() / denom)
+    loss, R, t, _ = ops.deepvcp_loss(x, y_pred, R_true, t_true, alpha)   # one HIP solve + the scalar
     if PRINT_LOSS:
         print(f"Loss: {loss}")
     return loss, R, t

@@ -306,6 +306,21 @@ def svd_optimization(x, y_pred, R_true, t_true):
     return R2, t2, x1, y2, partial
 
 
+def deepvcp_loss(x, y_pred, R_true, t_true, alpha):
+    """deepVCP_loss.py:105-121 on (B, 3, n) operands: (loss () fp64, R2, t2, partial (B, 2))."""
+    _lib.require_gpu(x, y_pred, R_true, t_true)
+    x, y_pred, Rt, tt = pose_inputs(x, y_pred, R_true, t_true)
+    B, _, n = x.shape
+    dev = x.device
+    R2 = torch.empty(B, 3, 3, dtype=torch.float64, device=dev)
+    t2 = torch.empty(B, 3, 1, dtype=torch.float64, device=dev)
+    partial = torch.empty(B, 2, dtype=torch.float64, device=dev)
+    loss = torch.empty((), dtype=torch.float64, device=dev)
+    call("dvcp_deepvcp_loss", ptr(x), ptr(y_pred), ptr(Rt), ptr(tt), B, n, float(alpha), ptr(R2), ptr(t2),
+         ptr(partial), ptr(loss), stream())
+    return loss, R2, t2, partial
+
+
 def registration_error(R_pred, t_pred, R_gt, t_gt):
     """train.py:112-120 (C8 fixed): per-pair rotation error (Euler xyz, degrees) and translation
     error, both nn.PairwiseDistance(p=2) with eps 1e-6.  R_pred (B,3,3), t_pred (B,3[,1]);

@@ -312,6 +312,13 @@ int dvcp_rigid_apply(int dtype, const void* in, int64_t ib, int64_t ic, int64_t 
  * :29 twice, the gathers of :81-82): dL/dy_pred (B x 3 x n fp64) for
  * loss = alpha*mean|y_true1 - y2| + (1-alpha)*|mean(y2 - y_true1)|.  partial: the forward's
  * (B x 2) per-pair sums; grad_loss: device scalar dL/dloss. */
+/* deepVCP_loss.py:105-121 in full: dvcp_svd_optimization (x1, y2 not returned) plus the scalar
+ * loss alpha * mean|y2 - y_true1| + (1 - alpha) * |mean(y2 - y_true1)| (loss: 1 fp64, partial:
+ * B x 2 fp64 scratch that also feeds dvcp_svd_optimization_backward). */
+int dvcp_deepvcp_loss(const double* x, const double* y_pred, const double* R_true, const double* t_true,
+                      int B, int n, double alpha, double* R2, double* t2, double* partial, double* loss,
+                      void* stream);
+
 int dvcp_svd_optimization_backward(const double* x, const double* y_pred, const double* R_true,
                                    const double* t_true, int B, int n, const double* partial,
                                    const double* grad_loss, double alpha, double* grad_y_pred,
