@@ -83,7 +83,7 @@ __global__ __launch_bounds__(kBqThreads) void ball_query_kernel(
 // bq_wave_kernel (any N): one wave = 64 centres with its own early exit; points are streamed in
 // ascending index order as wave-uniform scalar loads of packed (x, y, z, |p|^2) rows.
 //
-// bq_tiled_kernel (N <= 16384): a sparse radius (most centres far from nsample hits) makes the
+// bq_tiled_kernel (N <= 65536): a sparse radius (most centres far from nsample hits) makes the
 // scan above visit every point for every centre.  bq_build_kernel sorts the points along a Hilbert curve into
 // 64-point tiles with boxes and the centres into a Hilbert permutation, so a wave's 64 centres
 // have a compact box.  The wave marks, in an LDS bitmap indexed by ORIGINAL point index, every
@@ -97,8 +97,8 @@ __global__ __launch_bounds__(kBqThreads) void ball_query_kernel(
 __host__ __device__ constexpr int bq_padded_n(int N) { return (N + 15) & ~15; }
 
 constexpr int kBqTile = 64;
-constexpr int kBqMaxTiles = 256;              // tiled path: N <= 16384
-constexpr int kBqWords = kBqMaxTiles * 2;     // bitmap words per wave (N / 32)
+constexpr int kBqMaxTiles = 1024;             // tiled path: N <= 65536
+constexpr int kBqSmallTiles = 256;            // N <= 16384: the small-bitmap instantiation (occupancy)
 constexpr int kBqCap = 256;                   // candidate points staged in LDS per round
 
 struct BqLayout {
@@ -272,10 +272,12 @@ __device__ __forceinline__ float bq_gap(float lo, float hi, float v_lo, float v_
   return fmaxf(fmaxf(v_lo - hi, lo - v_hi), 0.0f);
 }
 
+// MAXT bounds the tile count; the per-wave bitmap holds MAXT * 2 words (one bit per point).
+template <int MAXT>
 __global__ __launch_bounds__(256) void bq_tiled_kernel(BqLayout L, int N, PointsView<float> ctr, int S, float r2,
                                                        int nsample, int32_t* __restrict__ count,
                                                        int32_t* __restrict__ list, int64_t* __restrict__ padded) {
-  __shared__ uint32_t bm[4][kBqWords];
+  __shared__ uint32_t bm[4][MAXT * 2];
   __shared__ float4 cpt[4][kBqCap];
   __shared__ int32_t cid[4][kBqCap];
   const int b = blockIdx.y;
@@ -441,8 +443,8 @@ static int launch_bq(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
       hipLaunchKernelGGL(bq_build_kernel, dim3(B), dim3(kBuildThreads), 0, st, pv, N, cv, S, L, tiled);
       if (int e = launch_status("dvcp_ball_query(build)")) return e;
       if (tiled)
-        hipLaunchKernelGGL(bq_tiled_kernel, dim3(ceil_div(S, 256), B), dim3(256), 0, st, L, N, cv, S, r2, nsample,
-                           count, list, padded);
+        hipLaunchKernelGGL(N <= kBqSmallTiles * kBqTile ? bq_tiled_kernel<kBqSmallTiles> : bq_tiled_kernel<kBqMaxTiles>,
+                           dim3(ceil_div(S, 256), B), dim3(256), 0, st, L, N, cv, S, r2, nsample, count, list, padded);
       else
         hipLaunchKernelGGL(bq_wave_kernel, dim3(ceil_div(S, 256), B), dim3(256), 0, st, L.packed, N, cv, S, r2,
                            nsample, count, list, padded);

@@ -526,7 +526,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_select_kernel(PointsView<T> p
   __shared__ __attribute__((aligned(16))) T cxx[kSelMax];
   __shared__ __attribute__((aligned(16))) T cyy[kSelMax];
   __shared__ __attribute__((aligned(16))) T czz[kSelMax];
-  __shared__ int prank[4][kSelMax];  // per quarter: count of preceding candidates | touched << 16
+  __shared__ int prank[W][kSelMax];  // per wave's i-range: count of preceding candidates | touched << 16
   __shared__ float wtf[W], wT[W];
   __shared__ uint32_t wpid[W];
   __shared__ uint32_t na_cnt, cand_fill;
@@ -872,38 +872,50 @@ __global__ __launch_bounds__(kFpsThreads) void fps_select_kernel(PointsView<T> p
       // ---- 4. rank and prefix test in one pass over candidate pairs ----------------------------
       // c_i precedes c_j (value desc, index asc) iff beats(i, j); rank_j = #{i : beats(i, j)}; c_j
       // is "touched" if some c_i preceding it lowers its running minimum (d(c_i, c_j) < v_j, the
-      // point update's formula).  Thread (j, q) covers i in [32q, 32q + 32), four candidates per
-      // 16-byte LDS read of each array.
-      const int j = tid & (kSelMax - 1), q = tid >> 7;
-      if (j < cnt) {
-        const float vj = cvv[j];
-        const int pj = cpid[j];
-        const T xj = cxx[j], yj = cyy[j], zj = czz[j];
-        int r = 0, touched = 0;
-#pragma unroll 2
-        for (int c4 = 0; c4 < 8 && q * 32 + 4 * c4 < cnt; ++c4) {  // (bound uniform per wave)
-          const int i0 = q * 32 + 4 * c4;
-          const float4 v4 = *reinterpret_cast<const float4*>(&cvv[i0]);
-          const int4 p4 = *reinterpret_cast<const int4*>(&cpid[i0]);
-          const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
-          const int pp[4] = {p4.x, p4.y, p4.z, p4.w};
-          T xx[4], yy[4], zz[4];
+      // point update's formula).  Wave w covers i in [16w, 16w + 16) for j = lane and lane + 64:
+      // every wave takes part, and each wave-uniform (broadcast) LDS read of four c_i serves both j.
+      {
+        const int i_lo = wave * (kSelMax / W);
+        int r0 = 0, r1 = 0, t0 = 0, t1 = 0;
+        if (i_lo < cnt) {  // wave-uniform
+          const int j0 = lane, j1 = lane + kWave;
+          const float v0 = cvv[j0], v1 = cvv[j1];
+          const int p0 = cpid[j0], p1 = cpid[j1];
+          const T x0 = cxx[j0], y0 = cyy[j0], z0 = czz[j0];
+          const T x1 = cxx[j1], y1 = cyy[j1], z1 = czz[j1];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            xx[k] = cxx[i0 + k];
-            yy[k] = cyy[i0 + k];
-            zz[k] = czz[i0 + k];
-          }
+          for (int c4 = 0; c4 < kSelMax / W / 4; ++c4) {
+            const int i0 = i_lo + 4 * c4;
+            if (i0 >= cnt) break;  // wave-uniform
+            const float4 v4 = *reinterpret_cast<const float4*>(&cvv[i0]);
+            const int4 p4 = *reinterpret_cast<const int4*>(&cpid[i0]);
+            const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
+            const int pp[4] = {p4.x, p4.y, p4.z, p4.w};
+            T xx[4], yy[4], zz[4];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const bool bt = (i0 + k < cnt) & ((vv[k] > vj) | ((vv[k] == vj) & (pp[k] < pj)));
-            const T dx = xj - xx[k], dy = yj - yy[k], dz = zj - zz[k];
-            const T d = (dx * dx + dy * dy) + dz * dz;
-            r += bt ? 1 : 0;
-            touched |= (bt & (d < static_cast<T>(vj))) ? 1 : 0;
+            for (int k = 0; k < 4; ++k) {
+              xx[k] = cxx[i0 + k];
+              yy[k] = cyy[i0 + k];
+              zz[k] = czz[i0 + k];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const bool in = i0 + k < cnt;
+              const bool b0 = in & ((vv[k] > v0) | ((vv[k] == v0) & (pp[k] < p0)));
+              const bool b1 = in & ((vv[k] > v1) | ((vv[k] == v1) & (pp[k] < p1)));
+              const T ax = x0 - xx[k], ay = y0 - yy[k], az = z0 - zz[k];
+              const T bx = x1 - xx[k], by = y1 - yy[k], bz = z1 - zz[k];
+              const T d0 = (ax * ax + ay * ay) + az * az;
+              const T d1 = (bx * bx + by * by) + bz * bz;
+              r0 += b0 ? 1 : 0;
+              r1 += b1 ? 1 : 0;
+              t0 |= (b0 & (d0 < static_cast<T>(v0))) ? 1 : 0;
+              t1 |= (b1 & (d1 < static_cast<T>(v1))) ? 1 : 0;
+            }
           }
         }
-        prank[q][j] = r | (touched << 16);
+        prank[wave][lane] = r0 | (t0 << 16);
+        prank[wave][lane + kWave] = r1 | (t1 << 16);
       }
       lds_barrier();
       tick(2);
@@ -916,9 +928,14 @@ __global__ __launch_bounds__(kFpsThreads) void fps_select_kernel(PointsView<T> p
         const int jj = hh * 64 + lane;
         rk[hh] = 0x7FFFFFFF;
         if (jj < cnt) {
-          const int w0 = prank[0][jj], w1 = prank[1][jj], w2 = prank[2][jj], w3 = prank[3][jj];
-          const int r = (w0 & 0xFFFF) + (w1 & 0xFFFF) + (w2 & 0xFFFF) + (w3 & 0xFFFF);
-          const bool touched = ((w0 | w1 | w2 | w3) >> 16) != 0;
+          int r = 0, tor = 0;
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            const int e = prank[w][jj];
+            r += e & 0xFFFF;
+            tor |= e;
+          }
+          const bool touched = (tor >> 16) != 0;
           rk[hh] = r;
           const bool fail = r >= left || (r > 0 && (touched || !(cvv[jj] > Tb)));
           failr = fail ? min(failr, static_cast<uint32_t>(r)) : failr;

@@ -186,28 +186,32 @@ def _bq_case(case, g):
         ctr[0, 5, 2] = float("nan")
         ctr[1, 600, 0] = float("-inf")
         return xyz, ctr, [(0.25, 64), (0.5, 16)]
-    if case == "untiled":
-        # above the tiled path's 16384 points: the index-order streaming kernel (C5's sa1)
+    if case == "wide":
+        # above 16384 points: the large-bitmap tiled instantiation (C5's sa1 uses N = 65536)
         xyz = torch.randint(-32, 33, (1, 20000, 3), generator=g).float() / 32
         return xyz, xyz[:, :900].contiguous(), [(0.125, 64), (0.25, 256)]
+    if case == "untiled":
+        # above the tiled path's 65536 points: the index-order streaming kernel
+        xyz = torch.randint(-32, 33, (1, 66000, 3), generator=g).float() / 32
+        return xyz, xyz[:, :600].contiguous(), [(0.125, 64)]
     raise ValueError(case)
 
 
-@pytest.mark.parametrize("case", ["kitti", "clusters", "ragged", "boundary", "nonfinite", "untiled"])
+@pytest.mark.parametrize("case", ["kitti", "clusters", "ragged", "boundary", "nonfinite", "wide", "untiled"])
 def test_ball_query_pruned_vs_oracle(cuda, case):
     """The spatially pruned fp32 ball query (tiles + per-wave candidate bitmap) against the
     oracle (pointnet2_utils.py:87-107 restated); exact where every d2 is exact (dyadic inputs),
     else only radius-boundary rounding may differ."""
     import oracle as O
     from dvcp import ops
-    g = torch.Generator().manual_seed(["kitti", "clusters", "ragged", "boundary", "nonfinite", "untiled"].index(case) + 140)
+    g = torch.Generator().manual_seed(["kitti", "clusters", "ragged", "boundary", "nonfinite", "wide", "untiled"].index(case) + 140)
     xyz, ctr, radii = _bq_case(case, g)
     for r, ns in radii:
         ns = min(ns, xyz.shape[1])
         want = O.query_ball_point(r, ns, xyz, ctr)
         cnt, lst, pad = ops.ball_query(xyz.to(cuda), ctr.to(cuda), r, ns, padded=True)
         got = pad.cpu()
-        if case in ("boundary", "nonfinite", "untiled"):
+        if case in ("boundary", "nonfinite", "wide", "untiled"):
             assert torch.equal(got, want), (case, r, ns)
         else:
             assert ball_mismatch_ok(xyz, ctr, got, want, r), (case, r, ns)

@@ -57,11 +57,12 @@ struct Config {
   KernelFn fn;
   int threads, ppt;
   bool timing;
+  bool sel = false;  // a threshold-select instantiation (its TIMING words are round statistics)
 };
 
 #define CFG(T, P, PR, TM, NAME) Config{NAME, dvcp::fps_kernel<float, T, P, PR, TM>, T, P, TM}
 #define SEL(P, NAME) Config{NAME, dvcp::fps_select_kernel<float, P, false>, 512, P, false}
-#define SELT(P, NAME) Config{NAME, dvcp::fps_select_kernel<float, P, true>, 512, P, true}
+#define SELT(P, NAME) Config{NAME, dvcp::fps_select_kernel<float, P, true>, 512, P, true, true}
 
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 16;
@@ -96,8 +97,8 @@ int main(int argc, char** argv) {
   const std::vector<Config> cfgs = {
       SEL(32, "select 512x32"),
       SELT(32, "select 512x32 +stats"),
-      SEL(24, "select 512x24"),
       SEL(20, "select 512x20"),
+      SELT(20, "select 512x20 +stats"),
       CFG(512, 32, true, false, "v3 512x32 prune"),
       CFG(512, 32, true, true, "v3 512x32 prune +timing"),
       CFG(512, 32, false, false, "v3 512x32 noprune"),
@@ -129,7 +130,7 @@ int main(int argc, char** argv) {
       for (int s = 0; s < npoint; ++s) bad += got[static_cast<size_t>(b) * npoint + s] != want[b][s];
     printf("%-28s B %3d N %6d npoint %6d  %8.3f ms  %6.3f us/step  mismatches %d\n", c.name, B, N, npoint, best,
            1e3f * best / npoint, bad);
-    if (c.timing && c.fn == reinterpret_cast<KernelFn>(dvcp::fps_select_kernel<float, 32, true>)) {
+    if (c.timing && c.sel) {
       std::vector<unsigned long long> pr(prof_words);
       CK(hipMemcpy(pr.data(), dprof, pr.size() * 8, hipMemcpyDeviceToHost));
       printf("   cloud 0: rounds %llu  scans %llu  fallbacks %llu  centres/round %.1f  rescans: none-above %llu "
