@@ -163,8 +163,18 @@ __global__ __launch_bounds__(kTiledThreads) void knn_tiled_query_kernel(const fl
                                                                         int64_t qb, int64_t qc, int64_t qn, int qf64,
                                                                         int Q, int k, float* __restrict__ dist,
                                                                         int32_t* __restrict__ idx,
-                                                                        int64_t* __restrict__ idx64) {
-  const int b = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+                                                                        int64_t* __restrict__ idx64, int B8) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // Cloud and block within it.  Workgroups reach the 8 XCDs round robin by linear id, so with
+  // B % 8 == 0 the linear id is re-mapped to give XCD x the clouds x, x + 8, ...: each cloud's
+  // sorted points and boxes are then fetched into one XCD's L2 instead of all eight.
+  int b = blockIdx.y, bx = blockIdx.x;
+  if ((B8 & 1) != 0) {
+    const int lin = static_cast<int>(blockIdx.y * gridDim.x + blockIdx.x);
+    const int xo = lin & 7, slot = lin >> 3;
+    b = xo + 8 * (slot / static_cast<int>(gridDim.x));
+    bx = slot % static_cast<int>(gridDim.x);
+  }
   const int T = (M + kTile - 1) / kTile;
   // the cloud's tile boxes in LDS (all four waves scan the same cloud): the per-lane box test
   // then reads LDS broadcasts kBoxBatch tiles at a time instead of waiting on a scalar load per tile
@@ -174,8 +184,8 @@ __global__ __launch_bounds__(kTiledThreads) void knn_tiled_query_kernel(const fl
     for (int i = threadIdx.x; i < 2 * T; i += kTiledThreads) sbox[i] = tbg[i];
     __syncthreads();
   }
-  const int sq = (blockIdx.x * (kTiledThreads / kWave) + wave) * kWave + lane;
-  if ((blockIdx.x * (kTiledThreads / kWave) + wave) * kWave >= Q) return;  // whole wave past the end
+  const int sq = (bx * (kTiledThreads / kWave) + wave) * kWave + lane;
+  if ((bx * (kTiledThreads / kWave) + wave) * kWave >= Q) return;  // whole wave past the end
   const bool live = sq < Q;
   const int q = live ? qperm[static_cast<int64_t>(b) * Q + sq] : 0;
   float qx, qy, qz;
@@ -363,10 +373,11 @@ extern "C" int dvcp_knn_tiled(int dtype, const void* ref, int64_t rb, int64_t rc
   const int T = dvcp::ceil_div(M, dvcp::kTile);
   const int qf64 = dtype == DVCP_F64;
   dim3 grid(dvcp::ceil_div(Q, dvcp::kTiledThreads), B);
+  const int xcd = B % 8 == 0 ? 1 : 0;  // XCD-aware cloud mapping (equal clouds per XCD)
 #define DVCP_KNNT(KK, RR)                                                                                          \
   if (k <= KK && T <= 64 * RR) {                                                                                   \
     hipLaunchKernelGGL((dvcp::knn_tiled_query_kernel<KK, RR>), grid, dim3(dvcp::kTiledThreads), 0, st, L.sorted,   \
-                       L.tbox, L.qperm, M, qry, qb, qc, qn, qf64, Q, k, dist, idx, idx64);                                                                                \
+                       L.tbox, L.qperm, M, qry, qb, qc, qn, qf64, Q, k, dist, idx, idx64, xcd);                                                                                \
     return dvcp::launch_status("dvcp_knn_tiled(query)");                                                           \
   }
   DVCP_KNNT(1, 1)

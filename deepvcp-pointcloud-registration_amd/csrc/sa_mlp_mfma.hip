@@ -133,7 +133,7 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
     PointsView<T> pts, PointsView<T> ctr, int S, int B, const float* __restrict__ feat, int64_t fb, int64_t fn,
     const int32_t* __restrict__ count, const int32_t* __restrict__ list, int nsample,
     const float* __restrict__ params, const float* __restrict__ U, int64_t ub, const int32_t* __restrict__ order,
-    float* __restrict__ out) {
+    float* __restrict__ out, int xcd) {
   using Sh = SaMfmaShape<D, C1, C2>;
   constexpr int C0 = Sh::C0, KS = Sh::KS, MT = Sh::MT, CT = Sh::CT;
   __shared__ SaMfmaLds<D, C1, C2> L;
@@ -183,9 +183,23 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
   __syncthreads();
 
   // ---- one centre per wave, grid-strided ------------------------------------------------
-  const int64_t total = static_cast<int64_t>(B) * S;
-  for (int64_t q = static_cast<int64_t>(blockIdx.x) * kMfmaWaves + wave; q < total;
-       q += static_cast<int64_t>(gridDim.x) * kMfmaWaves) {
+  // Centre index space.  xcd == 0: all B*S centres.  xcd != 0 (B % 8 == 0, grid a multiple of 8):
+  // workgroups reach the 8 XCDs round robin (blockIdx % 8), so XCD x walks the centres of clouds
+  // x, x + 8, ... and each cloud's U table and point rows are fetched into one XCD's L2.
+  int64_t total, q0, qs;
+  int xo = 0;
+  if (xcd) {
+    xo = static_cast<int>(blockIdx.x) & 7;
+    total = static_cast<int64_t>((B - xo + 7) / 8) * S;
+    q0 = static_cast<int64_t>(blockIdx.x >> 3) * kMfmaWaves + wave;
+    qs = static_cast<int64_t>(gridDim.x >> 3) * kMfmaWaves;
+  } else {
+    total = static_cast<int64_t>(B) * S;
+    q0 = static_cast<int64_t>(blockIdx.x) * kMfmaWaves + wave;
+    qs = static_cast<int64_t>(gridDim.x) * kMfmaWaves;
+  }
+  for (int64_t ql = q0; ql < total; ql += qs) {
+    const int64_t q = xcd ? (xo + 8 * (ql / S)) * static_cast<int64_t>(S) + ql % S : ql;
     // centre in curve order when `order` is given: consecutive waves then gather the U / point
     // rows of one spatial neighbourhood, which stay in L2 instead of being fetched again
     const int b = static_cast<int>(q / S);
@@ -313,6 +327,7 @@ int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, c
   PointsView<T> cv{static_cast<const T*>(c), cb, cc, cn};
   const int64_t centres = static_cast<int64_t>(B) * S;
   const int grid = static_cast<int>(centres < 4096 * kMfmaWaves ? (centres + kMfmaWaves - 1) / kMfmaWaves : 4096);
+  const int xcd = B % 8 == 0 && grid % 8 == 0 ? 1 : 0;
   if (order)
     hipLaunchKernelGGL((sa_order_kernel<T>), dim3(B), dim3(kBuildThreads), 0, st, cv, S, order);
   if (U) {
@@ -320,10 +335,10 @@ int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, c
     hipLaunchKernelGGL((sa_pre_kernel<D, C1>), dim3(ceil_div(rows, 256 / (C1 / 4))), dim3(256), 0, st, feat, fb, fn, N,
                        B, params, U);
     hipLaunchKernelGGL((sa_mlp_mfma_kernel<T, D, C1, C2, true>), dim3(grid), dim3(kMfmaWaves * kWave), 0, st, pv, cv,
-                       S, B, feat, fb, fn, count, list, nsample, params, U, static_cast<int64_t>(N) * C1, order, out);
+                       S, B, feat, fb, fn, count, list, nsample, params, U, static_cast<int64_t>(N) * C1, order, out, xcd);
   } else {
     hipLaunchKernelGGL((sa_mlp_mfma_kernel<T, D, C1, C2, false>), dim3(grid), dim3(kMfmaWaves * kWave), 0, st, pv,
-                       cv, S, B, feat, fb, fn, count, list, nsample, params, nullptr, 0, order, out);
+                       cv, S, B, feat, fb, fn, count, list, nsample, params, nullptr, 0, order, out, xcd);
   }
   return launch_status("dvcp_sa_group_mlp(mfma)");
 }

@@ -290,6 +290,17 @@ def test_knn_tiled_edges_equal_brute(cuda, M, Q, k):
     assert torch.equal(i64, i2.long())
 
 
+@pytest.mark.parametrize("B", [8, 16])
+def test_knn_tiled_xcd_clouds_equal_brute(cuda, B):
+    """B % 8 == 0 runs the tiled query kernel's XCD-aware cloud mapping (XCD x takes clouds x,
+    x + 8, ...); every cloud must still get its own queries and references."""
+    from dvcp import ops
+    ref, qry = _c3_knn_inputs(cuda, M=4000, Q=1500, B=B, seed=B)
+    d1, i1, _ = ops.knn(ref, qry, 32, method="brute")
+    d2, i2, _ = ops.knn(ref, qry, 32, method="tiled")
+    assert torch.equal(i1, i2) and torch.equal(d1, d2)
+
+
 def test_knn_tiled_dyadic_ties_full(cuda):
     """Coordinates on a 1/8 grid: nearly every distance is tied; order must be (d2, index)."""
     from dvcp import ops
@@ -331,17 +342,19 @@ def test_voxelize_golden(cuda):
 
 
 # ------------------------------------------------------------------------ set abstraction
-@pytest.mark.parametrize("layout", ["channel_first", "point_major"])
-@pytest.mark.parametrize("normals", [False, True])
-def test_set_abstraction_vs_oracle(cuda, normals, layout):
+@pytest.mark.parametrize("layout,normals,B", [("channel_first", False, 2), ("channel_first", True, 2),
+                                              ("point_major", False, 2), ("point_major", True, 2),
+                                              ("point_major", False, 8), ("point_major", False, 16)])
+def test_set_abstraction_vs_oracle(cuda, normals, layout, B):
     """All three SA tables.  Channel-first features run the row-per-thread kernel; point-major
     (each point's channels contiguous, as the forward produces them) the fp32 MFMA kernel for
-    the two-layer tables."""
+    the two-layer tables.  B = 8 and 16 run the MFMA kernel's XCD-aware centre mapping (clouds
+    x, x + 8, ... on XCD x)."""
     import oracle as O
     import dvcp.pointnet2_utils as P
     from tests_helpers import randomize_bn
     g = torch.Generator().manual_seed(106)
-    B, N, S = 2, 3000, 700
+    N, S = 3000, 700
     dt = torch.float64 if normals else torch.float32
     for cfg in O.fe_config(use_normal=normals, npoint=S):
         torch.manual_seed(7)
