@@ -276,13 +276,23 @@ __device__ __forceinline__ float bq_gap(float lo, float hi, float v_lo, float v_
 template <int MAXT>
 __global__ __launch_bounds__(256) void bq_tiled_kernel(BqLayout L, int N, PointsView<float> ctr, int S, float r2,
                                                        int nsample, int32_t* __restrict__ count,
-                                                       int32_t* __restrict__ list, int64_t* __restrict__ padded) {
+                                                       int32_t* __restrict__ list, int64_t* __restrict__ padded,
+                                                       int xcd) {
   __shared__ uint32_t bm[4][MAXT * 2];
   __shared__ float4 cpt[4][kBqCap];
   __shared__ int32_t cid[4][kBqCap];
-  const int b = blockIdx.y;
+  // cloud and block within it; xcd != 0 (B % 8 == 0): workgroups reach the XCDs round robin by
+  // linear id, which is re-mapped so XCD x takes clouds x, x + 8, ... (one cloud's tiles and rows
+  // per L2)
+  int b = blockIdx.y, bx = blockIdx.x;
+  if (xcd) {
+    const int lin = static_cast<int>(blockIdx.y * gridDim.x + blockIdx.x);
+    const int slot = lin >> 3;
+    b = (lin & 7) + 8 * (slot / static_cast<int>(gridDim.x));
+    bx = slot % static_cast<int>(gridDim.x);
+  }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int q0 = (blockIdx.x * 4 + wave) * 64;
+  const int q0 = (bx * 4 + wave) * 64;
   if (q0 >= S) return;
   const int T = (N + kBqTile - 1) / kBqTile;
   const int NW = (N + 31) >> 5;
@@ -444,7 +454,8 @@ static int launch_bq(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
       if (int e = launch_status("dvcp_ball_query(build)")) return e;
       if (tiled)
         hipLaunchKernelGGL(N <= kBqSmallTiles * kBqTile ? bq_tiled_kernel<kBqSmallTiles> : bq_tiled_kernel<kBqMaxTiles>,
-                           dim3(ceil_div(S, 256), B), dim3(256), 0, st, L, N, cv, S, r2, nsample, count, list, padded);
+                           dim3(ceil_div(S, 256), B), dim3(256), 0, st, L, N, cv, S, r2, nsample, count, list, padded,
+                           B % 8 == 0 ? 1 : 0);
       else
         hipLaunchKernelGGL(bq_wave_kernel, dim3(ceil_div(S, 256), B), dim3(256), 0, st, L.packed, N, cv, S, r2,
                            nsample, count, list, padded);

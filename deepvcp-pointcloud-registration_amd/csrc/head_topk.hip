@@ -11,12 +11,20 @@ __device__ __forceinline__ float relu(float v) { return v > 0.0f ? v : 0.0f; }
 // torch.nn.Softplus(beta=1, threshold=20)
 __device__ __forceinline__ float softplus(float v) { return v > 20.0f ? v : log1pf(expf(v)); }
 
-__global__ __launch_bounds__(256) void fe_head_kernel(const float* __restrict__ x, int P, const float* __restrict__ params,
+// rows != nullptr: output row i reads input row (i / S) * Nx + rows[i] (a per-cloud gather of the
+// per-point sa3 rows by the FPS order, folded into the load; indices clamped to [0, Nx)).
+__global__ __launch_bounds__(256) void fe_head_kernel(const float* __restrict__ x, const int64_t* __restrict__ rows,
+                                                      int S, int Nx, int P, const float* __restrict__ params,
                                                       float* __restrict__ feat, float* __restrict__ score) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P) return;
   float in[64];
-  const float4* src = reinterpret_cast<const float4*>(x + static_cast<int64_t>(i) * 64);
+  int64_t r = i;
+  if (rows) {
+    const int64_t n = rows[i];
+    r = static_cast<int64_t>(i / S) * Nx + (n < 0 ? 0 : (n >= Nx ? Nx - 1 : n));
+  }
+  const float4* src = reinterpret_cast<const float4*>(x + r * 64);
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const float4 v = src[q];
@@ -112,8 +120,18 @@ extern "C" int dvcp_fe_head(const float* x, int P, const float* params, float* f
   DVCP_REQUIRE(x && params && feat, "dvcp_fe_head: null pointer");
   if (P <= 0) return DVCP_OK;
   hipLaunchKernelGGL(dvcp::fe_head_kernel, dim3(dvcp::ceil_div(P, 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     x, P, params, feat, score);
+                     x, nullptr, 1, 1, P, params, feat, score);
   return dvcp::launch_status("dvcp_fe_head");
+}
+
+extern "C" int dvcp_fe_head_rows(const float* x, const int64_t* rows, int S, int Nx, int P, const float* params,
+                                 float* feat, float* score, void* stream) {
+  DVCP_REQUIRE(x && rows && params && feat, "dvcp_fe_head_rows: null pointer");
+  DVCP_REQUIRE(S > 0 && Nx > 0 && P % S == 0, "dvcp_fe_head_rows: bad sizes (S=%d, Nx=%d, P=%d)", S, Nx, P);
+  if (P <= 0) return DVCP_OK;
+  hipLaunchKernelGGL(dvcp::fe_head_kernel, dim3(dvcp::ceil_div(P, 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     x, rows, S, Nx, P, params, feat, score);
+  return dvcp::launch_status("dvcp_fe_head_rows");
 }
 
 extern "C" int dvcp_weighting(const float* feat, int P, const float* params, float* score, void* stream) {

@@ -126,7 +126,7 @@ template <typename T, int D, int C1, int C2>
 int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, const void* c, int64_t cb, int64_t cc,
                    int64_t cn, int S, int B, const float* feat, int64_t fb, int64_t fn, const int32_t* count,
                    const int32_t* list, int nsample, const float* params, float* U, int32_t* order, float* out,
-                   hipStream_t st);
+                   const int64_t* rows, int Nf, hipStream_t st);
 
 template <typename T, typename FT, int D, int C1, int C2, int C3>
 static int launch_sa(const void* xyz, int64_t sb, int64_t sc, int64_t sn, const void* c, int64_t cb, int64_t cc,
@@ -164,7 +164,7 @@ static int sa_group_mlp_impl(int dtype, const void* xyz, int64_t sb, int64_t sc,
                              int64_t cb, int64_t cc, int64_t cn, int S, int B, int feat_dtype, const void* feat,
                              int64_t fb, int64_t fd, int64_t fn, int D, const int32_t* count, const int32_t* list,
                              int nsample, int nlayer, const int* chans, const float* params, float* out, void* ws,
-                             void* stream) {
+                             void* stream, const int64_t* rows = nullptr, int Nf = 0) {
   DVCP_REQUIRE(xyz && ctr && count && list && chans && params && out, "dvcp_sa_group_mlp: null pointer");
   DVCP_REQUIRE(N > 0 || ws == nullptr, "dvcp_sa_group_mlp_ws: N must be given with a workspace");
   DVCP_REQUIRE(D == 0 || feat, "dvcp_sa_group_mlp: D=%d but feat is NULL", D);
@@ -197,13 +197,17 @@ static int sa_group_mlp_impl(int dtype, const void* xyz, int64_t sb, int64_t sc,
   // two-layer tables: fp32 MFMA when each point's features are a contiguous, 16-B aligned fp32 run
   const bool mfma_ok = !ff64 && fd == 1 && fb % 4 == 0 && fn % 4 == 0 &&
                        (reinterpret_cast<uintptr_t>(feat) & 15) == 0;
+  // a feature row map is applied by the MFMA tables' per-point pre-pass only
+  DVCP_REQUIRE(!rows || (mfma_ok && U && nlayer == 2 && Nf > 0),
+               "dvcp_sa_group_mlp_rows_ws: the row map needs a two-layer table, fp32 point-major features "
+               "(16-B aligned rows), a workspace and Nf > 0");
 #define DVCP_SA_M(DD, A, Bc)                                                                                     \
   return f64 ? dvcp::launch_sa_mfma<double, DD, A, Bc>(xyz, sb, sc, sn, N, ctr, cb, cc, cn, S, B,               \
                                                      static_cast<const float*>(feat), fb, fn, count, list,      \
-                                                     nsample, params, U, order, out, st)                        \
+                                                     nsample, params, U, order, out, rows, Nf, st)              \
              : dvcp::launch_sa_mfma<float, DD, A, Bc>(xyz, sb, sc, sn, N, ctr, cb, cc, cn, S, B,                \
                                                     static_cast<const float*>(feat), fb, fn, count, list, nsample, \
-                                                    params, U, order, out, st)
+                                                    params, U, order, out, rows, Nf, st)
   if (nlayer == 2 && D == 32 && chans[1] == 32 && chans[2] == 64) {
     if (mfma_ok) DVCP_SA_M(32, 32, 64);
     DVCP_SA_T(32, 32, 64, 0);
@@ -243,4 +247,18 @@ extern "C" int dvcp_sa_group_mlp_ws(int dtype, const void* xyz, int64_t sb, int6
   return sa_group_mlp_impl(dtype, xyz, sb, sc, sn, N, ctr, cb, cc, cn, S, B, feat_dtype, feat, fb, fd, fn, D, count,
                            list, nsample, nlayer, chans, params, out,
                            sa_ws_bytes(B, N, S, nlayer, chans) ? workspace : nullptr, stream);
+}
+
+extern "C" int dvcp_sa_group_mlp_rows_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
+                                         const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
+                                         const float* feat, int64_t fb, int64_t fn, int Nf, int D,
+                                         const int64_t* feat_rows, const int32_t* count, const int32_t* list,
+                                         int nsample, int nlayer, const int* chans, const float* params, float* out,
+                                         void* workspace, void* stream) {
+  DVCP_REQUIRE(feat && feat_rows, "dvcp_sa_group_mlp_rows_ws: null feature pointer or row map");
+  DVCP_REQUIRE(sa_ws_bytes(B, N, S, nlayer, chans) > 0 && workspace,
+               "dvcp_sa_group_mlp_rows_ws: needs a two-layer table and its workspace");
+  DVCP_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "dvcp_sa_group_mlp_rows_ws: workspace not 16-B aligned");
+  return sa_group_mlp_impl(dtype, xyz, sb, sc, sn, N, ctr, cb, cc, cn, S, B, DVCP_F32, feat, fb, 1, fn, D, count, list,
+                           nsample, nlayer, chans, params, out, workspace, stream, feat_rows, Nf);
 }

@@ -68,9 +68,11 @@ __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >
 // with two MFMA k-steps.  Only the summation order changes (features first, then xyz); the local
 // coordinates are still formed per (centre, point) pair, so no cancellation is introduced.
 template <int D, int C1>
+// rows != nullptr: point n of cloud b takes feature row rows[b * N + n] (clamped to [0, Nf)) --
+// the previous layer's per-point rows gathered by its FPS order, folded into this load.
 __global__ __launch_bounds__(256) void sa_pre_kernel(const float* __restrict__ feat, int64_t fb, int64_t fn, int N,
                                                      int B, const float* __restrict__ params,
-                                                     float* __restrict__ U) {
+                                                     float* __restrict__ U, const int64_t* __restrict__ rows, int Nf) {
   // Thread (point, 4-channel group): the C1/4 threads of a point write one contiguous U row
   // (coalesced float4 stores), and read the BN-folded weights from LDS as [k][c] float4 rows.
   constexpr int C0 = 3 + D, CG = C1 / 4, PPB = 256 / CG;  // channel groups, points per block
@@ -92,7 +94,12 @@ __global__ __launch_bounds__(256) void sa_pre_kernel(const float* __restrict__ f
   const int64_t i = static_cast<int64_t>(blockIdx.x) * PPB + threadIdx.x / CG;
   if (i >= static_cast<int64_t>(B) * N) return;
   const int b = static_cast<int>(i / N), n = static_cast<int>(i % N);
-  const float4* fr = reinterpret_cast<const float4*>(feat + b * fb + static_cast<int64_t>(n) * fn);
+  int64_t src = n;
+  if (rows) {
+    const int64_t r = rows[i];
+    src = r < 0 ? 0 : (r >= Nf ? Nf - 1 : r);
+  }
+  const float4* fr = reinterpret_cast<const float4*>(feat + b * fb + src * fn);
   float4 acc = bias[g];
 #pragma unroll 4
   for (int v = 0; v < D / 4; ++v) {
@@ -322,7 +329,7 @@ template <typename T, int D, int C1, int C2>
 int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, const void* c, int64_t cb, int64_t cc,
                    int64_t cn, int S, int B, const float* feat, int64_t fb, int64_t fn, const int32_t* count,
                    const int32_t* list, int nsample, const float* params, float* U, int32_t* order, float* out,
-                   hipStream_t st) {
+                   const int64_t* frows, int Nf, hipStream_t st) {
   PointsView<T> pv{static_cast<const T*>(xyz), sb, sc, sn};
   PointsView<T> cv{static_cast<const T*>(c), cb, cc, cn};
   const int64_t centres = static_cast<int64_t>(B) * S;
@@ -333,7 +340,7 @@ int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, c
   if (U) {
     const int64_t rows = static_cast<int64_t>(B) * N;
     hipLaunchKernelGGL((sa_pre_kernel<D, C1>), dim3(ceil_div(rows, 256 / (C1 / 4))), dim3(256), 0, st, feat, fb, fn, N,
-                       B, params, U);
+                       B, params, U, frows, Nf);
     hipLaunchKernelGGL((sa_mlp_mfma_kernel<T, D, C1, C2, true>), dim3(grid), dim3(kMfmaWaves * kWave), 0, st, pv, cv,
                        S, B, feat, fb, fn, count, list, nsample, params, U, static_cast<int64_t>(N) * C1, order, out, xcd);
   } else {
@@ -347,7 +354,7 @@ int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, c
   template int launch_sa_mfma<T, D, C1, C2>(const void*, int64_t, int64_t, int64_t, int, const void*, int64_t,  \
                                             int64_t, int64_t, int, int, const float*, int64_t, int64_t,         \
                                             const int32_t*, const int32_t*, int, const float*, float*,          \
-                                            int32_t*, float*, hipStream_t);
+                                            int32_t*, float*, const int64_t*, int, hipStream_t);
 DVCP_SA_MFMA_INST(float, 32, 32, 64)
 DVCP_SA_MFMA_INST(double, 32, 32, 64)
 DVCP_SA_MFMA_INST(float, 64, 64, 64)

@@ -32,7 +32,10 @@ SIGNATURES = {
                           _P, _P, _I, _I, _P, _P, _P, _P],
     "dvcp_sa_group_mlp_ws": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _L, _L, _L, _I,
                              _P, _P, _I, _I, _P, _P, _P, _P, _P],
+    "dvcp_sa_group_mlp_rows_ws": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _P, _L, _L, _I, _I, _P,
+                                  _P, _P, _I, _I, _P, _P, _P, _P, _P],
     "dvcp_fe_head": [_P, _I, _P, _P, _P, _P],
+    "dvcp_fe_head_rows": [_P, _P, _I, _I, _I, _P, _P, _P, _P],
     "dvcp_weighting": [_P, _I, _P, _P, _P],
     "dvcp_topk": [_P, _I, _I, _I, _P, _P],
     "dvcp_src_keypoints": [_I, _P, _P, _I, _P, _I, _I, _P, _D, _I, _P, _L, _P, _P, _P, _P],

@@ -74,38 +74,55 @@ class feat_extraction_layer(nn.Module):
             ev.record(main)
             events.append(ev)
             prev = c
+        # Inference folds the gathers of per-point layers into their consumers: the next layer's
+        # MLP reads its features through the FPS indices (dvcp_sa_group_mlp_rows_ws) and the head
+        # reads sa3's rows the same way (dvcp_fe_head_rows).  Training (``saved``) keeps the
+        # gathered tables, which its backward consumes.
+        fold = saved is None
         with torch.cuda.stream(side):
             pts_l, f = xyz, feat
+            f_rows = None  # (per-point table (B, Nf, C), FPS indices (B, n_l)): f is that gather
             for sa, i, c, ev in zip(layers, idxs, centres, events):
                 n_l = pts_l.shape[2]
                 ns = min(int(sa.nsample), n_l)
+                ctr_l = pts_l if sa.npoint >= n_l else c
+                if sa.npoint < n_l:
+                    side.wait_event(ev)
+                # Every point of a layer with npoint >= n_l becomes a centre (FPS output = a
+                # permutation, with repeats if npoint > n_l), and a centre's group and MLP depend
+                # only on its coordinates and the layer's point set.  So evaluate every point as its
+                # own centre now -- concurrently with this layer's FPS on the main stream -- and
+                # take the rows in FPS order once the indices exist.  Bit-identical results.
+                count, lst, _ = ops.ball_query(pts_l, ctr_l, sa.radius, ns, pdim=2, cdim_pts=2)
+                if f_rows is not None:
+                    res = ops.sa_group_mlp_rows(pts_l, ctr_l, f_rows[0], f_rows[1], count, lst, ns, sa.chans,
+                                                sa.packed_params())
+                else:
+                    res = ops.sa_group_mlp(pts_l, ctr_l, f, count, lst, ns, sa.chans, sa.packed_params(),
+                                           xyz_pdim=2, feat_ddim=1, feat_pdim=2)
+                f_rows = None
                 if sa.npoint >= n_l:
-                    # Every point of the layer becomes a centre (FPS output = a permutation, with
-                    # repeats if npoint > n_l), and a centre's group and MLP depend only on its
-                    # coordinates and the layer's point set.  So evaluate every point as its own
-                    # centre now -- concurrently with this layer's FPS on the main stream -- and
-                    # gather by the FPS indices once they exist.  Bit-identical results.
-                    count, lst, _ = ops.ball_query(pts_l, pts_l, sa.radius, ns, pdim=2, cdim_pts=2)
-                    per_point = ops.sa_group_mlp(pts_l, pts_l, f, count, lst, ns, sa.chans, sa.packed_params(),
-                                                 xyz_pdim=2, feat_ddim=1, feat_pdim=2)
                     side.wait_event(ev)
                     i.record_stream(side)
-                    out = torch.gather(per_point, 1, i.unsqueeze(-1).expand(-1, -1, per_point.shape[2]))
-                    ctr_l = pts_l
+                    if fold:
+                        f_rows = (res, i)
+                        out = None
+                    else:
+                        out = torch.gather(res, 1, i.unsqueeze(-1).expand(-1, -1, res.shape[2]))
                 else:
-                    side.wait_event(ev)
-                    count, lst, _ = ops.ball_query(pts_l, c, sa.radius, ns, pdim=2, cdim_pts=2)
-                    out = ops.sa_group_mlp(pts_l, c, f, count, lst, ns, sa.chans, sa.packed_params(),
-                                           xyz_pdim=2, feat_ddim=1, feat_pdim=2)
-                    ctr_l = c
+                    out = res
                 if saved is not None:
                     saved.setdefault("layers", []).append(dict(pts=pts_l, ctr=ctr_l, feat=f, count=count, lst=lst,
                                                                ns=ns, idx=i, per_point=sa.npoint >= n_l))
                 c.record_stream(side)
-                pts_l, f = c, out.permute(0, 2, 1)
+                pts_l, f = c, (out.permute(0, 2, 1) if out is not None else None)
             S = pts_l.shape[2]
-            f3 = f.permute(0, 2, 1).reshape(B * S, 64)  # sa output is (B, S, 64) in memory
-            head, score = ops.fe_head(f3, self.fc_params(wl), with_score=wl is not None)
+            if f_rows is not None:
+                f3 = None
+                head, score = ops.fe_head_rows(f_rows[0], f_rows[1], self.fc_params(wl), with_score=wl is not None)
+            else:
+                f3 = f.permute(0, 2, 1).reshape(B * S, 64)  # sa output is (B, S, 64) in memory
+                head, score = ops.fe_head(f3, self.fc_params(wl), with_score=wl is not None)
         if saved is not None:
             saved["f3"] = f3
         if side is not main:

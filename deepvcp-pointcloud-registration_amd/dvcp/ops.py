@@ -109,6 +109,31 @@ def sa_group_mlp(xyz, ctr, feat, count, lst, nsample, chans, params, xyz_pdim=2,
     return out
 
 
+def sa_group_mlp_rows(xyz, ctr, feat, rows, count, lst, nsample, chans, params, xyz_pdim=2):
+    """``sa_group_mlp`` for the two-layer tables with point n of cloud b taking feature row
+    ``rows[b, n]`` of ``feat`` (B, Nf, D) fp32 point-major: the previous layer's per-point rows
+    gathered by its FPS order (pointnet2_utils.py:59) without materialising the gathered table."""
+    _lib.require_gpu(xyz, ctr, feat, rows, count, lst, params)
+    B = xyz.shape[0]
+    N, sb, sc, sn = _pts(xyz, xyz_pdim)
+    S, cb, cc, cn = _pts(ctr, 2)
+    Nf, D = feat.shape[1], feat.shape[2]
+    if feat.dtype != torch.float32 or feat.stride(2) != 1 or rows.dtype != torch.int64 or tuple(rows.shape) != (B, N):
+        raise ValueError("sa_group_mlp_rows: feat must be (B, Nf, D) fp32 with contiguous rows, rows (B, N) int64")
+    rows = rows.contiguous()
+    ch = torch.tensor(list(chans), dtype=torch.int32)
+    out = torch.empty(B, S, chans[-1], dtype=torch.float32, device=xyz.device)
+    macs = sum(a * b for a, b in zip(chans[:-1], chans[1:]))
+    ws_bytes = _lib.load().dvcp_sa_group_mlp_workspace_bytes(B, N, S, len(chans) - 1, ch.data_ptr())
+    ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=xyz.device)
+    call("dvcp_sa_group_mlp_rows_ws", dtype_code(xyz), ptr(xyz), sb, sc, sn, N, ptr(ctr), cb, cc, cn, S, B,
+         ptr(feat), feat.stride(0), feat.stride(1), Nf, D, ptr(rows), ptr(count), ptr(lst), int(nsample),
+         len(chans) - 1, ptr(ch), ptr(params), ptr(out), ptr(ws), stream(),
+         work=(2.0 * macs * B * S * nsample, B * S * (4 * nsample + 4 * chans[-1]) + B * N * (4 * (3 + D) + 8),
+               _sa_exec_flops(chans, B, N, S, nsample)))
+    return out
+
+
 def _sa_exec_flops(chans, B, N, S, nsample):
     """Flops the kernels execute (upper bound: padded rows counted): the two-layer MFMA tables
     split layer 1 into a per-point part (D x C1 per input point) and a per-row part (3 x C1), and
@@ -126,6 +151,22 @@ def fe_head(x, params, with_score):
     feat = torch.empty(P, 32, dtype=torch.float32, device=x.device)
     score = torch.empty(P, dtype=torch.float32, device=x.device) if with_score else None
     call("dvcp_fe_head", ptr(x), P, ptr(params), ptr(feat), ptr(score), stream())
+    return feat, score
+
+
+def fe_head_rows(x, rows, params, with_score):
+    """``fe_head`` on x (B, Nx, 64) fp32 rows gathered per cloud by ``rows`` (B, S) int64 (sa3's
+    per-point rows in its FPS order, pointnet2_utils.py:59), without materialising the gather."""
+    _lib.require_gpu(x, rows, params)
+    B, Nx, C = x.shape
+    if C != 64 or x.dtype != torch.float32 or not x.is_contiguous() or rows.dtype != torch.int64 or rows.shape[0] != B:
+        raise ValueError("fe_head_rows: x must be contiguous (B, Nx, 64) fp32 and rows (B, S) int64")
+    rows = rows.contiguous()
+    S = rows.shape[1]
+    P = B * S
+    feat = torch.empty(P, 32, dtype=torch.float32, device=x.device)
+    score = torch.empty(P, dtype=torch.float32, device=x.device) if with_score else None
+    call("dvcp_fe_head_rows", ptr(x), ptr(rows), S, Nx, P, ptr(params), ptr(feat), ptr(score), stream())
     return feat, score
 
 

@@ -130,12 +130,31 @@ int dvcp_sa_group_mlp_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, int
                          int nlayer, const int* chans, const float* params, float* out,
                          void* workspace, void* stream);
 
+/* dvcp_sa_group_mlp_ws for the two-layer tables with the features given through a row map:
+ * point n of cloud b takes row feat_rows[b * N + n] (int64, clamped to [0, Nf)) of the fp32
+ * point-major table feat (cloud stride fb, row stride fn, 16-B aligned rows, Nf rows per cloud).
+ * This folds the gather of the previous layer's per-point rows by its FPS order
+ * (pointnet2_utils.py:59 index_points on the layer's new_points) into the MLP's per-point
+ * pre-pass, so the gathered table is never written.  Needs the workspace. */
+int dvcp_sa_group_mlp_rows_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
+                              const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
+                              const float* feat, int64_t fb, int64_t fn, int Nf, int D,
+                              const int64_t* feat_rows, const int32_t* count, const int32_t* list,
+                              int nsample, int nlayer, const int* chans, const float* params, float* out,
+                              void* workspace, void* stream);
+
 /* Per-point affine + weighting MLP.  Replaces deep_feat_extraction.py:15 (fc, applied per
  * REF-R R1) and weighting_layer.py:26-30 (Linear 32-16-8-1, ReLU, ReLU, Softplus).
  * x: P x 64 fp32 -> feat: P x 32 fp32 (= fc(x)); score (optional, may be NULL): P fp32.
  * params: fc.W(32x64), fc.b(32) [, wl1.W(16x32), wl1.b, wl2.W(8x16), wl2.b, wl3.W(1x8), wl3.b]. */
 int dvcp_fe_head(const float* x, int P, const float* params, float* feat, float* score,
                  void* stream);
+
+/* dvcp_fe_head on rows gathered per cloud: output row i reads x row (i / S) * Nx + rows[i]
+ * (int64, clamped to [0, Nx)); P = clouds x S.  Folds the gather of sa3's per-point rows by its
+ * FPS order (pointnet2_utils.py:59) into the head's load. */
+int dvcp_fe_head_rows(const float* x, const int64_t* rows, int S, int Nx, int P, const float* params,
+                      float* feat, float* score, void* stream);
 
 /* Weighting layer alone.  Replaces weighting_layer.py:26-30 on given features:
  * feat: P x 32 fp32 -> score: P fp32.  params: wl1.W(16x32), wl1.b, wl2.W(8x16), wl2.b,

@@ -186,6 +186,10 @@ def _bq_case(case, g):
         ctr[0, 5, 2] = float("nan")
         ctr[1, 600, 0] = float("-inf")
         return xyz, ctr, [(0.25, 64), (0.5, 16)]
+    if case == "clouds16":
+        # B % 8 == 0: the tiled kernel's XCD-aware cloud mapping
+        xyz = torch.randint(-16, 17, (16, 2000, 3), generator=g).float() / 16
+        return xyz, xyz[:, :600].contiguous(), [(0.25, 64)]
     if case == "wide":
         # above 16384 points: the large-bitmap tiled instantiation (C5's sa1 uses N = 65536)
         xyz = torch.randint(-32, 33, (1, 20000, 3), generator=g).float() / 32
@@ -197,21 +201,21 @@ def _bq_case(case, g):
     raise ValueError(case)
 
 
-@pytest.mark.parametrize("case", ["kitti", "clusters", "ragged", "boundary", "nonfinite", "wide", "untiled"])
+@pytest.mark.parametrize("case", ["kitti", "clusters", "ragged", "boundary", "nonfinite", "wide", "untiled", "clouds16"])
 def test_ball_query_pruned_vs_oracle(cuda, case):
     """The spatially pruned fp32 ball query (tiles + per-wave candidate bitmap) against the
     oracle (pointnet2_utils.py:87-107 restated); exact where every d2 is exact (dyadic inputs),
     else only radius-boundary rounding may differ."""
     import oracle as O
     from dvcp import ops
-    g = torch.Generator().manual_seed(["kitti", "clusters", "ragged", "boundary", "nonfinite", "wide", "untiled"].index(case) + 140)
+    g = torch.Generator().manual_seed(["kitti", "clusters", "ragged", "boundary", "nonfinite", "wide", "untiled", "clouds16"].index(case) + 140)
     xyz, ctr, radii = _bq_case(case, g)
     for r, ns in radii:
         ns = min(ns, xyz.shape[1])
         want = O.query_ball_point(r, ns, xyz, ctr)
         cnt, lst, pad = ops.ball_query(xyz.to(cuda), ctr.to(cuda), r, ns, padded=True)
         got = pad.cpu()
-        if case in ("boundary", "nonfinite", "wide", "untiled"):
+        if case in ("boundary", "nonfinite", "wide", "untiled", "clouds16"):
             assert torch.equal(got, want), (case, r, ns)
         else:
             assert ball_mismatch_ok(xyz, ctr, got, want, r), (case, r, ns)
@@ -416,6 +420,37 @@ def test_fe_head_and_weighting(cuda):
     torch.testing.assert_close(score.cpu(), s_ref, rtol=1e-5, atol=1e-6)
     s2 = mine_wl.scores(f_ref.view(1, 5000, 32).to(cuda))
     torch.testing.assert_close(s2.cpu()[0], s_ref, rtol=1e-5, atol=1e-6)
+
+
+def test_row_map_entries_equal_gather(cuda):
+    """dvcp_sa_group_mlp_rows_ws and dvcp_fe_head_rows (the FE's folded FPS-order gathers) give
+    bit-for-bit what the plain entries give on the torch-gathered tables, including repeated and
+    out-of-order rows."""
+    import dvcp
+    import dvcp.pointnet2_utils as P
+    from dvcp import ops
+    g = torch.Generator().manual_seed(121)
+    B, Nf, N = 3, 1200, 1000
+    for D, chans, radius in ((32, (35, 32, 64), 0.2), (64, (67, 64, 64), 0.4)):
+        sa = P.PointNetSetAbstraction(npoint=N, radius=radius, nsample=64, in_channel=3 + D, mlp=list(chans[1:]))
+        sa = sa.eval().to(cuda)
+        table = torch.randn(B, Nf, D, generator=g).to(cuda)
+        rows = torch.randint(0, Nf, (B, N), generator=g).to(cuda)
+        xyz = (torch.rand(B, 3, N, generator=g) * 2 - 1).to(cuda)
+        count, lst, _ = ops.ball_query(xyz, xyz, radius, 64, pdim=2, cdim_pts=2)
+        gathered = torch.gather(table, 1, rows.unsqueeze(-1).expand(-1, -1, D))          # (B, N, D)
+        want = ops.sa_group_mlp(xyz, xyz, gathered.permute(0, 2, 1), count, lst, 64, chans, sa.packed_params(),
+                                xyz_pdim=2, feat_ddim=1, feat_pdim=2)
+        got = ops.sa_group_mlp_rows(xyz, xyz, table, rows, count, lst, 64, chans, sa.packed_params())
+        assert torch.equal(got, want), D
+    fe = dvcp.feat_extraction_layer(use_normal=False, npoint=16).eval().to(cuda)
+    wl = dvcp.weighting_layer().eval().to(cuda)
+    x = torch.randn(B, Nf, 64, generator=g).to(cuda)
+    rows = torch.randint(0, Nf, (B, N), generator=g).to(cuda)
+    gathered = torch.gather(x, 1, rows.unsqueeze(-1).expand(-1, -1, 64)).reshape(B * N, 64)
+    f1, s1 = ops.fe_head(gathered, fe.fc_params(wl), with_score=True)
+    f2, s2 = ops.fe_head_rows(x, rows, fe.fc_params(wl), with_score=True)
+    assert torch.equal(f1, f2) and torch.equal(s1, s2)
 
 
 def test_topk(cuda):
