@@ -140,7 +140,7 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
 #pragma unroll
     for (int i = 0; i < kTW; ++i) {
       const int g = 16 * (wave + kW * i) + l16;
-      vx[i] = g < C ? cpg_halo(g, dG, dGG, PG, PGG) : 0;
+      vx[i] = cpg_halo(g < C ? g : 0, dG, dGG, PG, PGG);  // rows past C: voxel 0 (in-bounds taps, result unused)
     }
     f32x4 acc[kTW];
 #pragma unroll
@@ -369,7 +369,7 @@ __global__ __launch_bounds__(kCbThreads) void cpg_bwd_kernel(const float* __rest
 #pragma unroll
     for (int i = 0; i < kTW; ++i) {
       const int g = 16 * (wave + kW * i) + l16;
-      vx[i] = g < C ? cpg_halo(g, dG, dGG, PG, PGG) : 0;
+      vx[i] = cpg_halo(g < C ? g : 0, dG, dGG, PG, PGG);  // rows past C: voxel 0 (in-bounds taps, result unused)
     }
 #pragma unroll 1
     for (int cb = 0; cb < 2; ++cb) {

@@ -24,9 +24,10 @@ def _close(got, want, tol, what, floor=1e-30):
     return err / scale
 
 
-@pytest.mark.parametrize("B,K,r,s", [(2, 3, 1.0, 0.4), (1, 2, 2.0, 0.4)])
+@pytest.mark.parametrize("B,K,r,s", [(2, 3, 1.0, 0.4), (1, 2, 2.0, 0.4), (1, 3, 0.4, 0.4), (2, 2, 0.2, 0.4)])
 def test_cpg_backward_vs_oracle(cuda, B, K, r, s):
-    """cpg.py:27-60 backward: d src, d tgt (the (B,K,32,C) view), d conv weights."""
+    """cpg.py:27-60 backward: d src, d tgt (the (B,K,32,C) view), d conv weights.  G = 6, 11 and
+    the small grids G = 3, 2 (a single partial 16-voxel MFMA row tile, padding rows past C)."""
     import oracle as O
     import dvcp
     G = int(2 * r / s + 1)
