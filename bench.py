@@ -33,15 +33,17 @@ sys.path.insert(0, os.path.join(ROOT, "deepvcp-pointcloud-registration_amd"))
 # Hardware queues per process (read when HIP initialises, so set before torch touches the GPU).
 # Each in-flight batch drives two streams (the FPS chain and its side stream); with HIP's default
 # of 4 queues, streams that share a queue serialise behind each other's multi-millisecond FPS
-# launches.  8 measured +13% over 4; 16 (8 batches in flight x 2 streams) is the default, and
-# 24 queues or 12-16 batches measured no better (profiles/README.md).  --hw-queues overrides.
+# launches.  8 measured +13% over 4.  With the round-2 kernels, 10 batches in flight on 24 queues
+# measured ~1510 pairs/s against ~1413 for 8 on 16 (same box, 3 alternating reps each; 12 batches
+# drop to ~1260: profiles/round2/r2s_inflight_sweep*.log), so that is the default.  --hw-queues
+# overrides.
 def _hw_queues(argv):
     for i, a in enumerate(argv):
         if a == "--hw-queues" and i + 1 < len(argv):
             return argv[i + 1]
         if a.startswith("--hw-queues="):
             return a.split("=", 1)[1]
-    return "16"
+    return "24"
 
 
 os.environ["GPU_MAX_HW_QUEUES"] = _hw_queues(sys.argv)
@@ -68,10 +70,10 @@ def parse():
     p.add_argument("--K", type=int, default=None)
     p.add_argument("--r", type=float, default=2.0)
     p.add_argument("--s", type=float, default=0.4)
-    p.add_argument("--inflight", type=int, default=8,
+    p.add_argument("--inflight", type=int, default=10,
                    help="independent batches in flight (one stream each); 1 = strictly serial steps")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--hw-queues", type=int, default=16, help="GPU_MAX_HW_QUEUES for this process (<= 32)")
+    p.add_argument("--hw-queues", type=int, default=24, help="GPU_MAX_HW_QUEUES for this process (<= 32)")
     p.add_argument("--stage-report", action="store_true", help="print the per-kernel table to stderr")
     p.add_argument("--no-kernel-events", action="store_true",
                    help="diagnostic: no per-launch HIP events in the timed region")
