@@ -187,7 +187,7 @@ def main():
     S = model.FE1.sa1.npoint
     C = int((2 * r) / s + 1) ** 3
     stages, step_roof = stage_roofline(iso, args.iso_steps, floor_us, ms_step)
-    roofline = fps_roofline(live, iso, floor_us)
+    roofline = fps_roofline(live, iso, floor_us, traffic_ok=args.config == "c3")
     res_cpu = res.cpu()
     reg_err = {"rot_deg_mean": float(res_cpu[:, 12].mean()), "rot_deg_max": float(res_cpu[:, 12].max()),
                "trans_mean": float(res_cpu[:, 13].mean()), "trans_max": float(res_cpu[:, 13].max()),
@@ -313,9 +313,11 @@ def stage_roofline(iso, iso_steps, floor_us, ms_step):
     return stages, roof
 
 
-def fps_roofline(live, iso, floor_us):
+def fps_roofline(live, iso, floor_us, traffic_ok=True):
     """FPS is a serial chain of npoint dependent argmax steps per cloud: latency-bound, so its
-    roofline is microseconds per step against the measured step floor (dvcp_fps_step_floor)."""
+    roofline is microseconds per step against the measured step floor (dvcp_fps_step_floor).
+    ``traffic`` is the PMC figure of profiles/pmc_summary.json, which is measured at C3: null for
+    other configurations."""
     name = "dvcp_fps_ws"
     if name not in iso:
         return None
@@ -324,7 +326,8 @@ def fps_roofline(live, iso, floor_us):
     us_live = w["ms"] * 1e3 / w["steps"] if w and w["steps"] else None
     return {"bound": "latency", "kernel": name, "unit": "us/step", "achieved": round(us_iso, 4),
             "peak": round(floor_us, 4), "frac": round(floor_us / us_iso, 4),
-            "traffic": _pmc_traffic(name), "avg_launch_ms_isolated": round(v["ms"] / v["n"], 4),
+            "traffic": _pmc_traffic(name) if traffic_ok else None,
+            "avg_launch_ms_isolated": round(v["ms"] / v["n"], 4),
             "avg_launch_ms_live": round(w["ms"] / w["n"], 4) if w else None,
             "us_per_step_live": round(us_live, 4) if us_live else None,
             "algorithmic_bytes_per_launch": v["bytes"] / v["n"],
