@@ -70,10 +70,10 @@ def test_fps_live_vs_oracle(cuda):
 
 
 @pytest.mark.parametrize("case", ["dyadic", "duplicates", "surface", "npoint_gt_n", "f64"])
-def test_fps_batched_vs_oracle(cuda, case):
-    """The batched kernel (N >= 2048) on inputs that stress its exactness argument: equal
-    running minima everywhere (dyadic grid), exact duplicate points, a 2-D surface, npoint > N
-    (all minima reach 0), and fp64 coordinates."""
+def test_fps_select_vs_oracle(cuda, case):
+    """The threshold-select kernel (N >= 2048) on inputs that stress its exactness argument:
+    equal running minima everywhere (dyadic grid: the one-argmax fallback), exact duplicate
+    points, a 2-D surface, npoint > N (all minima reach 0), and fp64 coordinates."""
     import oracle as O
     import dvcp.pointnet2_utils as P
     g = torch.Generator().manual_seed(["dyadic", "duplicates", "surface", "npoint_gt_n", "f64"].index(case) + 200)

@@ -2,7 +2,7 @@
 
 Layer inputs mirror the FE: sa1 = 16384 points -> 10000 FPS centres (r 0.1, ns 256); sa2/sa3 =
 the 10000 centres against themselves (r 0.2 / 0.4, ns 128 / 64).  Prints ms per call (CUDA
-events) and the mean hit count.  DVCP_BQ_SCAN=1 selects the index-order scan for an A/B."""
+events) and the mean hit count."""
 import os
 import sys
 
@@ -36,8 +36,7 @@ def main():
         torch.cuda.synchronize()
         cf = cnt.float()
         print(f"{name}: {e0.elapsed_time(e1) / reps:.4f} ms/call  mean hits {cf.mean().item():.1f}"
-              f" max {cf.max().item():.0f} p99 {cf.flatten().quantile(0.99).item():.0f}"
-              f"  scan={os.environ.get('DVCP_BQ_SCAN', '0')}", flush=True)
+              f" max {cf.max().item():.0f} p99 {cf.flatten().quantile(0.99).item():.0f}", flush=True)
 
 
 if __name__ == "__main__":

@@ -51,8 +51,8 @@ def main():
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
     flops = 2.0 * (35 * 32 + 32 * 32 + 32 * 32) * 32 * qry.shape[0] * qry.shape[1]
-    print(f"dfe_tgt: {ms:.4f} ms/call  {flops / ms / 1e9:.1f} TFLOP/s  checksum {y.double().sum().item():.6e}"
-          f"  valu={os.environ.get('DVCP_DFE_VALU', '0')}", flush=True)
+    print(f"dfe_tgt: {ms:.4f} ms/call  {flops / ms / 1e9:.1f} TFLOP/s  checksum {y.double().sum().item():.6e}",
+          flush=True)
 
     # corresponding point generation on these embeddings (src side random)
     cpg = dvcp.cpg().eval().to(dev)
