@@ -61,6 +61,10 @@ SIGNATURES = {
     "dvcp_sa_group_mlp_backward": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _L, _L, _L, _I,
                                    _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P],
     "dvcp_fe_head_backward": [_P, _I, _P, _P, _P, _P, _P, _P],
+    "dvcp_sa_bn_stats": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _L, _L, _L, _I,
+                         _P, _P, _I, _I, _P, _P, _I, _P, _P, _P],
+    "dvcp_sa_bn_backward": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _L, _L, _L, _I,
+                            _P, _P, _I, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P],
 }
 
 _lib = None
@@ -98,6 +102,10 @@ def load():
                                                                ctypes.c_void_p]
     lib.dvcp_fe_head_backward_workspace_bytes.restype = ctypes.c_int64
     lib.dvcp_fe_head_backward_workspace_bytes.argtypes = [ctypes.c_int]
+    lib.dvcp_sa_bn_workspace_bytes.restype = ctypes.c_int64
+    lib.dvcp_sa_bn_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    lib.dvcp_sa_bn_pack_floats.restype = ctypes.c_int64
+    lib.dvcp_sa_bn_pack_floats.argtypes = [ctypes.c_int, ctypes.c_void_p]
     for name, args in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = ctypes.c_int
@@ -111,7 +119,8 @@ def exported_symbols():
             "dvcp_knn_tiled_workspace_bytes", "dvcp_ball_query_workspace_bytes",
             "dvcp_sa_group_mlp_workspace_bytes", "dvcp_dfe_backward_workspace_bytes",
             "dvcp_cpg_backward_workspace_bytes", "dvcp_sa_group_mlp_backward_workspace_bytes",
-            "dvcp_fe_head_backward_workspace_bytes"] + list(SIGNATURES)
+            "dvcp_fe_head_backward_workspace_bytes", "dvcp_sa_bn_workspace_bytes",
+            "dvcp_sa_bn_pack_floats"] + list(SIGNATURES)
 
 
 # When a list, every entry-point call appends (name, start_event, end_event, work) recorded on

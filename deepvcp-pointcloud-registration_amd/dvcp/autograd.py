@@ -14,21 +14,21 @@ feature extractor.  Here the head's backward runs in hand-written HIP kernels:
   * ``src_keypoints`` -- the key-point stage, differentiable in the source features (the
                       pointnet2_utils.py:59 gather, dvcp_src_keypoints_backward).
 
-  * ``feat_extraction`` -- the feature extractor (deep_feat_extraction.py:18-32 + REF-R R1) with
-                      its BatchNorm layers in eval mode (frozen-BN training: FE1.eval() with trainable
-                      parameters): fc (dvcp_fe_head_backward) and the three set-abstraction MLPs
-                      (dvcp_sa_group_mlp_backward), chained through the FPS-order gathers and the
-                      ball-query groupings.
+  * ``feat_extraction`` -- the feature extractor (deep_feat_extraction.py:18-32 + REF-R R1): fc
+                      (dvcp_fe_head_backward) and the three set-abstraction MLPs, chained through the
+                      FPS-order gathers and the ball-query groupings.  BatchNorm in eval mode
+                      (frozen-BN training, FE1.eval()): dvcp_sa_group_mlp_backward; in training mode
+                      (batch statistics, model.train() as train.py does): dvcp_sa_bn_backward
+                      (dvcp/batchnorm.py).
 
 The key points, candidates and kNN indices carry no gradient in the reference either (index
 ops, knn_cuda under no_grad); the weighting layer gets none (only its top-k indices are used).
-A feature extractor in training mode (batch-statistics BN) is not implemented: DeepVCP.forward
-raises rather than silently computing something else.  Parameter gradients come back summed over
+Parameter gradients come back summed over
 the batch in a fixed order (deterministic); the feature scatters use float atomics.
 """
 import torch
 
-from . import ops
+from . import batchnorm, ops
 
 
 def _pack(weights):
@@ -190,9 +190,12 @@ class _FeatExtract(torch.autograd.Function):
             n_l = lay["pts"].shape[2]
             g_out = _scatter_rows(g, lay["idx"], n_l) if lay["per_point"] else g
             first = sa is fe.sa1
-            gp, g_in = ops.sa_group_mlp_backward(lay["pts"], lay["ctr"], lay["feat"], lay["count"], lay["lst"],
-                                                 lay["ns"], sa.chans, sa.packed_params(), _bn_stats(sa), g_out,
-                                                 want_feat_grad=not first)
+            if lay["bn"] is not None:   # training-mode BN: batch statistics (dvcp/batchnorm.py)
+                gp, g_in = batchnorm.train_backward(sa, lay, g_out, want_feat_grad=not first)
+            else:
+                gp, g_in = ops.sa_group_mlp_backward(lay["pts"], lay["ctr"], lay["feat"], lay["count"], lay["lst"],
+                                                     lay["ns"], sa.chans, sa.packed_params(), _bn_stats(sa), g_out,
+                                                     want_feat_grad=not first)
             per_layer.append((sa, gp))
             g = g_in  # (B, n_l, D): the previous layer's outputs, in its centre order
         for sa, gp in reversed(per_layer):
@@ -209,7 +212,7 @@ class _FeatExtract(torch.autograd.Function):
 
 
 def feat_extraction(fe, pts, starts, wl=None, side_stream=None):
-    """FE1.run differentiable in FE1's parameters (eval-mode BN): -> (xyz, feat, score)."""
+    """FE1.run differentiable in FE1's parameters (BN in FE1's mode): -> (xyz, feat, score)."""
     return _FeatExtract.apply(fe, pts, starts, wl, side_stream, *_fe_params(fe))
 
 

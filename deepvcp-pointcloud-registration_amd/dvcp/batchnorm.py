@@ -1,0 +1,98 @@
+"""Batch-statistics BatchNorm for the grouped set-abstraction MLP (training mode).
+
+The reference trains the whole model in ``model.train()`` (train.py:105-125), so every
+``F.relu(bn(conv(x)))`` of pointnet2_utils.py:195-200 normalises with the statistics of the current
+batch over all B * S * nsample grouped entries (BatchNorm2d over (B, H, W); the padding slots of
+the ball query are entries like any other) and updates the running statistics (momentum, unbiased
+variance), once per FE1 call -- src and tgt are separate calls (deepVCP.py:29,72).
+
+Forward (``train_forward``): one statistics pass per layer (dvcp_sa_bn_stats: fp64 sums of z and
+z^2, the layers below normalised by their batch statistics), then the eval kernel
+(dvcp_sa_group_mlp) with the batch statistics folded into its scale / shift.
+Backward (``train_backward``): torch's batch-norm backward,
+    dz_l = scale_l (dy_l - mean(dy_l) - xhat_l mean(dy_l xhat_l)),
+whose mean terms make every entry's gradient non-zero: sums of the top layer over the routed
+(arg-max) rows, one dense pass per lower layer for its sums, and a final dense pass for dW, db and
+the feature gradient (dvcp_sa_bn_backward modes L..1, 0; csrc/sa_bn.hip).
+"""
+import torch
+
+from . import ops
+
+
+def _layer_offsets(chans):
+    """Per layer (offset, C_in, C_out) in the dvcp_sa_bn pack: W | bias | scale | shift | mean |
+    istd | A/M | B/M."""
+    offs, o = [], 0
+    for cin, cout in zip(chans[:-1], chans[1:]):
+        offs.append((o, cin, cout))
+        o += cout * cin + 7 * cout
+    return offs, o
+
+
+def _update_running(bn, mean, var, M):
+    """BatchNorm2d's running-statistics update in training mode (unbiased variance)."""
+    if not bn.track_running_stats:
+        return
+    with torch.no_grad():
+        bn.num_batches_tracked.add_(1)
+        f = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
+        unbiased = var * (M / max(M - 1, 1))
+        bn.running_mean.mul_(1.0 - f).add_(mean.to(bn.running_mean.dtype), alpha=f)
+        bn.running_var.mul_(1.0 - f).add_(unbiased.to(bn.running_var.dtype), alpha=f)
+
+
+def train_forward(sa, xyz, ctr, feat, count, lst, ns):
+    """pointnet2_utils.py:195-200 with ``sa`` in training mode, on (B, 3, N) points, (B, 3, S)
+    centres and (B, D, N) features.  Returns (out (B, S, C_last) fp32, state for the backward)."""
+    chans = sa.chans
+    offs, total = _layer_offsets(chans)
+    dev = xyz.device
+    B, S = ctr.shape[0], ctr.shape[2]
+    M = B * S * ns
+    parts = []
+    with torch.no_grad():
+        for conv, (o, cin, cout) in zip(sa.mlp_convs, offs):
+            one, zero = torch.ones(cout, device=dev), torch.zeros(cout, device=dev)
+            parts += [conv.weight.reshape(-1).float(), conv.bias.float(), one, zero, zero, one, zero, zero]
+        pack = torch.cat(parts).contiguous()
+        assert pack.numel() == total == ops.sa_bn_pack_floats(chans)
+        for layer, (bn, (o, cin, cout)) in enumerate(zip(sa.mlp_bns, offs), 1):
+            sums = ops.sa_bn_stats(xyz, ctr, feat, count, lst, ns, chans, pack, layer)
+            mean = sums[0] / M
+            var = (sums[1] / M - mean * mean).clamp_min(0.0)
+            istd = torch.rsqrt(var + bn.eps)
+            scale = bn.weight.double() * istd
+            shift = bn.bias.double() - mean * scale
+            v = o + cout * cin + cout
+            pack[v:v + 4 * cout] = torch.cat([scale, shift, mean, istd]).float()
+            _update_running(bn, mean, var, M)
+        fwd = torch.cat([pack[o:o + cout * cin + 3 * cout] for o, cin, cout in offs]).contiguous()
+    out = ops.sa_group_mlp(xyz, ctr, feat, count, lst, ns, chans, fwd)
+    return out, dict(pack=pack, M=M)
+
+
+def train_backward(sa, lay, g_out, want_feat_grad):
+    """Backward of ``train_forward``: (packed parameter gradient -- per layer dW, db, dgamma,
+    dbeta -- and dL/d feat (B, N, D) fp32 or None)."""
+    chans = sa.chans
+    offs, _ = _layer_offsets(chans)
+    st = lay["bn"]
+    pack, M = st["pack"].clone(), st["M"]
+    args = (lay["pts"], lay["ctr"], lay["feat"], lay["count"], lay["lst"], lay["ns"], chans)
+    g = g_out.float().contiguous()
+    sums = [None] * len(offs)
+    for k in range(len(offs), 0, -1):   # the top layer's sums first: each lower one needs those above
+        s = ops.sa_bn_backward(*args, pack, g, k)
+        o, cin, cout = offs[k - 1]
+        v = o + cout * cin + 5 * cout
+        pack[v:v + 2 * cout] = (s / M).reshape(-1).float()
+        sums[k - 1] = s
+    gp, gF = ops.sa_bn_backward(*args, pack, g, 0, want_feat_grad=want_feat_grad)
+    q = 0
+    for (o, cin, cout), s in zip(offs, sums):
+        q += cout * cin + cout
+        gp[q:q + cout] = s[1].float()          # dgamma = sum dy * xhat
+        gp[q + cout:q + 2 * cout] = s[0].float()  # dbeta = sum dy
+        q += 2 * cout
+    return gp, gF

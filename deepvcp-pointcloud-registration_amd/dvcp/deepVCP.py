@@ -47,20 +47,14 @@ class DeepVCP(nn.Module):
     def _training_mode(self):
         """(train_head, train_fe) for this forward (train.py:105-125).  Autograd records through
         the head (DFE, CPG) when it is enabled and any head or extractor parameter requires
-        gradients; through the feature extractor when its parameters require gradients.  The
-        extractor's BatchNorm must then be in eval mode (frozen-BN training, FE1.eval()): batch-
-        statistics BN is not implemented, and a module left in training mode raises instead of
-        silently computing something else."""
+        gradients; through the feature extractor when its parameters require gradients.  FE1's
+        BatchNorm follows FE1's mode like torch's: batch statistics (and running-statistics
+        updates) in training mode, running statistics after FE1.eval() (frozen-BN fine-tuning)."""
         head = [p for m in (self.DFE, self.cpg) for p in m.parameters()]
         fe_grad = any(p.requires_grad for p in self.FE1.parameters())
         grad = torch.is_grad_enabled()
         train_fe = grad and fe_grad
         train_head = grad and (any(p.requires_grad for p in head) or train_fe)
-        if self.FE1.training and (train_head or self.training):
-            raise NotImplementedError(
-                "dvcp.DeepVCP: the feature extractor trains with frozen BatchNorm only -- batch-statistics BN "
-                "(FE1 in training mode) is not implemented.  Call model.FE1.eval(); its parameters may stay "
-                "trainable (frozen-BN fine-tuning) or be frozen with model.FE1.requires_grad_(False).")
         if not train_head and self.training:
             raise NotImplementedError("dvcp.DeepVCP: training mode with autograd disabled or no trainable parameter")
         if not train_head:
@@ -80,8 +74,6 @@ class DeepVCP(nn.Module):
         no trainable head parameter, so with the extractor frozen a training loop can run it for
         upcoming batches on other streams while the current batch's head trains
         (tools/train_step_bench.py --prefetch)."""
-        if self.FE1.training:
-            _inference_only(self.FE1)
         _lib.require_gpu(src_pts, tgt_pts)   # no CPU fallback
         B = src_pts.shape[0]
         dev = src_pts.device
@@ -94,8 +86,9 @@ class DeepVCP(nn.Module):
                 return autograd.feat_extraction(self.FE1, pts, st, wl=wl, side_stream=side)
         else:
             run = self.FE1.run
-        if src_pts.shape == tgt_pts.shape and src_pts.dtype == tgt_pts.dtype:
+        if src_pts.shape == tgt_pts.shape and src_pts.dtype == tgt_pts.dtype and not self.FE1.training:
             # src and tgt share FE1's weights and eval-mode FE is per cloud: one 2B-cloud pass
+            # (in training mode each call normalises with its own batch statistics: two passes)
             # (the serial FPS chain then runs once for both clouds, on 2B workgroups)
             both = torch.cat([src_pts, tgt_pts], 0)
             fe_starts = [torch.cat([starts[i], starts[4 + i]]) for i in range(3)]

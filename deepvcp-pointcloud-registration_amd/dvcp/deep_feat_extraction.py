@@ -7,9 +7,9 @@ the reference feeds sa2/sa3 the raw normals and never applies ``fc``, which cras
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import batchnorm, ops
 from ._params import cached_pack, linear_pack, linear_tensors
-from .pointnet2_utils import PointNetSetAbstraction, _inference_only
+from .pointnet2_utils import PointNetSetAbstraction
 
 
 def fe_config(use_normal=True, npoint=10000):
@@ -50,8 +50,12 @@ class feat_extraction_layer(nn.Module):
         three FPS launches (the serial critical path) run back to back on the current stream
         while each layer's ball query + grouped MLP runs on ``side_stream``.  A layer whose FPS
         picks every point (npoint >= its point count, layers 2 and 3 of the reference) is
-        evaluated per point before its FPS finishes and gathered by the FPS order."""
-        _inference_only(self)
+        evaluated per point before its FPS finishes and gathered by the FPS order.
+
+        In training mode (``self.training``) the set-abstraction BatchNorms use batch statistics
+        over this call's grouped entries and update their running statistics (dvcp/batchnorm.py);
+        every layer is then evaluated on its FPS centres (the statistics are over the centres)."""
+        train_bn = self.training
         B, _, N = pts.shape
         if self.use_normal:
             xyz, feat = pts[:, :3, :], pts[:, 3:, :]
@@ -66,7 +70,6 @@ class feat_extraction_layer(nn.Module):
         idxs, centres, events = [], [], []
         prev = xyz
         for sa, st in zip(layers, starts):
-            _inference_only(sa)
             i, c = ops.fps(prev, sa.npoint, st.to(prev.device), pdim=2)
             idxs.append(i)
             centres.append(c)
@@ -78,15 +81,16 @@ class feat_extraction_layer(nn.Module):
         # MLP reads its features through the FPS indices (dvcp_sa_group_mlp_rows_ws) and the head
         # reads sa3's rows the same way (dvcp_fe_head_rows).  Training (``saved``) keeps the
         # gathered tables, which its backward consumes.
-        fold = saved is None
+        fold = saved is None and not train_bn
         with torch.cuda.stream(side):
             pts_l, f = xyz, feat
             f_rows = None  # (per-point table (B, Nf, C), FPS indices (B, n_l)): f is that gather
             for sa, i, c, ev in zip(layers, idxs, centres, events):
                 n_l = pts_l.shape[2]
                 ns = min(int(sa.nsample), n_l)
-                ctr_l = pts_l if sa.npoint >= n_l else c
-                if sa.npoint < n_l:
+                per_point = sa.npoint >= n_l and not train_bn
+                ctr_l = pts_l if per_point else c
+                if not per_point:
                     side.wait_event(ev)
                 # Every point of a layer with npoint >= n_l becomes a centre (FPS output = a
                 # permutation, with repeats if npoint > n_l), and a centre's group and MLP depend
@@ -94,14 +98,17 @@ class feat_extraction_layer(nn.Module):
                 # own centre now -- concurrently with this layer's FPS on the main stream -- and
                 # take the rows in FPS order once the indices exist.  Bit-identical results.
                 count, lst, _ = ops.ball_query(pts_l, ctr_l, sa.radius, ns, pdim=2, cdim_pts=2)
-                if f_rows is not None:
+                bn_state = None
+                if train_bn:
+                    res, bn_state = batchnorm.train_forward(sa, pts_l, ctr_l, f, count, lst, ns)
+                elif f_rows is not None:
                     res = ops.sa_group_mlp_rows(pts_l, ctr_l, f_rows[0], f_rows[1], count, lst, ns, sa.chans,
                                                 sa.packed_params())
                 else:
                     res = ops.sa_group_mlp(pts_l, ctr_l, f, count, lst, ns, sa.chans, sa.packed_params(),
                                            xyz_pdim=2, feat_ddim=1, feat_pdim=2)
                 f_rows = None
-                if sa.npoint >= n_l:
+                if per_point:
                     side.wait_event(ev)
                     i.record_stream(side)
                     if fold:
@@ -113,7 +120,7 @@ class feat_extraction_layer(nn.Module):
                     out = res
                 if saved is not None:
                     saved.setdefault("layers", []).append(dict(pts=pts_l, ctr=ctr_l, feat=f, count=count, lst=lst,
-                                                               ns=ns, idx=i, per_point=sa.npoint >= n_l))
+                                                               ns=ns, idx=i, per_point=per_point, bn=bn_state))
                 c.record_stream(side)
                 pts_l, f = c, (out.permute(0, 2, 1) if out is not None else None)
             S = pts_l.shape[2]

@@ -507,6 +507,66 @@ def sa_group_mlp_backward(xyz, ctr, feat, count, lst, nsample, chans, params, bn
     return gp, gF
 
 
+def _bn_common(xyz, ctr, feat, count, lst, nsample, chans, pack, xyz_pdim, feat_ddim, feat_pdim):
+    """The grouping arguments shared by dvcp_sa_bn_stats / dvcp_sa_bn_backward."""
+    _lib.require_gpu(xyz, ctr, count, lst, pack)
+    B = xyz.shape[0]
+    N, sb, sc, sn = _pts(xyz, xyz_pdim)
+    S, cb, cc, cn = _pts(ctr, 2)
+    if feat is not None:
+        st = feat.stride()
+        D = feat.shape[feat_ddim]
+        fb, fd, fn = st[0], st[feat_ddim], st[feat_pdim]
+        fdt = dtype_code(feat)
+    else:
+        D, fb, fd, fn, fdt = 0, 0, 0, 0, _lib.F32
+    ch = torch.tensor(list(chans), dtype=torch.int32)
+    nl = len(chans) - 1
+    ws_bytes = int(_lib.load().dvcp_sa_bn_workspace_bytes(B, S, nl, ch.data_ptr()))
+    ws = torch.empty(max(1, ws_bytes // 4), dtype=torch.float32, device=xyz.device)
+    args = (dtype_code(xyz), ptr(xyz), sb, sc, sn, N, ptr(ctr), cb, cc, cn, S, B, fdt, ptr(feat), fb, fd, fn, D,
+            ptr(count), ptr(lst), int(nsample), nl, ptr(ch), ptr(pack))
+    return args, ws, (B, N, S, D), ch
+
+
+def sa_bn_pack_floats(chans):
+    ch = torch.tensor(list(chans), dtype=torch.int32)
+    return int(_lib.load().dvcp_sa_bn_pack_floats(len(chans) - 1, ch.data_ptr()))
+
+
+def sa_bn_stats(xyz, ctr, feat, count, lst, nsample, chans, pack, layer, xyz_pdim=2, feat_ddim=1, feat_pdim=2):
+    """Training-mode BatchNorm statistics of the grouped MLP (pointnet2_utils.py:198 in train()):
+    (2, C_layer) fp64 = per-channel sum z and sum z^2 of layer ``layer``'s conv output over all
+    B * S * nsample grouped entries, the layers below it normalised by ``pack``."""
+    args, ws, (B, N, S, D), ch = _bn_common(xyz, ctr, feat, count, lst, nsample, chans, pack, xyz_pdim, feat_ddim,
+                                            feat_pdim)
+    sums = torch.empty(2, chans[layer], dtype=torch.float64, device=xyz.device)
+    macs = sum(a * b for a, b in zip(chans[:layer], chans[1:layer + 1]))
+    call("dvcp_sa_bn_stats", *args, int(layer), ptr(ws), ptr(sums), stream(),
+         work=(2.0 * macs * B * S * nsample, B * S * 4 * nsample + B * N * 4 * (3 + D)))
+    return sums
+
+
+def sa_bn_backward(xyz, ctr, feat, count, lst, nsample, chans, pack, grad_out, mode, want_feat_grad=False,
+                   xyz_pdim=2, feat_ddim=1, feat_pdim=2):
+    """Training-mode (batch-statistics) backward of the grouped MLP.  mode k >= 1: (2, C_k) fp64
+    sums (A_k = dbeta_k, B_k = dgamma_k); mode 0: (packed dW, db, 0, 0 per layer; dL/d feat
+    (B, N, D) fp32 or None)."""
+    args, ws, (B, N, S, D), ch = _bn_common(xyz, ctr, feat, count, lst, nsample, chans, pack, xyz_pdim, feat_ddim,
+                                            feat_pdim)
+    dev = xyz.device
+    g = grad_out.float().contiguous()
+    if mode > 0:
+        sums = torch.empty(2, chans[mode], dtype=torch.float64, device=dev)
+        call("dvcp_sa_bn_backward", *args, int(mode), ptr(g), None, ptr(ws), ptr(sums), None, stream())
+        return sums
+    npar = sum(a * b + 3 * b for a, b in zip(chans[:-1], chans[1:]))
+    gp = torch.empty(npar, dtype=torch.float32, device=dev)
+    gF = torch.zeros(B, N, D, dtype=torch.float32, device=dev) if (want_feat_grad and D > 0) else None
+    call("dvcp_sa_bn_backward", *args, 0, ptr(g), ptr(gF), ptr(ws), None, ptr(gp), stream())
+    return gp, gF
+
+
 def fe_head_backward(x, params, grad):
     """Backward of the feature extractor's fc (deep_feat_extraction.py:15) on rows x (P, 64):
     (packed dW | db, dL/dx (P, 64))."""

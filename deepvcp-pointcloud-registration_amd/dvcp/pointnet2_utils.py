@@ -2,13 +2,13 @@
 
 Same names, arguments and outputs as pointnet2_utils.py:19-202 (the part the DeepVCP forward
 uses); the work runs in hand-written gfx950 kernels (dvcp_fps, dvcp_ball_query,
-dvcp_sa_group_mlp, dvcp_square_distance).  Inference only: the fused set-abstraction has no
-backward yet, so training mode raises.
+dvcp_sa_group_mlp, dvcp_square_distance).  Training mode uses batch-statistics BatchNorm
+(dvcp/batchnorm.py); the backward runs through dvcp.autograd.feat_extraction.
 """
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import batchnorm, ops
 from ._params import bn_affine, cached_pack
 
 __all__ = ["square_distance", "index_points", "farthest_point_sample", "query_ball_point", "sample_and_group",
@@ -61,8 +61,8 @@ def sample_and_group(npoint, radius, nsample, xyz, points, returnidx=False, star
 
 def _inference_only(module):
     if module.training:
-        raise NotImplementedError(f"dvcp: {type(module).__name__} is inference-only (call .eval()); training "
-                                  "mode needs batch-statistics BN and backward kernels (SURVEY.md 8(f) rank 1)")
+        raise NotImplementedError(f"dvcp: {type(module).__name__}.forward in training mode needs autograd "
+                                  "(train through DeepVCP.forward with gradients enabled) or .eval()")
 
 
 class PointNetSetAbstraction(nn.Module):
@@ -100,14 +100,18 @@ class PointNetSetAbstraction(nn.Module):
         return cached_pack(self, "sa", tensors, build)
 
     def forward(self, xyz, points, start=None):
-        """xyz (B, 3, N), points (B, D, N) or None -> new_xyz (B, 3, S), features (B, D', S)."""
-        _inference_only(self)
+        """xyz (B, 3, N), points (B, D, N) or None -> new_xyz (B, 3, S), features (B, D', S).
+        In training mode the BatchNorms use batch statistics and update their running statistics
+        (forward only here; autograd runs through dvcp.autograd.feat_extraction)."""
         B, _, N = xyz.shape
         if start is None:
             start = torch.randint(0, N, (B,), dtype=torch.long)
         _, new_xyz = ops.fps(xyz, self.npoint, start.to(xyz.device), pdim=2)
         ns = min(int(self.nsample), N)
         count, lst, _ = ops.ball_query(xyz, new_xyz, self.radius, ns, pdim=2, cdim_pts=2)
+        if self.training:
+            out, _ = batchnorm.train_forward(self, xyz, new_xyz, points, count, lst, ns)
+            return new_xyz, out.permute(0, 2, 1)
         out = ops.sa_group_mlp(xyz, new_xyz, points, count, lst, ns, self.chans, self.packed_params(),
                                xyz_pdim=2, feat_ddim=1, feat_pdim=2)
         return new_xyz, out.permute(0, 2, 1)

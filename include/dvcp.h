@@ -260,6 +260,38 @@ int dvcp_sa_group_mlp_backward(int dtype, const void* xyz, int64_t sb, int64_t s
                                const float* bnstat, const float* grad_out, float* grad_feat,
                                void* workspace, float* grad_params, void* stream);
 
+/* The grouped set-abstraction MLP with BatchNorm in TRAINING mode (batch statistics) --
+ * pointnet2_utils.py:195-200 with the module in train() (train.py:105-125 trains the whole model).
+ * Same grouping arguments as dvcp_sa_group_mlp_backward.  pack: per layer l (C_l -> C_{l+1})
+ * W (C_{l+1} x C_l) | conv bias | scale | shift | batch mean | 1/sqrt(batch var + eps) | A/M | B/M
+ * (fp32; dvcp_sa_bn_pack_floats(nlayer, chans) floats), scale = gamma * istd, shift = beta -
+ * mean * scale, M = B * S * nsample grouped entries (padding slots included), A_l / B_l the
+ * batch-norm backward sums of layer l (zero until known).
+ * dvcp_sa_bn_stats: sums (2 x C_layer fp64) = per-channel sum z and sum z^2 of the conv output of
+ *   `layer` (1-based) over all M entries, the layers below it normalised by their pack entries.
+ * dvcp_sa_bn_backward(mode): mode = k >= 1 -> sums (2 x C_k fp64) = A_k = sum dL/dy_k (dbeta) and
+ *   B_k = sum dL/dy_k * xhat_k (dgamma), needing A, B of the layers above k (mode = nlayer needs
+ *   none); mode = 0 -> grad_params (per layer dW, db, 0, 0: the host fills dgamma / dbeta with
+ *   B, A) and, if grad_feat is given (zeroed by the caller), dL/d feat (B x N x D fp32) through
+ *   the grouping.  grad_out: B x S x C_last fp32.  workspace: dvcp_sa_bn_workspace_bytes bytes.
+ * Replaces the training-mode forward/backward of pointnet2_utils.py:176-202 (BatchNorm2d batch
+ * statistics, running-stat update done by the host). */
+int64_t dvcp_sa_bn_pack_floats(int nlayer, const int* chans);
+int64_t dvcp_sa_bn_workspace_bytes(int B, int S, int nlayer, const int* chans);
+int dvcp_sa_bn_stats(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
+                     const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
+                     int feat_dtype, const void* feat, int64_t fb, int64_t fd, int64_t fn, int D,
+                     const int32_t* count, const int32_t* list, int nsample, int nlayer,
+                     const int* chans, const float* pack, int layer, void* workspace,
+                     double* sums, void* stream);
+int dvcp_sa_bn_backward(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
+                        const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
+                        int feat_dtype, const void* feat, int64_t fb, int64_t fd, int64_t fn,
+                        int D, const int32_t* count, const int32_t* list, int nsample, int nlayer,
+                        const int* chans, const float* pack, int mode, const float* grad_out,
+                        float* grad_feat, void* workspace, double* sums, float* grad_params,
+                        void* stream);
+
 /* Backward of the feature extractor's fc (deep_feat_extraction.py:15, Linear 64 -> 32):
  * x: P x 64 fp32 (its input rows), params: fc.W (32 x 64) | fc.b (32), grad: P x 32;
  * grad_x (optional): P x 64; grad_params: dW (32 x 64) | db (32), summed in fixed order.

@@ -71,13 +71,13 @@ def test_no_cpu_fallback():
 
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU behaviour")
 def test_training_guards_and_no_cpu_fallback():
-    """Training mode: a feature extractor with batch-statistics BN (FE1 in training mode) is refused
-    (not implemented); with FE1.eval() it trains in frozen-BN mode, frozen or not it takes the
-    autograd path, which has no CPU fallback either."""
+    """Training mode: the whole model in training mode (batch-statistics BN in FE1), FE1.eval()
+    (frozen-BN training) and a frozen FE1 all take the autograd path, which has no CPU fallback."""
     import dvcp
     m = dvcp.DeepVCP(use_normal=False, fe_npoint=16)
     args = (torch.rand(1, 3, 64), torch.rand(1, 3, 64), torch.eye(3, dtype=torch.float64)[None], torch.zeros(1, 3))
-    with pytest.raises(NotImplementedError, match="FE1.eval"):
+    assert m._training_mode() == (True, True)      # model.train(): batch-statistics BN
+    with pytest.raises(RuntimeError, match="no GPU"):
         m(*args)
     m.FE1.eval()
     assert m._training_mode() == (True, True)      # frozen-BN training of the extractor and the head

@@ -1,5 +1,7 @@
 """Training step throughput at C3 (train.py:96-125): the head with the feature extractor frozen,
-or (--train-fe) the whole model with the extractor trainable in frozen-BN mode (FE1.eval()).
+(--train-fe) the whole model with the extractor trainable in frozen-BN mode (FE1.eval()), or
+(--train-fe --bn-train) train.py's own setting: model.train(), FE1's BatchNorms on batch
+statistics.
 
 One step = model(src, tgt, R_gt, t_init) with autograd on the head -> deepVCP_loss -> backward
 -> Adam step, on one batch of synthetic KITTI-like pairs (8 x 16384 points, K=64, r=2.0, s=0.4).
@@ -37,7 +39,11 @@ def main():
     ap.add_argument("--prefetch", type=int, default=0)
     ap.add_argument("--train-fe", action="store_true",
                     help="train FE1 too (frozen-BN: eval-mode BatchNorm, trainable parameters); no prefetch")
+    ap.add_argument("--bn-train", action="store_true",
+                    help="with --train-fe: FE1 in training mode (batch-statistics BatchNorm, as model.train())")
     args = ap.parse_args()
+    if args.bn_train and not args.train_fe:
+        ap.error("--bn-train needs --train-fe")
     if args.train_fe and args.prefetch:
         ap.error("--train-fe trains the extractor, so its forward cannot run ahead (--prefetch 0)")
     import dvcp
@@ -53,6 +59,8 @@ def main():
         _, calib, _ = model.FE1.run(src)
     condition_weights(model, feats=calib)
     model.FE1.requires_grad_(args.train_fe)
+    if args.bn_train:
+        model.FE1.train()
     opt = torch.optim.Adam([p for p in model.parameters() if p.requires_grad], lr=1e-4)
     t_init = torch.zeros(1, 3)
 
@@ -113,7 +121,9 @@ def main():
                   "total_ms_per_step": round(sum(v) / args.steps, 4)}
               for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1]))}
     print(json.dumps({
-        "metric": ("training steps (forward + deepVCP_loss + backward + Adam), FE trainable with frozen BN"
+        "metric": ("training steps (forward + deepVCP_loss + backward + Adam), whole model in training mode "
+                   "(FE1 batch-statistics BN)" if args.bn_train else
+                   "training steps (forward + deepVCP_loss + backward + Adam), FE trainable with frozen BN"
                    if args.train_fe else "head-training steps (forward + deepVCP_loss + backward + Adam), FE frozen"),
         "prefetch": P,
         "value": round(args.batch * args.steps / dt, 3), "unit": "pairs/s",
