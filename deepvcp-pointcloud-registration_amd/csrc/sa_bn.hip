@@ -21,10 +21,11 @@
 // gz_l is dense (every entry carries the mean terms), so layer l's sums need A, B of the layers
 // above it.  mode = L: A_L, B_L over the routed (arg-max) rows only (gy_L is zero elsewhere);
 // mode = k < L: one dense recompute pass over every entry gives A_k, B_k; mode = 0: the dense pass
-// with every A, B known accumulates dW, db and scatters the feature gradient.  The nsample - cnt
-// padding entries of a centre are one virtual row of weight nsample - cnt (identical rows, never
-// routed: torch.max takes the first of equal maxima).  Per-wave partials are summed in a fixed
-// order in fp64, so all parameter gradients are deterministic; the feature scatter uses atomics.
+// with every A, B known writes each entry's gz_l and layer input (channel-major rows: dW_l, db_l
+// are then plain GEMMs over the entries, done by the host) and scatters the feature gradient.
+// The padding slots are evaluated as the copies of the first hit they are (never routed:
+// torch.max takes the first of equal maxima).  The sums are per-wave fp64 partials summed in a
+// fixed order (deterministic); the feature scatter uses float atomics.
 #include "common.h"
 
 #include <algorithm>
@@ -57,12 +58,6 @@ struct BnTable {
   static constexpr int O1 = 0;
   static constexpr int O2 = bn_layer_size(C0, C1);
   static constexpr int O3 = O2 + bn_layer_size(C1, C2);
-  // packed parameter gradient (dvcp_sa_group_mlp_backward's layout): per layer W, b, gamma, beta
-  static constexpr int P1 = C0 * C1 + 3 * C1;
-  static constexpr int P2 = C1 * C2 + 3 * C2;
-  static constexpr int P3 = C3 > 0 ? C2 * C3 + 3 * C3 : 0;
-  static constexpr int P = P1 + P2 + P3;
-  static constexpr int LW1 = C1 * (C0 + 1), LW2 = C2 * (C1 + 1), LW3 = C3 > 0 ? C3 * (C2 + 1) : 0;
 };
 
 // lane = slot: h = relu((W x + b) * scale + shift), weights as wave-uniform scalar loads
@@ -179,95 +174,272 @@ __global__ __launch_bounds__(kBnThreads) void sa_bn_stats_kernel(PointsView<T> p
   }
 }
 
-// ---- dense backward pass ------------------------------------------------------------------------
-// Lane-per-output-channel helpers over LDS-staged weights (row stride CIN + 1).
-template <int CIN>
-__device__ __forceinline__ float bn_dot_row(const float* __restrict__ W, const float* __restrict__ v, int row) {
-  float acc = 0.0f;
-#pragma unroll 8
-  for (int k = 0; k < CIN; ++k) acc = __fmaf_rn(W[row * (CIN + 1) + k], v[k], acc);
-  return acc;
-}
-template <int CIN, int COUT>
-__device__ __forceinline__ float bn_dot_col(const float* __restrict__ W, const float* __restrict__ gz, int col) {
-  float acc = 0.0f;
-#pragma unroll 8
-  for (int c = 0; c < COUT; ++c) acc = __fmaf_rn(W[c * (CIN + 1) + col], gz[c], acc);
-  return acc;
-}
-
-// Per-lane constants of one layer (lane = output channel).
-struct BnLane {
-  float bias, scale, shift, mean, istd, ga, gb;
-  __device__ __forceinline__ void load(const float* p, int cin, int cout, int c) {
-    const float* v = p + cout * cin;
-    bias = v[c];
-    scale = v[cout + c];
-    shift = v[2 * cout + c];
-    mean = v[3 * cout + c];
-    istd = v[4 * cout + c];
-    ga = v[5 * cout + c];
-    gb = v[6 * cout + c];
-  }
-  // gz = scale (gy - w (A/M + xh B/M)): w entries of this row (padding rows folded)
-  __device__ __forceinline__ float gz(float gy, float xh, float w) const {
-    return scale * (gy - w * (ga + xh * gb));
-  }
-};
-
 __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 }
 
-// MODE: 0 = parameter / feature gradients; k in 1..L = the sums A_k, B_k.
+// Row layout of the z / gradient / input rows: 64-entry blocks, channel-major inside a block --
+// element (entry e, channel c) of a C-channel table at (e / 64) * C * 64 + c * 64 + e % 64 -- so a
+// wave's 64 consecutive entries of one channel are one 256-byte run and its whole chunk one
+// contiguous C x 256-byte region (tables are padded to a multiple of 64 entries).
+template <typename P>
+__device__ __forceinline__ P* bn_at(P* base, int C, int64_t e) {
+  return base + (e >> 6) * (static_cast<int64_t>(C) * 64) + (e & 63);
+}
+
+// z = W x + b stored to its row (channel-major), h = relu(z * scale + shift), channel by channel
+template <int CIN, int COUT>
+__device__ __forceinline__ void bn_layer_store(const float (&x)[CIN], float (&h)[COUT], const float* __restrict__ p,
+                                               float* __restrict__ zr, int64_t M, int64_t e) {
+#pragma unroll
+  for (int co = 0; co < COUT; ++co) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int ci = 0; ci < CIN; ++ci) acc = __fmaf_rn(p[co * CIN + ci], x[ci], acc);
+    const float z = acc + p[CIN * COUT + co];
+    bn_at(zr, COUT, e)[co * 64] = z;
+    const float y = z * p[CIN * COUT + COUT + co] + p[CIN * COUT + 2 * COUT + co];
+    h[co] = y > 0.0f ? y : 0.0f;
+  }
+}
+
+// ---- forward rows -------------------------------------------------------------------------------
+// Every entry's conv outputs z_l of every layer (batch statistics final), channel-major
+// (C_l x M per layer, e = centre * nsample + slot): the backward passes read them instead of
+// recomputing the MLP.  lane = slot.
+template <typename T, typename FT, int D, int C1, int C2, int C3>
+__global__ __launch_bounds__(kBnThreads) void sa_bn_zrows_kernel(PointsView<T> pts, PointsView<T> ctr, int S, int B,
+                                                                 BnFeat<FT> feat, const int32_t* __restrict__ count,
+                                                                 const int32_t* __restrict__ list, int nsample,
+                                                                 const float* __restrict__ pack,
+                                                                 float* __restrict__ zrows) {
+  using Tb = BnTable<D, C1, C2, C3>;
+  constexpr int C0 = Tb::C0;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float* p1 = pack + Tb::O1;
+  const float* p2 = pack + Tb::O2;
+  const float* p3 = pack + Tb::O3;
+  const int64_t M = (static_cast<int64_t>(B) * S * nsample + 63) & ~static_cast<int64_t>(63);  // padded
+  float* z1r = zrows;
+  float* z2r = z1r + C1 * M;
+  float* z3r = z2r + C2 * M;
+  const int64_t total = static_cast<int64_t>(B) * S;
+  for (int64_t cs = static_cast<int64_t>(blockIdx.x) * kBnWaves + wave; cs < total;
+       cs += static_cast<int64_t>(gridDim.x) * kBnWaves) {
+    const int b = static_cast<int>(cs / S), s = static_cast<int>(cs - static_cast<int64_t>(b) * S);
+    int cnt = count[cs];
+    cnt = cnt < 1 ? 1 : (cnt > nsample ? nsample : cnt);
+    const int32_t* lst = list + cs * nsample;
+    const T cx = ctr.at(b, 0, s), cy = ctr.at(b, 1, s), cz = ctr.at(b, 2, s);
+    for (int r0 = 0; r0 < nsample; r0 += kWave) {
+      const int r = r0 + lane;
+      if (r >= nsample) continue;
+      const int64_t e = cs * nsample + r;
+      float x[C0];
+      bn_load_x<T, FT, D>(x, pts, feat, b, lst[r < cnt ? r : 0], cx, cy, cz);
+      float h1[C1], h2[C2];
+      bn_layer_store<C0, C1>(x, h1, p1, z1r, M, e);
+      bn_layer_store<C1, C2>(h1, h2, p2, z2r, M, e);
+      if constexpr (C3 > 0) {
+        float h3[C3];
+        bn_layer_store<C2, C3>(h2, h3, p3, z3r, M, e);
+      }
+    }
+  }
+}
+
+// ---- backward (lane = grouped entry) ------------------------------------------------------------
+// Per centre (one wave).  Pass 1 finds each last-layer channel's arg-max slot among the distinct
+// hits from the z rows (first of equal maxima) and keeps that row's z; mode L takes A_L, B_L from
+// those rows directly.  Otherwise pass 2 walks the centre's nsample slots in chunks of 64 (lane =
+// slot; padding slots are the copies of the first hit they are, never routed) and runs the
+// batch-norm backward top-down, channel by channel, streaming each layer's z rows (coalesced:
+// consecutive lanes, consecutive entries) with the weights as wave-uniform scalar loads.  Mode k
+// stops at layer k and sums gy_k and gy_k xhat_k through an LDS tile (fp64 column sums); mode 0
+// writes each entry's gz_l and layer input h_{l-1} (plus a ones row, for the bias) as
+// channel-major rows for the host's weight-gradient GEMMs, and scatters W_1^T gz_1 to the input
+// features (float atomics).
+
+template <int C>
+__device__ __forceinline__ void bn_put(float* __restrict__ base, int64_t M, int64_t e, const float (&v)[C], bool ones) {
+  float* o = bn_at(base, ones ? C + 1 : C, e);
+#pragma unroll
+  for (int k = 0; k < C; ++k) o[k * 64] = v[k];
+  if (ones) o[C * 64] = 1.0f;
+}
+
+template <int COUT>
+struct BnVec {  // one layer's per-channel vectors (wave-uniform)
+  const float* v;
+  __device__ __forceinline__ float y(int c, float z) const { return z * v[COUT + c] + v[2 * COUT + c]; }
+  __device__ __forceinline__ float xh(int c, float z) const { return (z - v[3 * COUT + c]) * v[4 * COUT + c]; }
+  // gz = scale (gy - (A/M + xhat B/M))
+  __device__ __forceinline__ float gz(int c, float z, float gy) const {
+    return v[COUT + c] * (gy - (v[5 * COUT + c] + xh(c, z) * v[6 * COUT + c]));
+  }
+};
+
+// The last layer: gy from the centre's route table (slot r; routable = a distinct hit), gz written
+// (mode 0) and propagated: gprev = W^T gz.
+template <int CIN, int COUT, bool FINAL>
+__device__ __forceinline__ void bn_bwd_top(const float* __restrict__ zr, int64_t M, int64_t e, bool act,
+                                           const float* __restrict__ p, const int* sarg, const float* srg, int r,
+                                           bool routable, float (&gprev)[CIN], float* __restrict__ gzr) {
+  const BnVec<COUT> q{p + COUT * CIN};
+#pragma unroll
+  for (int k = 0; k < CIN; ++k) gprev[k] = 0.0f;
+#pragma unroll
+  for (int c = 0; c < COUT; ++c) {
+    const float z = act ? bn_at(zr, COUT, e)[c * 64] : 0.0f;
+    const float gy = (routable && sarg[c] == r && q.y(c, z) > 0.0f) ? srg[c] : 0.0f;
+    const float gz = q.gz(c, z, gy);
+    if constexpr (FINAL) {
+      if (act) bn_at(gzr, COUT, e)[c * 64] = gz;
+    }
+#pragma unroll
+    for (int k = 0; k < CIN; ++k) gprev[k] = __fmaf_rn(p[c * CIN + k], gz, gprev[k]);
+  }
+}
+
+// A lower layer: g = dL/dh on entry, gy = [y > 0] g, gz written (mode 0), gprev = W^T gz.
+template <int CIN, int COUT, bool FINAL>
+__device__ __forceinline__ void bn_bwd_mid(const float* __restrict__ zr, int64_t M, int64_t e, bool act,
+                                           const float* __restrict__ p, const float (&g)[COUT], float (&gprev)[CIN],
+                                           float* __restrict__ gzr) {
+  const BnVec<COUT> q{p + COUT * CIN};
+#pragma unroll
+  for (int k = 0; k < CIN; ++k) gprev[k] = 0.0f;
+#pragma unroll
+  for (int c = 0; c < COUT; ++c) {
+    const float z = act ? bn_at(zr, COUT, e)[c * 64] : 0.0f;
+    const float gz = q.gz(c, z, q.y(c, z) > 0.0f ? g[c] : 0.0f);
+    if constexpr (FINAL) {
+      if (act) bn_at(gzr, COUT, e)[c * 64] = gz;
+    }
+#pragma unroll
+    for (int k = 0; k < CIN; ++k) gprev[k] = __fmaf_rn(p[c * CIN + k], gz, gprev[k]);
+  }
+}
+
+// Mode 0: the input rows of layer l+1, h_l = relu(y_l), and a ones row.
+template <int CIN, int COUT>
+__device__ __forceinline__ void bn_put_h(const float* __restrict__ zr, int64_t M, int64_t e, const float* __restrict__ p,
+                                         float* __restrict__ har) {
+  const BnVec<COUT> q{p + COUT * CIN};
+#pragma unroll
+  for (int c = 0; c < COUT; ++c) {
+    const float y = q.y(c, bn_at(zr, COUT, e)[c * 64]);
+    bn_at(har, COUT + 1, e)[c * 64] = y > 0.0f ? y : 0.0f;
+  }
+  bn_at(har, COUT + 1, e)[COUT * 64] = 1.0f;
+}
+
+// The sums of one layer over the chunk: A += sum gy, B += sum gy xhat (gy = [y > 0] g), through
+// the wave's LDS tile (two phases, z re-read); lanes = (channel lane % COUT, slot group lane / COUT).
+template <int CIN, int COUT, int TW>
+__device__ __forceinline__ void bn_bwd_sums(const float* __restrict__ zr, int64_t M, int64_t e, bool act,
+                                            const float* __restrict__ p, const float (&g)[COUT], float (*tl)[TW + 1],
+                                            int lane, int rn, double& s1, double& s2) {
+  constexpr int G = kWave / COUT;
+  const BnVec<COUT> q{p + COUT * CIN};
+  const int c = lane % COUT, grp = lane / COUT;
+#pragma unroll
+  for (int k = 0; k < COUT; ++k) {
+    const float z = act ? bn_at(zr, COUT, e)[k * 64] : 0.0f;
+    tl[lane][k] = (act && q.y(k, z) > 0.0f) ? g[k] : 0.0f;
+  }
+  wave_sync_lds();
+  for (int j = grp; j < rn; j += G) s1 += static_cast<double>(tl[j][c]);
+  wave_sync_lds();
+#pragma unroll
+  for (int k = 0; k < COUT; ++k) {
+    const float z = act ? bn_at(zr, COUT, e)[k * 64] : 0.0f;
+    tl[lane][k] = (act && q.y(k, z) > 0.0f) ? g[k] * q.xh(k, z) : 0.0f;
+  }
+  wave_sync_lds();
+  for (int j = grp; j < rn; j += G) s2 += static_cast<double>(tl[j][c]);
+  wave_sync_lds();
+}
+
+// Layer 1 in mode 0: gz_1 written (g becomes gz_1).
+template <int CIN, int COUT>
+__device__ __forceinline__ void bn_bwd_first(const float* __restrict__ zr, int64_t e, bool act,
+                                             const float* __restrict__ p, float (&g)[COUT], float* __restrict__ gzr) {
+  const BnVec<COUT> q{p + COUT * CIN};
+#pragma unroll
+  for (int c = 0; c < COUT; ++c) {
+    const float z = act ? bn_at(zr, COUT, e)[c * 64] : 0.0f;
+    g[c] = q.gz(c, z, q.y(c, z) > 0.0f ? g[c] : 0.0f);
+    if (act) bn_at(gzr, COUT, e)[c * 64] = g[c];
+  }
+}
+
+// The feature gradient of the chunk, W_1^T gz_1 (input columns 3..), scattered to the points:
+// the chunk's gz_1 rows go through the LDS tile, then row by row lane d < D adds its channel
+// (one coalesced atomic per row instead of D scattered ones per lane).
+template <int D, int C0, int C1, int TW>
+__device__ __forceinline__ void bn_scatter_feat(const float (&g)[C1], float (*tl)[TW + 1], const float* __restrict__ p1,
+                                                int lane, int rn, int n, bool act, float* __restrict__ gfb) {
+#pragma unroll
+  for (int k = 0; k < C1; ++k) tl[lane][k] = act ? g[k] : 0.0f;
+  wave_sync_lds();
+  const int d = lane < D ? lane : 0;
+  float w[C1];
+#pragma unroll
+  for (int c = 0; c < C1; ++c) w[c] = p1[c * C0 + 3 + d];
+  for (int j = 0; j < rn; ++j) {
+    const int nj = __builtin_amdgcn_readlane(n, j);
+    float acc = 0.0f;
+#pragma unroll
+    for (int c = 0; c < C1; ++c) acc = __fmaf_rn(w[c], tl[j][c], acc);
+    if (lane < D && acc != 0.0f) atomicAdd(gfb + static_cast<int64_t>(nj) * D + lane, acc);
+  }
+  wave_sync_lds();
+}
+
+// MODE: 0 = per-entry gradient rows + feature gradient; k in 1..L = the sums A_k, B_k.
 template <typename T, typename FT, int D, int C1, int C2, int C3, int MODE>
 __global__ __launch_bounds__(kBnThreads) void sa_bn_bwd_kernel(
     PointsView<T> pts, PointsView<T> ctr, int S, int B, BnFeat<FT> feat, const int32_t* __restrict__ count,
-    const int32_t* __restrict__ list, int nsample, const float* __restrict__ pack, const float* __restrict__ gout,
-    float* __restrict__ gfeat, int64_t gfb, float* __restrict__ partial, double* __restrict__ dpartial) {
+    const int32_t* __restrict__ list, int nsample, const float* __restrict__ pack, const float* __restrict__ zrows,
+    const float* __restrict__ gout, float* __restrict__ gfeat, int64_t gfb, double* __restrict__ dpartial,
+    float* __restrict__ rows) {
   using Tb = BnTable<D, C1, C2, C3>;
   constexpr int C0 = Tb::C0, CL = Tb::CL, L = Tb::L;
   constexpr bool FINAL = MODE == 0;
-  __shared__ float sW1[Tb::LW1], sW2[Tb::LW2], sW3[Tb::LW3 > 0 ? Tb::LW3 : 1];
-  __shared__ float tile[kBnWaves][kWave][CL + 1];  // pass 1: last-layer rows
-  __shared__ float vx[kBnWaves][C0 + 1];           // pass 2: the row's input
-  __shared__ float vh[kBnWaves][2][Tb::CMAX];      // h1, h2 of the row
-  __shared__ float vg[kBnWaves][Tb::CMAX];         // gz of the layer above
-
+  constexpr int CM = MODE == 1 ? C1 : (MODE == 2 ? C2 : (MODE == 3 ? C3 : 1));
+  constexpr int TW = CL > CM ? (CL > C1 ? CL : C1) : (CM > C1 ? CM : C1);
+  constexpr int CINL = C3 > 0 ? C2 : C1;
+  __shared__ float tile[kBnWaves][kWave][TW + 1];
+  __shared__ int s_arg[kBnWaves][CL];
+  __shared__ float s_rg[kBnWaves][CL];
+  __shared__ double red[kBnWaves][2][kWave];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* p1 = pack + Tb::O1;
   const float* p2 = pack + Tb::O2;
   const float* p3 = pack + Tb::O3;
-  for (int i = tid; i < C1 * C0; i += kBnThreads) sW1[(i / C0) * (C0 + 1) + i % C0] = p1[i];
-  for (int i = tid; i < C2 * C1; i += kBnThreads) sW2[(i / C1) * (C1 + 1) + i % C1] = p2[i];
-  if constexpr (C3 > 0)
-    for (int i = tid; i < C3 * C2; i += kBnThreads) sW3[(i / C2) * (C2 + 1) + i % C2] = p3[i];
-  __syncthreads();
-
-  const int c1 = lane < C1 ? lane : 0, c2 = lane < C2 ? lane : 0, c3 = lane < (C3 > 0 ? C3 : 1) ? lane : 0;
-  BnLane q1, q2, q3;
-  q1.load(p1, C0, C1, c1);
-  q2.load(p2, C1, C2, c2);
-  if constexpr (C3 > 0) q3.load(p3, C2, C3, c3);
-
-  // accumulators: FINAL -- lane c owns row c of each dW and db_l[c]; sums -- A, B of layer MODE
-  constexpr int NW1 = FINAL ? C0 : 1, NW2 = FINAL ? C1 : 1, NW3 = (FINAL && C3 > 0) ? C2 : 1;
-  float dW1[NW1], dW2[NW2], dW3[NW3];
-  float db1 = 0.f, db2 = 0.f, db3 = 0.f;
-#pragma unroll
-  for (int k = 0; k < NW1; ++k) dW1[k] = 0.f;
-#pragma unroll
-  for (int k = 0; k < NW2; ++k) dW2[k] = 0.f;
-#pragma unroll
-  for (int k = 0; k < NW3; ++k) dW3[k] = 0.f;
-  double accA = 0.0, accB = 0.0;
-
-  float(*tl)[CL + 1] = tile[wave];
-  float* x_s = vx[wave];
-  float* h1_s = vh[wave][0];
-  float* h2_s = vh[wave][1];
-  float* g_s = vg[wave];
+  const float* pL = C3 > 0 ? p3 : p2;
+  const float* vL = pL + CL * CINL;
+  const int cL = lane < CL ? lane : 0;
+  const float scL = vL[CL + cL], shL = vL[2 * CL + cL], muL = vL[3 * CL + cL], isL = vL[4 * CL + cL];
+  const int64_t M = (static_cast<int64_t>(B) * S * nsample + 63) & ~static_cast<int64_t>(63);  // padded
+  const float* z1r = zrows;
+  const float* z2r = z1r + C1 * M;
+  const float* z3r = z2r + C2 * M;
+  const float* zLr = C3 > 0 ? z3r : z2r;
+  // mode 0 rows, per layer l: gz_l (C_l x M) | its input h_{l-1} and a ones row (C_{l-1} + 1 x M)
+  float *gz1r = nullptr, *ha1r = nullptr, *gz2r = nullptr, *ha2r = nullptr, *gz3r = nullptr, *ha3r = nullptr;
+  if constexpr (FINAL) {
+    gz1r = rows;
+    ha1r = gz1r + C1 * M;
+    gz2r = ha1r + (C0 + 1) * M;
+    ha2r = gz2r + C2 * M;
+    gz3r = ha2r + (C1 + 1) * M;
+    ha3r = gz3r + C3 * M;
+  }
+  double s1 = 0.0, s2 = 0.0;
+  float(*tl)[TW + 1] = tile[wave];
   const int64_t total = static_cast<int64_t>(B) * S;
   for (int64_t cs = static_cast<int64_t>(blockIdx.x) * kBnWaves + wave; cs < total;
        cs += static_cast<int64_t>(gridDim.x) * kBnWaves) {
@@ -279,201 +451,114 @@ __global__ __launch_bounds__(kBnThreads) void sa_bn_bwd_kernel(
     int cnt = count[cs];
     cnt = cnt < 1 ? 1 : (cnt > nsample ? nsample : cnt);
     const int32_t* lst = list + cs * nsample;
-    const T cx = ctr.at(b, 0, s), cy = ctr.at(b, 1, s), cz = ctr.at(b, 2, s);
 
-    // ---- pass 1: each channel's arg-max row among the distinct slots (lane = slot) -------------
-    float best = -1.0f;  // outputs are >= 0
+    // ---- pass 1: each channel's arg-max slot among the distinct hits, and its z ------------------
+    float best = -1.0f, zbest = 0.0f;  // outputs are >= 0
     int arg = 0;
     for (int r0 = 0; r0 < cnt; r0 += kWave) {
       const int r = r0 + lane;
       if (r < cnt) {
-        float x[C0];
-        bn_load_x<T, FT, D>(x, pts, feat, b, lst[r], cx, cy, cz);
-        float h1[C1], h2[C2];
-        bn_rows<C0, C1>(x, h1, p1);
-        bn_rows<C1, C2>(h1, h2, p2);
-        if constexpr (C3 > 0) {
-          float h3[C3];
-          bn_rows<C2, C3>(h2, h3, p3);
 #pragma unroll
-          for (int k = 0; k < C3; ++k) tl[lane][k] = h3[k];
-        } else {
-#pragma unroll
-          for (int k = 0; k < C2; ++k) tl[lane][k] = h2[k];
-        }
+        for (int k = 0; k < CL; ++k) tl[lane][k] = bn_at(zLr, CL, cs * nsample + r)[k * 64];
       }
       wave_sync_lds();
       if (lane < CL) {
         const int rn = min(kWave, cnt - r0);
         for (int j = 0; j < rn; ++j) {
-          const float v = tl[j][lane];
-          if (v > best) {  // strict: the first row among equal maxima
-            best = v;
+          const float z = tl[j][lane];
+          const float y = z * scL + shL;
+          const float h = y > 0.0f ? y : 0.0f;
+          if (h > best) {  // strict: the first row among equal maxima
+            best = h;
+            zbest = z;
             arg = r0 + j;
           }
         }
       }
       wave_sync_lds();
     }
-    // lane c < CL: the routed gradient of channel c goes to row `arg` (nothing if the max is 0)
-    const float rg = (lane < CL && best > 0.0f) ? g_c : 0.0f;
-    const int rarg = (lane < CL && best > 0.0f && g_c != 0.0f) ? arg : -1;
+    const bool routed = lane < CL && best > 0.0f && g_c != 0.0f;
+    if constexpr (MODE == L) {
+      if (routed) {
+        s1 += static_cast<double>(g_c);
+        s2 += static_cast<double>(g_c) * static_cast<double>((zbest - muL) * isL);
+      }
+      continue;
+    }
+    if (lane < CL) {
+      s_arg[wave][lane] = routed ? arg : -1;
+      s_rg[wave][lane] = g_c;
+    }
+    wave_sync_lds();
 
-    // ---- pass 2: the rows (lane = output channel) -----------------------------------------------
-    // MODE == L: the distinct routed rows; otherwise every distinct row plus one virtual row for
-    // the nsample - cnt padding slots.
-    uint64_t pending = MODE == L ? __ballot(rarg >= 0) : 0ull;
-    const int nv = MODE == L ? 0 : cnt + (cnt < nsample ? 1 : 0);
-    for (int v = 0;; ++v) {
-      int r;
-      float w = 1.0f;
-      if constexpr (MODE == L) {
-        if (!pending) break;
-        const int lead = __ffsll(static_cast<long long>(pending)) - 1;
-        r = __builtin_amdgcn_readlane(rarg, lead);
-        pending &= ~__ballot(rarg == r);
-      } else {
-        if (v >= nv) break;
-        if (v < cnt) {
-          r = v;
-        } else {
-          r = 0;
-          w = static_cast<float>(nsample - cnt);
+    // ---- pass 2: every slot (lane = slot) --------------------------------------------------------
+    const T cx = ctr.at(b, 0, s), cy = ctr.at(b, 1, s), cz = ctr.at(b, 2, s);
+    for (int r0 = 0; r0 < nsample; r0 += kWave) {
+      const int r = r0 + lane;
+      const bool act = r < nsample;
+      const int rn = min(kWave, nsample - r0);
+      const int64_t e = cs * nsample + (act ? r : 0);
+      const int n = lst[(act && r < cnt) ? r : 0];
+      if constexpr (FINAL) {
+        if (act) {
+          float x[C0];
+          bn_load_x<T, FT, D>(x, pts, feat, b, n, cx, cy, cz);
+          bn_put<C0>(ha1r, M, e, x, true);
         }
       }
-      const bool routed_row = v < cnt || MODE == L;  // the padding row is never routed
-      const int n = lst[r];
-      if (lane < C0) {
-        float xv;
-        if (lane == 0) xv = static_cast<float>(pts.at(b, 0, n) - cx);
-        else if (lane == 1) xv = static_cast<float>(pts.at(b, 1, n) - cy);
-        else if (lane == 2) xv = static_cast<float>(pts.at(b, 2, n) - cz);
-        else xv = feat.at(b, lane - 3, n);
-        x_s[lane] = xv;
-      }
-      if constexpr (C0 > kWave) {
-        if (lane + kWave < C0) x_s[lane + kWave] = feat.at(b, lane + kWave - 3, n);
-      }
-      wave_sync_lds();
-      // forward, one output channel per lane
-      const float z1 = bn_dot_row<C0>(sW1, x_s, c1) + q1.bias;
-      const float y1 = z1 * q1.scale + q1.shift;
-      const float xh1 = (z1 - q1.mean) * q1.istd;
-      if (lane < C1) h1_s[lane] = y1 > 0.0f ? y1 : 0.0f;
-      wave_sync_lds();
-      const float z2 = bn_dot_row<C1>(sW2, h1_s, c2) + q2.bias;
-      const float y2 = z2 * q2.scale + q2.shift;
-      const float xh2 = (z2 - q2.mean) * q2.istd;
-      float gy2;
       if constexpr (C3 > 0) {
-        if (lane < C2) h2_s[lane] = y2 > 0.0f ? y2 : 0.0f;
-        wave_sync_lds();
-        const float z3 = bn_dot_row<C2>(sW3, h2_s, c3) + q3.bias;
-        const float y3 = z3 * q3.scale + q3.shift;
-        const float xh3 = (z3 - q3.mean) * q3.istd;
-        const float gh3 = (routed_row && rarg == r) ? rg : 0.0f;
-        const float gy3 = (lane < C3 && y3 > 0.0f) ? gh3 : 0.0f;
-        if constexpr (MODE == 3) {
-          accA += static_cast<double>(gy3);
-          accB += static_cast<double>(gy3) * static_cast<double>(xh3);
-          wave_sync_lds();
+        float g2[C2], g1[C1];
+        bn_bwd_top<C2, C3, FINAL>(z3r, M, e, act, p3, s_arg[wave], s_rg[wave], r, r < cnt, g2, gz3r);
+        if constexpr (MODE == 2) {
+          bn_bwd_sums<C1, C2, TW>(z2r, M, e, act, p2, g2, tl, lane, rn, s1, s2);
           continue;
         }
-        const float gz3 = lane < C3 ? q3.gz(gy3, xh3, w) : 0.0f;
         if constexpr (FINAL) {
-          db3 += gz3;
-#pragma unroll
-          for (int k = 0; k < NW3; ++k) dW3[k] = __fmaf_rn(gz3, h2_s[k], dW3[k]);
+          if (act) bn_put_h<C1, C2>(z2r, M, e, p2, ha3r);
         }
-        wave_sync_lds();
-        if (lane < C3) g_s[lane] = gz3;
-        wave_sync_lds();
-        const float gh2 = bn_dot_col<C2, C3>(sW3, g_s, c2);
-        gy2 = (lane < C2 && y2 > 0.0f) ? gh2 : 0.0f;
+        bn_bwd_mid<C1, C2, FINAL>(z2r, M, e, act, p2, g2, g1, gz2r);
+        if constexpr (MODE == 1) {
+          bn_bwd_sums<C0, C1, TW>(z1r, M, e, act, p1, g1, tl, lane, rn, s1, s2);
+          continue;
+        }
+        if constexpr (FINAL) {
+          if (act) bn_put_h<C0, C1>(z1r, M, e, p1, ha2r);
+          bn_bwd_first<C0, C1>(z1r, e, act, p1, g1, gz1r);
+          if constexpr (D > 0)
+            if (gfeat) bn_scatter_feat<D, C0, C1, TW>(g1, tl, p1, lane, rn, n, act, gfeat + b * gfb);
+        }
       } else {
-        const float gh2 = (routed_row && rarg == r) ? rg : 0.0f;
-        gy2 = (lane < C2 && y2 > 0.0f) ? gh2 : 0.0f;
-      }
-      if constexpr (MODE == 2) {
-        accA += static_cast<double>(gy2);
-        accB += static_cast<double>(gy2) * static_cast<double>(xh2);
-        wave_sync_lds();
-        continue;
-      }
-      const float gz2 = lane < C2 ? q2.gz(gy2, xh2, w) : 0.0f;
-      if constexpr (FINAL) {
-        db2 += gz2;
-#pragma unroll
-        for (int k = 0; k < NW2; ++k) dW2[k] = __fmaf_rn(gz2, h1_s[k], dW2[k]);
-      }
-      wave_sync_lds();
-      if (lane < C2) g_s[lane] = gz2;
-      wave_sync_lds();
-      const float gh1 = bn_dot_col<C1, C2>(sW2, g_s, c1);
-      const float gy1 = (lane < C1 && y1 > 0.0f) ? gh1 : 0.0f;
-      if constexpr (MODE == 1) {
-        accA += static_cast<double>(gy1);
-        accB += static_cast<double>(gy1) * static_cast<double>(xh1);
-        wave_sync_lds();
-        continue;
-      }
-      if constexpr (FINAL) {
-        const float gz1 = lane < C1 ? q1.gz(gy1, xh1, w) : 0.0f;
-        db1 += gz1;
-#pragma unroll
-        for (int k = 0; k < NW1; ++k) dW1[k] = __fmaf_rn(gz1, x_s[k], dW1[k]);
-        if constexpr (D > 0) {
-          if (gfeat) {  // the gather's backward: g_f_n += (W1^T gz1)[3:] (w folded into gz1)
-            wave_sync_lds();
-            if (lane < C1) g_s[lane] = gz1;
-            wave_sync_lds();
-            float* gf = gfeat + b * gfb + static_cast<int64_t>(n) * D;
-            for (int d = lane; d < D; d += kWave) {
-              const float gx = bn_dot_col<C0, C1>(sW1, g_s, 3 + d);
-              if (gx != 0.0f) atomicAdd(gf + d, gx);
-            }
-          }
+        float g1[C1];
+        bn_bwd_top<C1, C2, FINAL>(z2r, M, e, act, p2, s_arg[wave], s_rg[wave], r, r < cnt, g1, gz2r);
+        if constexpr (MODE == 1) {
+          bn_bwd_sums<C0, C1, TW>(z1r, M, e, act, p1, g1, tl, lane, rn, s1, s2);
+          continue;
+        }
+        if constexpr (FINAL) {
+          if (act) bn_put_h<C0, C1>(z1r, M, e, p1, ha2r);
+          bn_bwd_first<C0, C1>(z1r, e, act, p1, g1, gz1r);
+          if constexpr (D > 0)
+            if (gfeat) bn_scatter_feat<D, C0, C1, TW>(g1, tl, p1, lane, rn, n, act, gfeat + b * gfb);
         }
       }
-      wave_sync_lds();
     }
+    wave_sync_lds();  // s_arg / s_rg are rewritten by the next centre
   }
-  const int64_t gw = static_cast<int64_t>(blockIdx.x) * kBnWaves + wave;
-  if constexpr (FINAL) {
-    // this wave's partial gradients in the packed layout (gamma / beta slots: zero, the host fills
-    // them from the sums passes)
-    float* o = partial + gw * Tb::P;
-    if (lane < C1) {
-#pragma unroll
-      for (int k = 0; k < C0; ++k) o[lane * C0 + k] = dW1[k];
-      o[C0 * C1 + lane] = db1;
-      o[C0 * C1 + C1 + lane] = 0.f;
-      o[C0 * C1 + 2 * C1 + lane] = 0.f;
-    }
-    float* o2 = o + Tb::P1;
-    if (lane < C2) {
-#pragma unroll
-      for (int k = 0; k < C1; ++k) o2[lane * C1 + k] = dW2[k];
-      o2[C1 * C2 + lane] = db2;
-      o2[C1 * C2 + C2 + lane] = 0.f;
-      o2[C1 * C2 + 2 * C2 + lane] = 0.f;
-    }
-    if constexpr (C3 > 0) {
-      float* o3 = o2 + Tb::P2;
-      if (lane < C3) {
-#pragma unroll
-        for (int k = 0; k < C2; ++k) o3[lane * C2 + k] = dW3[k];
-        o3[C2 * C3 + lane] = db3;
-        o3[C2 * C3 + C3 + lane] = 0.f;
-        o3[C2 * C3 + 2 * C3 + lane] = 0.f;
-      }
-    }
-  } else {
-    constexpr int CM = MODE == 1 ? C1 : (MODE == 2 ? C2 : C3);
+  if constexpr (!FINAL) {
+    // this wave's per-channel sums, the slot groups combined in a fixed order
+    constexpr int G = kWave / CM;
+    red[wave][0][lane] = s1;
+    red[wave][1][lane] = s2;
+    wave_sync_lds();
     if (lane < CM) {
-      double* o = dpartial + gw * (2 * CM);
-      o[lane] = accA;
-      o[CM + lane] = accB;
+      double a = 0.0, q = 0.0;
+      for (int g = 0; g < G; ++g) {
+        a += red[wave][0][g * CM + lane];
+        q += red[wave][1][g * CM + lane];
+      }
+      double* o = dpartial + (static_cast<int64_t>(blockIdx.x) * kBnWaves + wave) * (2 * CM);
+      o[lane] = a;
+      o[CM + lane] = q;
     }
   }
 }
@@ -533,26 +618,23 @@ static int launch_stats(const BnArgs& a, void* ws, double* sums) {
 }
 
 template <typename T, typename FT, int D, int C1, int C2, int C3, int MODE>
-static int launch_bwd(const BnArgs& a, const float* gout, float* gfeat, int64_t gfb, void* ws, double* sums,
-                      float* gparams) {
-  using Tb = BnTable<D, C1, C2, C3>;
+static int launch_bwd(const BnArgs& a, const float* zrows, const float* gout, float* gfeat, int64_t gfb, void* ws,
+                      double* sums, float* rows) {
   const int grid = bn_grid(static_cast<int64_t>(a.B) * a.S);
   PointsView<T> pv{static_cast<const T*>(a.xyz), a.sb, a.sc, a.sn};
   PointsView<T> cv{static_cast<const T*>(a.ctr), a.cb, a.cc, a.cn};
   BnFeat<FT> fv{static_cast<const FT*>(a.feat), a.fb, a.fd, a.fn};
   hipLaunchKernelGGL((sa_bn_bwd_kernel<T, FT, D, C1, C2, C3, MODE>), dim3(grid), dim3(kBnThreads), 0, a.st, pv, cv,
-                     a.S, a.B, fv, a.count, a.list, a.nsample, a.pack, gout, gfeat, gfb, static_cast<float*>(ws),
-                     static_cast<double*>(ws));
+                     a.S, a.B, fv, a.count, a.list, a.nsample, a.pack, zrows, gout, gfeat, gfb,
+                     static_cast<double*>(ws), rows);
   if (int e = launch_status("dvcp_sa_bn_backward")) return e;
-  if constexpr (MODE == 0) {
-    hipLaunchKernelGGL((bn_sum_kernel<float, float>), dim3(ceil_div(Tb::P, 64)), dim3(1024), 0, a.st,
-                       static_cast<const float*>(ws), grid * kBnWaves, Tb::P, gparams);
-  } else {
+  if constexpr (MODE != 0) {
     constexpr int CM = MODE == 1 ? C1 : (MODE == 2 ? C2 : C3);
     hipLaunchKernelGGL((bn_sum_kernel<double, double>), dim3(ceil_div(2 * CM, 64)), dim3(1024), 0, a.st,
                        static_cast<const double*>(ws), grid * kBnWaves, 2 * CM, sums);
+    return launch_status("dvcp_sa_bn_backward(sum)");
   }
-  return launch_status("dvcp_sa_bn_backward(sum)");
+  return DVCP_OK;
 }
 
 template <typename T, typename FT, int D, int C1, int C2, int C3>
@@ -566,15 +648,49 @@ static int dispatch_stats(const BnArgs& a, int layer, void* ws, double* sums) {
 }
 
 template <typename T, typename FT, int D, int C1, int C2, int C3>
-static int dispatch_bwd(const BnArgs& a, int mode, const float* gout, float* gfeat, int64_t gfb, void* ws,
-                        double* sums, float* gparams) {
-  if (mode == 0) return launch_bwd<T, FT, D, C1, C2, C3, 0>(a, gout, gfeat, gfb, ws, sums, gparams);
-  if (mode == 1) return launch_bwd<T, FT, D, C1, C2, C3, 1>(a, gout, gfeat, gfb, ws, sums, gparams);
-  if (mode == 2) return launch_bwd<T, FT, D, C1, C2, C3, 2>(a, gout, gfeat, gfb, ws, sums, gparams);
+static int dispatch_bwd(const BnArgs& a, int mode, const float* zrows, const float* gout, float* gfeat, int64_t gfb,
+                        void* ws, double* sums, float* rows) {
+  if (mode == -1) {  // the z rows (forward)
+    const int grid = bn_grid(static_cast<int64_t>(a.B) * a.S);
+    PointsView<T> pv{static_cast<const T*>(a.xyz), a.sb, a.sc, a.sn};
+    PointsView<T> cv{static_cast<const T*>(a.ctr), a.cb, a.cc, a.cn};
+    BnFeat<FT> fv{static_cast<const FT*>(a.feat), a.fb, a.fd, a.fn};
+    hipLaunchKernelGGL((sa_bn_zrows_kernel<T, FT, D, C1, C2, C3>), dim3(grid), dim3(kBnThreads), 0, a.st, pv, cv, a.S,
+                       a.B, fv, a.count, a.list, a.nsample, a.pack, rows);
+    return launch_status("dvcp_sa_bn_zrows");
+  }
+  if (mode == 0) return launch_bwd<T, FT, D, C1, C2, C3, 0>(a, zrows, gout, gfeat, gfb, ws, sums, rows);
+  if (mode == 1) return launch_bwd<T, FT, D, C1, C2, C3, 1>(a, zrows, gout, gfeat, gfb, ws, sums, rows);
+  if (mode == 2) return launch_bwd<T, FT, D, C1, C2, C3, 2>(a, zrows, gout, gfeat, gfb, ws, sums, rows);
   if constexpr (C3 > 0)
-    if (mode == 3) return launch_bwd<T, FT, D, C1, C2, C3, 3>(a, gout, gfeat, gfb, ws, sums, gparams);
+    if (mode == 3) return launch_bwd<T, FT, D, C1, C2, C3, 3>(a, zrows, gout, gfeat, gfb, ws, sums, rows);
   set_error("dvcp_sa_bn_backward: mode %d out of range", mode);
   return DVCP_EINVAL;
+}
+
+// Feature dtypes: fp64 only for the 3-channel normals table (ModelNet's double clouds); the
+// 32 / 64-channel tables read the previous layer's fp32 outputs.
+template <typename T, int DD, int A1, int A2, int A3>
+static int stats_ft(const BnArgs& a, bool ff64, int layer, void* ws, double* sums) {
+  if constexpr (DD == 3) {
+    if (ff64) return dispatch_stats<T, double, DD, A1, A2, A3>(a, layer, ws, sums);
+  } else if (DD > 0 && ff64) {
+    set_error("dvcp_sa_bn_stats: fp64 features are taken for the 3-channel table only (D=%d)", DD);
+    return DVCP_EINVAL;
+  }
+  return dispatch_stats<T, float, DD, A1, A2, A3>(a, layer, ws, sums);
+}
+
+template <typename T, int DD, int A1, int A2, int A3>
+static int bwd_ft(const BnArgs& a, bool ff64, int mode, const float* zrows, const float* gout, float* gfeat,
+                  int64_t gfb, void* ws, double* sums, float* rows) {
+  if constexpr (DD == 3) {
+    if (ff64) return dispatch_bwd<T, double, DD, A1, A2, A3>(a, mode, zrows, gout, gfeat, gfb, ws, sums, rows);
+  } else if (DD > 0 && ff64) {
+    set_error("dvcp_sa_bn_backward: fp64 features are taken for the 3-channel table only (D=%d)", DD);
+    return DVCP_EINVAL;
+  }
+  return dispatch_bwd<T, float, DD, A1, A2, A3>(a, mode, zrows, gout, gfeat, gfb, ws, sums, rows);
 }
 
 static int64_t bn_pack_floats(int nlayer, const int* chans) {
@@ -594,13 +710,17 @@ static int64_t bn_pack_floats(int nlayer, const int* chans) {
 
 extern "C" int64_t dvcp_sa_bn_workspace_bytes(int B, int S, int nlayer, const int* chans) {
   if (B < 0 || S < 0 || !chans || (nlayer != 2 && nlayer != 3)) return -1;
-  int64_t P = 0, cmax = 0;
-  for (int l = 0; l < nlayer; ++l) {
-    P += static_cast<int64_t>(chans[l]) * chans[l + 1] + 3 * chans[l + 1];
-    cmax = std::max<int64_t>(cmax, chans[l + 1]);
-  }
+  int64_t cmax = 0;
+  for (int l = 0; l < nlayer; ++l) cmax = std::max<int64_t>(cmax, chans[l + 1]);
   const int64_t nw = static_cast<int64_t>(dvcp::bn_grid(static_cast<int64_t>(B) * S)) * dvcp::kBnWaves;
-  return std::max(nw * P * 4, nw * 2 * cmax * 8);
+  return nw * 2 * cmax * 8;
+}
+
+extern "C" int64_t dvcp_sa_bn_rows_floats(int B, int S, int nsample, int nlayer, const int* chans) {
+  if (B < 0 || S < 0 || nsample < 0 || !chans || (nlayer != 2 && nlayer != 3)) return -1;
+  int64_t per = 0;
+  for (int l = 0; l < nlayer; ++l) per += chans[l + 1] + chans[l] + 1;
+  return per * ((static_cast<int64_t>(B) * S * nsample + 63) / 64 * 64);
 }
 
 extern "C" int64_t dvcp_sa_bn_pack_floats(int nlayer, const int* chans) {
@@ -640,13 +760,9 @@ extern "C" int dvcp_sa_bn_stats(int dtype, const void* xyz, int64_t sb, int64_t 
   const dvcp::BnArgs a{xyz, sb, sc, sn, ctr, cb, cc, cn, S, B, feat, fb, fd, fn, count, list, nsample, pack, st};
   const bool f64 = dtype == DVCP_F64, ff64 = feat_dtype == DVCP_F64;
 #define DVCP_BN_S(DD, A1, A2, A3)                                                                           \
-  if (D == DD && chans[1] == A1 && chans[2] == A2 && (nlayer == 2 ? 0 : chans[3]) == A3) {                 \
-    if (f64)                                                                                                \
-      return ff64 ? dvcp::dispatch_stats<double, double, DD, A1, A2, A3>(a, layer, workspace, sums)         \
-                  : dvcp::dispatch_stats<double, float, DD, A1, A2, A3>(a, layer, workspace, sums);         \
-    return ff64 ? dvcp::dispatch_stats<float, double, DD, A1, A2, A3>(a, layer, workspace, sums)            \
-                : dvcp::dispatch_stats<float, float, DD, A1, A2, A3>(a, layer, workspace, sums);            \
-  }
+  if (D == DD && chans[1] == A1 && chans[2] == A2 && (nlayer == 2 ? 0 : chans[3]) == A3)                   \
+    return f64 ? dvcp::stats_ft<double, DD, A1, A2, A3>(a, ff64, layer, workspace, sums)                    \
+               : dvcp::stats_ft<float, DD, A1, A2, A3>(a, ff64, layer, workspace, sums);
   DVCP_BN_TABLES(DVCP_BN_S)
 #undef DVCP_BN_S
   dvcp::set_error("dvcp_sa_bn_stats: unsupported table D=%d chans=%d,%d", D, chans[1], chans[2]);
@@ -657,40 +773,64 @@ extern "C" int dvcp_sa_bn_backward(int dtype, const void* xyz, int64_t sb, int64
                                    const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B, int feat_dtype,
                                    const void* feat, int64_t fb, int64_t fd, int64_t fn, int D, const int32_t* count,
                                    const int32_t* list, int nsample, int nlayer, const int* chans, const float* pack,
-                                   int mode, const float* grad_out, float* grad_feat, void* workspace, double* sums,
-                                   float* grad_params, void* stream) {
+                                   const float* zrows, int mode, const float* grad_out, float* grad_feat,
+                                   void* workspace, double* sums, float* rows, void* stream) {
   if (int e = bn_check("dvcp_sa_bn_backward", dtype, xyz, ctr, N, S, B, feat_dtype, feat, D, count, list, nsample,
                        nlayer, chans, pack, workspace))
     return e;
-  DVCP_REQUIRE(grad_out, "dvcp_sa_bn_backward: null grad_out");
+  DVCP_REQUIRE(grad_out && zrows, "dvcp_sa_bn_backward: null grad_out / zrows");
   DVCP_REQUIRE(mode >= 0 && mode <= nlayer, "dvcp_sa_bn_backward: mode %d of %d", mode, nlayer);
-  DVCP_REQUIRE(mode == 0 ? grad_params != nullptr : sums != nullptr, "dvcp_sa_bn_backward: null output");
+  DVCP_REQUIRE(mode == 0 ? rows != nullptr : sums != nullptr, "dvcp_sa_bn_backward: null output");
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (B == 0 || S == 0) {
-    int64_t P = 0;
-    for (int l = 0; l < nlayer; ++l) P += static_cast<int64_t>(chans[l]) * chans[l + 1] + 3 * chans[l + 1];
-    const hipError_t e = mode == 0 ? hipMemsetAsync(grad_params, 0, P * 4, st)
-                                   : hipMemsetAsync(sums, 0, 2 * chans[mode] * sizeof(double), st);
-    if (e != hipSuccess) return dvcp::launch_status("dvcp_sa_bn_backward(empty)");
+    if (mode != 0 && hipMemsetAsync(sums, 0, 2 * chans[mode] * sizeof(double), st) != hipSuccess)
+      return dvcp::launch_status("dvcp_sa_bn_backward(empty)");
     return DVCP_OK;
   }
   const dvcp::BnArgs a{xyz, sb, sc, sn, ctr, cb, cc, cn, S, B, feat, fb, fd, fn, count, list, nsample, pack, st};
   const bool f64 = dtype == DVCP_F64, ff64 = feat_dtype == DVCP_F64;
   const int64_t gfb = static_cast<int64_t>(N) * D;  // grad_feat: (B, N, D) fp32 rows
-#define DVCP_BN_B(DD, A1, A2, A3)                                                                                   \
-  if (D == DD && chans[1] == A1 && chans[2] == A2 && (nlayer == 2 ? 0 : chans[3]) == A3) {                         \
-    if (f64)                                                                                                        \
-      return ff64 ? dvcp::dispatch_bwd<double, double, DD, A1, A2, A3>(a, mode, grad_out, grad_feat, gfb,          \
-                                                                        workspace, sums, grad_params)               \
-                  : dvcp::dispatch_bwd<double, float, DD, A1, A2, A3>(a, mode, grad_out, grad_feat, gfb,           \
-                                                                       workspace, sums, grad_params);               \
-    return ff64 ? dvcp::dispatch_bwd<float, double, DD, A1, A2, A3>(a, mode, grad_out, grad_feat, gfb, workspace,   \
-                                                                     sums, grad_params)                             \
-                : dvcp::dispatch_bwd<float, float, DD, A1, A2, A3>(a, mode, grad_out, grad_feat, gfb, workspace,    \
-                                                                    sums, grad_params);                             \
-  }
+#define DVCP_BN_B(DD, A1, A2, A3)                                                                           \
+  if (D == DD && chans[1] == A1 && chans[2] == A2 && (nlayer == 2 ? 0 : chans[3]) == A3)                   \
+    return f64 ? dvcp::bwd_ft<double, DD, A1, A2, A3>(a, ff64, mode, zrows, grad_out, grad_feat, gfb,       \
+                                                       workspace, sums, rows)                               \
+               : dvcp::bwd_ft<float, DD, A1, A2, A3>(a, ff64, mode, zrows, grad_out, grad_feat, gfb,        \
+                                                      workspace, sums, rows);
   DVCP_BN_TABLES(DVCP_BN_B)
 #undef DVCP_BN_B
   dvcp::set_error("dvcp_sa_bn_backward: unsupported table D=%d chans=%d,%d", D, chans[1], chans[2]);
+  return DVCP_EINVAL;
+}
+
+extern "C" int64_t dvcp_sa_bn_zrows_floats(int B, int S, int nsample, int nlayer, const int* chans) {
+  if (B < 0 || S < 0 || nsample < 0 || !chans || (nlayer != 2 && nlayer != 3)) return -1;
+  int64_t per = 0;
+  for (int l = 0; l < nlayer; ++l) per += chans[l + 1];
+  return per * ((static_cast<int64_t>(B) * S * nsample + 63) / 64 * 64);
+}
+
+extern "C" int dvcp_sa_bn_zrows(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, const void* ctr,
+                                int64_t cb, int64_t cc, int64_t cn, int S, int B, int feat_dtype, const void* feat,
+                                int64_t fb, int64_t fd, int64_t fn, int D, const int32_t* count, const int32_t* list,
+                                int nsample, int nlayer, const int* chans, const float* pack, float* zrows,
+                                void* stream) {
+  const int dummy_ws = 0;
+  if (int e = bn_check("dvcp_sa_bn_zrows", dtype, xyz, ctr, N, S, B, feat_dtype, feat, D, count, list, nsample, nlayer,
+                       chans, pack, &dummy_ws))
+    return e;
+  DVCP_REQUIRE(zrows, "dvcp_sa_bn_zrows: null zrows");
+  if (B == 0 || S == 0) return DVCP_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const dvcp::BnArgs a{xyz, sb, sc, sn, ctr, cb, cc, cn, S, B, feat, fb, fd, fn, count, list, nsample, pack, st};
+  const bool f64 = dtype == DVCP_F64, ff64 = feat_dtype == DVCP_F64;
+#define DVCP_BN_Z(DD, A1, A2, A3)                                                                           \
+  if (D == DD && chans[1] == A1 && chans[2] == A2 && (nlayer == 2 ? 0 : chans[3]) == A3)                   \
+    return f64 ? dvcp::bwd_ft<double, DD, A1, A2, A3>(a, ff64, -1, nullptr, nullptr, nullptr, 0, nullptr,  \
+                                                       nullptr, zrows)                                      \
+               : dvcp::bwd_ft<float, DD, A1, A2, A3>(a, ff64, -1, nullptr, nullptr, nullptr, 0, nullptr,   \
+                                                      nullptr, zrows);
+  DVCP_BN_TABLES(DVCP_BN_Z)
+#undef DVCP_BN_Z
+  dvcp::set_error("dvcp_sa_bn_zrows: unsupported table D=%d chans=%d,%d", D, chans[1], chans[2]);
   return DVCP_EINVAL;
 }

@@ -64,7 +64,9 @@ SIGNATURES = {
     "dvcp_sa_bn_stats": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _L, _L, _L, _I,
                          _P, _P, _I, _I, _P, _P, _I, _P, _P, _P],
     "dvcp_sa_bn_backward": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _L, _L, _L, _I,
-                            _P, _P, _I, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P],
+                            _P, _P, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P],
+    "dvcp_sa_bn_zrows": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _L, _L, _L, _I,
+                         _P, _P, _I, _I, _P, _P, _P, _P],
 }
 
 _lib = None
@@ -104,6 +106,10 @@ def load():
     lib.dvcp_fe_head_backward_workspace_bytes.argtypes = [ctypes.c_int]
     lib.dvcp_sa_bn_workspace_bytes.restype = ctypes.c_int64
     lib.dvcp_sa_bn_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    lib.dvcp_sa_bn_rows_floats.restype = ctypes.c_int64
+    lib.dvcp_sa_bn_rows_floats.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    lib.dvcp_sa_bn_zrows_floats.restype = ctypes.c_int64
+    lib.dvcp_sa_bn_zrows_floats.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     lib.dvcp_sa_bn_pack_floats.restype = ctypes.c_int64
     lib.dvcp_sa_bn_pack_floats.argtypes = [ctypes.c_int, ctypes.c_void_p]
     for name, args in SIGNATURES.items():
@@ -120,7 +126,7 @@ def exported_symbols():
             "dvcp_sa_group_mlp_workspace_bytes", "dvcp_dfe_backward_workspace_bytes",
             "dvcp_cpg_backward_workspace_bytes", "dvcp_sa_group_mlp_backward_workspace_bytes",
             "dvcp_fe_head_backward_workspace_bytes", "dvcp_sa_bn_workspace_bytes",
-            "dvcp_sa_bn_pack_floats"] + list(SIGNATURES)
+            "dvcp_sa_bn_pack_floats", "dvcp_sa_bn_rows_floats", "dvcp_sa_bn_zrows_floats"] + list(SIGNATURES)
 
 
 # When a list, every entry-point call appends (name, start_event, end_event, work) recorded on

@@ -9,11 +9,14 @@ variance), once per FE1 call -- src and tgt are separate calls (deepVCP.py:29,72
 Forward (``train_forward``): one statistics pass per layer (dvcp_sa_bn_stats: fp64 sums of z and
 z^2, the layers below normalised by their batch statistics), then the eval kernel
 (dvcp_sa_group_mlp) with the batch statistics folded into its scale / shift.
-Backward (``train_backward``): torch's batch-norm backward,
+Backward (``train_backward``): every entry's conv outputs z_l are written once (dvcp_sa_bn_zrows,
+64-entry blocks, a few GB at C3 -- HBM is 288 GB), then torch's batch-norm backward,
     dz_l = scale_l (dy_l - mean(dy_l) - xhat_l mean(dy_l xhat_l)),
 whose mean terms make every entry's gradient non-zero: sums of the top layer over the routed
 (arg-max) rows, one dense pass per lower layer for its sums, and a final dense pass for dW, db and
-the feature gradient (dvcp_sa_bn_backward modes L..1, 0; csrc/sa_bn.hip).
+the per-entry rows of the weight gradients and the feature gradient (dvcp_sa_bn_backward modes
+L..1, 0; csrc/sa_bn.hip); dW_l, db_l are then GEMMs over the entries (hipBLASLt via torch.bmm,
+K-chunked, chunk sums in fp64).
 """
 import torch
 
@@ -81,18 +84,37 @@ def train_backward(sa, lay, g_out, want_feat_grad):
     pack, M = st["pack"].clone(), st["M"]
     args = (lay["pts"], lay["ctr"], lay["feat"], lay["count"], lay["lst"], lay["ns"], chans)
     g = g_out.float().contiguous()
+    # every entry's conv outputs, with this batch's statistics (held only during this backward)
+    zrows = ops.sa_bn_zrows(*args, st["pack"])
     sums = [None] * len(offs)
     for k in range(len(offs), 0, -1):   # the top layer's sums first: each lower one needs those above
-        s = ops.sa_bn_backward(*args, pack, g, k)
+        s = ops.sa_bn_backward(*args, pack, zrows, g, k)
         o, cin, cout = offs[k - 1]
         v = o + cout * cin + 5 * cout
         pack[v:v + 2 * cout] = (s / M).reshape(-1).float()
         sums[k - 1] = s
-    gp, gF = ops.sa_bn_backward(*args, pack, g, 0, want_feat_grad=want_feat_grad)
-    q = 0
-    for (o, cin, cout), s in zip(offs, sums):
-        q += cout * cin + cout
-        gp[q:q + cout] = s[1].float()          # dgamma = sum dy * xhat
-        gp[q + cout:q + 2 * cout] = s[0].float()  # dbeta = sum dy
-        q += 2 * cout
-    return gp, gF
+    rows, gF = ops.sa_bn_backward(*args, pack, zrows, g, 0, want_feat_grad=want_feat_grad)
+    del zrows
+    parts = []
+    for (o, cin, cout), s, (gz, ha) in zip(offs, sums, rows):
+        dwb = _gemm_nt(gz, ha)                  # [dW | db] = dz [h; 1]^T over the M entries
+        parts += [dwb[:, :cin].reshape(-1), dwb[:, cin], s[1], s[0]]   # dW, db, dgamma, dbeta
+    return torch.cat([p.float() for p in parts]), gF
+
+
+def _gemm_nt(a, b, q=1024):
+    """sum over blocks of a_blk @ b_blk^T for (nb, m, 64) / (nb, n, 64) blocked row tables (up to
+    ~10^8 entries): fp32 GEMMs (hipBLASLt via torch.bmm) over chunks of q blocks, the chunk
+    products summed in fp64 in a fixed order."""
+    nb, m, n = a.shape[0], a.shape[1], b.shape[1]
+    nch = nb // q
+    acc = torch.zeros(m, n, dtype=torch.float64, device=a.device)
+    if nch:
+        ca = a[:nch * q].view(nch, q, m, 64).permute(0, 2, 1, 3).reshape(nch, m, q * 64)
+        cb = b[:nch * q].view(nch, q, n, 64).permute(0, 1, 3, 2).reshape(nch, q * 64, n)
+        acc += torch.bmm(ca, cb).double().sum(0)
+    if nb > nch * q:
+        ra = a[nch * q:].permute(1, 0, 2).reshape(m, -1)
+        rb = b[nch * q:].permute(1, 0, 2).reshape(n, -1)
+        acc += (ra @ rb.t()).double()
+    return acc

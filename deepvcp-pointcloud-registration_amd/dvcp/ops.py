@@ -507,7 +507,7 @@ def sa_group_mlp_backward(xyz, ctr, feat, count, lst, nsample, chans, params, bn
     return gp, gF
 
 
-def _bn_common(xyz, ctr, feat, count, lst, nsample, chans, pack, xyz_pdim, feat_ddim, feat_pdim):
+def _bn_common(xyz, ctr, feat, count, lst, nsample, chans, pack, xyz_pdim, feat_ddim, feat_pdim, workspace=True):
     """The grouping arguments shared by dvcp_sa_bn_stats / dvcp_sa_bn_backward."""
     _lib.require_gpu(xyz, ctr, count, lst, pack)
     B = xyz.shape[0]
@@ -522,8 +522,10 @@ def _bn_common(xyz, ctr, feat, count, lst, nsample, chans, pack, xyz_pdim, feat_
         D, fb, fd, fn, fdt = 0, 0, 0, 0, _lib.F32
     ch = torch.tensor(list(chans), dtype=torch.int32)
     nl = len(chans) - 1
-    ws_bytes = int(_lib.load().dvcp_sa_bn_workspace_bytes(B, S, nl, ch.data_ptr()))
-    ws = torch.empty(max(1, ws_bytes // 4), dtype=torch.float32, device=xyz.device)
+    ws = None
+    if workspace:
+        ws_bytes = int(_lib.load().dvcp_sa_bn_workspace_bytes(B, S, nl, ch.data_ptr()))
+        ws = torch.empty(max(1, ws_bytes // 4), dtype=torch.float32, device=xyz.device)
     args = (dtype_code(xyz), ptr(xyz), sb, sc, sn, N, ptr(ctr), cb, cc, cn, S, B, fdt, ptr(feat), fb, fd, fn, D,
             ptr(count), ptr(lst), int(nsample), nl, ptr(ch), ptr(pack))
     return args, ws, (B, N, S, D), ch
@@ -547,24 +549,48 @@ def sa_bn_stats(xyz, ctr, feat, count, lst, nsample, chans, pack, layer, xyz_pdi
     return sums
 
 
-def sa_bn_backward(xyz, ctr, feat, count, lst, nsample, chans, pack, grad_out, mode, want_feat_grad=False,
+def sa_bn_zrows(xyz, ctr, feat, count, lst, nsample, chans, pack, xyz_pdim=2, feat_ddim=1, feat_pdim=2):
+    """Every grouped entry's conv outputs z_l of every layer with the batch statistics in ``pack``:
+    flat fp32, per layer (M / 64, C_l, 64) blocks (what dvcp_sa_bn_backward reads)."""
+    args, _, (B, N, S, D), ch = _bn_common(xyz, ctr, feat, count, lst, nsample, chans, pack, xyz_pdim, feat_ddim,
+                                           feat_pdim, workspace=False)
+    n = int(_lib.load().dvcp_sa_bn_zrows_floats(B, S, int(nsample), len(chans) - 1, ch.data_ptr()))
+    z = torch.empty(max(n, 1), dtype=torch.float32, device=xyz.device)
+    macs = sum(a * b for a, b in zip(chans[:-1], chans[1:]))
+    call("dvcp_sa_bn_zrows", *args, ptr(z), stream(), work=(2.0 * macs * B * S * nsample, 4.0 * n))
+    return z
+
+
+def sa_bn_backward(xyz, ctr, feat, count, lst, nsample, chans, pack, zrows, grad_out, mode, want_feat_grad=False,
                    xyz_pdim=2, feat_ddim=1, feat_pdim=2):
     """Training-mode (batch-statistics) backward of the grouped MLP.  mode k >= 1: (2, C_k) fp64
-    sums (A_k = dbeta_k, B_k = dgamma_k); mode 0: (packed dW, db, 0, 0 per layer; dL/d feat
-    (B, N, D) fp32 or None)."""
+    sums (A_k = dbeta_k, B_k = dgamma_k); mode 0: (per layer (dL/dz_l, [h_{l-1}; 1]) as
+    (M / 64, C, 64) blocked fp32 views, dL/d feat (B, N, D) fp32 or None)."""
     args, ws, (B, N, S, D), ch = _bn_common(xyz, ctr, feat, count, lst, nsample, chans, pack, xyz_pdim, feat_ddim,
                                             feat_pdim)
     dev = xyz.device
     g = grad_out.float().contiguous()
     if mode > 0:
         sums = torch.empty(2, chans[mode], dtype=torch.float64, device=dev)
-        call("dvcp_sa_bn_backward", *args, int(mode), ptr(g), None, ptr(ws), ptr(sums), None, stream())
+        call("dvcp_sa_bn_backward", *args, ptr(zrows), int(mode), ptr(g), None, ptr(ws), ptr(sums), None, stream())
         return sums
-    npar = sum(a * b + 3 * b for a, b in zip(chans[:-1], chans[1:]))
-    gp = torch.empty(npar, dtype=torch.float32, device=dev)
+    M = B * S * int(nsample)
+    nrows = int(_lib.load().dvcp_sa_bn_rows_floats(B, S, int(nsample), len(chans) - 1, ch.data_ptr()))
+    rows = torch.empty(max(nrows, 1), dtype=torch.float32, device=dev)
     gF = torch.zeros(B, N, D, dtype=torch.float32, device=dev) if (want_feat_grad and D > 0) else None
-    call("dvcp_sa_bn_backward", *args, 0, ptr(g), ptr(gF), ptr(ws), None, ptr(gp), stream())
-    return gp, gF
+    call("dvcp_sa_bn_backward", *args, ptr(zrows), 0, ptr(g), ptr(gF), ptr(ws), None, ptr(rows), stream())
+    Mp = -(-M // 64) * 64   # tables are 64-entry blocks, channel-major inside (csrc/sa_bn.hip bn_at)
+    views, o = [], 0
+    for cin, cout in zip(chans[:-1], chans[1:]):
+        gz = rows[o:o + cout * Mp].view(Mp // 64, cout, 64)
+        o += cout * Mp
+        ha = rows[o:o + (cin + 1) * Mp].view(Mp // 64, cin + 1, 64)
+        o += (cin + 1) * Mp
+        if Mp > M:  # the padding entries of the last block take no part in the GEMMs
+            gz[-1, :, M % 64:] = 0.0
+            ha[-1, :, M % 64:] = 0.0
+        views.append((gz, ha))
+    return views, gF
 
 
 def fe_head_backward(x, params, grad):

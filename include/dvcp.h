@@ -269,15 +269,27 @@ int dvcp_sa_group_mlp_backward(int dtype, const void* xyz, int64_t sb, int64_t s
  * batch-norm backward sums of layer l (zero until known).
  * dvcp_sa_bn_stats: sums (2 x C_layer fp64) = per-channel sum z and sum z^2 of the conv output of
  *   `layer` (1-based) over all M entries, the layers below it normalised by their pack entries.
+ * dvcp_sa_bn_zrows: zrows (dvcp_sa_bn_zrows_floats floats) = every entry's conv output z_l of
+ *   every layer, channel-major (C_l x M per layer, entry e = centre * nsample + slot), with the
+ *   pack's final batch statistics; the backward reads them instead of recomputing the MLP.
  * dvcp_sa_bn_backward(mode): mode = k >= 1 -> sums (2 x C_k fp64) = A_k = sum dL/dy_k (dbeta) and
  *   B_k = sum dL/dy_k * xhat_k (dgamma), needing A, B of the layers above k (mode = nlayer needs
- *   none); mode = 0 -> grad_params (per layer dW, db, 0, 0: the host fills dgamma / dbeta with
- *   B, A) and, if grad_feat is given (zeroed by the caller), dL/d feat (B x N x D fp32) through
- *   the grouping.  grad_out: B x S x C_last fp32.  workspace: dvcp_sa_bn_workspace_bytes bytes.
+ *   none); mode = 0 -> rows (dvcp_sa_bn_rows_floats floats): per layer l, dL/dz_l of every entry
+ *   (C_l x M, channel-major) then the layer's input rows and a ones row (C_{l-1} + 1 x M), so
+ *   [dW_l | db_l] = dz_l [h_{l-1}; 1]^T is a plain GEMM over the entries (the host runs it); and,
+ *   if grad_feat is given (zeroed by the caller), dL/d feat (B x N x D fp32) through the grouping.
+ *   grad_out: B x S x C_last fp32.  workspace: dvcp_sa_bn_workspace_bytes bytes.
  * Replaces the training-mode forward/backward of pointnet2_utils.py:176-202 (BatchNorm2d batch
  * statistics, running-stat update done by the host). */
 int64_t dvcp_sa_bn_pack_floats(int nlayer, const int* chans);
 int64_t dvcp_sa_bn_workspace_bytes(int B, int S, int nlayer, const int* chans);
+int64_t dvcp_sa_bn_rows_floats(int B, int S, int nsample, int nlayer, const int* chans);
+int64_t dvcp_sa_bn_zrows_floats(int B, int S, int nsample, int nlayer, const int* chans);
+int dvcp_sa_bn_zrows(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
+                     const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
+                     int feat_dtype, const void* feat, int64_t fb, int64_t fd, int64_t fn, int D,
+                     const int32_t* count, const int32_t* list, int nsample, int nlayer,
+                     const int* chans, const float* pack, float* zrows, void* stream);
 int dvcp_sa_bn_stats(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
                      const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
                      int feat_dtype, const void* feat, int64_t fb, int64_t fd, int64_t fn, int D,
@@ -288,9 +300,9 @@ int dvcp_sa_bn_backward(int dtype, const void* xyz, int64_t sb, int64_t sc, int6
                         const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
                         int feat_dtype, const void* feat, int64_t fb, int64_t fd, int64_t fn,
                         int D, const int32_t* count, const int32_t* list, int nsample, int nlayer,
-                        const int* chans, const float* pack, int mode, const float* grad_out,
-                        float* grad_feat, void* workspace, double* sums, float* grad_params,
-                        void* stream);
+                        const int* chans, const float* pack, const float* zrows, int mode,
+                        const float* grad_out, float* grad_feat, void* workspace, double* sums,
+                        float* rows, void* stream);
 
 /* Backward of the feature extractor's fc (deep_feat_extraction.py:15, Linear 64 -> 32):
  * x: P x 64 fp32 (its input rows), params: fc.W (32 x 64) | fc.b (32), grad: P x 32;
