@@ -15,4 +15,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAF
   -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --inflight 1 --steps 6 --warmup 2 > "$GRAFT_REPO_ROOT/gpurun_out/prof_iso.log" 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_p10" -o run \
   -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/prof_p10.log" 2>&1 || exit $?
-bash "$GRAFT_REPO_ROOT/tools/gpu_pmc.sh" pmc_r2t
+bash "$GRAFT_REPO_ROOT/tools/gpu_pmc.sh" "${1:-pmc_r2v}"
