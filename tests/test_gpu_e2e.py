@@ -183,7 +183,7 @@ def test_module_surface_errors(cuda):
     import dvcp
     m = dvcp.DeepVCP(use_normal=False).to(cuda)   # training mode by default, like nn.Module
     x = torch.zeros(1, 3, 64, device=cuda)
-    with pytest.raises(NotImplementedError):
+    with torch.no_grad(), pytest.raises(NotImplementedError):   # training mode needs autograd
         m(x, x, torch.eye(3, dtype=torch.float64, device=cuda)[None], torch.zeros(1, 3))
     m.eval()
     with pytest.raises(RuntimeError, match="float64"):
