@@ -64,8 +64,11 @@ def parse():
     p.add_argument("--warmup", type=int, default=4)
     p.add_argument("--config", choices=["c3", "c5"], default="c3",
                    help="c3: BASELINE's headline (8 pairs x 16384 points, K=64); c5: the stress config "
-                        "(65536 points, K=256, 2 pairs per batch, fp32 features, no CPU baseline)")
+                        "(65536 points, K=256, 2 pairs per batch, fp16 features, no CPU baseline)")
     p.add_argument("--batch", type=int, default=None, help="pairs per GPU (c3: 8, c5: 2)")
+    p.add_argument("--feat-dtype", choices=["f32", "f16"], default=None,
+                   help="target feature-table storage (c3: f32 = the reference's; c5: f16, BASELINE's "
+                        "'fp16 features')")
     p.add_argument("--npoints", type=int, default=None)
     p.add_argument("--K", type=int, default=None)
     p.add_argument("--r", type=float, default=2.0)
@@ -85,6 +88,7 @@ def parse():
     a.batch = a.batch if a.batch is not None else (2 if c5 else 8)
     a.npoints = a.npoints if a.npoints is not None else (65536 if c5 else 16384)
     a.K = a.K if a.K is not None else (256 if c5 else 64)
+    a.feat_dtype = a.feat_dtype or ("f16" if c5 else "f32")
     if c5:
         a.no_cpu_baseline = True   # minutes per pair on the host: not a bounded sample
     return a
@@ -107,7 +111,8 @@ def main():
     B, N, K, r, s = args.batch, args.npoints, args.K, args.r, args.s
     P = max(1, args.inflight)
     torch.manual_seed(0)
-    model = dvcp.DeepVCP(use_normal=False, K=K, r=r, s=s).eval().to(dev)
+    model = dvcp.DeepVCP(use_normal=False, K=K, r=r, s=s,
+                         feat_dtype=torch.float16 if args.feat_dtype == "f16" else torch.float32).eval().to(dev)
     # one distinct synthetic batch per in-flight lane
     batches = []
     for lane in range(P):
@@ -197,13 +202,13 @@ def main():
     value = pairs / elapsed
     c5 = args.config == "c5"
     out = {
-        "metric": ("pairs/sec (full DeepVCP forward) at N=65536, K=256 (C5 stress, fp32 features)" if c5 else
+        "metric": (f"pairs/sec (full DeepVCP forward) at N=65536, K=256 (C5 stress, {args.feat_dtype} features)" if c5 else
                    "pairs/sec (full DeepVCP forward) at N=16384, K=64; rot/trans error vs ref"),
         "value": round(value, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": ("C5: synthetic 65536-point pairs, K=256, DeepVCP.forward + deepVCP_loss (eval), fp32 "
-                                "features (the fp16-feature variant is not built)" if c5 else
+        "config": {"workload": ("C5: synthetic 65536-point pairs, K=256, DeepVCP.forward + deepVCP_loss (eval), "
+                                f"{args.feat_dtype} target feature table (dvcp_dfe_tgt_f16 for f16)" if c5 else
                                 "C3: KITTI-like synthetic pairs, DeepVCP.forward + deepVCP_loss (eval)"),
                    "pairs_per_gpu": B, "global_batch": B * world, "n_points": N, "K": K, "r": r, "s": s,
                    "candidates": C, "fe_npoint": S, "parallelism": f"pairs sharded x{world}, all_gather(R,t)",

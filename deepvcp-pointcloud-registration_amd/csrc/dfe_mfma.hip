@@ -158,9 +158,12 @@ struct Dfe1Lds {
   float w[kDfe1Waves][32];  // per-wave w_j of the current candidate (fp64 quotient rounded to fp32)
 };
 
-template <typename T>
+// FT: the feature table's element type -- float, or _Float16 (the C5 "fp16 features" storage:
+// half the gathered bytes; each row is widened to fp32 before the weighting, which then runs in
+// fp32 exactly as for a float table holding the same values).
+template <typename T, typename FT = float>
 __global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
-    PointsView<T> ref, const float* __restrict__ feat, int M, const float* __restrict__ cand,
+    PointsView<T> ref, const FT* __restrict__ feat, int M, const float* __restrict__ cand,
     const float* __restrict__ dist, const int32_t* __restrict__ idx, int Q, int B, const float* __restrict__ params,
     float* __restrict__ out, int xcd) {
   __shared__ Dfe1Lds L;
@@ -236,6 +239,7 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
   };
   struct Gathered {
     float4 f[4];
+    uint4 hf[2];  // fp16 table: the row's 16 halves of this lane half, widened in embed
     T px, py, pz;
     float cx, cy, cz;
   };
@@ -243,9 +247,15 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
     const int gc = glob(gg < total ? gg : total - 1);
     const int bb = gc / Q;
     const int n = nraw < 0 ? 0 : (nraw >= M ? M - 1 : nraw);
-    const float4* fr = reinterpret_cast<const float4*>(feat + (static_cast<int64_t>(bb) * M + n) * 32 + 16 * h);
+    if constexpr (sizeof(FT) == 4) {
+      const float4* fr = reinterpret_cast<const float4*>(feat + (static_cast<int64_t>(bb) * M + n) * 32 + 16 * h);
 #pragma unroll
-    for (int v = 0; v < 4; ++v) G.f[v] = fr[v];
+      for (int v = 0; v < 4; ++v) G.f[v] = fr[v];
+    } else {
+      const uint4* fr = reinterpret_cast<const uint4*>(feat + (static_cast<int64_t>(bb) * M + n) * 32 + 16 * h);
+      G.hf[0] = fr[0];
+      G.hf[1] = fr[1];
+    }
     G.px = ref.at(bb, 0, n);
     G.py = ref.at(bb, 1, n);
     G.pz = ref.at(bb, 2, n);
@@ -272,13 +282,28 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
     // the wave's own w row, read back as 16-byte broadcasts
     __builtin_amdgcn_wave_barrier();
     const float4* wr = reinterpret_cast<const float4*>(&L.w[wave][16 * h]);
+    float4 fv[4];
+    if constexpr (sizeof(FT) == 4) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) fv[v] = G.f[v];
+    } else {
+      const uint32_t* hw = reinterpret_cast<const uint32_t*>(G.hf);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const uint32_t lo = hw[2 * v], hi = hw[2 * v + 1];
+        fv[v].x = static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(lo & 0xFFFFu)));
+        fv[v].y = static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(lo >> 16)));
+        fv[v].z = static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(hi & 0xFFFFu)));
+        fv[v].w = static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(hi >> 16)));
+      }
+    }
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const float4 w4 = wr[v];
-      x[3 + 4 * v] = G.f[v].x * w4.x;
-      x[4 + 4 * v] = G.f[v].y * w4.y;
-      x[5 + 4 * v] = G.f[v].z * w4.z;
-      x[6 + 4 * v] = G.f[v].w * w4.w;
+      x[3 + 4 * v] = fv[v].x * w4.x;
+      x[4 + 4 * v] = fv[v].y * w4.y;
+      x[5 + 4 * v] = fv[v].z * w4.z;
+      x[6 + 4 * v] = fv[v].w * w4.w;
     }
     int zo = 0;  // opaque zero: E fragments are re-read from LDS per candidate, not hoisted
     asm volatile("" : "+v"(zo));
@@ -341,9 +366,45 @@ int launch_dfe_tgt_mfma(PointsView<T> ref, const float* feat, int M, const float
   return launch_status("dvcp_dfe_tgt(mfma)");
 }
 
+// The fp16-feature table (C5): the non-literal kernel only.
+template <typename T>
+int launch_dfe_tgt_mfma_f16(PointsView<T> ref, const _Float16* feat, int M, const float* cand, const float* dist,
+                            const int32_t* idx, int B, int Q, const float* params, float* out, hipStream_t st) {
+  const int64_t total = static_cast<int64_t>(B) * Q;
+  if (total >= (int64_t(1) << 31) / 32) {
+    set_error("dvcp_dfe_tgt_f16: B*Q=%lld too large", static_cast<long long>(total));
+    return DVCP_EINVAL;
+  }
+  const int64_t need = (total + kDfeMfmaWaves - 1) / kDfeMfmaWaves;
+  const int xcd = B % 8 == 0 && need >= 2048 ? 1 : 0;
+  const int grid = static_cast<int>(need < 2048 ? need : 2048);
+  hipLaunchKernelGGL((dfe_tgt_mfma1_kernel<T, _Float16>), dim3(grid), dim3(kDfe1Waves * kWave), 0, st, ref, feat, M,
+                     cand, dist, idx, Q, B, params, out, xcd);
+  return launch_status("dvcp_dfe_tgt_f16");
+}
+
 template int launch_dfe_tgt_mfma<float>(PointsView<float>, const float*, int, const float*, const float*,
                                         const int32_t*, int, int, const float*, float*, bool, hipStream_t);
 template int launch_dfe_tgt_mfma<double>(PointsView<double>, const float*, int, const float*, const float*,
                                          const int32_t*, int, int, const float*, float*, bool, hipStream_t);
 
 }  // namespace dvcp
+
+extern "C" int dvcp_dfe_tgt_f16(int dtype, const void* ref_xyz, int64_t rb, int64_t rc, int64_t rn, int M,
+                                const uint16_t* ref_feat, const float* cand, const float* dist, const int32_t* idx,
+                                int B, int Q, const float* params, float* out, void* stream) {
+  DVCP_REQUIRE(ref_xyz && ref_feat && cand && dist && idx && params && out, "dvcp_dfe_tgt_f16: null pointer");
+  DVCP_REQUIRE(M > 0 && B >= 0 && B <= 65535 && Q >= 0, "dvcp_dfe_tgt_f16: bad sizes");
+  if (B == 0 || Q == 0) return DVCP_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const _Float16* f = reinterpret_cast<const _Float16*>(ref_feat);
+  if (dtype == DVCP_F32)
+    return dvcp::launch_dfe_tgt_mfma_f16<float>(dvcp::PointsView<float>{static_cast<const float*>(ref_xyz), rb, rc, rn},
+                                                f, M, cand, dist, idx, B, Q, params, out, st);
+  if (dtype == DVCP_F64)
+    return dvcp::launch_dfe_tgt_mfma_f16<double>(
+        dvcp::PointsView<double>{static_cast<const double*>(ref_xyz), rb, rc, rn}, f, M, cand, dist, idx, B, Q, params,
+        out, st);
+  dvcp::set_error("dvcp_dfe_tgt_f16: bad dtype %d", dtype);
+  return DVCP_EINVAL;
+}

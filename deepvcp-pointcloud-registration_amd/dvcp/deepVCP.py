@@ -27,8 +27,14 @@ from .weighting_layer import weighting_layer
 
 
 class DeepVCP(nn.Module):
-    def __init__(self, use_normal, K=64, r=1.0, s=0.4, fe_npoint=10000):
+    def __init__(self, use_normal, K=64, r=1.0, s=0.4, fe_npoint=10000, feat_dtype=torch.float32):
+        """``feat_dtype``: storage of the target feature table the fused target stage gathers
+        (torch.float16: BASELINE C5's "fp16 features", dvcp_dfe_tgt_f16; inference only -- the
+        reference keeps fp32 features, so float16 is not reference precision)."""
         super().__init__()
+        if feat_dtype not in (torch.float32, torch.float16):
+            raise ValueError(f"feat_dtype must be torch.float32 or torch.float16, got {feat_dtype}")
+        self.feat_dtype = feat_dtype
         self.FE1 = feat_extraction_layer(use_normal=use_normal, npoint=fe_npoint)
         self.WL = weighting_layer()
         self.DFE = feat_embedding_layer()
@@ -156,7 +162,8 @@ class DeepVCP(nn.Module):
             tgt_dfe = autograd.dfe_tgt(tgt_xyz, tgt_feat, qry, dist, idx, self.DFE).view(B, K, C, 32)
             vcp = autograd.cpg(src_dfe, tgt_dfe.permute(0, 1, 3, 2), cand, G, self.cpg)
         else:
-            tgt_dfe = ops.dfe_tgt(tgt_xyz, tgt_feat, qry, dist, idx, self.DFE.packed_params(), ref_pdim=2)
+            feat_t = tgt_feat if self.feat_dtype == torch.float32 else tgt_feat.to(self.feat_dtype)
+            tgt_dfe = ops.dfe_tgt(tgt_xyz, feat_t, qry, dist, idx, self.DFE.packed_params(), ref_pdim=2)
             tgt_dfe = tgt_dfe.view(B, K, C, 32)
             vcp = ops.cpg(src_dfe, tgt_dfe.permute(0, 1, 3, 2), cand, G, self.cpg.packed_params())
         if trace is not None:

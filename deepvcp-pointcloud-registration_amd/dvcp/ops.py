@@ -290,10 +290,16 @@ def dfe_tgt(ref_xyz, ref_feat, cand, dist, idx, params, ref_pdim=2, literal=Fals
     Q = cand.shape[1]
     feat_c, cand_c, dist_c, idx_c = ref_feat.contiguous(), cand.contiguous(), dist.contiguous(), idx.contiguous()
     out = torch.empty(B, Q, 32, dtype=torch.float32, device=ref_xyz.device)
-    call("dvcp_dfe_tgt_literal" if literal else "dvcp_dfe_tgt", dtype_code(ref_xyz), ptr(ref_xyz), rb, rc, rn, M,
-         ptr(feat_c), ptr(cand_c), ptr(dist_c),
+    half = feat_c.dtype == torch.float16   # the C5 fp16-feature storage (dvcp_dfe_tgt_f16)
+    if half and literal:
+        raise ValueError("dfe_tgt: the literal (Q14) path takes fp32 features only")
+    if not half and feat_c.dtype != torch.float32:
+        raise TypeError(f"dfe_tgt: features must be float32 or float16, got {feat_c.dtype}")
+    name = "dvcp_dfe_tgt_f16" if half else ("dvcp_dfe_tgt_literal" if literal else "dvcp_dfe_tgt")
+    row = 64 if half else 128
+    call(name, dtype_code(ref_xyz), ptr(ref_xyz), rb, rc, rn, M, ptr(feat_c), ptr(cand_c), ptr(dist_c),
          ptr(idx_c), B, Q, ptr(params), ptr(out), stream(),
-         work=(2.0 * 3168 * 32 * B * Q, B * (M * (12 + 128) + Q * (12 + 32 * 8 + 128)),
+         work=(2.0 * 3168 * 32 * B * Q, B * (M * (12 + row) + Q * (12 + 32 * 8 + 128)),
                2.0 * (3168 if literal else 35 * 32) * 32 * B * Q))
     return out
 

@@ -233,6 +233,15 @@ int dvcp_dfe_tgt(int dtype, const void* ref_xyz, int64_t rb, int64_t rc, int64_t
                  const float* ref_feat, const float* cand, const float* dist, const int32_t* idx,
                  int B, int Q, const float* params, float* out, void* stream);
 
+/* dvcp_dfe_tgt with the target feature table stored as fp16 (ref_feat: B x M x 32 IEEE halves) --
+ * BASELINE C5's "fp16 features" storage, half the gathered feature bytes.  Each gathered row is
+ * widened to fp32 and the rest is dvcp_dfe_tgt's fp32 arithmetic: the output equals dvcp_dfe_tgt
+ * on the fp32 table holding the same (fp16-rounded) values.  Not reference precision (the
+ * reference keeps fp32/fp64 features); an opt-in storage mode (DeepVCP(feat_dtype=float16)). */
+int dvcp_dfe_tgt_f16(int dtype, const void* ref_xyz, int64_t rb, int64_t rc, int64_t rn, int M,
+                     const uint16_t* ref_feat, const float* cand, const float* dist, const int32_t* idx,
+                     int B, int Q, const float* params, float* out, void* stream);
+
 /* dvcp_dfe_tgt evaluating fc1, fc2, fc3 one after the other exactly as deep_feat_embedding.py:
  * 48-50 chains them.  dvcp_dfe_tgt instead collapses the three linear
  * layers into one 32 x 35 map (formed in fp64, rounded once to fp32); both agree within fp32

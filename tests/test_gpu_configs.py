@@ -6,9 +6,9 @@ test_gpu_e2e.py's):
   eval mode), and pair 0 matches the oracle (key points exact, R, t within 1e-4).
 * C5 -- synthetic 65536-point clouds, K = 256: the first FPS (65536 -> 10000, the dense kernel
   above the register-resident limit) is bit-exact against the oracle, and the full forward +
-  pose solve runs with its structural properties intact.  C5's "fp16 features" is a stress
-  variant; the path keeps fp32 features (parity with the reference's fp32 FE), so it is run here
-  in fp32.
+  pose solve runs with its structural properties intact, with the reference's fp32 features and
+  with BASELINE's fp16 feature storage (DeepVCP(feat_dtype=torch.float16): same key points, vcp
+  and R, t within the features' fp16 rounding of the fp32 run).
 """
 import pytest
 import torch
@@ -108,6 +108,36 @@ def test_c5_forward_properties(cuda):
     torch.testing.assert_close(R @ R.transpose(1, 2), torch.eye(3, dtype=R.dtype, device=cuda).expand_as(R),
                                rtol=0, atol=1e-9)
     assert float(det.abs().min()) == pytest.approx(1.0, abs=1e-9)
+
+
+def test_c5_fp16_features_vs_fp32(cuda):
+    """C5 with BASELINE's "fp16 features" (the target feature table stored as fp16, gathered by
+    dvcp_dfe_tgt_f16) against the same forward on fp32 features: identical key points and
+    candidates, vcp within 1e-2 (fp16 rounding of the features, through the CPG softmax), R, t
+    within 1e-3."""
+    import dvcp
+    from dvcp.synthetic import make_pairs
+    B, N, K, r, s = 1, 65536, 256, 2.0, 0.4
+    src, tgt, R_gt, t_gt = [x.to(cuda) for x in make_pairs(B, N, seed=556)]
+    torch.manual_seed(0)
+    m32 = dvcp.DeepVCP(use_normal=False, K=K, r=r, s=s).eval().to(cuda)
+    m16 = dvcp.DeepVCP(use_normal=False, K=K, r=r, s=s, feat_dtype=torch.float16).eval().to(cuda)
+    m16.load_state_dict(m32.state_dict())
+    starts = m32.draw_starts(B, N, N)
+    out = []
+    with torch.no_grad():
+        for m in (m32, m16):
+            tr = {}
+            kp, vcp = m(src, tgt, R_gt, torch.zeros(1, 3), starts=starts, trace=tr)
+            _, R, t = dvcp.deepVCP_loss(kp, vcp, R_gt, t_gt, 0.5)
+            out.append((kp, vcp, R, t, tr["cand"]))
+    (kp0, v0, R0, t0, c0), (kp1, v1, R1, t1, c1) = out
+    assert torch.equal(kp0, kp1) and torch.equal(c0, c1)
+    print(f"C5 fp16 vs fp32 features: vcp max|d| {float((v0 - v1).abs().max()):.2e}, "
+          f"R max|d| {float((R0 - R1).abs().max()):.2e}, t max|d| {float((t0 - t1).abs().max()):.2e}")
+    torch.testing.assert_close(v1, v0, rtol=0, atol=1e-2)
+    torch.testing.assert_close(R1, R0, rtol=0, atol=1e-3)
+    torch.testing.assert_close(t1, t0, rtol=0, atol=1e-3)
 
 
 @pytest.mark.parametrize("dtype,N,npoint,B", [(torch.float32, 40000, 3000, 3), (torch.float64, 20000, 2000, 2)])

@@ -646,3 +646,34 @@ def test_paper_pose_vs_checker(cuda, fix):
     assert (np.abs(dets - 1.0) < 1e-9).all() if fix else (dets[3] < 0 and dets[4] < 0)
     R2, t2 = dvcp.paper.weighted_rigid_transform(T(x), T(y), T(w), reflection_fix=fix)
     assert torch.equal(R2, R) and torch.equal(t2, t)
+
+
+@pytest.mark.parametrize("f64", [False, True])
+def test_dfe_tgt_fp16_features(cuda, f64):
+    """BASELINE C5's fp16 feature storage (dvcp_dfe_tgt_f16): the gathered rows are widened to fp32
+    and the rest is the fp32 kernel's arithmetic, so the output equals dvcp_dfe_tgt on the fp32
+    table holding the same fp16-rounded values bit for bit (that kernel is checked against the
+    oracle in test_dfe_tgt_fused_vs_oracle); against the unrounded table it differs by the
+    features' fp16 rounding only (<= 2e-3 relative here).  Both XCD mappings (B = 2 and 8)."""
+    import dvcp
+    from dvcp import ops
+    g = torch.Generator().manual_seed(111)
+    dt = torch.float64 if f64 else torch.float32
+    mine = dvcp.feat_embedding_layer().eval().to(cuda)
+    for B, K, G, M in ((2, 3, 6, 900), (8, 8, 11, 2000)):
+        C = G ** 3
+        ref_xyz = (torch.rand(B, M, 3, generator=g, dtype=torch.float64) * 2 - 1).to(dt).to(cuda)
+        feat = torch.randn(B, M, 32, generator=g).to(cuda)
+        qry = ((torch.rand(B, K * C, 3, generator=g, dtype=torch.float64) * 2 - 1).float()).to(cuda)
+        dist, idx, _ = ops.knn(ref_xyz, qry, 32, ref_pdim=1, qry_pdim=1)
+        half = feat.half()
+        got = ops.dfe_tgt(ref_xyz, half, qry, dist, idx, mine.packed_params(), ref_pdim=1)
+        same = ops.dfe_tgt(ref_xyz, half.float(), qry, dist, idx, mine.packed_params(), ref_pdim=1)
+        assert torch.equal(got, same)
+        full = ops.dfe_tgt(ref_xyz, feat, qry, dist, idx, mine.packed_params(), ref_pdim=1)
+        rel = float((got - full).abs().max() / full.abs().max())
+        print(f"B={B}: fp16-feature DFE vs fp32 features: max rel {rel:.2e}")
+        assert rel < 2e-3
+    with pytest.raises(ValueError):
+        ops.dfe_tgt(ref_xyz, half, qry, dist, idx, mine.packed_params(), ref_pdim=1, literal=True)
+
