@@ -208,10 +208,13 @@ def _sa_case(table, g):
     if table == "sa1":
         xyz = torch.rand(B, 3, N, generator=g) * 0.6 - 0.3
         return 3, [16, 16, 32], 0.1, 256, xyz, None
-    if table == "sa1_normals":
+    if table in ("sa1_normals", "sa1_normals_f64"):
         xyz = torch.rand(B, 3, N, generator=g) * 0.6 - 0.3
         nrm = torch.randn(B, 3, N, generator=g)
-        return 6, [16, 16, 32], 0.1, 256, xyz, nrm / nrm.norm(dim=1, keepdim=True)
+        nrm = nrm / nrm.norm(dim=1, keepdim=True)
+        if table.endswith("f64"):   # ModelNet's double clouds (C1/C2)
+            xyz, nrm = xyz.double(), nrm.double()
+        return 6, [16, 16, 32], 0.1, 256, xyz, nrm
     if table == "sa2":
         return 35, [32, 64], 0.2, 128, torch.rand(B, 3, N, generator=g) * 1.2 - 0.6, torch.randn(B, 32, N, generator=g)
     return 67, [64, 64], 0.4, 64, torch.rand(B, 3, N, generator=g) * 2 - 1, torch.randn(B, 64, N, generator=g)
@@ -289,7 +292,7 @@ def test_sa_backward_vs_oracle(cuda, table):
           "relative gradient errors:", {k: f"{v:.1e}" for k, v in errs.items()})
 
 
-@pytest.mark.parametrize("table", ["sa1", "sa1_normals", "sa2", "sa3"])
+@pytest.mark.parametrize("table", ["sa1", "sa1_normals", "sa1_normals_f64", "sa2", "sa3"])
 def test_sa_batch_stats_train_vs_oracle(cuda, table):
     """pointnet2_utils.py:176-202 with the module in training mode (batch-statistics BatchNorm, as
     train.py's model.train()): the forward output, the running-statistics update and every conv /
@@ -301,7 +304,7 @@ def test_sa_batch_stats_train_vs_oracle(cuda, table):
     import dvcp
     from dvcp import batchnorm, ops
     from tests_helpers import randomize_bn
-    g = torch.Generator().manual_seed(["sa1", "sa1_normals", "sa2", "sa3"].index(table) + 400)
+    g = torch.Generator().manual_seed(["sa1", "sa1_normals", "sa1_normals_f64", "sa2", "sa3"].index(table) + 400)
     cin, mlp, radius, ns, xyz, feat = _sa_case(table, g)
     B, _, N = xyz.shape
     S = 512
@@ -317,9 +320,9 @@ def test_sa_batch_stats_train_vs_oracle(cuda, table):
     near = _near_tie_mask(copy.deepcopy(ref).double().train(), xyz.double(),
                           None if feat is None else feat.double(), S, radius, ns, start)
     G[near] = 0.0
-    feat_o = None if feat is None else feat.clone().requires_grad_(table != "sa1_normals")
+    feat_o = None if feat is None else feat.clone().requires_grad_(not table.startswith("sa1_normals"))
     with O.fps_starts([start]):
-        _, out_o = ref(xyz, feat_o)                # fp32, batch statistics
+        _, out_o = ref(xyz, feat_o)                # fp32 MLP (:198 .float()), batch statistics
     (out_o * G).sum().backward()
 
     x, f = xyz.to(cuda), (None if feat is None else feat.to(cuda))
