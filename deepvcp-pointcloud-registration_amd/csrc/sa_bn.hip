@@ -188,6 +188,16 @@ __device__ __forceinline__ P* bn_at(P* base, int C, int64_t e) {
   return base + (e >> 6) * (static_cast<int64_t>(C) * 64) + (e & 63);
 }
 
+// The mode-0 gradient / input rows (the host's weight-gradient GEMM operands): 65536-entry
+// chunks, channel-major inside a chunk -- (e / 65536) * C * 65536 + c * 65536 + e % 65536 -- so
+// each chunk of a table is one (C x 65536) row-major GEMM operand (no layout copy on the host);
+// tables are padded to a multiple of 65536 entries.
+constexpr int kBnRowChunkLog = 16;
+constexpr int64_t kBnRowChunk = int64_t(1) << kBnRowChunkLog;
+__device__ __forceinline__ float* bn_at_rows(float* base, int C, int64_t e) {
+  return base + (e >> kBnRowChunkLog) * (static_cast<int64_t>(C) * kBnRowChunk) + (e & (kBnRowChunk - 1));
+}
+
 // z = W x + b stored to its row (channel-major), h = relu(z * scale + shift), channel by channel
 template <int CIN, int COUT>
 __device__ __forceinline__ void bn_layer_store(const float (&x)[CIN], float (&h)[COUT], const float* __restrict__ p,
@@ -263,10 +273,10 @@ __global__ __launch_bounds__(kBnThreads) void sa_bn_zrows_kernel(PointsView<T> p
 
 template <int C>
 __device__ __forceinline__ void bn_put(float* __restrict__ base, int64_t M, int64_t e, const float (&v)[C], bool ones) {
-  float* o = bn_at(base, ones ? C + 1 : C, e);
+  float* o = bn_at_rows(base, ones ? C + 1 : C, e);
 #pragma unroll
-  for (int k = 0; k < C; ++k) o[k * 64] = v[k];
-  if (ones) o[C * 64] = 1.0f;
+  for (int k = 0; k < C; ++k) o[k * kBnRowChunk] = v[k];
+  if (ones) o[C * kBnRowChunk] = 1.0f;
 }
 
 template <int COUT>
@@ -295,7 +305,7 @@ __device__ __forceinline__ void bn_bwd_top(const float* __restrict__ zr, int64_t
     const float gy = (routable && sarg[c] == r && q.y(c, z) > 0.0f) ? srg[c] : 0.0f;
     const float gz = q.gz(c, z, gy);
     if constexpr (FINAL) {
-      if (act) bn_at(gzr, COUT, e)[c * 64] = gz;
+      if (act) bn_at_rows(gzr, COUT, e)[c * kBnRowChunk] = gz;
     }
 #pragma unroll
     for (int k = 0; k < CIN; ++k) gprev[k] = __fmaf_rn(p[c * CIN + k], gz, gprev[k]);
@@ -315,7 +325,7 @@ __device__ __forceinline__ void bn_bwd_mid(const float* __restrict__ zr, int64_t
     const float z = act ? bn_at(zr, COUT, e)[c * 64] : 0.0f;
     const float gz = q.gz(c, z, q.y(c, z) > 0.0f ? g[c] : 0.0f);
     if constexpr (FINAL) {
-      if (act) bn_at(gzr, COUT, e)[c * 64] = gz;
+      if (act) bn_at_rows(gzr, COUT, e)[c * kBnRowChunk] = gz;
     }
 #pragma unroll
     for (int k = 0; k < CIN; ++k) gprev[k] = __fmaf_rn(p[c * CIN + k], gz, gprev[k]);
@@ -330,9 +340,9 @@ __device__ __forceinline__ void bn_put_h(const float* __restrict__ zr, int64_t M
 #pragma unroll
   for (int c = 0; c < COUT; ++c) {
     const float y = q.y(c, bn_at(zr, COUT, e)[c * 64]);
-    bn_at(har, COUT + 1, e)[c * 64] = y > 0.0f ? y : 0.0f;
+    bn_at_rows(har, COUT + 1, e)[c * kBnRowChunk] = y > 0.0f ? y : 0.0f;
   }
-  bn_at(har, COUT + 1, e)[COUT * 64] = 1.0f;
+  bn_at_rows(har, COUT + 1, e)[COUT * kBnRowChunk] = 1.0f;
 }
 
 // The sums of one layer over the chunk: A += sum gy, B += sum gy xhat (gy = [y > 0] g), through
@@ -371,7 +381,7 @@ __device__ __forceinline__ void bn_bwd_first(const float* __restrict__ zr, int64
   for (int c = 0; c < COUT; ++c) {
     const float z = act ? bn_at(zr, COUT, e)[c * 64] : 0.0f;
     g[c] = q.gz(c, z, q.y(c, z) > 0.0f ? g[c] : 0.0f);
-    if (act) bn_at(gzr, COUT, e)[c * 64] = g[c];
+    if (act) bn_at_rows(gzr, COUT, e)[c * kBnRowChunk] = g[c];
   }
 }
 
@@ -431,12 +441,13 @@ __global__ __launch_bounds__(kBnThreads) void sa_bn_bwd_kernel(
   // mode 0 rows, per layer l: gz_l (C_l x M) | its input h_{l-1} and a ones row (C_{l-1} + 1 x M)
   float *gz1r = nullptr, *ha1r = nullptr, *gz2r = nullptr, *ha2r = nullptr, *gz3r = nullptr, *ha3r = nullptr;
   if constexpr (FINAL) {
+    const int64_t Mk = (M + kBnRowChunk - 1) / kBnRowChunk * kBnRowChunk;
     gz1r = rows;
-    ha1r = gz1r + C1 * M;
-    gz2r = ha1r + (C0 + 1) * M;
-    ha2r = gz2r + C2 * M;
-    gz3r = ha2r + (C1 + 1) * M;
-    ha3r = gz3r + C3 * M;
+    ha1r = gz1r + C1 * Mk;
+    gz2r = ha1r + (C0 + 1) * Mk;
+    ha2r = gz2r + C2 * Mk;
+    gz3r = ha2r + (C1 + 1) * Mk;
+    ha3r = gz3r + C3 * Mk;
   }
   double s1 = 0.0, s2 = 0.0;
   float(*tl)[TW + 1] = tile[wave];
@@ -720,7 +731,8 @@ extern "C" int64_t dvcp_sa_bn_rows_floats(int B, int S, int nsample, int nlayer,
   if (B < 0 || S < 0 || nsample < 0 || !chans || (nlayer != 2 && nlayer != 3)) return -1;
   int64_t per = 0;
   for (int l = 0; l < nlayer; ++l) per += chans[l + 1] + chans[l] + 1;
-  return per * ((static_cast<int64_t>(B) * S * nsample + 63) / 64 * 64);
+  const int64_t K = dvcp::kBnRowChunk;
+  return per * ((static_cast<int64_t>(B) * S * nsample + K - 1) / K * K);
 }
 
 extern "C" int64_t dvcp_sa_bn_pack_floats(int nlayer, const int* chans) {

@@ -15,8 +15,8 @@ Backward (``train_backward``): every entry's conv outputs z_l are written once (
 whose mean terms make every entry's gradient non-zero: sums of the top layer over the routed
 (arg-max) rows, one dense pass per lower layer for its sums, and a final dense pass for dW, db and
 the per-entry rows of the weight gradients and the feature gradient (dvcp_sa_bn_backward modes
-L..1, 0; csrc/sa_bn.hip); dW_l, db_l are then GEMMs over the entries (hipBLASLt via torch.bmm,
-K-chunked, chunk sums in fp64).
+L..1, 0; csrc/sa_bn.hip); dW_l, db_l are then GEMMs over the entries (hipBLASLt via torch.bmm
+over the rows' 65536-entry chunks, chunk sums in fp64).
 """
 import torch
 
@@ -102,19 +102,8 @@ def train_backward(sa, lay, g_out, want_feat_grad):
     return torch.cat([p.float() for p in parts]), gF
 
 
-def _gemm_nt(a, b, q=1024):
-    """sum over blocks of a_blk @ b_blk^T for (nb, m, 64) / (nb, n, 64) blocked row tables (up to
-    ~10^8 entries): fp32 GEMMs (hipBLASLt via torch.bmm) over chunks of q blocks, the chunk
-    products summed in fp64 in a fixed order."""
-    nb, m, n = a.shape[0], a.shape[1], b.shape[1]
-    nch = nb // q
-    acc = torch.zeros(m, n, dtype=torch.float64, device=a.device)
-    if nch:
-        ca = a[:nch * q].view(nch, q, m, 64).permute(0, 2, 1, 3).reshape(nch, m, q * 64)
-        cb = b[:nch * q].view(nch, q, n, 64).permute(0, 1, 3, 2).reshape(nch, q * 64, n)
-        acc += torch.bmm(ca, cb).double().sum(0)
-    if nb > nch * q:
-        ra = a[nch * q:].permute(1, 0, 2).reshape(m, -1)
-        rb = b[nch * q:].permute(1, 0, 2).reshape(n, -1)
-        acc += (ra @ rb.t()).double()
-    return acc
+def _gemm_nt(a, b):
+    """sum over chunks of a_k @ b_k^T for (nch, m, K) / (nch, n, K) chunked row tables: fp32 GEMMs
+    (hipBLASLt via torch.bmm, B transposed by strides, no copy), the chunk products summed in fp64
+    in a fixed order."""
+    return torch.bmm(a, b.transpose(1, 2)).double().sum(0)

@@ -571,7 +571,7 @@ def sa_bn_backward(xyz, ctr, feat, count, lst, nsample, chans, pack, zrows, grad
                    xyz_pdim=2, feat_ddim=1, feat_pdim=2):
     """Training-mode (batch-statistics) backward of the grouped MLP.  mode k >= 1: (2, C_k) fp64
     sums (A_k = dbeta_k, B_k = dgamma_k); mode 0: (per layer (dL/dz_l, [h_{l-1}; 1]) as
-    (M / 64, C, 64) blocked fp32 views, dL/d feat (B, N, D) fp32 or None)."""
+    (chunks, C, 65536) fp32 views, dL/d feat (B, N, D) fp32 or None)."""
     args, ws, (B, N, S, D), ch = _bn_common(xyz, ctr, feat, count, lst, nsample, chans, pack, xyz_pdim, feat_ddim,
                                             feat_pdim)
     dev = xyz.device
@@ -585,16 +585,17 @@ def sa_bn_backward(xyz, ctr, feat, count, lst, nsample, chans, pack, zrows, grad
     rows = torch.empty(max(nrows, 1), dtype=torch.float32, device=dev)
     gF = torch.zeros(B, N, D, dtype=torch.float32, device=dev) if (want_feat_grad and D > 0) else None
     call("dvcp_sa_bn_backward", *args, ptr(zrows), 0, ptr(g), ptr(gF), ptr(ws), None, ptr(rows), stream())
-    Mp = -(-M // 64) * 64   # tables are 64-entry blocks, channel-major inside (csrc/sa_bn.hip bn_at)
+    Kc = 65536              # tables are 65536-entry chunks, channel-major inside (csrc/sa_bn.hip bn_at_rows)
+    Mk = -(-M // Kc) * Kc
     views, o = [], 0
     for cin, cout in zip(chans[:-1], chans[1:]):
-        gz = rows[o:o + cout * Mp].view(Mp // 64, cout, 64)
-        o += cout * Mp
-        ha = rows[o:o + (cin + 1) * Mp].view(Mp // 64, cin + 1, 64)
-        o += (cin + 1) * Mp
-        if Mp > M:  # the padding entries of the last block take no part in the GEMMs
-            gz[-1, :, M % 64:] = 0.0
-            ha[-1, :, M % 64:] = 0.0
+        gz = rows[o:o + cout * Mk].view(Mk // Kc, cout, Kc)
+        o += cout * Mk
+        ha = rows[o:o + (cin + 1) * Mk].view(Mk // Kc, cin + 1, Kc)
+        o += (cin + 1) * Mk
+        if Mk > M:  # the padding entries of the last chunk take no part in the GEMMs
+            gz[-1, :, M % Kc:] = 0.0
+            ha[-1, :, M % Kc:] = 0.0
         views.append((gz, ha))
     return views, gF
 

@@ -1,6 +1,6 @@
 """CPU checks of the batch-statistics BatchNorm host logic (dvcp/batchnorm.py): the pack layout
 the HIP kernels read, the running-statistics update against torch's BatchNorm2d in training
-mode, and the blocked weight-gradient GEMM (no GPU: the kernels themselves are checked in
+mode, and the chunked weight-gradient GEMM (no GPU: the kernels themselves are checked in
 tests/test_gpu_train.py)."""
 import pytest
 import torch
@@ -40,15 +40,15 @@ def test_running_update_matches_batchnorm2d(momentum):
     assert int(mine.num_batches_tracked) == int(ref.num_batches_tracked) == 2
 
 
-@pytest.mark.parametrize("nb,q", [(3, 1024), (1024, 512), (2050, 512)])
-def test_blocked_gemm(nb, q):
-    """_gemm_nt over (nb, m, 64) / (nb, n, 64) blocked row tables == the plain product over the
-    nb * 64 entries (full chunks through bmm, the remainder through one mm)."""
+@pytest.mark.parametrize("nch,K", [(1, 64), (3, 4096), (5, 1000)])
+def test_chunked_gemm(nch, K):
+    """_gemm_nt over (nch, m, K) / (nch, n, K) chunked row tables == the plain product over the
+    nch * K entries."""
     from dvcp.batchnorm import _gemm_nt
-    g = torch.Generator().manual_seed(nb)
-    a = torch.randn(nb, 16, 64, generator=g)
-    b = torch.randn(nb, 17, 64, generator=g)
+    g = torch.Generator().manual_seed(nch * K)
+    a = torch.randn(nch, 16, K, generator=g)
+    b = torch.randn(nch, 17, K, generator=g)
     want = a.permute(1, 0, 2).reshape(16, -1).double() @ b.permute(1, 0, 2).reshape(17, -1).double().t()
-    got = _gemm_nt(a, b, q=q)
+    got = _gemm_nt(a, b)
     assert got.dtype == torch.float64
     torch.testing.assert_close(got, want, rtol=0, atol=1e-3)
