@@ -13,10 +13,12 @@ the timed region.  Rank 0 prints one JSON line.  At N=1 the CPU oracle (REF-R re
 torch CPU ops) is timed on the same pairs with the same weights and FPS starts (median of
 --cpu-pairs), and its R, t are compared with the GPU's.
 
-Roofline fields: ``roofline`` is the FPS chain's latency roofline (us per
-dependent step against the measured step floor); ``step_roofline`` and ``stages`` are SURVEY.md
-8(d)'s per-stage ceilings from one batch in flight; ``live_launch_ms`` are per-launch durations
-over the timed region (batches in flight contend, so they exceed the isolated ones).
+Roofline fields: ``roofline`` is the dominant entry point's (largest device
+time per step) executed work against the fp32 / HBM peak with its PMC counters; ``fps_roofline``
+is the FPS chain against its measured step floor and the fp32 VALU peak; ``step_roofline`` and
+``stages`` are SURVEY.md 8(d)'s per-stage ceilings on executed work from one batch in flight;
+``live_launch_ms`` are per-launch durations over the timed region (batches in flight contend, so
+they exceed the isolated ones).
 """
 import argparse
 import json
@@ -106,6 +108,7 @@ def main():
 
     import dvcp
     from dvcp import _lib
+    from dvcp import dist as D
     from dvcp.synthetic import condition_weights, make_pairs, randomize_bn
 
     B, N, K, r, s = args.batch, args.npoints, args.K, args.r, args.s
@@ -113,11 +116,13 @@ def main():
     torch.manual_seed(0)
     model = dvcp.DeepVCP(use_normal=False, K=K, r=r, s=s,
                          feat_dtype=torch.float16 if args.feat_dtype == "f16" else torch.float32).eval().to(dev)
-    # one distinct synthetic batch per in-flight lane
+    # one distinct synthetic global batch (B pairs per GPU x world) per in-flight lane; every rank
+    # takes its contiguous dvcp.dist.shard of it (weak scaling: B pairs per GPU)
+    lo, hi = D.shard(B * world, rank, world)
     batches = []
     for lane in range(P):
-        src, tgt, R_gt, t_gt = make_pairs(B, N, seed=1234 + 7919 * rank + 104729 * lane)
-        batches.append((src.to(dev), tgt.to(dev), R_gt.to(dev), t_gt.to(dev)))
+        src, tgt, R_gt, t_gt = make_pairs(B * world, N, seed=1234 + 104729 * lane)
+        batches.append(tuple(x[lo:hi].contiguous().to(dev) for x in (src, tgt, R_gt, t_gt)))
     src, tgt, R_gt, t_gt = batches[0]
     # random init, conditioned so key-point scores are separated beyond fp32 noise (the default
     # init's scores are 0.62 +- 1e-4): BN stats randomised, WL calibrated on this batch's features
@@ -164,18 +169,13 @@ def main():
     # per pair: R (9), t (3), rotation error (deg), translation error -> (steps*B, 14)
     res = torch.cat([torch.cat([o[0].reshape(B, 9), o[1].reshape(B, 3), o[2].reshape(B, 1), o[3].reshape(B, 1)], 1)
                      for o in outs])
-    if world > 1:
-        gathered = [torch.empty_like(res) for _ in range(world)]
-        dist.all_gather(gathered, res)
-        res = torch.cat(gathered)
+    res = D.gather_results(res, world)      # the one collective: RCCL all_gather of the rows
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     log, _lib.EVENT_LOG = _lib.EVENT_LOG or [], None
     if world > 1:
         dist.barrier()
-        tmax = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        elapsed = float(tmax.item())
+    elapsed = D.max_over_ranks(elapsed, dev)
 
     # ---- per-kernel HIP-event timing (events on the stream each kernel is launched on) --------
     # (1) live over the timed region, 8 batches in flight: per-launch durations under contention
@@ -191,8 +191,10 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     S = model.FE1.sa1.npoint
     C = int((2 * r) / s + 1) ** 3
-    stages, step_roof = stage_roofline(iso, args.iso_steps, floor_us, ms_step)
-    roofline = fps_roofline(live, iso, floor_us, traffic_ok=args.config == "c3")
+    stages, step_roof = stage_roofline(iso, args.iso_steps, ms_step)
+    pmc = _pmc() if args.config == "c3" else {}   # the PMC figures are measured at C3
+    roofline = dominant_roofline(live, iso, stages, pmc)
+    fps_roof = fps_roofline(live, iso, floor_us, pmc)
     res_cpu = res.cpu()
     reg_err = {"rot_deg_mean": float(res_cpu[:, 12].mean()), "rot_deg_max": float(res_cpu[:, 12].max()),
                "trans_mean": float(res_cpu[:, 13].mean()), "trans_max": float(res_cpu[:, 13].max()),
@@ -217,6 +219,7 @@ def main():
         "host_issue_ms_per_step": round(t_issue / args.steps * 1e3, 3),
         "registration_error_vs_gt": reg_err,
         "roofline": roofline,
+        "fps_roofline": fps_roof,
         "step_roofline": step_roof,
         "stages": stages,
         "live_launch_ms": {k: round(v["ms"] / v["n"], 4) for k, v in sorted(live.items(), key=lambda kv: -kv[1]["ms"])},
@@ -240,20 +243,27 @@ def main():
 
 
 def _per_kernel(log):
-    """EVENT_LOG -> {entry point: {n, ms, flops, bytes, exec_flops, wgs, steps}} (sums)."""
+    """EVENT_LOG -> {entry point: {n, ms, flops, bytes, exec_flops, mfma_flops, wgs, steps}} (sums).
+    Executed work given as a callable (the SA tables' real ball-query hit counts) is evaluated
+    here, after the timed region."""
     out = {}
     for name, e0, e1, w in log:
         d = out.setdefault(name, {"n": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0, "exec_flops": 0.0,
-                                  "exec_known": True, "wgs": None, "steps": 0})
+                                  "mfma_flops": 0.0, "exec_known": True, "wgs": None, "steps": 0})
         d["n"] += 1
         d["ms"] += e0.elapsed_time(e1)
         w = tuple(w or ()) + (None,) * 5
         d["flops"] += w[0] or 0.0
         d["bytes"] += w[1] or 0.0
-        if w[2] is None:
+        ex = w[2]
+        if callable(ex):
+            ex = ex()
+        if ex is None:
             d["exec_known"] = False
         else:
-            d["exec_flops"] += w[2]
+            tot, mf = (ex, 0.0) if isinstance(ex, (int, float)) else ex
+            d["exec_flops"] += tot
+            d["mfma_flops"] += mf
         if w[3] is not None:
             d["wgs"] = w[3]
             d["steps"] += w[4]
@@ -275,79 +285,120 @@ def fps_step_floor_us(dev, steps=20000):
     return e0.elapsed_time(e1) * 1e3 / steps
 
 
-def stage_roofline(iso, iso_steps, floor_us, ms_step):
-    """per stage, its ceiling time max(bytes/BW, flops/peak) (FPS: the latency
-    floor x its dependent steps) against the isolated measured time; the step roofline is the
-    sum of the ceilings in device-time over the measured step time.  Device time of a kernel
-    whose grid covers only part of the GPU (the FPS chain: one workgroup per cloud) is its
-    duration x its share of the 256 CUs, so the per-step device times add up like the work does."""
+def stage_roofline(iso, iso_steps, ms_step):
+    """SURVEY.md 8(d) per stage, on the work each kernel EXECUTES.
+
+    For every entry point (one batch in flight, ``--iso-steps`` steps): its device time = measured
+    duration x the share of the 256 CUs its grid can occupy (the FPS chain: one workgroup per
+    cloud, 16/256), and its ceiling = max(algorithmic bytes / 8 TB/s, work / 157.3 TF/s) in
+    full-chip time, where work = the flops the kernels execute when the entry point counts them
+    (the SA tables from the ball query's real hit counts, the DFE's MFMA count) and the
+    reference-graph flops otherwise (ball query, kNN, FPS: an upper bound of what their pruned
+    scans execute).  frac_of_ceiling = ceiling / device time.  The step roofline is the sum of
+    the ceilings over ``ms_per_step`` (measured with the default batches in flight)."""
     stages, ideal_dev, meas_dev = {}, 0.0, 0.0
     for k, v in sorted(iso.items(), key=lambda kv: -kv[1]["ms"]):
         ms = v["ms"] / iso_steps
         share = min(1.0, v["wgs"] / N_CU) if v["wgs"] else 1.0
-        t_flop = v["flops"] / iso_steps / (PEAK_FP32_TFLOPS * 1e12) * 1e3
+        dev_ms = ms * share
         t_byte = v["bytes"] / iso_steps / (PEAK_HBM_GBS * 1e9) * 1e3
-        ideal, bound = (t_flop, "fp32") if t_flop >= t_byte else (t_byte, "hbm")
-        if v["wgs"]:
-            # one dependent step per sampled centre; a step's FPS launches run back to back
-            t_lat = v["steps"] / iso_steps * floor_us * 1e-3
-            if t_lat > ideal:
-                ideal, bound = t_lat, "latency"
-        dev_ms, dev_ideal = ms * share, ideal * share
-        ideal_dev += dev_ideal
+        t_ref = v["flops"] / iso_steps / (PEAK_FP32_TFLOPS * 1e12) * 1e3
+        known = v["exec_known"] and v["exec_flops"] > 0
+        t_exec = v["exec_flops"] / iso_steps / (PEAK_FP32_TFLOPS * 1e12) * 1e3 if known else None
+        t_work = t_exec if known else t_ref
+        ceil, bound = (t_work, "fp32") if t_work >= t_byte else (t_byte, "hbm")
+        if bound == "fp32" and known and v["mfma_flops"] > 0.5 * v["exec_flops"]:
+            bound = "mfma"
+        ideal_dev += ceil
         meas_dev += dev_ms
-        stages[k] = {"launches_per_step": round(v["n"] / iso_steps, 2), "isolated_ms_per_step": round(ms, 4),
-                     "cu_share": round(share, 4), "device_ms_per_step": round(dev_ms, 4),
-                     "ceiling_ms_per_step": round(ideal, 4), "bound": bound,
-                     "frac_of_ceiling": round(ideal / ms, 4) if ms > 0 else None,
-                     "ref_graph_gflop": round(v["flops"] / iso_steps / 1e9, 3),
-                     "executed_gflop": round(v["exec_flops"] / iso_steps / 1e9, 3) if v["exec_known"] else None,
-                     "tflops_ref_graph": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 3) if v["flops"] else None,
-                     "tflops_executed": (round(v["exec_flops"] / (v["ms"] * 1e-3) / 1e12, 3)
-                                         if v["exec_known"] and v["exec_flops"] else None),
-                     # the kernel against its own work: executed flops (upper bound) at the fp32 peak
-                     "frac_of_executed_ceiling": (round(max(v["exec_flops"] / iso_steps / (PEAK_FP32_TFLOPS * 1e12) * 1e3,
-                                                            t_byte) / ms, 4)
-                                                  if v["exec_known"] and v["exec_flops"] and ms > 0 else None)}
-    roof = {"formula": "sum_s max(bytes_s/BW, flops_s/peak_s [, FPS: steps x floor]) x cu_share_s / ms_per_step",
+        st = {"launches_per_step": round(v["n"] / iso_steps, 2), "isolated_ms_per_step": round(ms, 4),
+              "cu_share": round(share, 4), "device_ms_per_step": round(dev_ms, 4),
+              "ceiling_ms_per_step": round(ceil, 4), "bound": bound,
+              "work_basis": "executed" if known else "reference graph (upper bound of the executed work)",
+              "frac_of_ceiling": round(ceil / dev_ms, 4) if dev_ms > 0 else None,
+              "ref_graph_gflop": round(v["flops"] / iso_steps / 1e9, 3),
+              "executed_gflop": round(v["exec_flops"] / iso_steps / 1e9, 3) if known else None,
+              "mfma_gflop": round(v["mfma_flops"] / iso_steps / 1e9, 3) if known else None,
+              # rate over the CUs the grid occupies (work / (duration x share of the chip))
+              "tflops": round((v["exec_flops"] if known else v["flops"]) / (v["ms"] * 1e-3) / share / 1e12, 3)
+              if v["ms"] > 0 and (known or v["flops"]) else None}
+        if st["frac_of_ceiling"] is not None and st["frac_of_ceiling"] > 1.0:
+            st["ceiling_note"] = "ceiling above the measured time: the counted work exceeds what the kernel runs"
+        stages[k] = st
+    roof = {"formula": "sum_s max(bytes_s / 8 TB/s, executed flops_s / 157.3 TF/s) / ms_per_step; "
+                       "stages without an executed count use their reference-graph flops",
             "ceiling_device_ms_per_step": round(ideal_dev, 4), "measured_device_ms_per_step_isolated": round(meas_dev, 4),
             "ms_per_step": round(ms_step, 4), "achieved_frac": round(ideal_dev / ms_step, 4),
             "isolated_frac": round(ideal_dev / meas_dev, 4) if meas_dev else None,
             "note": "stage times from one batch in flight (bench --iso-steps); ms_per_step with the default "
-                    "batches in flight; flops on the reference's op graph (executed flops listed per stage)"}
+                    "batches in flight; device time = duration x CU share of the grid"}
     return stages, roof
 
 
-def fps_roofline(live, iso, floor_us, traffic_ok=True):
-    """FPS is a serial chain of npoint dependent argmax steps per cloud: latency-bound, so its
-    roofline is microseconds per step against the measured step floor (dvcp_fps_step_floor).
-    ``traffic`` is the PMC figure of profiles/pmc_summary.json, which is measured at C3: null for
-    other configurations."""
+def dominant_roofline(live, iso, stages, pmc):
+    """The JSON ``roofline``: the entry point with the largest device time per step (what bounds
+    pairs/s), its executed work per average isolated launch against the fp32 peak (157.3 TF/s:
+    the fp32 MFMA and fp32 VALU rates are equal on gfx950) or HBM, and its PMC counters
+    (profiles/pmc_summary.json: HBM bytes per launch, MFMA / VALU busy)."""
+    name = max(stages, key=lambda k: stages[k]["device_ms_per_step"])
+    v, st = iso[name], stages[name]
+    known = v["exec_known"] and v["exec_flops"] > 0
+    flops = v["exec_flops"] if known else v["flops"]
+    launch_ms = v["ms"] / v["n"]
+    share = st["cu_share"]
+    if st["bound"] == "hbm":
+        achieved, peak, unit = v["bytes"] / v["n"] / (launch_ms * 1e-3) / 1e9, PEAK_HBM_GBS, "GB/s"
+    else:
+        achieved, peak, unit = flops / v["n"] / (launch_ms * 1e-3) / 1e12, PEAK_FP32_TFLOPS * share, "TFLOP/s"
+    w = live.get(name)
+    p = pmc.get(name, {})
+    return {"bound": "hbm" if st["bound"] == "hbm" else "mfma",
+            "pipe": {"mfma": "mfma", "fp32": "valu", "hbm": "hbm"}[st["bound"]],
+            "kernel": name, "achieved": round(achieved, 3), "peak": round(peak, 3), "unit": unit,
+            "frac": round(achieved / peak, 4), "traffic": p.get("hbm_bytes_per_launch"),
+            "work_basis": st["work_basis"], "flops_per_launch": flops / v["n"],
+            "algorithmic_bytes_per_launch": v["bytes"] / v["n"],
+            "avg_launch_ms_isolated": round(launch_ms, 4),
+            "avg_launch_ms_live": round(w["ms"] / w["n"], 4) if w else None,
+            "pmc": {k: p[k] for k in ("mfma_util", "valu_busy", "valu_util_lanes", "note") if k in p} or None,
+            "note": "dominant = largest device time per step (duration x CU share), one batch in flight; "
+                    "achieved = executed flops (reference-graph flops if not counted) per launch / average "
+                    "isolated launch time; peak = fp32 157.3 TF/s x the grid's CU share (fp32 MFMA = fp32 "
+                    "VALU rate on gfx950) or 8 TB/s; traffic = PMC HBM bytes per launch"}
+
+
+def fps_roofline(live, iso, floor_us, pmc):
+    """FPS is a serial chain of npoint dependent argmax steps per cloud, one workgroup per cloud:
+    reported against the measured step floor of its synchronisation (dvcp_fps_step_floor, us per
+    centre) AND against the fp32 VALU peak, both of the whole chip and of the 16 CUs a C3 batch's
+    16 clouds occupy (reference-graph flops: 9 per point-update, npoint x N per cloud)."""
     name = "dvcp_fps_ws"
     if name not in iso:
         return None
     v, w = iso[name], live.get(name)
     us_iso = v["ms"] * 1e3 / v["steps"]
     us_live = w["ms"] * 1e3 / w["steps"] if w and w["steps"] else None
-    return {"bound": "latency", "kernel": name, "unit": "us/step", "achieved": round(us_iso, 4),
-            "peak": round(floor_us, 4), "frac": round(floor_us / us_iso, 4),
-            "traffic": _pmc_traffic(name) if traffic_ok else None,
+    tf = v["flops"] / (v["ms"] * 1e-3) / 1e12
+    share = min(1.0, v["wgs"] / N_CU)
+    return {"kernel": name, "us_per_centre": round(us_iso, 4), "step_floor_us": round(floor_us, 4),
+            "frac_of_step_floor": round(floor_us / us_iso, 4),
+            "tflops_ref_graph": round(tf, 3), "frac_of_fp32_peak_chip": round(tf / PEAK_FP32_TFLOPS, 4),
+            "frac_of_fp32_peak_own_cus": round(tf / (PEAK_FP32_TFLOPS * share), 4),
             "avg_launch_ms_isolated": round(v["ms"] / v["n"], 4),
             "avg_launch_ms_live": round(w["ms"] / w["n"], 4) if w else None,
-            "us_per_step_live": round(us_live, 4) if us_live else None,
+            "us_per_centre_live": round(us_live, 4) if us_live else None,
+            "traffic": pmc.get(name, {}).get("hbm_bytes_per_launch"),
             "algorithmic_bytes_per_launch": v["bytes"] / v["n"],
-            "note": "achieved = isolated launch time / sampled centres (one batch in flight); peak = the measured "
-                    "per-step floor of the chain's synchronisation (DPP argmax + LDS slot + barrier + slot "
-                    "reduction, no point work); the batched kernel accepts several centres per round, so frac > 1 "
-                    "is possible; live = with the default batches in flight"}
+            "note": "frac_of_step_floor: the select kernel certifies several centres per round, so it can pass "
+                    "1; the fp32 fractions count the reference graph's 9 flop per point-update"}
 
 
-def _pmc_traffic(kernel):
-    pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
+def _pmc():
+    """profiles/pmc_summary.json (measured at C3), {} if absent."""
     try:
-        return json.load(open(pmc)).get(kernel, {}).get("hbm_bytes_per_launch")
+        return json.load(open(os.path.join(ROOT, "profiles", "pmc_summary.json")))
     except Exception:
-        return None
+        return {}
 
 
 def _cpu_topology():

@@ -1132,8 +1132,8 @@ __global__ __launch_bounds__(kFpsThreads) void fps_dense_kernel(PointsView<T> pt
 // workgroup only ever waits for peers of that one cloud, which take the next free slots on the
 // device (S - 1 slots per concurrent launch).  The wait is still bounded (spin_cap polls) as a
 // guard: a workgroup that gives up raises the launch's error word, which the host checks
-// (dvcp/_lib.py check_device_flags), and writes in-range indices (the start point) for the
-// steps it could not finish, so nothing downstream reads out of bounds.
+// (dvcp/_lib.py check_device_flags), and writes the start point (index and coordinates) for the
+// steps it could not finish, so nothing downstream reads out of bounds or a garbage centre.
 constexpr int kFpsSplitMax = 16;
 constexpr uint32_t kFpsSpinCap = 1u << 22;
 
@@ -1236,10 +1236,22 @@ __global__ __launch_bounds__(kFpsThreads) void fps_split_kernel(PointsView<T> pt
     cz = pts.at(b, 2, cur);
     __syncthreads();  // gbest / wbest are rewritten next step
   }
-  if (step < npoint) {  // gave up waiting: flag the launch, keep every index in range
+  if (step < npoint) {  // gave up waiting: flag the launch, keep every index and centre valid
     if (tid == 0) __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (s == 0)
-      for (int k = step + tid; k < npoint; k += kFpsThreads) out_idx[static_cast<int64_t>(b) * npoint + k] = first;
+    if (s == 0) {
+      // the remaining steps repeat the start point: in-range indices AND finite centres, so the
+      // ball query / MLP launched behind this one read real points before the host raises
+      const T fx = pts.at(b, 0, first), fy = pts.at(b, 1, first), fz = pts.at(b, 2, first);
+      T* ox = out_xyz ? out_xyz + static_cast<int64_t>(b) * 3 * npoint : nullptr;
+      for (int k = step + tid; k < npoint; k += kFpsThreads) {
+        out_idx[static_cast<int64_t>(b) * npoint + k] = first;
+        if (ox) {
+          ox[k] = fx;
+          ox[npoint + k] = fy;
+          ox[2 * npoint + k] = fz;
+        }
+      }
+    }
   }
 }
 
@@ -1352,8 +1364,8 @@ extern "C" int dvcp_fps_step_floor(int steps, int blocks, float* out, void* stre
 // Test hook for the split kernel's guard: runs the split path with the given poll cap and
 // `withhold` workgroups left out of the grid (so the last cloud cannot complete).
 extern "C" int dvcp_fps_split_probe(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N,
-                                    int npoint, const int64_t* start, int64_t* out_idx, float* ws, int32_t* err,
-                                    uint32_t spin_cap, int withhold, void* stream) {
+                                    int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz, float* ws,
+                                    int32_t* err, uint32_t spin_cap, int withhold, void* stream) {
   DVCP_REQUIRE(xyz && start && out_idx && ws && err, "dvcp_fps_split_probe: null pointer");
   DVCP_REQUIRE(B > 0 && N > 0 && npoint > 0 && withhold >= 0, "dvcp_fps_split_probe: bad sizes");
   const int P = dtype == DVCP_F32 ? 32 : 16;
@@ -1362,10 +1374,12 @@ extern "C" int dvcp_fps_split_probe(int dtype, const void* xyz, int64_t sb, int6
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (dtype == DVCP_F32)
     return dvcp::launch_fps_split<float>(dvcp::PointsView<float>{static_cast<const float*>(xyz), sb, sc, sn}, B, N,
-                                         npoint, start, out_idx, nullptr, ws, err, spin_cap, withhold, st);
+                                         npoint, start, out_idx, static_cast<float*>(out_xyz), ws, err, spin_cap,
+                                         withhold, st);
   if (dtype == DVCP_F64)
     return dvcp::launch_fps_split<double>(dvcp::PointsView<double>{static_cast<const double*>(xyz), sb, sc, sn}, B,
-                                          N, npoint, start, out_idx, nullptr, ws, err, spin_cap, withhold, st);
+                                          N, npoint, start, out_idx, static_cast<double*>(out_xyz), ws, err, spin_cap,
+                                          withhold, st);
   dvcp::set_error("dvcp_fps_split_probe: bad dtype %d", dtype);
   return DVCP_EINVAL;
 }

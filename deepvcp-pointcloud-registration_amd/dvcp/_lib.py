@@ -24,7 +24,7 @@ SIGNATURES = {
     "dvcp_fps": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P],
     "dvcp_fps_ws": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P, _P],
     "dvcp_fps_step_floor": [_I, _I, _P, _P],
-    "dvcp_fps_split_probe": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, ctypes.c_uint32, _I, _P],
+    "dvcp_fps_split_probe": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P, ctypes.c_uint32, _I, _P],
     "dvcp_ball_query": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _D, _I, _P, _P, _P, _P],
     "dvcp_ball_query_ws": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _D, _I, _P, _P, _P, _P, _P],
     "dvcp_square_distance": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _P, _P],
@@ -132,10 +132,12 @@ def exported_symbols():
 
 # When a list, every entry-point call appends (name, start_event, end_event, work) recorded on
 # torch's current stream (the stream the kernel is launched on) -- bench.py's live per-kernel
-# HIP-event timing.  `work` = (algorithmic flops, algorithmic bytes[, executed flops[, workgroups,
+# HIP-event timing.  `work` = (algorithmic flops, algorithmic bytes[, executed[, workgroups,
 # serial steps]]) of that launch: flops and bytes on the reference's op graph (DESIGN.md section
-# 6), the flops the kernel actually executes where they differ (None: not counted), and for the
-# latency-bound FPS chain its workgroup count and dependent steps.  None (the default) costs nothing.
+# 6); `executed` = (flops the kernels execute, of which on MFMA) where known -- a tuple, or a
+# callable returning one that the bench evaluates after its timed region (the SA tables count
+# their real ball-query hits) -- None when not counted; and for the latency-bound FPS chain its
+# workgroup count and dependent steps.  None (the default) costs nothing.
 EVENT_LOG = None
 
 

@@ -14,6 +14,8 @@ The seven FPS start indices are drawn up front with torch.randint on the CPU gen
 reference's order (src sa1, sa2, sa3, key points, tgt sa1, sa2, sa3), so a seeded run draws the
 same starts as the reference.  t_init is unused, as in the reference (deepVCP.py:86).
 """
+import warnings
+
 import torch
 import torch.nn as nn
 
@@ -24,6 +26,20 @@ from .deep_feat_extraction import feat_extraction_layer
 from .pointnet2_utils import _inference_only
 from .voxelize import grid_side
 from .weighting_layer import weighting_layer
+
+
+_F16_WARNED = False
+
+
+def _warn_f16_autograd():
+    """feat_dtype=float16 is an inference storage format (dvcp_dfe_tgt_f16); the autograd path
+    gathers the fp32 table, so say so once instead of silently ignoring it."""
+    global _F16_WARNED
+    if not _F16_WARNED:
+        _F16_WARNED = True
+        warnings.warn("dvcp.DeepVCP(feat_dtype=torch.float16) applies to inference (torch.no_grad()) only; "
+                      "this forward records autograd and uses the fp32 target feature table", RuntimeWarning,
+                      stacklevel=3)
 
 
 class DeepVCP(nn.Module):
@@ -55,7 +71,13 @@ class DeepVCP(nn.Module):
         the head (DFE, CPG) when it is enabled and any head or extractor parameter requires
         gradients; through the feature extractor when its parameters require gradients.  FE1's
         BatchNorm follows FE1's mode like torch's: batch statistics (and running-statistics
-        updates) in training mode, running statistics after FE1.eval() (frozen-BN fine-tuning)."""
+        updates) in training mode, running statistics after FE1.eval() (frozen-BN fine-tuning).
+
+        This follows autograd, not ``eval()``: ``model.eval()`` followed by a forward WITHOUT
+        ``torch.no_grad()`` (parameters trainable, the torch default) records the autograd path,
+        as the reference's modules would -- every saved table stays alive until the graph is freed
+        and the inference path's folded gathers are not used.  Inference belongs under
+        ``torch.no_grad()`` (train.py's test loop, vis_utils.py:85)."""
         head = [p for m in (self.DFE, self.cpg) for p in m.parameters()]
         fe_grad = any(p.requires_grad for p in self.FE1.parameters())
         grad = torch.is_grad_enabled()
@@ -159,6 +181,8 @@ class DeepVCP(nn.Module):
         qry = cand.view(B, K * C, 3)
         dist, idx, _ = ops.knn(tgt_xyz, qry, 32, ref_pdim=2, qry_pdim=1, want_idx64=False)
         if train_head:
+            if self.feat_dtype != torch.float32:
+                _warn_f16_autograd()
             tgt_dfe = autograd.dfe_tgt(tgt_xyz, tgt_feat, qry, dist, idx, self.DFE).view(B, K, C, 32)
             vcp = autograd.cpg(src_dfe, tgt_dfe.permute(0, 1, 3, 2), cand, G, self.cpg)
         else:

@@ -137,11 +137,23 @@ class feat_extraction_layer(nn.Module):
             keep = [head, score]
             if saved is not None:
                 keep += [saved["f3"]] + [t for lay in saved["layers"] for t in lay.values() if torch.is_tensor(t)]
+                # the training-BN state (dvcp/batchnorm.py) nests its tensors one level down (the
+                # pack is read on the main stream by the backward's z-row pass)
+                keep += [t for lay in saved["layers"] if isinstance(lay.get("bn"), dict)
+                         for t in lay["bn"].values() if torch.is_tensor(t)]
             for t in keep:
                 if t is not None:
                     t.record_stream(main)  # allocated on the side stream, consumed on main
         return pts_l, head.view(B, S, 32), (score.view(B, S) if score is not None else None)
 
     def forward(self, pts):
-        xyz, feat, _ = self.run(pts)
+        """deep_feat_extraction.py:18-32.  With gradients enabled and a trainable parameter the
+        call is differentiable in FE1's parameters (dvcp.autograd.feat_extraction; BatchNorm in this
+        module's mode, batch statistics when training), so ``model.FE1(pts)`` in a training loop
+        back-propagates like the reference's; otherwise the inference path."""
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            from . import autograd
+            xyz, feat, _ = autograd.feat_extraction(self, pts, None)
+        else:
+            xyz, feat, _ = self.run(pts)
         return xyz.permute(0, 2, 1), feat

@@ -105,7 +105,7 @@ def sa_group_mlp(xyz, ctr, feat, count, lst, nsample, chans, params, xyz_pdim=2,
          ptr(feat), fb, fd, fn, D, ptr(count), ptr(lst), int(nsample), len(chans) - 1, ptr(ch), ptr(params), ptr(out),
          ptr(ws), stream(),
          work=(2.0 * macs * B * S * nsample, B * S * (4 * nsample + 4 * chans[-1]) + B * N * 4 * (3 + D),
-               _sa_exec_flops(chans, B, N, S, nsample)))
+               _sa_exec_flops(chans, B, N, S, nsample, count)))
     return out
 
 
@@ -130,18 +130,39 @@ def sa_group_mlp_rows(xyz, ctr, feat, rows, count, lst, nsample, chans, params, 
          ptr(feat), feat.stride(0), feat.stride(1), Nf, D, ptr(rows), ptr(count), ptr(lst), int(nsample),
          len(chans) - 1, ptr(ch), ptr(params), ptr(out), ptr(ws), stream(),
          work=(2.0 * macs * B * S * nsample, B * S * (4 * nsample + 4 * chans[-1]) + B * N * (4 * (3 + D) + 8),
-               _sa_exec_flops(chans, B, N, S, nsample)))
+               _sa_exec_flops(chans, B, N, S, nsample, count)))
     return out
 
 
-def _sa_exec_flops(chans, B, N, S, nsample):
-    """Flops the kernels execute (upper bound: padded rows counted): the two-layer MFMA tables
-    split layer 1 into a per-point part (D x C1 per input point) and a per-row part (3 x C1), and
-    the layer-2 ReLU + max fold (csrc/sa_mlp_mfma.hip); other tables run the reference graph."""
+MFMA_F32_32X32X2_FLOPS = 2 * 32 * 32 * 2   # one v_mfma_f32_32x32x2_f32
+
+
+def _sa_exec_flops(chans, B, N, S, nsample, count):
+    """The flops the kernels execute on this launch, from the ball query's real hit counts
+    (evaluated lazily -- after the timed region -- by bench.py: one device reduction of ``count``).
+
+    * two-layer MFMA tables (sa2 35-32-64, sa3 67-64-64; csrc/sa_mlp_mfma.hip): layer 1 is split
+      into the per-point pass sa_pre_kernel (VALU, 2 D C1 per input point) and, per 32-row tile of
+      a centre's distinct hits (ceil(clamp(count, 1, ns) / 32) tiles; padded lanes of a tile
+      execute like real ones), 2 MT + MT 16 CT v_mfma_f32_32x32x2_f32 (xyz k-steps + layer 2);
+    * other tables (sa1, csrc/sa_mlp.hip, VALU): one row per distinct hit, clamp(count, 0, ns)
+      rows x 2 sum(C_l C_l+1).
+    Returns a callable -> (executed flops, of which MFMA flops)."""
     if len(chans) == 3 and chans[0] - 3 in (32, 64):
         D, C1, C2 = chans[0] - 3, chans[1], chans[2]
-        return 2.0 * B * (N * D * C1 + S * nsample * (3 * C1 + C1 * C2))
-    return 2.0 * B * S * nsample * sum(a * b for a, b in zip(chans[:-1], chans[1:]))
+        mt, ct = C1 // 32, C2 // 32
+        per_tile = (2 * mt + mt * 16 * ct) * MFMA_F32_32X32X2_FLOPS
+
+        def f():
+            tiles = float(((count.clamp(1, nsample).long() + 31) // 32).sum())
+            mfma = tiles * per_tile
+            return 2.0 * B * N * D * C1 + mfma, mfma
+        return f
+    macs = sum(a * b for a, b in zip(chans[:-1], chans[1:]))
+
+    def g():
+        return 2.0 * macs * float(count.clamp(0, nsample).long().sum()), 0.0
+    return g
 
 
 def fe_head(x, params, with_score):
@@ -300,7 +321,9 @@ def dfe_tgt(ref_xyz, ref_feat, cand, dist, idx, params, ref_pdim=2, literal=Fals
     call(name, dtype_code(ref_xyz), ptr(ref_xyz), rb, rc, rn, M, ptr(feat_c), ptr(cand_c), ptr(dist_c),
          ptr(idx_c), B, Q, ptr(params), ptr(out), stream(),
          work=(2.0 * 3168 * 32 * B * Q, B * (M * (12 + row) + Q * (12 + 32 * 8 + 128)),
-               2.0 * (3168 if literal else 35 * 32) * 32 * B * Q))
+               # executed: one v_mfma_f32_32x32x2_f32 per k-step per candidate (35 input channels
+               # padded to 19 k-steps; literal: + 16 + 16 for fc2, fc3)
+               ((51 if literal else 19) * MFMA_F32_32X32X2_FLOPS * float(B * Q),) * 2))
     return out
 
 
@@ -320,7 +343,9 @@ def cpg(src, tgt, cand, G, params, want_weight=False):
     call("dvcp_cpg", ptr(srcc), ptr(tgt), tgt.stride(1), tgt.stride(2), tgt.stride(3), ptr(candc), B * K, int(G),
          ptr(params), ptr(vcp), ptr(w), stream(),
          work=(2.0 * 27 * (32 * 16 + 16 * 4 + 4) * B * K * C, B * K * (128 + C * (128 + 12) + 12),
-               2.0 * 27 * (32 * 16 + 16 * 4 + 4) * B * K * C))
+               # executed (reference graph; halo padding of the implicit GEMM not counted), of which
+               # conv1 runs on v_mfma_f32_16x16x4_f32
+               (2.0 * 27 * (32 * 16 + 16 * 4 + 4) * B * K * C, 2.0 * 27 * 32 * 16 * B * K * C)))
     return (vcp, w) if want_weight else vcp
 
 

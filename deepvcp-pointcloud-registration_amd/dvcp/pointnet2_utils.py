@@ -101,8 +101,15 @@ class PointNetSetAbstraction(nn.Module):
 
     def forward(self, xyz, points, start=None):
         """xyz (B, 3, N), points (B, D, N) or None -> new_xyz (B, 3, S), features (B, D', S).
-        In training mode the BatchNorms use batch statistics and update their running statistics
-        (forward only here; autograd runs through dvcp.autograd.feat_extraction)."""
+        In training mode the BatchNorms use batch statistics and update their running statistics.
+        This module has no autograd path of its own (its backward runs inside
+        dvcp.autograd.feat_extraction, i.e. through feat_extraction_layer / DeepVCP): with
+        gradients enabled and a trainable parameter it raises instead of returning features that
+        silently carry no gradient."""
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError(
+                "dvcp: PointNetSetAbstraction.forward is not differentiable on its own; train it through "
+                "feat_extraction_layer / DeepVCP (dvcp.autograd.feat_extraction), or call it under torch.no_grad()")
         B, _, N = xyz.shape
         if start is None:
             start = torch.randint(0, N, (B,), dtype=torch.long)

@@ -66,8 +66,8 @@ int dvcp_fps_step_floor(int steps, int blocks, float* out, void* stream);
  * `withhold` workgroups left out of the grid, so that the last cloud cannot complete and must
  * raise *err. */
 int dvcp_fps_split_probe(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B,
-                         int N, int npoint, const int64_t* start, int64_t* out_idx, float* ws,
-                         int32_t* err, uint32_t spin_cap, int withhold, void* stream);
+                         int N, int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz,
+                         float* ws, int32_t* err, uint32_t spin_cap, int withhold, void* stream);
 
 /* Ball query.  Replaces pointnet2_utils.py:87-107 query_ball_point (and the
  * square_distance expansion it uses, :19-40): the first `nsample` ascending point indices

@@ -22,6 +22,13 @@ repairs of SURVEY.md Appendix A.2:
   R7  K, r, s are parameters (defaults reproduce the literals K=64, r=1, s=0.4).
   R8  voxelize.py:23 ``.view(-1, 3)`` -> ``.reshape(-1, 3)`` (the permuted key
       points from deepVCP.py:91 are non-contiguous, so ``view`` raises for B>1).
+  R9  query_ball_point pads with ``gidx.shape[2]`` columns of the first hit instead of
+      ``nsample`` (pointnet2_utils.py:104 repeats to nsample).  The two agree whenever
+      nsample <= N; for nsample > N (the key-point grouping with K < 32, deepVCP.py:54,
+      or tiny test clouds) the reference's mask ``group_idx == N`` has N columns while
+      the repeated head has nsample, and the boolean index raises.  The repair keeps
+      the first min(nsample, N) slots, i.e. the rows the reference would have
+      produced had the shapes matched.
 
 The optional ``chunk`` arguments only bound peak memory (row blocks of the same
 ops); results are row-independent.
@@ -145,6 +152,7 @@ def query_ball_point(radius, nsample, xyz, new_xyz, chunk=2048):
         d2 = square_distance(ctr, xyz)
         gidx[d2 > radius ** 2] = n
         gidx = gidx.sort(dim=-1)[0][:, :, :nsample]
+        # R9: pad to the sliced width (= nsample unless nsample > N, where :104 raises)
         head = gidx[:, :, 0].view(nb, s, 1).repeat([1, 1, gidx.shape[2]])
         miss = gidx == n
         gidx[miss] = head[miss]

@@ -426,21 +426,25 @@ def test_fe_train_step_vs_oracle(cuda):
     assert not torch.equal(before, mine.FE1.sa1.mlp_convs[0].weight.detach())
 
 
-def test_whole_model_train_mode_step_vs_oracle(cuda):
+@pytest.mark.parametrize("B,n_tgt", [(1, 2048), (2, 1800)])
+def test_whole_model_train_mode_step_vs_oracle(cuda, B, n_tgt):
     """train.py:105-125 as written: the whole model in training mode (model.train(): FE1's
     BatchNorms use each call's batch statistics -- src and tgt separately -- and update their
     running statistics) and every parameter trainable.  Loss, every parameter gradient and the
-    running statistics after the step match the oracle's autograd; then one Adam step."""
+    running statistics after the step match the oracle's autograd; then one Adam step.
+    B = 2 with a 1800-point target: the statistics run over M = B * S * ns entries of several
+    clouds, and src / tgt are two FE1 calls of different shapes."""
     import oracle as O
     import dvcp
     from dvcp.synthetic import condition_weights, make_pairs, randomize_bn
-    src, tgt, R_gt, t_gt = make_pairs(1, 2048, seed=93)
+    src, tgt, R_gt, t_gt = make_pairs(B, 2048, seed=93)
+    tgt = tgt[:, :, :n_tgt].contiguous()
     torch.manual_seed(0)
     ref = O.DeepVCP(use_normal=False, K=32, r=1.0, s=0.4, fe_npoint=512)
     randomize_bn(ref)
     ref.FE1.eval()
     with torch.no_grad():
-        _, calib = ref.FE1(src)
+        _, calib = ref.FE1(src[:1])
     condition_weights(ref, feats=calib)
     mine = dvcp.DeepVCP(use_normal=False, K=32, r=1.0, s=0.4, fe_npoint=512)
     mine.load_state_dict(ref.state_dict())
@@ -474,9 +478,15 @@ def test_whole_model_train_mode_step_vs_oracle(cuda):
         # 2.2e-3 on sa1's first BN bias
         floor, tol = (1e-3 if name == "cpg.conv3.bias" else 1e-30), (5e-3 if name.startswith("FE1.") else 2e-3)
         if ".mlp_convs." in name and name.endswith(".bias"):
-            # analytically zero under batch statistics (summation noise on both sides): compared
-            # at the scale of its layer's weight gradient
-            floor, tol = float(dict(ref.named_parameters())[name[:-4] + "weight"].grad.abs().max()), 5e-2
+            # analytically zero under batch statistics (the batch mean removes a shift): both sides
+            # hold summation noise only.  The GPU sums in fp64, the oracle in fp32 over M = B S ns
+            # entries, so the GPU's value must be no larger than 5e-2 of the layer's weight
+            # gradient or twice the oracle's own noise, whichever is larger (sa1's first layer sees
+            # local coordinates of ~0.05, so its weight gradient is small next to that noise at B=2)
+            wscale = float(dict(ref.named_parameters())[name[:-4] + "weight"].grad.abs().max())
+            bound = max(5e-2 * wscale, 2.0 * float(p_ref.grad.abs().max()))
+            errs[name] = (float(got.detach().abs().max()) / bound, 1.0)
+            continue
         errs[name] = _close(got, p_ref.grad, tol, name, floor=floor, check=False)
     worst = sorted(errs.items(), key=lambda kv: -kv[1][0])[:6]
     print("largest relative gradient errors:", {k: f"{v[0]:.1e}" for k, v in worst})
@@ -600,3 +610,35 @@ def test_src_keypoints_feature_grad_vs_oracle(cuda):
     torch.testing.assert_close(cat.cpu(), cat_o.float(), rtol=1e-5, atol=1e-6)
     (cat * G.to(cuda)).sum().backward()
     _close(fg.grad, fo.grad, 1e-5, "d source features")
+
+
+def test_direct_module_calls_keep_or_refuse_gradients(cuda):
+    """Calling the extractor directly in a training loop (``model.FE1(pts)``) records autograd like
+    the reference's module: the features carry a grad_fn and a backward reaches every FE1
+    parameter, in training mode (batch statistics) and after FE1.eval() (frozen BN).  A standalone
+    PointNetSetAbstraction has no autograd path of its own, so with gradients enabled it raises
+    rather than returning features that silently drop the gradient; under no_grad it runs."""
+    import dvcp
+    from dvcp.synthetic import make_pairs
+    src, _, _, _ = make_pairs(2, 2048, seed=95)
+    torch.manual_seed(0)
+    fe = dvcp.feat_extraction_layer(use_normal=False, npoint=256).to(cuda)
+    for mode in ("train", "eval"):
+        getattr(fe, mode)()
+        fe.zero_grad(set_to_none=True)
+        xyz, feat = fe(src.to(cuda))
+        assert xyz.shape == (2, 256, 3) and feat.shape == (2, 256, 32)
+        assert feat.requires_grad and feat.grad_fn is not None, mode
+        feat.square().sum().backward()
+        missing = [n for n, p in fe.named_parameters() if p.grad is None]
+        assert not missing, (mode, missing)
+        with torch.no_grad():
+            _, f_ng = fe(src.to(cuda))
+        assert not f_ng.requires_grad
+    sa = fe.sa1
+    x = src.to(cuda)
+    with pytest.raises(NotImplementedError, match="not differentiable"):
+        sa(x, None)
+    with torch.no_grad():
+        new_xyz, out = sa.eval()(x, None)
+    assert out.shape == (2, 32, 256)
