@@ -438,6 +438,21 @@ __device__ __forceinline__ uint32_t wave_umin(uint32_t v) {
   v = dpp_umin<0x143, 0xC>(v);
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
 }
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_uadd(uint32_t v) {
+  return v + static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, ROWS, 0xF, false));
+}
+// Inclusive prefix sum over the wave on DPP (row_shr 1, 2, 4, 8 inside each 16-lane row, then
+// row_bcast 15 / 31 across rows): no ds_bpermute round trips in the per-round critical path.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  v = dpp_uadd<0x111, 0xF>(v);
+  v = dpp_uadd<0x112, 0xF>(v);
+  v = dpp_uadd<0x114, 0xF>(v);
+  v = dpp_uadd<0x118, 0xF>(v);
+  v = dpp_uadd<0x142, 0xA>(v);
+  v = dpp_uadd<0x143, 0xC>(v);
+  return v;
+}
 __device__ __forceinline__ float float_unorder_fps(uint32_t u) {  // inverse of float_order
   const uint32_t flip = (u >> 31) ? 0x80000000u : 0xFFFFFFFFu;
   return __uint_as_float(u ^ flip);
@@ -507,16 +522,16 @@ __device__ __forceinline__ float prev_float(float v) {  // largest float below v
 // wave-wide max / min of non-negative floats (as ordered bits)
 __device__ __forceinline__ float wave_fmax_nn(float v) { return float_unorder_fps(wave_umax(float_order(v))); }
 
-template <typename T, int PPT, bool TIMING = false>
-__global__ __launch_bounds__(kFpsThreads) void fps_select_kernel(PointsView<T> pts, int N, int npoint,
+template <typename T, int PPT, bool TIMING = false, int THREADS = kFpsThreads>
+__global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, int N, int npoint,
                                                                  const int64_t* __restrict__ start,
                                                                  int64_t* __restrict__ out_idx,
                                                                  T* __restrict__ out_xyz,
                                                                  unsigned long long* __restrict__ prof) {
-  constexpr int W = kFpsThreads / kWave;
-  static_assert(PPT <= 32 && kSelMax == 128 && kFpsThreads == 512, "layout");
+  constexpr int W = THREADS / kWave;
+  static_assert(PPT <= 32 && kSelMax == 128 && (THREADS == 512 || THREADS == 1024), "layout");
   __shared__ uint32_t bins[kMortonBins];  // setup; then the list's values [0, kSelCap) and positions
-  __shared__ uint16_t perm[kFpsThreads * PPT];
+  __shared__ uint16_t perm[THREADS * PPT];
   __shared__ T red[2][3][W];
   __shared__ uint32_t wsum[W];
   __shared__ T lx[kSelCap], ly[kSelCap], lz[kSelCap];
@@ -534,7 +549,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_select_kernel(PointsView<T> p
   uint32_t* lpos = bins + kSelCap;
 
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  fps_morton_sort<T, kFpsThreads>(pts, b, N, bins, perm, red, wsum);
+  fps_morton_sort<T, THREADS>(pts, b, N, bins, perm, red, wsum);
 
   T px[PPT], py[PPT], pz[PPT];
   float dmin[PPT];
@@ -607,7 +622,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_select_kernel(PointsView<T> p
     m = wave_fmax_nn(fmaxf(m, 0.f));
     if (lane == 0) wtf[wave] = m;
   }
-  for (int i = tid; i < kSelBins; i += kFpsThreads) hist[i] = 0u;
+  for (int i = tid; i < kSelBins; i += THREADS) hist[i] = 0u;
   if (tid == 0) {
     na_cnt = 0u;
     cand_fill = 0u;
@@ -653,11 +668,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_select_kernel(PointsView<T> p
         nh += hit ? 1u : 0u;
       }
       // this lane's list offset: one wave scan and one LDS atomic per wave
-      uint32_t incl = nh;
-      for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t u = __shfl_up(incl, off, kWave);
-        incl += lane >= off ? u : 0u;
-      }
+      const uint32_t incl = wave_incl_scan(nh);
       const uint32_t wtot = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
       uint32_t wbase = 0;
       if (wtot) {
@@ -701,14 +712,10 @@ __global__ __launch_bounds__(kFpsThreads) void fps_select_kernel(PointsView<T> p
       hs[2] = h[2] + hs[3];
       hs[1] = h[1] + hs[2];
       hs[0] = h[0] + hs[1];
-      uint32_t above = 0;  // hits in lanes > this lane
+      uint32_t above = 0;  // hits in lanes > this lane: the wave total minus the inclusive prefix
       {
-        uint32_t incl = hs[0];
-        for (int off = 1; off < 64; off <<= 1) {
-          const uint32_t u = __shfl_down(incl, off, kWave);
-          incl += (lane + off < 64) ? u : 0u;
-        }
-        above = incl - hs[0];
+        const uint32_t incl = wave_incl_scan(hs[0]);
+        above = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63)) - incl;
       }
       // the largest bin k with suf(k) >= need (suf is non-increasing in k)
       auto last_bin_at_least = [&](uint32_t need) -> int {
@@ -777,7 +784,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_select_kernel(PointsView<T> p
       }
       if (mode == 1) {  // rescan: everyone has read hist / na / wtf; clear them
         lds_barrier();
-        for (int i = tid; i < kSelBins; i += kFpsThreads) hist[i] = 0u;
+        for (int i = tid; i < kSelBins; i += THREADS) hist[i] = 0u;
         if (tid == 0) na_cnt = 0u;
         lds_barrier();
         continue;
@@ -791,7 +798,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_select_kernel(PointsView<T> p
         bv = wave_fmax_nn(fmaxf(bv, 0.f));
         lds_barrier();  // (wtf / hist reads above are done)
         if (lane == 0) wtf[wave] = bv;
-        for (int i = tid; i < kSelBins; i += kFpsThreads) hist[i] = 0u;
+        for (int i = tid; i < kSelBins; i += THREADS) hist[i] = 0u;
         if (tid == 0) na_cnt = 0u;
         lds_barrier();
         float gmax = wtf[0];
@@ -867,7 +874,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_select_kernel(PointsView<T> p
         na_cnt = 0u;
         cand_fill = 0u;
       }
-      for (int i = tid; i < kSelBins; i += kFpsThreads) hist[i] = 0u;
+      for (int i = tid; i < kSelBins; i += THREADS) hist[i] = 0u;
       tick(1);
       // ---- 4. rank and prefix test in one pass over candidate pairs ----------------------------
       // c_i precedes c_j (value desc, index asc) iff beats(i, j); rank_j = #{i : beats(i, j)}; c_j

@@ -43,6 +43,7 @@ SIGNATURES = {
     "dvcp_knn": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P],
     "dvcp_knn_grid": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P],
     "dvcp_knn_tiled": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P],
+    "dvcp_knn_tiled_insert": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P],
     "dvcp_dfe": [_I, _P, _L, _P, _P, _P],
     "dvcp_dfe_tgt": [_I, _P, _L, _L, _L, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P],
     "dvcp_dfe_tgt_f16": [_I, _P, _L, _L, _L, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P],

@@ -245,9 +245,11 @@ def voxelize(pts, r, s, G, pdim=1):
     return cand, err
 
 
-# kNN method choice.  All three are exact and return identical results.
-#   tiled: Morton-sorted reference tiles scanned nearest-first per wave (dvcp_knn_tiled);
-#          M <= KNN_TILED_MAX_M.
+# kNN method choice.  All are exact and return identical results.
+#   tiled: Morton-sorted reference tiles scanned nearest-first per wave (dvcp_knn_tiled; k > 16:
+#          lane-private candidate buffers merged by bitonic networks); M <= KNN_TILED_MAX_M.
+#   tiled_insert: the same scan inserting every candidate into the sorted list at once (the
+#          round-2 kernel, dvcp_knn_tiled_insert), kept for parity tests and A/B timing.
 #   brute: index-order scan of every reference point (dvcp_knn); best for small M.
 #   grid:  per-query cell-shell search (dvcp_knn_grid); loses on the forward's workload, where
 #          most voxel candidates lie outside the target cloud (profiles/round1: 35.8 ms vs 12.4 ms
@@ -274,9 +276,9 @@ def knn(ref, qry, k, ref_pdim=1, qry_pdim=1, want_idx64=True, method=None):
     idx64 = torch.empty(B, Q, k, dtype=torch.int64, device=dev) if want_idx64 else None
     work = (9.0 * B * Q * M, B * (12 * (M + Q) + Q * k * (8 + (8 if want_idx64 else 0))))
     method = method or knn_method(M)
-    if method == "tiled":
+    if method in ("tiled", "tiled_insert"):
         ws = torch.empty(int(_lib.load().dvcp_knn_tiled_workspace_bytes(B, M, Q)), dtype=torch.uint8, device=dev)
-        call("dvcp_knn_tiled", dtype_code(ref), ptr(ref), rb, rc, rn, M, ptr(qry), qb, qc, qn, Q, B, int(k), ptr(ws),
+        call("dvcp_knn_tiled" if method == "tiled" else "dvcp_knn_tiled_insert", dtype_code(ref), ptr(ref), rb, rc, rn, M, ptr(qry), qb, qc, qn, Q, B, int(k), ptr(ws),
              ptr(dist), ptr(idx), ptr(idx64), stream(), work=work)
     elif method == "grid":
         ws = torch.empty(int(_lib.load().dvcp_knn_grid_workspace_bytes(B, M)), dtype=torch.uint8, device=dev)

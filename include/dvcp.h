@@ -206,13 +206,19 @@ int64_t dvcp_knn_grid_workspace_bytes(int B, int M);
 
 /* Exact kNN over spatially sorted reference tiles: same contract and results as dvcp_knn
  * (replaces knn_cuda.KNN at get_cat_feat_tgt.py:45,52).  References are Morton-sorted into
- * 64-point tiles with boxes and queries into Morton order; each wave of 64 queries scans tiles in
+ * 16-point tiles with boxes and queries into Morton order; each wave of 64 queries scans tiles in
  * ascending lower-bound order and stops once no unscanned tile can hold a point at or below any
- * lane's k-th distance.  M <= 16384, k <= 32.
+ * lane's k-th distance.  For k > 16 each lane buffers its candidates in LDS and the wave merges
+ * them into the sorted lists with bitonic networks.  M <= 16384, k <= 32.
  * workspace: dvcp_knn_tiled_workspace_bytes(B, M, Q) bytes of device memory. */
 int dvcp_knn_tiled(int dtype, const void* ref, int64_t rb, int64_t rc, int64_t rn, int M,
                    const void* qry, int64_t qb, int64_t qc, int64_t qn, int Q, int B, int k,
                    void* workspace, float* dist, int32_t* idx, int64_t* idx64, void* stream);
+/* dvcp_knn_tiled with every candidate inserted into the sorted list at once, for every k (the
+ * round-2 kernel): a second exact implementation for the parity tests and A/B timing. */
+int dvcp_knn_tiled_insert(int dtype, const void* ref, int64_t rb, int64_t rc, int64_t rn, int M,
+                          const void* qry, int64_t qb, int64_t qc, int64_t qn, int Q, int B, int k,
+                          void* workspace, float* dist, int32_t* idx, int64_t* idx64, void* stream);
 int64_t dvcp_knn_tiled_workspace_bytes(int B, int M, int Q);
 
 /* Deep feature embedding on a materialised input.  Replaces deep_feat_embedding.py:23-61

@@ -246,7 +246,7 @@ def test_knn_golden(cuda, name):
     assert torch.equal(d.cpu(), T(z["dist"]))
 
 
-@pytest.mark.parametrize("method", ["tiled", "brute", "grid"])
+@pytest.mark.parametrize("method", ["tiled", "tiled_insert", "brute", "grid"])
 @pytest.mark.parametrize("name", ["knn_f32", "knn_dyadic"])
 def test_knn_methods_golden(cuda, name, method):
     """Every kNN method on the golden fixtures (forced regardless of M)."""
@@ -270,8 +270,8 @@ def _c3_knn_inputs(cuda, M=10000, Q=20000, B=2, seed=113):
     return ref.to(cuda), qry.to(cuda)
 
 
-@pytest.mark.parametrize("method", ["tiled", "grid"])
-@pytest.mark.parametrize("k", [1, 5, 32])
+@pytest.mark.parametrize("method", ["tiled", "tiled_insert", "grid"])
+@pytest.mark.parametrize("k", [1, 5, 20, 32])
 def test_knn_method_equals_brute_full_size(cuda, k, method):
     from dvcp import ops
     ref, qry = _c3_knn_inputs(cuda)
@@ -281,7 +281,7 @@ def test_knn_method_equals_brute_full_size(cuda, k, method):
 
 
 @pytest.mark.parametrize("M,Q,k", [(16384, 3001, 32), (8193, 777, 16), (100, 1000, 32), (20, 300, 32), (1, 65, 4),
-                                   (64, 64, 32), (4096, 1, 8)])
+                                   (64, 64, 32), (4096, 1, 8), (5000, 900, 17), (700, 130, 31)])
 def test_knn_tiled_edges_equal_brute(cuda, M, Q, k):
     """Tile-count boundaries (1, 2, 129, 256 tiles; partial last tile), fewer references than k
     (slots past M are (inf, -1) like knn.hip), a single query, ragged wave tails."""
@@ -312,8 +312,9 @@ def test_knn_tiled_dyadic_ties_full(cuda):
     ref = (torch.randint(-16, 17, (2, 12000, 3), generator=g).float() / 8).to(cuda)
     qry = (torch.randint(-20, 21, (2, 5000, 3), generator=g).float() / 8).to(cuda)
     d1, i1, _ = ops.knn(ref, qry, 32, method="brute")
-    d2, i2, _ = ops.knn(ref, qry, 32, method="tiled")
-    assert torch.equal(i1, i2) and torch.equal(d1, d2)
+    for method in ("tiled", "tiled_insert"):
+        d2, i2, _ = ops.knn(ref, qry, 32, method=method)
+        assert torch.equal(i1, i2) and torch.equal(d1, d2), method
 
 
 def test_knn_k1_transpose_false(cuda):

@@ -63,6 +63,8 @@ struct Config {
 #define CFG(T, P, PR, TM, NAME) Config{NAME, dvcp::fps_kernel<float, T, P, PR, TM>, T, P, TM}
 #define SEL(P, NAME) Config{NAME, dvcp::fps_select_kernel<float, P, false>, 512, P, false}
 #define SELT(P, NAME) Config{NAME, dvcp::fps_select_kernel<float, P, true>, 512, P, true, true}
+#define SEL16(P, NAME) Config{NAME, dvcp::fps_select_kernel<float, P, false, 1024>, 1024, P, false}
+#define SELT16(P, NAME) Config{NAME, dvcp::fps_select_kernel<float, P, true, 1024>, 1024, P, true, true}
 
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 16;
@@ -97,8 +99,12 @@ int main(int argc, char** argv) {
   const std::vector<Config> cfgs = {
       SEL(32, "select 512x32"),
       SELT(32, "select 512x32 +stats"),
+      SEL16(16, "select 1024x16"),
+      SELT16(16, "select 1024x16 +stats"),
       SEL(20, "select 512x20"),
       SELT(20, "select 512x20 +stats"),
+      SEL16(10, "select 1024x10"),
+      SELT16(10, "select 1024x10 +stats"),
       CFG(512, 32, true, false, "v3 512x32 prune"),
       CFG(512, 32, true, true, "v3 512x32 prune +timing"),
       CFG(512, 32, false, false, "v3 512x32 noprune"),
@@ -136,7 +142,7 @@ int main(int argc, char** argv) {
       printf("   cloud 0: rounds %llu  scans %llu  fallbacks %llu  centres/round %.1f  rescans: none-above %llu "
              "over-cap %llu under-min %llu crowded %llu\n", pr[0], pr[1], pr[2],
              pr[0] ? double(npoint - 1) / pr[0] : 0.0, pr[8], pr[9], pr[10], pr[11]);
-      for (int w = 0; w < 8; ++w) {
+      for (int w = 0; w < c.threads / 64; ++w) {
         const unsigned long long* q = &pr[static_cast<size_t>(w) * dvcp::kFpsProf];
         const double r = q[0] ? double(q[0]) : 1.0;
         printf("   wave %d clk/round: scan %.0f  decide+list %.0f  rank %.0f  prefix %.0f  update %.0f\n", w,

@@ -22,18 +22,24 @@ def main():
     ax = torch.arange(-2.0, 2.0001, 0.4)
     off = torch.tensor(list(itertools.product(ax.tolist(), repeat=3)), dtype=torch.float32)  # (1331, 3)
     qry = (kp[:, :, None, :] + off[None, None]).reshape(8, -1, 3).to(dev).contiguous()
-    for _ in range(3):
-        dist, idx, _ = ops.knn(ref, qry, 32, ref_pdim=2, qry_pdim=1, want_idx64=False)
-    torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     reps = 10
-    e0.record()
-    for _ in range(reps):
-        ops.knn(ref, qry, 32, ref_pdim=2, qry_pdim=1, want_idx64=False)
-    e1.record()
-    torch.cuda.synchronize()
-    print(f"knn: {e0.elapsed_time(e1) / reps:.4f} ms/call  queries {qry.shape[0] * qry.shape[1]}  "
-          f"checksum {dist.double().sum().item():.6e} {idx.long().sum().item()}", flush=True)
+    outs = {}
+    for method in ("tiled_insert", "tiled", "tiled_insert", "tiled"):
+        for _ in range(3):
+            dist, idx, _ = ops.knn(ref, qry, 32, ref_pdim=2, qry_pdim=1, want_idx64=False, method=method)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(reps):
+            ops.knn(ref, qry, 32, ref_pdim=2, qry_pdim=1, want_idx64=False, method=method)
+        e1.record()
+        torch.cuda.synchronize()
+        outs[method] = (dist, idx)
+        print(f"knn {method}: {e0.elapsed_time(e1) / reps:.4f} ms/call (build + query)  queries "
+              f"{qry.shape[0] * qry.shape[1]}  checksum {dist.double().sum().item():.6e} {idx.long().sum().item()}",
+              flush=True)
+    same = all(torch.equal(a, b) for a, b in zip(outs["tiled"], outs["tiled_insert"]))
+    print(f"knn tiled == tiled_insert: {same}", flush=True)
 
     # the target-side deep feature embedding on these neighbour lists (features random)
     import dvcp
