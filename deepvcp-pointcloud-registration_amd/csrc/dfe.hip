@@ -25,6 +25,11 @@ int launch_dfe_tgt_mfma(PointsView<T> ref, const float* feat, int M, const float
                         const int32_t* idx, int B, int Q, const float* params, float* out, bool literal,
                         hipStream_t st);
 
+// segsum.hip: deterministic per-row sums of keyed 32-float contribution rows.
+int64_t segment_sum_workspace_bytes(int64_t E, int64_t nrows);
+int segment_sum(const uint32_t* keys, const float* contrib, int64_t E, int64_t nrows, float* out, void* ws,
+                hipStream_t st);
+
 constexpr int kDfeRowsPerQ = 32;
 constexpr int kDfeThreads = 256;
 constexpr int kDfeQPerBlock = kDfeThreads / kDfeRowsPerQ;
@@ -182,7 +187,8 @@ __global__ __launch_bounds__(kDfeThreads) void dfe_bwd_kernel(const T* __restric
                                                               const int32_t* __restrict__ idx, int Q, int64_t R,
                                                               const float* __restrict__ Ee,
                                                               const float* __restrict__ gout, float* __restrict__ part,
-                                                              float* __restrict__ gX, float* __restrict__ gF) {
+                                                              float* __restrict__ gX, float* __restrict__ gF,
+                                                              uint32_t* __restrict__ gkey, uint32_t key_none) {
   __shared__ float xs[kDfeThreads][37];
   __shared__ float Es[32][37];  // E (the bias e shifts a channel's rows alike: not needed for the arg-max)
   __shared__ double wq[kDfeQPerBlock][32];
@@ -276,15 +282,26 @@ __global__ __launch_bounds__(kDfeThreads) void dfe_bwd_kernel(const T* __restric
         if (live)
           for (int i = 0; i < 35; ++i) gX[(q * 32 + j) * 35 + i] = dx[i];
       } else {
-        // get_cat_feat_tgt.py:85,95: x[3 + c] = F[idx_j, c] * w[c] (fp64 weight) -> dF[idx_j, c] += dx * w[c]
-        if (live && any) {
+        // get_cat_feat_tgt.py:85,95: x[3 + c] = F[idx_j, c] * w[c] (fp64 weight) -> entry (q, j)
+        // contributes dx[3 + c] * w[c] to dF[idx_j, c]: its contribution row and target row are
+        // written here and summed per target row by segment_sum (segsum.hip, deterministic)
+        if (live) {
+          const int64_t e = q * 32 + j;
           const int b = static_cast<int>(q / Q);
-          int n = idx[q * 32 + j];
+          int n = idx[e];
           n = n < 0 ? 0 : (n >= M ? M - 1 : n);
-          float* dst = gF + (static_cast<int64_t>(b) * M + n) * 32;
+          gkey[e] = any ? static_cast<uint32_t>(static_cast<int64_t>(b) * M + n) : key_none;
+          if (any) {
+            float4* dst = reinterpret_cast<float4*>(gF + e * 32);
 #pragma unroll
-          for (int c = 0; c < 32; ++c)
-            if (dx[3 + c] != 0.f) atomicAdd(dst + c, static_cast<float>(static_cast<double>(dx[3 + c]) * wq[ql][c]));
+            for (int c4 = 0; c4 < 8; ++c4) {
+              float v[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u)
+                v[u] = static_cast<float>(static_cast<double>(dx[3 + 4 * c4 + u]) * wq[ql][4 * c4 + u]);
+              dst[c4] = make_float4(v[0], v[1], v[2], v[3]);
+            }
+          }
         }
       }
       __syncthreads();  // rsel / rg are rewritten by the next group
@@ -420,10 +437,23 @@ extern "C" int64_t dvcp_dfe_backward_workspace_bytes(int64_t R) {  // (same for 
 }
 
 // mode 0: X (R, 32, 35) rows (x_dtype); mode 1: fused target rows (the dvcp_dfe_tgt arguments, R = B*Q).
+// Target-feature gradient (mode 1, gF): after the parameter-gradient workspace, the entries'
+// target rows (R * 32 u32), their contribution rows (R * 32 * 32 fp32) and segment_sum's own.
+static int64_t tgt_feat_ws_offset(int64_t R) { return (dvcp_dfe_backward_workspace_bytes(R) + 255) / 256 * 256; }
+static int64_t tgt_contrib_offset(int64_t R) { return tgt_feat_ws_offset(R) + (R * 32 * 4 + 255) / 256 * 256; }
+static int64_t tgt_segsum_offset(int64_t R) { return tgt_contrib_offset(R) + R * 32 * 32 * 4; }
+
+extern "C" int64_t dvcp_dfe_tgt_backward_workspace_bytes(int B, int Q, int M, int want_feat_grad) {
+  const int64_t R = static_cast<int64_t>(B) * Q;
+  if (!want_feat_grad || R <= 0) return dvcp_dfe_backward_workspace_bytes(R);
+  const int64_t seg = dvcp::segment_sum_workspace_bytes(R * 32, static_cast<int64_t>(B) * M);
+  return seg < 0 ? -1 : tgt_segsum_offset(R) + seg;
+}
+
 static int dfe_backward_launch(int mode, int dtype, const void* X, const void* ref_xyz, int64_t rb, int64_t rc,
                                int64_t rn, int M, const float* ref_feat, const float* cand, const float* dist,
                                const int32_t* idx, int Q, int64_t R, const float* params, const float* grad_out,
-                               float* ws, float* grad_params, float* gX, float* gF, hipStream_t st) {
+                               float* ws, float* grad_params, float* gX, float* gF_out, hipStream_t st) {
   if (R <= 0) {  // no rows: zero gradients
     hipLaunchKernelGGL(dvcp::dfe_bwd_finish_kernel, dim3(1), dim3(1024), 0, st, nullptr, params, grad_params);
     return dvcp::launch_status("dvcp_dfe_backward");
@@ -433,22 +463,26 @@ static int dfe_backward_launch(int mode, int dtype, const void* X, const void* r
   float* Ee = reinterpret_cast<float*>(Gs + dvcp::kDfeGPart);
   hipLaunchKernelGGL(dvcp::dfe_collapse_kernel, dim3(1), dim3(1024), 0, st, params, Ee);
   const dim3 grid(nblk), block(dvcp::kDfeThreads);
+  char* wsb = reinterpret_cast<char*>(ws);
+  uint32_t* gkey = gF_out ? reinterpret_cast<uint32_t*>(wsb + tgt_feat_ws_offset(R)) : nullptr;
+  float* gF = gF_out ? reinterpret_cast<float*>(wsb + tgt_contrib_offset(R)) : nullptr;
+  const uint32_t key_none = static_cast<uint32_t>((R / Q) * M);
   if (mode == 0 && dtype == DVCP_F32)
     hipLaunchKernelGGL((dvcp::dfe_bwd_kernel<0, float>), grid, block, 0, st, static_cast<const float*>(X),
                        dvcp::PointsView<float>{nullptr, 0, 0, 0}, nullptr, 0, nullptr, nullptr, nullptr, 1, R, Ee,
-                       grad_out, ws, gX, gF);
+                       grad_out, ws, gX, gF, gkey, key_none);
   else if (mode == 0 && dtype == DVCP_F64)
     hipLaunchKernelGGL((dvcp::dfe_bwd_kernel<0, double>), grid, block, 0, st, static_cast<const double*>(X),
                        dvcp::PointsView<double>{nullptr, 0, 0, 0}, nullptr, 0, nullptr, nullptr, nullptr, 1, R, Ee,
-                       grad_out, ws, gX, gF);
+                       grad_out, ws, gX, gF, gkey, key_none);
   else if (mode == 1 && dtype == DVCP_F32)
     hipLaunchKernelGGL((dvcp::dfe_bwd_kernel<1, float>), grid, block, 0, st, nullptr,
                        dvcp::PointsView<float>{static_cast<const float*>(ref_xyz), rb, rc, rn}, ref_feat, M, cand, dist,
-                       idx, Q, R, Ee, grad_out, ws, gX, gF);
+                       idx, Q, R, Ee, grad_out, ws, gX, gF, gkey, key_none);
   else if (mode == 1 && dtype == DVCP_F64)
     hipLaunchKernelGGL((dvcp::dfe_bwd_kernel<1, double>), grid, block, 0, st, nullptr,
                        dvcp::PointsView<double>{static_cast<const double*>(ref_xyz), rb, rc, rn}, ref_feat, M, cand,
-                       dist, idx, Q, R, Ee, grad_out, ws, gX, gF);
+                       dist, idx, Q, R, Ee, grad_out, ws, gX, gF, gkey, key_none);
   else {
     dvcp::set_error("dvcp_dfe_backward: bad dtype %d", dtype);
     return DVCP_EINVAL;
@@ -456,6 +490,12 @@ static int dfe_backward_launch(int mode, int dtype, const void* X, const void* r
   hipLaunchKernelGGL(dvcp::dfe_bwd_sum_kernel, dim3(dvcp::ceil_div(dvcp::kDfeGPart, 64)), dim3(1024), 0, st, ws, nblk,
                      Gs);
   hipLaunchKernelGGL(dvcp::dfe_bwd_finish_kernel, dim3(1), dim3(1024), 0, st, Gs, params, grad_params);
+  if (gF_out) {
+    const int rc2 = dvcp::launch_status("dvcp_dfe_tgt_backward");
+    if (rc2 != DVCP_OK) return rc2;
+    return dvcp::segment_sum(gkey, gF, R * 32, static_cast<int64_t>(R / Q) * M, gF_out, wsb + tgt_segsum_offset(R),
+                             st);
+  }
   return dvcp::launch_status("dvcp_dfe_backward");
 }
 

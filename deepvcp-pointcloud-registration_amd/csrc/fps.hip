@@ -85,6 +85,7 @@ struct alignas(16) FpsSlot {
 };
 
 constexpr int kFpsThreads = 512;  // 8 waves: 2 per SIMD, up to 256 VGPRs each
+constexpr int kFpsSel1024 = 1024;  // the fp32 select kernel's workgroup: 16 waves, 4 per SIMD
 constexpr int kMortonBins = 4096;
 constexpr int kFpsProf = 12;      // timing probe words per wave (fps_kernel<..., TIMING=true>)
 
@@ -483,9 +484,12 @@ __device__ __forceinline__ float fps_update(float m, T px, T py, T pz, T cx, T c
 // ---------------------------------------------------------------------------------------------
 // Threshold-select FPS (the default for 2048 <= N <= 16384 fp32 / 8192 fp64 points per cloud).
 //
-// Same point layout as the batched kernel (Morton-sorted 64-point groups, slot p of wave w holds
-// sorted positions (w*PPT + p)*64 + lane, coordinates and running minima in VGPRs), but a round
-// is decided without a serial walk:
+// Same point layout as the batched kernel (Morton-sorted 64-point groups, coordinates and running
+// minima in VGPRs), except that the groups are dealt to the waves round robin -- slot p of wave w
+// holds sorted positions (p*W + w)*64 + lane -- so every wave owns groups all over the cloud and
+// the update of a round's accepted centres (which land in the cloud's largest holes, wherever
+// they are) is spread evenly instead of falling on the few waves whose region holds them.  A
+// round is decided without a serial walk:
 //   1. scan: every point above a floor f is appended to an LDS list (value, position, xyz) and
 //      counted in a 256-bin histogram of its float bits over (f, vmax]; T_f = the largest
 //      running minimum at or below f (the floor adapts: raised from the histogram when more than
@@ -548,7 +552,7 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
   float* lv = reinterpret_cast<float*>(bins);
   uint32_t* lpos = bins + kSelCap;
 
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x, tid = threadIdx.x, lane_outer = tid & 63, lane = lane_outer, wave = tid >> 6;
   fps_morton_sort<T, THREADS>(pts, b, N, bins, perm, red, wsum);
 
   T px[PPT], py[PPT], pz[PPT];
@@ -561,7 +565,7 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
   }
 #pragma unroll 1
   for (int p = 0; p < PPT; ++p) {
-    const int pos = (wave * PPT + p) * kWave + lane;
+    const int pos = (p * W + wave) * kWave + lane;  // groups interleaved over the waves
     const bool real = pos < N;
     const uint32_t n = perm[real ? pos : 0];
     const T x = pts.at(b, 0, n), y = pts.at(b, 1, n), z = pts.at(b, 2, n);
@@ -587,7 +591,7 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
   }
 #pragma unroll
   for (int a = 0; a < 6; ++a) wb[a] = readfirstlane_t(wb[a]);
-  const bool grp = lane < PPT && (wave * PPT + lane) * kWave < N;  // lane p: a non-empty group
+  const bool grp = lane < PPT && (lane * W + wave) * kWave < N;  // lane p: a non-empty group
 
   int64_t* oi = out_idx + static_cast<int64_t>(b) * npoint;
   T* ox = out_xyz ? out_xyz + static_cast<int64_t>(b) * 3 * npoint : nullptr;
@@ -647,11 +651,20 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
     }
   };
   while (step < npoint) {
+    // The lane index laundered through an empty asm once per round: the round's LDS addresses are
+    // then recomputed from it (a few VALU ops) instead of being hoisted out of the loop as ~40
+    // lane-dependent constants, which at 1024 threads (128 VGPRs) were spilled to scratch.
+    int lane_r = lane_outer;
+    asm volatile("" : "+v"(lane_r));
+    const int lane = lane_r;
     ++n_round;
     int kstar = 0;
     uint64_t acc0 = 0, acc1 = 0;  // accepted candidates (slots 0-63, 64-127)
     bool raised = false;
     for (int scan = 0;; ++scan) {
+      int lane_s = lane_outer;  // laundered again per scan (see the round loop)
+      asm volatile("" : "+v"(lane_s));
+      const int lane = lane_s;
       ++n_scan;
       tick(-1);
       // ---- 1. scan: list the points above f, histogram their float bits over (f, vmax] ----------
@@ -686,7 +699,7 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
             atomicAdd(&hist[bin], 1u);
             if (li < kSelCap) {
               lv[li] = v;
-              lpos[li] = static_cast<uint32_t>((wave * PPT + p) * kWave + lane);
+              lpos[li] = static_cast<uint32_t>((p * W + wave) * kWave + lane);
               lx[li] = px[p];
               ly[li] = py[p];
               lz[li] = pz[p];
@@ -807,7 +820,7 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
         uint32_t mp = 0xFFFFFFFFu;
 #pragma unroll
         for (int p = 0; p < PPT; ++p) {
-          const int pos = (wave * PPT + p) * kWave + lane;
+          const int pos = (p * W + wave) * kWave + lane;
           if (__ballot(dmin[p] == gmax)) {
             if (dmin[p] == gmax) mp = min(mp, static_cast<uint32_t>(perm[pos]));
           }
@@ -1303,6 +1316,27 @@ static int launch_fps(const T* xyz, int64_t sb, int64_t sc, int64_t sn, int B, i
   PointsView<T> v{xyz, sb, sc, sn};
   const int ppt = ceil_div(N, kFpsThreads);
   dim3 grid(B), block(kFpsThreads);
+  // fp32 clouds of 2048..16384 points: the select kernel with 1024 threads (16 waves, 4 per SIMD,
+  // up to 16 points per lane): per-wave scan and update halve while the per-round decisions stay
+  // (tools/fps_lab: 16384 -> 10000 5.52 -> 5.07 ms, 10000 -> 10000 4.13 -> 3.30 ms on 16 clouds)
+  if constexpr (sizeof(T) == 4) {
+    if (N >= kFpsBatchedMinN && N <= 16 * kFpsSel1024) {
+      const int p16 = ceil_div(N, kFpsSel1024);
+      const dim3 blk(kFpsSel1024);
+#define DVCP_FPS_SEL1024(P)                                                                                   \
+  if (p16 <= P) {                                                                                             \
+    hipLaunchKernelGGL((fps_select_kernel<T, P, false, kFpsSel1024>), grid, blk, 0, st, v, N, npoint, start,    \
+                       out_idx, out_xyz, nullptr);                                                            \
+    return launch_status("dvcp_fps");                                                                         \
+  }
+      DVCP_FPS_SEL1024(2)
+      DVCP_FPS_SEL1024(4)
+      DVCP_FPS_SEL1024(8)
+      DVCP_FPS_SEL1024(10)
+      DVCP_FPS_SEL1024(16)
+#undef DVCP_FPS_SEL1024
+    }
+  }
   // threshold-select kernel from 2048 points; below, the one-centre-per-step kernel (box-pruned)
 #define DVCP_FPS_CASE(P)                                                                                   \
   if (ppt <= P) {                                                                                          \

@@ -436,25 +436,26 @@ __global__ void registration_error_kernel(const double* __restrict__ Rp, const d
 // Paper-faithful pose solve (DeepVCP paper, Sec. 3.4-3.5; SURVEY.md 8(f) rank 4 -- not reference
 // parity, the reference solves unweighted with no reflection fix): weighted Kabsch with the key
 // points' weights w_i, c_x = sum w x / sum w, H = sum w (x - c_x)(y - c_y)^T, and the det-sign
-// correction R = V diag(1, 1, d) U^T, d = sign(det(V U^T)).  With the ground truth it also forms
+// correction R = V diag(1, 1, d) U^T, d = sign(det(V U^T)).  Sec. 3.5's outlier rejection: with
+// inlier_ratio < 1 the int(inlier_ratio n) pairs with the smallest residual |R1 x + t1 - y| under
+// the first solve (ties: the lower index) are solved again.  With the ground truth it also forms
 // the paper's two loss terms per pair: sum |y_gt - y*| (the VCPs against the ground-truth
-// correspondences) and sum |y_gt - (R x + t)| (the solved pose applied to the key points).
-__global__ __launch_bounds__(kRgThreads) void paper_pose_kernel(const double* __restrict__ xg,
-                                                                const double* __restrict__ yg,
-                                                                const double* __restrict__ wg, int n, int reflection_fix,
-                                                                const double* __restrict__ Rtrue,
-                                                                const double* __restrict__ ttrue,
-                                                                double* __restrict__ Rout, double* __restrict__ tout,
-                                                                double* __restrict__ partial) {
-  __shared__ double scratch[16];
-  __shared__ double rt[12];
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const double* x = xg + static_cast<int64_t>(b) * 3 * n;
-  const double* y = yg + static_cast<int64_t>(b) * 3 * n;
-  const double* w = wg ? wg + static_cast<int64_t>(b) * n : nullptr;
+// correspondences) and sum |y_gt - (R x + t)| (the final pose applied to every key point).
+
+struct PaperSolve {
+  double R[3][3], t[3], U[3][3], sig[3], cen[6], wsum;
+  int kmin;       // the singular direction the reflection fix flipped (-1: none)
+};
+
+// Block-wide weighted Kabsch over the columns sel[0..m) (all n when sel == nullptr); every thread
+// returns the solve.  `rt` holds >= 32 doubles of LDS.
+__device__ void weighted_kabsch(const double* x, const double* y, const double* w, int n, const int* sel, int m,
+                                int reflection_fix, PaperSolve& S, double* scratch, double* rt) {
+  const int tid = threadIdx.x;
   double c[7];
   for (int a = 0; a < 7; ++a) c[a] = 0;
-  for (int j = tid; j < n; j += kRgThreads) {
+  for (int k = tid; k < m; k += blockDim.x) {
+    const int j = sel ? sel[k] : k;
     const double wj = w ? w[j] : 1.0;
     for (int a = 0; a < 3; ++a) {
       c[a] = fma(wj, x[a * n + j], c[a]);
@@ -468,7 +469,8 @@ __global__ __launch_bounds__(kRgThreads) void paper_pose_kernel(const double* __
   for (int a = 0; a < 6; ++a) cen[a] /= wsum;
   double h[9];
   for (int a = 0; a < 9; ++a) h[a] = 0;
-  for (int j = tid; j < n; j += kRgThreads) {
+  for (int k = tid; k < m; k += blockDim.x) {
+    const int j = sel ? sel[k] : k;
     const double wj = w ? w[j] : 1.0;
     double dx[3], dy[3];
     for (int a = 0; a < 3; ++a) {
@@ -486,6 +488,7 @@ __global__ __launch_bounds__(kRgThreads) void paper_pose_kernel(const double* __
     const double det = R[0][0] * (R[1][1] * R[2][2] - R[1][2] * R[2][1]) -
                        R[0][1] * (R[1][0] * R[2][2] - R[1][2] * R[2][0]) +
                        R[0][2] * (R[1][0] * R[2][1] - R[1][1] * R[2][0]);
+    int kmin = -1;
     if (reflection_fix && det < 0) {  // V diag(1,1,-1) U^T = R - 2 v_min u_min^T, v_min = R u_min
       int k = 0;
       for (int j = 1; j < 3; ++j) k = sig[j] < sig[k] ? j : k;
@@ -493,19 +496,85 @@ __global__ __launch_bounds__(kRgThreads) void paper_pose_kernel(const double* __
       for (int a = 0; a < 3; ++a) v[a] = R[a][0] * U[0][k] + R[a][1] * U[1][k] + R[a][2] * U[2][k];
       for (int a = 0; a < 3; ++a)
         for (int bb = 0; bb < 3; ++bb) R[a][bb] -= 2.0 * v[a] * U[bb][k];
+      kmin = k;
     }
     for (int a = 0; a < 3; ++a) {
-      for (int bb = 0; bb < 3; ++bb) rt[a * 3 + bb] = R[a][bb];
+      for (int bb = 0; bb < 3; ++bb) {
+        rt[a * 3 + bb] = R[a][bb];
+        rt[12 + a * 3 + bb] = U[a][bb];
+      }
       rt[9 + a] = cen[3 + a] - (R[a][0] * cen[0] + R[a][1] * cen[1] + R[a][2] * cen[2]);
+      rt[21 + a] = sig[a];
     }
+    rt[24] = static_cast<double>(kmin);
   }
   __syncthreads();
-  double R[3][3], t[3];
-  for (int a = 0; a < 9; ++a) R[a / 3][a % 3] = rt[a];
-  for (int a = 0; a < 3; ++a) t[a] = rt[9 + a];
+  for (int a = 0; a < 9; ++a) {
+    S.R[a / 3][a % 3] = rt[a];
+    S.U[a / 3][a % 3] = rt[12 + a];
+  }
+  for (int a = 0; a < 3; ++a) {
+    S.t[a] = rt[9 + a];
+    S.sig[a] = rt[21 + a];
+  }
+  S.kmin = static_cast<int>(rt[24]);
+  for (int a = 0; a < 6; ++a) S.cen[a] = cen[a];
+  S.wsum = wsum;
+  __syncthreads();
+}
+
+// The paper's solve with rejection: the first solve, residual ranks, the kept list sel[0..m) in
+// index order, the second solve.  Returns m (n when nothing is rejected, then sel is unused).
+__device__ int paper_solve(const double* x, const double* y, const double* w, int n, int m_keep, int reflection_fix,
+                           PaperSolve& S, double* res, int* sel, double* scratch, double* rt) {
+  weighted_kabsch(x, y, w, n, nullptr, n, reflection_fix, S, scratch, rt);
+  if (m_keep >= n) return n;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    double d2 = 0;
+    for (int a = 0; a < 3; ++a) {
+      const double e = S.R[a][0] * x[j] + S.R[a][1] * x[n + j] + S.R[a][2] * x[2 * n + j] + S.t[a] - y[a * n + j];
+      d2 += e * e;
+    }
+    res[j] = sqrt(d2);
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {  // rank: strictly smaller, or equal with a lower index
+    const double v = res[j];
+    int r = 0;
+    for (int i = 0; i < n; ++i) r += (res[i] < v || (res[i] == v && i < j)) ? 1 : 0;
+    sel[kRgMaxN + j] = r < m_keep ? 1 : 0;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int k = 0;
+    for (int j = 0; j < n; ++j)
+      if (sel[kRgMaxN + j]) sel[k++] = j;
+  }
+  __syncthreads();
+  weighted_kabsch(x, y, w, n, sel, m_keep, reflection_fix, S, scratch, rt);
+  return m_keep;
+}
+
+__global__ __launch_bounds__(kRgThreads) void paper_pose_kernel(const double* __restrict__ xg,
+                                                                const double* __restrict__ yg,
+                                                                const double* __restrict__ wg, int n, int reflection_fix,
+                                                                int m_keep, const double* __restrict__ Rtrue,
+                                                                const double* __restrict__ ttrue,
+                                                                double* __restrict__ Rout, double* __restrict__ tout,
+                                                                double* __restrict__ partial) {
+  __shared__ double scratch[16];
+  __shared__ double rt[32];
+  __shared__ double res[kRgMaxN];
+  __shared__ int sel[2 * kRgMaxN];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const double* x = xg + static_cast<int64_t>(b) * 3 * n;
+  const double* y = yg + static_cast<int64_t>(b) * 3 * n;
+  const double* w = wg ? wg + static_cast<int64_t>(b) * n : nullptr;
+  PaperSolve S;
+  paper_solve(x, y, w, n, m_keep, reflection_fix, S, res, sel, scratch, rt);
   if (tid == 0) {
-    for (int a = 0; a < 9; ++a) Rout[b * 9 + a] = R[a / 3][a % 3];
-    for (int a = 0; a < 3; ++a) tout[b * 3 + a] = t[a];
+    for (int a = 0; a < 9; ++a) Rout[b * 9 + a] = S.R[a / 3][a % 3];
+    for (int a = 0; a < 3; ++a) tout[b * 3 + a] = S.t[a];
   }
   if (partial) {
     double Rg[3][3], tg[3];
@@ -515,7 +584,7 @@ __global__ __launch_bounds__(kRgThreads) void paper_pose_kernel(const double* __
     for (int j = tid; j < n; j += kRgThreads) {
       for (int a = 0; a < 3; ++a) {
         const double ygt = Rg[a][0] * x[j] + Rg[a][1] * x[n + j] + Rg[a][2] * x[2 * n + j] + tg[a];
-        const double yp = R[a][0] * x[j] + R[a][1] * x[n + j] + R[a][2] * x[2 * n + j] + t[a];
+        const double yp = S.R[a][0] * x[j] + S.R[a][1] * x[n + j] + S.R[a][2] * x[2 * n + j] + S.t[a];
         s1 += fabs(ygt - y[a * n + j]);
         s2 += fabs(ygt - yp);
       }
@@ -525,6 +594,115 @@ __global__ __launch_bounds__(kRgThreads) void paper_pose_kernel(const double* __
     if (tid == 0) {
       partial[b * 2] = s1;
       partial[b * 2 + 1] = s2;
+    }
+  }
+}
+
+// Backward of the paper loss  alpha / cnt sum |y_gt - y| + (1 - alpha) / cnt sum |y_gt - (R x + t)|
+// in y and w.  The rejection's selection is piecewise constant, so the gradient reaches the pose
+// through the second solve only.  For that solve (sums over the kept set, W = sum w):
+//   g_i = c2 sign(p_i - ygt_i) (every key point), gt = sum g_i, GR = sum g_i (x_i - c_x)^T;
+//   H^T = R P' with P' = U diag(s') U^T (s' = sigma with the reflection-flipped direction
+//   negated) gives dL/dH = -2 Y R^T, P' Y + Y P' = skew(R^T GR), solved in U's basis as
+//   Y~_ij = M~_ij / (s'_i + s'_j) (the unweighted form is dvcp_svd_optimization_backward's);
+//   dL/dy_j = w_j GH^T dx_j + (w_j / W) gt,
+//   dL/dw_j = dx_j^T GH dy_j + (dy_j . gt - dx_j . R^T gt) / W   (the centroids' share),
+// plus c1 sign(y_j - ygt_j) from the first term on every key point.
+__global__ __launch_bounds__(kRgThreads) void paper_pose_bwd_kernel(
+    const double* __restrict__ xg, const double* __restrict__ yg, const double* __restrict__ wg, int n,
+    int reflection_fix, int m_keep, const double* __restrict__ Rtrue, const double* __restrict__ ttrue,
+    const double* __restrict__ grad_loss, double alpha, double inv_cnt, double* __restrict__ gyg,
+    double* __restrict__ gwg) {
+  const double c1 = alpha * grad_loss[0] * inv_cnt, c2 = (1.0 - alpha) * grad_loss[0] * inv_cnt;
+  __shared__ double scratch[16];
+  __shared__ double rt[32];
+  __shared__ double res[kRgMaxN];
+  __shared__ int sel[2 * kRgMaxN];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const double* x = xg + static_cast<int64_t>(b) * 3 * n;
+  const double* y = yg + static_cast<int64_t>(b) * 3 * n;
+  const double* w = wg ? wg + static_cast<int64_t>(b) * n : nullptr;
+  double* gy = gyg + static_cast<int64_t>(b) * 3 * n;
+  double* gw = gwg ? gwg + static_cast<int64_t>(b) * n : nullptr;
+  PaperSolve S;
+  const int m = paper_solve(x, y, w, n, m_keep, reflection_fix, S, res, sel, scratch, rt);
+  double Rg[3][3], tg[3];
+  for (int a = 0; a < 9; ++a) Rg[a / 3][a % 3] = Rtrue[b * 9 + a];
+  for (int a = 0; a < 3; ++a) tg[a] = ttrue[b * 3 + a];
+  // the first term, and g_i of the second on every key point
+  double acc[12];  // gt (3), GR (9)
+  for (int a = 0; a < 12; ++a) acc[a] = 0;
+  for (int j = tid; j < n; j += kRgThreads) {
+    double dx[3];
+    for (int a = 0; a < 3; ++a) dx[a] = x[a * n + j] - S.cen[a];
+    for (int a = 0; a < 3; ++a) {
+      const double ygt = Rg[a][0] * x[j] + Rg[a][1] * x[n + j] + Rg[a][2] * x[2 * n + j] + tg[a];
+      const double yp = S.R[a][0] * x[j] + S.R[a][1] * x[n + j] + S.R[a][2] * x[2 * n + j] + S.t[a];
+      const double e1 = y[a * n + j] - ygt, e2 = yp - ygt;
+      gy[a * n + j] = c1 * (e1 > 0 ? 1.0 : (e1 < 0 ? -1.0 : 0.0));
+      const double g = c2 * (e2 > 0 ? 1.0 : (e2 < 0 ? -1.0 : 0.0));
+      acc[a] += g;
+      for (int c = 0; c < 3; ++c) acc[3 + a * 3 + c] = fma(g, dx[c], acc[3 + a * 3 + c]);
+    }
+    if (gw) gw[j] = 0.0;
+  }
+  double gt[3], GR[3][3];
+  for (int a = 0; a < 3; ++a) gt[a] = block_sum(acc[a], scratch);
+  for (int a = 0; a < 9; ++a) GR[a / 3][a % 3] = block_sum(acc[3 + a], scratch);
+  // dL/dH = -2 Y R^T  (every thread computes the same 3x3 algebra)
+  double A[3][3];  // R^T GR
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) A[i][j] = S.R[0][i] * GR[0][j] + S.R[1][i] * GR[1][j] + S.R[2][i] * GR[2][j];
+  double Mk[3][3], Mt[3][3], Yt[3][3], Y[3][3], T[3][3], GH[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Mk[i][j] = 0.5 * (A[i][j] - A[j][i]);
+  for (int i = 0; i < 3; ++i)  // U^T Mk U
+    for (int j = 0; j < 3; ++j) {
+      double v = 0;
+      for (int p = 0; p < 3; ++p)
+        for (int q = 0; q < 3; ++q) v += S.U[p][i] * Mk[p][q] * S.U[q][j];
+      Mt[i][j] = v;
+    }
+  double sp[3];
+  for (int i = 0; i < 3; ++i) sp[i] = i == S.kmin ? -S.sig[i] : S.sig[i];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      const double den = sp[i] + sp[j];
+      Yt[i][j] = (i == j || den == 0.0) ? 0.0 : Mt[i][j] / den;
+    }
+  for (int i = 0; i < 3; ++i)  // U Yt U^T
+    for (int j = 0; j < 3; ++j) {
+      double v = 0;
+      for (int p = 0; p < 3; ++p)
+        for (int q = 0; q < 3; ++q) v += S.U[i][p] * Yt[p][q] * S.U[j][q];
+      Y[i][j] = v;
+    }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) T[i][j] = Y[i][0] * S.R[j][0] + Y[i][1] * S.R[j][1] + Y[i][2] * S.R[j][2];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) GH[i][j] = -2.0 * T[i][j];
+  double Rtg[3];
+  for (int a = 0; a < 3; ++a) Rtg[a] = S.R[0][a] * gt[0] + S.R[1][a] * gt[1] + S.R[2][a] * gt[2];
+  __syncthreads();  // gy's first-term writes are read back below by the same thread only
+  for (int k = tid; k < m; k += kRgThreads) {
+    const int j = m < n ? sel[k] : k;
+    const double wj = w ? w[j] : 1.0;
+    double dx[3], dy[3];
+    for (int a = 0; a < 3; ++a) {
+      dx[a] = x[a * n + j] - S.cen[a];
+      dy[a] = y[a * n + j] - S.cen[3 + a];
+    }
+    for (int a = 0; a < 3; ++a) {
+      const double ghx = GH[0][a] * dx[0] + GH[1][a] * dx[1] + GH[2][a] * dx[2];  // (GH^T dx)_a
+      gy[a * n + j] += wj * ghx + (wj / S.wsum) * gt[a];
+    }
+    if (gw) {
+      double q = 0;
+      for (int a = 0; a < 3; ++a)
+        for (int c = 0; c < 3; ++c) q += dx[a] * GH[a][c] * dy[c];
+      const double cy = dy[0] * gt[0] + dy[1] * gt[1] + dy[2] * gt[2];
+      const double cx = dx[0] * Rtg[0] + dx[1] * Rtg[1] + dx[2] * Rtg[2];
+      gw[j] = q + (cy - cx) / S.wsum;
     }
   }
 }
@@ -594,15 +772,35 @@ extern "C" int dvcp_svd_optimization_backward(const double* x, const double* y_p
 }
 
 extern "C" int dvcp_paper_pose(const double* x, const double* y, const double* w, int B, int n, int reflection_fix,
-                               const double* R_true, const double* t_true, double* R, double* t, double* partial,
-                               void* stream) {
+                               double inlier_ratio, const double* R_true, const double* t_true, double* R, double* t,
+                               double* partial, void* stream) {
   DVCP_REQUIRE(x && y && R && t, "dvcp_paper_pose: null pointer");
   DVCP_REQUIRE(!partial || (R_true && t_true), "dvcp_paper_pose: the loss terms need R_true and t_true");
   DVCP_REQUIRE(B >= 0 && B <= 65535 && n > 0, "dvcp_paper_pose: bad sizes B=%d n=%d", B, n);
+  DVCP_REQUIRE(inlier_ratio > 0 && inlier_ratio <= 1, "dvcp_paper_pose: inlier_ratio %g not in (0, 1]", inlier_ratio);
+  const int m_keep = static_cast<int>(inlier_ratio * n);  // the paper's 80 %: int(0.8 n), like deepVCP_loss.py:76
+  DVCP_REQUIRE(m_keep >= 1 && (m_keep >= n || n <= dvcp::kRgMaxN), "dvcp_paper_pose: rejection needs 1 <= int(ratio n) and n <= %d",
+               dvcp::kRgMaxN);
   if (B == 0) return DVCP_OK;
   hipLaunchKernelGGL(dvcp::paper_pose_kernel, dim3(B), dim3(dvcp::kRgThreads), 0, static_cast<hipStream_t>(stream), x,
-                     y, w, n, reflection_fix, R_true, t_true, R, t, partial);
+                     y, w, n, reflection_fix, m_keep, R_true, t_true, R, t, partial);
   return dvcp::launch_status("dvcp_paper_pose");
+}
+
+extern "C" int dvcp_paper_pose_backward(const double* x, const double* y, const double* w, int B, int n,
+                                        int reflection_fix, double inlier_ratio, const double* R_true,
+                                        const double* t_true, double alpha, const double* grad_loss, double* grad_y,
+                                        double* grad_w, void* stream) {
+  DVCP_REQUIRE(x && y && R_true && t_true && grad_loss && grad_y, "dvcp_paper_pose_backward: null pointer");
+  DVCP_REQUIRE(B >= 0 && B <= 65535 && n > 0, "dvcp_paper_pose_backward: bad sizes B=%d n=%d", B, n);
+  DVCP_REQUIRE(inlier_ratio > 0 && inlier_ratio <= 1, "dvcp_paper_pose_backward: inlier_ratio %g", inlier_ratio);
+  const int m_keep = static_cast<int>(inlier_ratio * n);
+  DVCP_REQUIRE(m_keep >= 1 && (m_keep >= n || n <= dvcp::kRgMaxN), "dvcp_paper_pose_backward: bad rejection size");
+  if (B == 0) return DVCP_OK;
+  const double inv_cnt = 1.0 / (static_cast<double>(B) * 3.0 * n);
+  hipLaunchKernelGGL(dvcp::paper_pose_bwd_kernel, dim3(B), dim3(dvcp::kRgThreads), 0, static_cast<hipStream_t>(stream),
+                     x, y, w, n, reflection_fix, m_keep, R_true, t_true, grad_loss, alpha, inv_cnt, grad_y, grad_w);
+  return dvcp::launch_status("dvcp_paper_pose_backward");
 }
 
 extern "C" int dvcp_deepvcp_loss(const double* x, const double* y_pred, const double* R_true, const double* t_true,

@@ -194,6 +194,11 @@ static int sa_group_mlp_impl(int dtype, const void* xyz, int64_t sb, int64_t sc,
     if (D == 0) DVCP_SA_T(0, 16, 16, 32);
     if (D == 3) DVCP_SA_T(3, 16, 16, 32);
   }
+  // the paper-faithful FE's first table (paper supplement: 32-32 on xyz [+ normals]; dvcp.paper)
+  if (nlayer == 2 && chans[1] == 32 && chans[2] == 32) {
+    if (D == 0) DVCP_SA_T(0, 32, 32, 0);
+    if (D == 3) DVCP_SA_T(3, 32, 32, 0);
+  }
   // two-layer tables: fp32 MFMA when each point's features are a contiguous, 16-B aligned fp32 run
   const bool mfma_ok = !ff64 && fd == 1 && fb % 4 == 0 && fn % 4 == 0 &&
                        (reinterpret_cast<uintptr_t>(feat) & 15) == 0;

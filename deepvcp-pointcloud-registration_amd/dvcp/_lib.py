@@ -50,7 +50,12 @@ SIGNATURES = {
     "dvcp_dfe_tgt_literal": [_I, _P, _L, _L, _L, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P],
     "dvcp_cpg": [_P, _P, _L, _L, _L, _P, _I, _I, _P, _P, _P, _P],
     "dvcp_rigid_transform": [_P, _P, _I, _I, _P, _P, _P],
-    "dvcp_paper_pose": [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P],
+    "dvcp_paper_pose": [_P, _P, _P, _I, _I, _I, _D, _P, _P, _P, _P, _P, _P],
+    "dvcp_paper_pose_backward": [_P, _P, _P, _I, _I, _I, _D, _P, _P, _D, _P, _P, _P, _P],
+    "dvcp_feature_propagation": [_P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _P, _L, _L, _L, _I, _P, _L, _L, _I,
+                                 _I, _P, _P, _P, _P, _P],
+    "dvcp_group_rows": [_P, _L, _L, _L, _I, _P, _L, _L, _L, _P, _L, _L, _I, _P, _P, _I, _I, _D, _I, _P, _P],
+    "dvcp_cpg1d": [_P, _P, _P, _I, _I, _P, _P, _P, _P],
     "dvcp_svd_optimization": [_P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P],
     "dvcp_deepvcp_loss": [_P, _P, _P, _P, _I, _I, _D, _P, _P, _P, _P, _P],
     "dvcp_registration_error": [_P, _P, _P, _L, _P, _L, _I, _P, _P, _P],
@@ -99,6 +104,8 @@ def load():
                                                       ctypes.c_void_p]
     lib.dvcp_dfe_backward_workspace_bytes.restype = ctypes.c_int64
     lib.dvcp_dfe_backward_workspace_bytes.argtypes = [ctypes.c_int64]
+    lib.dvcp_dfe_tgt_backward_workspace_bytes.restype = ctypes.c_int64
+    lib.dvcp_dfe_tgt_backward_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
     lib.dvcp_cpg_backward_workspace_bytes.restype = ctypes.c_int64
     lib.dvcp_cpg_backward_workspace_bytes.argtypes = [ctypes.c_int]
     lib.dvcp_sa_group_mlp_backward_workspace_bytes.restype = ctypes.c_int64
@@ -112,6 +119,8 @@ def load():
     lib.dvcp_sa_bn_rows_floats.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     lib.dvcp_sa_bn_zrows_floats.restype = ctypes.c_int64
     lib.dvcp_sa_bn_zrows_floats.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    lib.dvcp_cpg1d_nparams.restype = ctypes.c_int
+    lib.dvcp_cpg1d_nparams.argtypes = []
     lib.dvcp_sa_bn_pack_floats.restype = ctypes.c_int64
     lib.dvcp_sa_bn_pack_floats.argtypes = [ctypes.c_int, ctypes.c_void_p]
     for name, args in SIGNATURES.items():
@@ -126,9 +135,11 @@ def exported_symbols():
     return ["dvcp_last_error", "dvcp_abi_version", "dvcp_knn_grid_workspace_bytes",
             "dvcp_knn_tiled_workspace_bytes", "dvcp_ball_query_workspace_bytes",
             "dvcp_sa_group_mlp_workspace_bytes", "dvcp_dfe_backward_workspace_bytes",
+            "dvcp_dfe_tgt_backward_workspace_bytes",
             "dvcp_cpg_backward_workspace_bytes", "dvcp_sa_group_mlp_backward_workspace_bytes",
             "dvcp_fe_head_backward_workspace_bytes", "dvcp_sa_bn_workspace_bytes",
-            "dvcp_sa_bn_pack_floats", "dvcp_sa_bn_rows_floats", "dvcp_sa_bn_zrows_floats"] + list(SIGNATURES)
+            "dvcp_sa_bn_pack_floats", "dvcp_sa_bn_rows_floats", "dvcp_sa_bn_zrows_floats",
+            "dvcp_cpg1d_nparams"] + list(SIGNATURES)
 
 
 # When a list, every entry-point call appends (name, start_event, end_event, work) recorded on

@@ -451,17 +451,20 @@ def dfe_backward(X, params, grad_out, want_input_grad=False):
 
 def dfe_tgt_backward(ref_xyz, ref_feat, cand, dist, idx, params, grad_out, ref_pdim=2, want_feat_grad=False):
     """Parameter gradient of ``dfe_tgt`` (get_cat_feat_tgt.py:54-96 + deep_feat_embedding.py:47-60),
-    and (``want_feat_grad``) the gradient of ``ref_feat`` (B, M, 32) through the :85 gather."""
+    and (``want_feat_grad``) the gradient of ``ref_feat`` (B, M, 32) through the :85 gather, summed
+    per target row in a fixed order (bit-identical run to run)."""
     _lib.require_gpu(ref_xyz, ref_feat, cand, dist, idx, params, grad_out)
     B = ref_xyz.shape[0]
     M, rb, rc, rn = _pts(ref_xyz, ref_pdim)
     Q = cand.shape[1]
     feat_c, cand_c, dist_c, idx_c = ref_feat.contiguous(), cand.contiguous(), dist.contiguous(), idx.contiguous()
     g = grad_out.reshape(B, Q, 32).float().contiguous()
-    ws = torch.empty(max(1, int(_lib.load().dvcp_dfe_backward_workspace_bytes(B * Q)) // 4), dtype=torch.float32,
-                     device=ref_xyz.device)
+    nbytes = int(_lib.load().dvcp_dfe_tgt_backward_workspace_bytes(B, Q, M, int(bool(want_feat_grad))))
+    if nbytes < 0:
+        raise RuntimeError("dvcp_dfe_tgt_backward_workspace_bytes: size query failed")
+    ws = torch.empty(max(1, (nbytes + 3) // 4), dtype=torch.float32, device=ref_xyz.device)
     gp = torch.empty(DFE_NPARAMS, dtype=torch.float32, device=ref_xyz.device)
-    gF = torch.zeros(B, M, 32, dtype=torch.float32, device=ref_xyz.device) if want_feat_grad else None
+    gF = torch.empty(B, M, 32, dtype=torch.float32, device=ref_xyz.device) if want_feat_grad else None
     call("dvcp_dfe_tgt_backward", dtype_code(ref_xyz), ptr(ref_xyz), rb, rc, rn, M, ptr(feat_c), ptr(cand_c),
          ptr(dist_c), ptr(idx_c), B, Q, ptr(params), ptr(g), ptr(ws), ptr(gp), ptr(gF), stream(),
          work=(2.0 * 3168 * 32 * B * Q, B * (M * (12 + 128) + Q * (12 + 32 * 8 + 128))))
@@ -667,3 +670,91 @@ def svd_optimization_backward(x, y_pred, R_true, t_true, partial, grad_loss, alp
     call("dvcp_svd_optimization_backward", ptr(x), ptr(y_pred), ptr(R_true), ptr(t_true), B, n,
          ptr(partial.contiguous()), ptr(gl), float(alpha), ptr(g), stream())
     return g
+
+
+# ---- paper-faithful mode (dvcp/paper.py) -----------------------------------
+
+def feature_propagation(xyz1, xyz2, p2_rows, p1, chans, relu, params):
+    """pointnet2_utils.py:265-315 (PointNetFeaturePropagation) + an optional last linear layer:
+    xyz1 (B, 3, N1), xyz2 (B, 3, N2) (any strides), p2_rows (B, N2, D2) fp32 with contiguous rows,
+    p1 None or a (B, D1, N1) fp32 strided view -> (B, N1, chans[-1]) fp32."""
+    _lib.require_gpu(xyz1, xyz2, p2_rows, params)
+    B = xyz1.shape[0]
+    N1, x1b, x1c, x1n = _pts(xyz1, 2)
+    N2, x2b, x2c, x2n = _pts(xyz2, 2)
+    if p2_rows.dtype != torch.float32 or p2_rows.stride(2) != 1:
+        raise ValueError("feature_propagation: p2 rows must be fp32 with contiguous channels")
+    D2 = p2_rows.shape[2]
+    if p1 is not None:
+        if p1.dtype != torch.float32:
+            p1 = p1.float()
+        D1, (p1b, p1d, p1n) = p1.shape[1], p1.stride()
+    else:
+        D1, p1b, p1d, p1n = 0, 0, 0, 0
+    ch = torch.tensor(list(chans), dtype=torch.int32)
+    rl = torch.tensor([int(bool(r)) for r in relu], dtype=torch.int32)
+    out = torch.empty(B, N1, chans[-1], dtype=torch.float32, device=xyz1.device)
+    macs = sum(a * b for a, b in zip(chans[:-1], chans[1:]))
+    call("dvcp_feature_propagation", ptr(xyz1), x1b, x1c, x1n, N1, ptr(xyz2), x2b, x2c, x2n, N2, B, ptr(p1), p1b,
+         p1d, p1n, D1, ptr(p2_rows), p2_rows.stride(0), p2_rows.stride(1), D2, len(chans) - 1, ptr(ch), ptr(rl),
+         ptr(params), ptr(out), stream(),
+         work=(B * N1 * (9.0 * N2 + 2.0 * macs), 4.0 * B * (3 * (N1 + N2) + N2 * D2 + N1 * (D1 + chans[-1]))))
+    return out
+
+
+def group_rows(ctr, xyz, feat, count, lst, nsample, radius, ctr_pdim=1, xyz_pdim=2):
+    """Paper Sec. 3.3 DFE input: (B, Q, nsample, 3 + D) rows [(p - c) / radius, feat(p)] over the
+    ball-query lists (first-hit padding; zero rows where a centre has no point in range)."""
+    _lib.require_gpu(ctr, xyz, count, lst)
+    B = ctr.shape[0]
+    Q, cb, cc, cn = _pts(ctr, ctr_pdim)
+    _, sb, sc, sn = _pts(xyz, xyz_pdim)
+    D = 0 if feat is None else feat.shape[2]
+    if feat is not None and (feat.dtype != torch.float32 or feat.stride(2) != 1):
+        raise ValueError("group_rows: features must be (B, N, D) fp32 with contiguous rows")
+    rows = torch.empty(B, Q, nsample, 3 + D, dtype=torch.float32, device=ctr.device)
+    call("dvcp_group_rows", ptr(ctr), cb, cc, cn, Q, ptr(xyz), sb, sc, sn, ptr(feat),
+         0 if feat is None else feat.stride(0), 0 if feat is None else feat.stride(1), D, ptr(count), ptr(lst),
+         lst.shape[2], int(nsample), float(radius), B, ptr(rows), stream())
+    return rows
+
+
+def cpg1d(src, tgt, cand, params, want_weight=False):
+    """Paper Sec. 3.6's 1-D CPG: src (B, K, 32), tgt (B, K, Gz, 32), cand (B, K, Gz, 3) -> vcp (B, K, 3)
+    [, weights (B, K, Gz)]."""
+    _lib.require_gpu(src, tgt, cand, params)
+    B, K, Gz, _ = cand.shape
+    s, t, c = src.reshape(B * K, 32).float().contiguous(), tgt.float().contiguous(), cand.float().contiguous()
+    vcp = torch.empty(B, K, 3, dtype=torch.float32, device=cand.device)
+    w = torch.empty(B, K, Gz, dtype=torch.float32, device=cand.device) if want_weight else None
+    call("dvcp_cpg1d", ptr(s), ptr(t), ptr(c), B * K, Gz, ptr(params), ptr(vcp), ptr(w), stream(),
+         work=(2.0 * 3 * (32 * 16 + 16 * 4 + 4) * B * K * Gz, 4.0 * B * K * (32 + Gz * 35 + 3)))
+    return (vcp, w) if want_weight else vcp
+
+
+def paper_pose(x, y, w, reflection_fix=True, inlier_ratio=1.0, R_true=None, t_true=None):
+    """Weighted Kabsch with reflection fix and the paper's outlier rejection on (B, 3, n) fp64
+    operands (w (B, n) or None) -> R (B, 3, 3), t (B, 3, 1)[, partial (B, 2) with R_true, t_true]."""
+    _lib.require_gpu(x, y, w)
+    x, y = x.double().contiguous(), y.double().contiguous()
+    B, _, n = x.shape
+    wc = None if w is None else w.double().reshape(B, n).contiguous()
+    R = torch.empty(B, 3, 3, dtype=torch.float64, device=x.device)
+    t = torch.empty(B, 3, 1, dtype=torch.float64, device=x.device)
+    partial = torch.empty(B, 2, dtype=torch.float64, device=x.device) if R_true is not None else None
+    call("dvcp_paper_pose", ptr(x), ptr(y), ptr(wc), B, n, int(bool(reflection_fix)), float(inlier_ratio),
+         ptr(R_true), ptr(t_true), ptr(R), ptr(t), ptr(partial), stream())
+    return (R, t) if partial is None else (R, t, partial)
+
+
+def paper_pose_backward(x, y, w, R_true, t_true, alpha, grad_loss, reflection_fix=True, inlier_ratio=1.0,
+                        want_w=True):
+    """d loss / d y (B, 3, n) and d loss / d w (B, n) of the paper loss (dvcp_paper_pose_backward)."""
+    _lib.require_gpu(x, y, R_true, t_true, grad_loss)
+    B, _, n = x.shape
+    gy = torch.empty(B, 3, n, dtype=torch.float64, device=x.device)
+    gw = torch.empty(B, n, dtype=torch.float64, device=x.device) if (want_w and w is not None) else None
+    gl = grad_loss.double().reshape(1).contiguous()   # alive across the launch
+    call("dvcp_paper_pose_backward", ptr(x), ptr(y), ptr(w), B, n, int(bool(reflection_fix)), float(inlier_ratio),
+         ptr(R_true), ptr(t_true), float(alpha), ptr(gl), ptr(gy), ptr(gw), stream())
+    return gy, gw

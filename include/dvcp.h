@@ -331,12 +331,57 @@ int dvcp_fe_head_backward(const float* x, int P, const float* params, const floa
  * parity -- the reference's get_rigid_transform, deepVCP_loss.py:13-44, is unweighted with no
  * reflection fix): weighted Kabsch with per-point weights w (B x n fp64, NULL = uniform),
  * centroids sum(w x) / sum(w), and with reflection_fix the det-sign correction
- * R = V diag(1,1,sign det(V U^T)) U^T.  x, y: B x 3 x n fp64 -> R (B x 3 x 3), t (B x 3 x 1).
- * partial (optional, B x 2 fp64, needs R_true (B x 3 x 3) and t_true (B x 3 x 1)): per pair
- * sum |R_true x + t_true - y| and sum |R_true x + t_true - (R x + t)| (the paper's two L1 terms). */
+ * R = V diag(1,1,sign det(V U^T)) U^T.  inlier_ratio in (0, 1]: below 1, the paper's outlier
+ * rejection -- the int(inlier_ratio n) pairs with the smallest |R x + t - y| under the first
+ * solve (ties: the lower index) are solved again (n <= 1024).  x, y: B x 3 x n fp64 ->
+ * R (B x 3 x 3), t (B x 3 x 1).  partial (optional, B x 2 fp64, needs R_true (B x 3 x 3) and
+ * t_true (B x 3 x 1)): per pair sum |R_true x + t_true - y| and sum |R_true x + t_true - (R x + t)|
+ * (the paper's two L1 terms, on every key point). */
 int dvcp_paper_pose(const double* x, const double* y, const double* w, int B, int n, int reflection_fix,
-                    const double* R_true, const double* t_true, double* R, double* t, double* partial,
-                    void* stream);
+                    double inlier_ratio, const double* R_true, const double* t_true, double* R, double* t,
+                    double* partial, void* stream);
+/* Backward of the paper loss alpha * S1 / (3 B n) + (1 - alpha) * S2 / (3 B n) (S1, S2 the sums
+ * of dvcp_paper_pose's partial) in y and w: grad_loss (1 fp64, device) -> grad_y (B x 3 x n),
+ * grad_w (B x n, optional).  The rejection's selection carries no gradient (piecewise constant);
+ * the second solve does (weighted Procrustes derivative, reflection fix included). */
+int dvcp_paper_pose_backward(const double* x, const double* y, const double* w, int B, int n,
+                             int reflection_fix, double inlier_ratio, const double* R_true,
+                             const double* t_true, double alpha, const double* grad_loss, double* grad_y,
+                             double* grad_w, void* stream);
+
+/* Paper-faithful mode, PointNet++ feature propagation (paper Sec. 3.1 + supplement; the
+ * reference's own PointNetFeaturePropagation, pointnet2_utils.py:265-315, which it never calls):
+ * for every xyz1 point (B x N1, strided) the 3 nearest xyz2 points (B x N2, strided) under the
+ * expansion-form squared distance (:296; ties to the lower index), weights 1/(d + 1e-8)
+ * normalised (:300-302), the interpolated p2 rows (B x N2 x D2 point-major, strides p2b, p2n)
+ * appended to the p1 rows (B x D1 x N1 strided, optional) (:305-307); then nlayer layers
+ * chans[0] = D1 + D2 -> ... -> chans[nlayer] (<= 64), each y = (W x + b) * scale + shift
+ * (packed W | b | scale | shift per layer: eval BN folded) with ReLU where relu[l] != 0 (:312-314;
+ * a last layer with relu 0, scale 1, shift 0 is a plain fully connected layer).
+ * out: B x N1 x chans[nlayer] fp32. */
+int dvcp_feature_propagation(const float* xyz1, int64_t x1b, int64_t x1c, int64_t x1n, int N1,
+                             const float* xyz2, int64_t x2b, int64_t x2c, int64_t x2n, int N2, int B,
+                             const float* p1, int64_t p1b, int64_t p1d, int64_t p1n, int D1,
+                             const float* p2, int64_t p2b, int64_t p2n, int D2, int nlayer,
+                             const int* chans, const int* relu, const float* params, float* out,
+                             void* stream);
+/* Paper-faithful mode, the DFE input of paper Sec. 3.3: rows [(p - c) / radius, feat(p)] for
+ * every centre (B x Q, strided) over its ball-query list (count B x Q, list B x Q x ns_list from
+ * dvcp_ball_query), padded with the first hit (pointnet2_utils.py:104-106) up to ns_out; a centre
+ * with no point within radius gets zero rows.  xyz: B x N strided, feat: B x N x D point-major.
+ * rows: B x Q x ns_out x (3 + D) fp32. */
+int dvcp_group_rows(const float* ctr, int64_t cb, int64_t cc, int64_t cn, int Q, const float* xyz,
+                    int64_t sb, int64_t sc, int64_t sn, const float* feat, int64_t fb, int64_t fn, int D,
+                    const int32_t* count, const int32_t* list, int ns_list, int ns_out, double radius, int B,
+                    float* rows, void* stream);
+/* Paper-faithful mode, the duplicated network's CPG (paper Sec. 3.6): per key point the cost
+ * (src - tgt)^2 over its Gz (<= 64) candidates on a z line, Conv1d 32-16-4-1 (k 3, p 1, no
+ * activations), softmax over the line, vcp = sum(w cand) / sum(w).  src: P x 32, tgt: P x Gz x 32,
+ * cand: P x Gz x 3 fp32; params: conv1.W | b | conv2.W | b | conv3.W | b (dvcp_cpg1d_nparams()
+ * floats, torch Conv1d layout); vcp: P x 3, weight (optional): P x Gz. */
+int dvcp_cpg1d(const float* src, const float* tgt, const float* cand, int P, int Gz, const float* params,
+               float* vcp, float* weight, void* stream);
+int dvcp_cpg1d_nparams(void);
 
 /* Corresponding point generation.  Replaces cpg.py:27-60: cost volume
  * (src - scrambled tgt)^2 (Q11), Conv3d 32-16-4-1 (k3, p1, no activations), softmax over C,
@@ -412,9 +457,12 @@ int dvcp_dfe_backward(int x_dtype, const void* X, int64_t R, const float* params
 
 /* Target-side backward.  Replaces autograd through get_cat_feat_tgt.py:54-96 +
  * deep_feat_embedding.py:47-60; same arguments as dvcp_dfe_tgt plus grad_out (B x Q x 32 fp32),
- * ws (dvcp_dfe_backward_workspace_bytes(B*Q)) and grad_params (3264 fp32).  grad_ref_feat
- * (optional, B x M x 32 fp32, accumulated: zero it first) receives the gradient of the gathered
- * target features (the get_cat_feat_tgt.py:85 gather, weighted as :95). */
+ * ws (dvcp_dfe_tgt_backward_workspace_bytes(B, Q, M, grad_ref_feat != NULL); -1: the size query
+ * failed) and grad_params (3264 fp32).  grad_ref_feat (optional, B x M x 32 fp32, overwritten)
+ * receives the gradient of the gathered target features (the get_cat_feat_tgt.py:85 gather,
+ * weighted as :95), summed per target row in a fixed order (a stable radix sort of the routed
+ * entries by target row): bit-identical run to run.  Needs B*Q*32 < 2^31 and B*M < 2^31. */
+int64_t dvcp_dfe_tgt_backward_workspace_bytes(int B, int Q, int M, int want_feat_grad);
 int dvcp_dfe_tgt_backward(int dtype, const void* ref_xyz, int64_t rb, int64_t rc, int64_t rn, int M,
                           const float* ref_feat, const float* cand, const float* dist, const int32_t* idx,
                           int B, int Q, const float* params, const float* grad_out, float* ws,

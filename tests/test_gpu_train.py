@@ -586,6 +586,37 @@ def test_dfe_tgt_feature_grad_vs_oracle(cuda):
     _close(fg.grad, fo.grad, 1e-5, "d target features")
 
 
+def test_dfe_tgt_feature_grad_bit_identical(cuda):
+    """The target-feature gradient is summed per target row in a fixed order (segsum.hip: stable
+    radix sort of the routed entries, one wave per row): two runs give the same bits, on a case
+    where every target point collects hundreds of entries (11^3 candidate grids around 8 key
+    points over 2000 targets); rows no entry reaches are exactly zero (values: the oracle test
+    above)."""
+    from dvcp import ops
+    import dvcp
+    torch.manual_seed(12)
+    B, M, K, G = 2, 2000, 8, 11
+    xyz = (torch.rand(B, 3, M) * 2 - 1).to(cuda)
+    feat = torch.rand(B, M, 32).to(cuda)
+    ax = (torch.arange(G, dtype=torch.float64) - (G - 1) / 2) * 0.08
+    grid = torch.stack(torch.meshgrid(ax, ax, ax, indexing="ij"), -1).reshape(-1, 3)
+    kp = torch.rand(B, K, 3, dtype=torch.float64) * 1.2 - 0.6
+    qry = (kp[:, :, None, :] + grid).float().reshape(B, K * G ** 3, 3).to(cuda)
+    dist, idx, _ = ops.knn(xyz, qry, 32, ref_pdim=2, qry_pdim=1, want_idx64=False)
+    mine = dvcp.feat_embedding_layer().to(cuda)
+    g = torch.randn(B, qry.shape[1], 32, device=cuda)
+    params = mine.packed_params()
+    runs = [ops.dfe_tgt_backward(xyz, feat, qry, dist, idx, params, g, want_feat_grad=True) for _ in range(3)]
+    for gp, gF in runs[1:]:
+        assert torch.equal(gF, runs[0][1])
+        assert torch.equal(gp, runs[0][0])
+    gF = runs[0][1]
+    hit = torch.zeros(B, M, dtype=torch.bool, device=cuda)
+    hit.scatter_(1, idx.reshape(B, -1).long(), True)
+    assert (~hit).any() and bool((gF[~hit] == 0).all())
+    assert int(torch.bincount(idx[0].reshape(-1).long(), minlength=M).max()) > 200
+
+
 def test_src_keypoints_feature_grad_vs_oracle(cuda):
     """The key-point stage's gather (pointnet2_utils.py:59) + weighting (get_cat_feat_src.py:50)
     backward: dL/d(source FE features)."""

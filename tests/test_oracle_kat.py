@@ -224,3 +224,68 @@ def test_paper_pose_checker_kats():
     R0, _ = OP.weighted_rigid_transform(x, M @ x, None, reflection_fix=False)
     R1, _ = OP.weighted_rigid_transform(x, M @ x, None, reflection_fix=True)
     assert np.isclose(np.linalg.det(R0), -1.0) and np.isclose(np.linalg.det(R1), 1.0)
+
+
+def test_paper_rejection_and_fp_kats():
+    """oracle/paper.py, the rest of the paper mode's checker:
+    * the rejection step (Sec. 3.5): 20 % planted outliers are exactly the rejected pairs and the
+      second solve recovers the exact rotation (the first, contaminated one does not);
+    * feature propagation (pointnet2_utils.py:265-315): a constant field interpolates to itself,
+      a point coinciding with an xyz2 point takes (to 1e-6) that point's value (weight 1/1e-8);
+    * group_rows: a centre with no neighbour in range gives zero rows, fewer neighbours than
+      nsample are padded with the first hit;
+    * the 1-D CPG with zero conv weights scores every candidate alike: vcp = the line's mean."""
+    import numpy as np
+    from oracle import paper as OP
+    rng = np.random.default_rng(11)
+    n = 50
+    x = rng.standard_normal((3, n))
+    th = 1.1
+    Rz = np.array([[np.cos(th), -np.sin(th), 0], [np.sin(th), np.cos(th), 0], [0, 0, 1.0]])
+    t = np.array([0.5, 0.2, -0.7])
+    y = Rz @ x + t[:, None]
+    bad = rng.choice(n, 10, replace=False)
+    y[:, bad] += rng.standard_normal((3, 10)) * 3.0
+    w = rng.random(n) + 0.1
+    R1, _ = OP.weighted_rigid_transform(x, y, w)
+    R, tt, keep = OP.paper_pose(x, y, w, inlier_ratio=0.8)
+    assert not np.allclose(R1, Rz, atol=1e-3)
+    assert sorted(set(range(n)) - set(keep.tolist())) == sorted(bad.tolist())
+    assert np.allclose(R, Rz, atol=1e-12) and np.allclose(tt, t, atol=1e-12)
+
+    torch.manual_seed(0)
+    fp = OP.PointNetFeaturePropagation(in_channel=4, mlp=[4]).eval()
+    with torch.no_grad():
+        fp.mlp_convs[0].weight.copy_(torch.eye(4)[:, :, None])
+        fp.mlp_convs[0].bias.zero_()
+    xyz1 = torch.rand(1, 3, 20)
+    xyz2 = torch.rand(1, 3, 7)
+    xyz2[0, :, 3] = xyz1[0, :, 5]
+    p2 = torch.arange(28, dtype=torch.float32).view(1, 4, 7) * 0.1
+    const = torch.full((1, 4, 7), 2.5)
+    with torch.no_grad():
+        out_c = fp(xyz1, xyz2, None, const)
+        out = fp(xyz1, xyz2, None, p2)
+    bn_scale = 1.0 / math.sqrt(1.0 + 1e-5)                # eval BatchNorm1d at its init
+    assert torch.allclose(out_c, torch.full_like(out_c, 2.5 * bn_scale), rtol=1e-6)
+    assert torch.allclose(out[0, :, 5], p2[0, :, 3] * bn_scale, rtol=1e-6, atol=1e-6)
+
+    xyz = torch.tensor([[[0.0, 0.0, 0.0], [0.1, 0.0, 0.0], [5.0, 5.0, 5.0]]])
+    feats = torch.tensor([[[1.0], [2.0], [3.0]]])
+    ctr = torch.tensor([[[0.0, 0.0, 0.0], [20.0, 20.0, 20.0]]])
+    rows = OP.group_rows(ctr, xyz, feats, 0.5, 4)
+    assert rows.shape == (1, 2, 4, 4)
+    assert torch.equal(rows[0, 1], torch.zeros(4, 4))
+    assert torch.equal(rows[0, 0, :, 3], torch.tensor([1.0, 2.0, 1.0, 1.0]))
+    assert torch.allclose(rows[0, 0, 1, :3], torch.tensor([0.2, 0.0, 0.0]))
+
+    c1 = OP.CPG1D()
+    with torch.no_grad():
+        for c in (c1.conv1, c1.conv2, c1.conv3):
+            c.weight.zero_()
+            c.bias.zero_()
+        cand = torch.zeros(1, 2, 9, 3)
+        cand[..., 2] = torch.arange(9, dtype=torch.float32) * 0.25 - 1.0
+        cand[:, 1, :, 0] = 3.0
+        vcp = c1(torch.rand(1, 2, 32), torch.rand(1, 2, 9, 32), cand)
+    assert torch.allclose(vcp, cand.mean(2), atol=1e-6)
