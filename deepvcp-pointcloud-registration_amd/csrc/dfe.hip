@@ -27,7 +27,7 @@ int launch_dfe_tgt_mfma(PointsView<T> ref, const float* feat, int M, const float
 
 // segsum.hip: deterministic per-row sums of keyed 32-float contribution rows.
 int64_t segment_sum_workspace_bytes(int64_t E, int64_t nrows);
-int segment_sum(const uint32_t* keys, const float* contrib, int64_t E, int64_t nrows, float* out, void* ws,
+int segment_sum(const uint32_t* keys, const float* contrib, int64_t E, int64_t nrows, int ncol, float* out, void* ws,
                 hipStream_t st);
 
 constexpr int kDfeRowsPerQ = 32;
@@ -493,7 +493,7 @@ static int dfe_backward_launch(int mode, int dtype, const void* X, const void* r
   if (gF_out) {
     const int rc2 = dvcp::launch_status("dvcp_dfe_tgt_backward");
     if (rc2 != DVCP_OK) return rc2;
-    return dvcp::segment_sum(gkey, gF, R * 32, static_cast<int64_t>(R / Q) * M, gF_out, wsb + tgt_segsum_offset(R),
+    return dvcp::segment_sum(gkey, gF, R * 32, static_cast<int64_t>(R / Q) * M, 32, gF_out, wsb + tgt_segsum_offset(R),
                              st);
   }
   return dvcp::launch_status("dvcp_dfe_backward");

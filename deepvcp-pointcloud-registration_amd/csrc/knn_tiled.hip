@@ -119,6 +119,21 @@ __device__ __forceinline__ float wave_max_nonneg(float x) {
   return __uint_as_float(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63)));
 }
 
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_or_u(uint32_t v) {
+  return v | static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, ROWS, 0xF, false));
+}
+// bitwise or over the wave (wave-uniform result)
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+  v = dpp_or_u<0x111, 0xF>(v);
+  v = dpp_or_u<0x112, 0xF>(v);
+  v = dpp_or_u<0x114, 0xF>(v);
+  v = dpp_or_u<0x118, 0xF>(v);
+  v = dpp_or_u<0x142, 0xA>(v);
+  v = dpp_or_u<0x143, 0xC>(v);
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+}
+
 // max over the wave of any floats (order-preserving bits)
 __device__ __forceinline__ float wave_max_nonneg_signed(float x) {
   uint32_t v = float_order(x);
@@ -535,29 +550,30 @@ __global__ __launch_bounds__(kTiledThreads) void knn_sel_query_kernel(const floa
 #pragma unroll
       for (int u = 0; u < 4 * kTile; ++u) c[u] = tp[u];
       float d2v[kTile];
-      uint32_t piv[kTile];
       uint32_t cm = 0;
+      // Filter on the distance alone, d2 <= kf: a superset of the keys below the k-th key (a tie
+      // with a higher index is appended too and dropped by the merge, which orders full keys);
+      // kf is finite, so inf and NaN (padding) never pass, as in dvcp_knn.
+      const float kf = fminf(kth, __builtin_bit_cast(float, 0x7F7FFFFFu));
 #pragma unroll
       for (int j = 0; j < kTile; ++j) {
         const float dx = c[4 * j] - qx, dy = c[4 * j + 1] - qy, dz = c[4 * j + 2] - qz;
         d2v[j] = (dx * dx + dy * dy) + dz * dz;
-        piv[j] = __float_as_uint(c[4 * j + 3]);
-        const uint64_t pk = (static_cast<uint64_t>(__float_as_uint(d2v[j])) << 32) | piv[j];
-        // d2 < inf also rejects NaN (padding) and infinite distances, as dvcp_knn does
-        cm |= (act & (d2v[j] < __builtin_huge_valf()) & (pk < kkey)) ? (1u << j) : 0u;
+        cm |= (act && d2v[j] <= kf) ? (1u << j) : 0u;
       }
       if (wave_umax_i(static_cast<uint32_t>(fill + __popc(cm))) > static_cast<uint32_t>(kSelBufN)) {
         merge();  // room for the whole tile; then re-filter against the new k-th key
+        const float kf2 = fminf(kth, __builtin_bit_cast(float, 0x7F7FFFFFu));
 #pragma unroll
-        for (int j = 0; j < kTile; ++j) {
-          const uint64_t pk = (static_cast<uint64_t>(__float_as_uint(d2v[j])) << 32) | piv[j];
-          cm &= (pk < kkey) ? ~0u : ~(1u << j);
-        }
+        for (int j = 0; j < kTile; ++j) cm &= d2v[j] <= kf2 ? ~0u : ~(1u << j);
       }
-#pragma unroll
-      for (int j = 0; j < kTile; ++j) {
+      // appends: only the points some lane takes (wave-uniform loop over the union of the masks)
+      uint32_t u = wave_or_u32(cm);
+      while (u != 0) {
+        const int j = __builtin_ctz(u);
+        u &= u - 1;
         if ((cm >> j) & 1u) {
-          mybuf[fill][lane] = make_uint2(__float_as_uint(d2v[j]), piv[j]);
+          mybuf[fill][lane] = make_uint2(__float_as_uint(d2v[j]), __float_as_uint(tp[4 * j + 3]));
           ++fill;
         }
       }

@@ -60,28 +60,46 @@ struct BnTable {
   static constexpr int O3 = O2 + bn_layer_size(C1, C2);
 };
 
-// lane = slot: h = relu((W x + b) * scale + shift), weights as wave-uniform scalar loads
-template <int CIN, int COUT>
-__device__ __forceinline__ void bn_rows(const float (&x)[CIN], float (&h)[COUT], const float* __restrict__ p) {
+// An opaque zero ordered after a value of the previous output channel's arithmetic: added to a
+// weight-row offset, it keeps one row's scalar loads from being scheduled (or hoisted out of the
+// centre loop) ahead of the previous row's use -- a layer's up-to-64 x 67 weights held at once
+// spilled to VGPR lanes.  (The pointer keeps the kernel argument's provenance: loads stay scalar.)
+__device__ __forceinline__ int bn_zero_after(float dep) {
+  int z = 0;
+  asm volatile("" : "+s"(z) : "v"(dep));
+  return z;
+}
+
+// acc = W x (fp32, input channels in ascending order per output), one weight row at a time;
+// epi(co, acc, q) finishes output co with q = p offset by the same opaque zero (its per-channel
+// vector loads ordered likewise).
+template <int CIN, int COUT, typename Epi>
+__device__ __forceinline__ void bn_matvec(const float (&x)[CIN], const float* __restrict__ p, Epi epi) {
+  float prev = 0.0f;
 #pragma unroll
   for (int co = 0; co < COUT; ++co) {
-    float acc = 0.0f;
+    const float* q = p + bn_zero_after(prev);
+    const float* w = q + co * CIN;
+    float a = 0.0f;
 #pragma unroll
-    for (int ci = 0; ci < CIN; ++ci) acc = __fmaf_rn(p[co * CIN + ci], x[ci], acc);
-    const float v = (acc + p[CIN * COUT + co]) * p[CIN * COUT + COUT + co] + p[CIN * COUT + 2 * COUT + co];
-    h[co] = v > 0.0f ? v : 0.0f;
+    for (int ci = 0; ci < CIN; ++ci) a = __fmaf_rn(w[ci], x[ci], a);
+    epi(co, a, q);
+    prev = a;
   }
+}
+
+// lane = slot: h = relu((W x + b) * scale + shift)
+template <int CIN, int COUT>
+__device__ __forceinline__ void bn_rows(const float (&x)[CIN], float (&h)[COUT], const float* __restrict__ p) {
+  bn_matvec<CIN, COUT>(x, p, [&](int co, float acc, const float* q) {
+    const float v = (acc + q[CIN * COUT + co]) * q[CIN * COUT + COUT + co] + q[CIN * COUT + 2 * COUT + co];
+    h[co] = v > 0.0f ? v : 0.0f;
+  });
 }
 // lane = slot: z = W x + b (the layer whose statistics are being taken)
 template <int CIN, int COUT>
 __device__ __forceinline__ void bn_rows_raw(const float (&x)[CIN], float (&z)[COUT], const float* __restrict__ p) {
-#pragma unroll
-  for (int co = 0; co < COUT; ++co) {
-    float acc = 0.0f;
-#pragma unroll
-    for (int ci = 0; ci < CIN; ++ci) acc = __fmaf_rn(p[co * CIN + ci], x[ci], acc);
-    z[co] = acc + p[CIN * COUT + co];
-  }
+  bn_matvec<CIN, COUT>(x, p, [&](int co, float acc, const float* q) { z[co] = acc + q[CIN * COUT + co]; });
 }
 
 template <typename T, typename FT, int D>
@@ -202,16 +220,12 @@ __device__ __forceinline__ float* bn_at_rows(float* base, int C, int64_t e) {
 template <int CIN, int COUT>
 __device__ __forceinline__ void bn_layer_store(const float (&x)[CIN], float (&h)[COUT], const float* __restrict__ p,
                                                float* __restrict__ zr, int64_t M, int64_t e) {
-#pragma unroll
-  for (int co = 0; co < COUT; ++co) {
-    float acc = 0.0f;
-#pragma unroll
-    for (int ci = 0; ci < CIN; ++ci) acc = __fmaf_rn(p[co * CIN + ci], x[ci], acc);
-    const float z = acc + p[CIN * COUT + co];
+  bn_matvec<CIN, COUT>(x, p, [&](int co, float acc, const float* q) {
+    const float z = acc + q[CIN * COUT + co];
     bn_at(zr, COUT, e)[co * 64] = z;
-    const float y = z * p[CIN * COUT + COUT + co] + p[CIN * COUT + 2 * COUT + co];
+    const float y = z * q[CIN * COUT + COUT + co] + q[CIN * COUT + 2 * COUT + co];
     h[co] = y > 0.0f ? y : 0.0f;
-  }
+  });
 }
 
 // ---- forward rows -------------------------------------------------------------------------------
@@ -294,12 +308,12 @@ struct BnVec {  // one layer's per-channel vectors (wave-uniform)
 // (mode 0) and propagated: gprev = W^T gz.
 template <int CIN, int COUT, bool FINAL>
 __device__ __forceinline__ void bn_bwd_top(const float* __restrict__ zr, int64_t M, int64_t e, bool act,
-                                           const float* __restrict__ p, const int* sarg, const float* srg, int r,
+                                           const float* __restrict__ p, const float* sv, const int* sarg, const float* srg, int r,
                                            bool routable, float (&gprev)[CIN], float* __restrict__ gzr) {
-  const BnVec<COUT> q{p + COUT * CIN};
+  const BnVec<COUT> q{sv};
 #pragma unroll
   for (int k = 0; k < CIN; ++k) gprev[k] = 0.0f;
-#pragma unroll
+#pragma unroll 1
   for (int c = 0; c < COUT; ++c) {
     const float z = act ? bn_at(zr, COUT, e)[c * 64] : 0.0f;
     const float gy = (routable && sarg[c] == r && q.y(c, z) > 0.0f) ? srg[c] : 0.0f;
@@ -315,12 +329,12 @@ __device__ __forceinline__ void bn_bwd_top(const float* __restrict__ zr, int64_t
 // A lower layer: g = dL/dh on entry, gy = [y > 0] g, gz written (mode 0), gprev = W^T gz.
 template <int CIN, int COUT, bool FINAL>
 __device__ __forceinline__ void bn_bwd_mid(const float* __restrict__ zr, int64_t M, int64_t e, bool act,
-                                           const float* __restrict__ p, const float (&g)[COUT], float (&gprev)[CIN],
+                                           const float* __restrict__ p, const float* sv, const float (&g)[COUT], float (&gprev)[CIN],
                                            float* __restrict__ gzr) {
-  const BnVec<COUT> q{p + COUT * CIN};
+  const BnVec<COUT> q{sv};
 #pragma unroll
   for (int k = 0; k < CIN; ++k) gprev[k] = 0.0f;
-#pragma unroll
+#pragma unroll 1
   for (int c = 0; c < COUT; ++c) {
     const float z = act ? bn_at(zr, COUT, e)[c * 64] : 0.0f;
     const float gz = q.gz(c, z, q.y(c, z) > 0.0f ? g[c] : 0.0f);
@@ -334,9 +348,9 @@ __device__ __forceinline__ void bn_bwd_mid(const float* __restrict__ zr, int64_t
 
 // Mode 0: the input rows of layer l+1, h_l = relu(y_l), and a ones row.
 template <int CIN, int COUT>
-__device__ __forceinline__ void bn_put_h(const float* __restrict__ zr, int64_t M, int64_t e, const float* __restrict__ p,
+__device__ __forceinline__ void bn_put_h(const float* __restrict__ zr, int64_t M, int64_t e, const float* sv,
                                          float* __restrict__ har) {
-  const BnVec<COUT> q{p + COUT * CIN};
+  const BnVec<COUT> q{sv};
 #pragma unroll
   for (int c = 0; c < COUT; ++c) {
     const float y = q.y(c, bn_at(zr, COUT, e)[c * 64]);
@@ -349,10 +363,10 @@ __device__ __forceinline__ void bn_put_h(const float* __restrict__ zr, int64_t M
 // the wave's LDS tile (two phases, z re-read); lanes = (channel lane % COUT, slot group lane / COUT).
 template <int CIN, int COUT, int TW>
 __device__ __forceinline__ void bn_bwd_sums(const float* __restrict__ zr, int64_t M, int64_t e, bool act,
-                                            const float* __restrict__ p, const float (&g)[COUT], float (*tl)[TW + 1],
+                                            const float* sv, const float (&g)[COUT], float (*tl)[TW + 1],
                                             int lane, int rn, double& s1, double& s2) {
   constexpr int G = kWave / COUT;
-  const BnVec<COUT> q{p + COUT * CIN};
+  const BnVec<COUT> q{sv};
   const int c = lane % COUT, grp = lane / COUT;
 #pragma unroll
   for (int k = 0; k < COUT; ++k) {
@@ -375,8 +389,8 @@ __device__ __forceinline__ void bn_bwd_sums(const float* __restrict__ zr, int64_
 // Layer 1 in mode 0: gz_1 written (g becomes gz_1).
 template <int CIN, int COUT>
 __device__ __forceinline__ void bn_bwd_first(const float* __restrict__ zr, int64_t e, bool act,
-                                             const float* __restrict__ p, float (&g)[COUT], float* __restrict__ gzr) {
-  const BnVec<COUT> q{p + COUT * CIN};
+                                             const float* sv, float (&g)[COUT], float* __restrict__ gzr) {
+  const BnVec<COUT> q{sv};
 #pragma unroll
   for (int c = 0; c < COUT; ++c) {
     const float z = act ? bn_at(zr, COUT, e)[c * 64] : 0.0f;
@@ -408,13 +422,41 @@ __device__ __forceinline__ void bn_scatter_feat(const float (&g)[C1], float (*tl
   wave_sync_lds();
 }
 
+// D = 32 / 64 (C1 = D): the entry's dL/dz_1 row, row-major (C1 floats), for the feature gradient
+//   dL/df_n = W_1f^T sum_{e: n(e) = n} gz_1[e]
+// -- segment_sum adds each point's rows in entry order (deterministic, no float atomics), then
+// bn_feat_grad_kernel applies W_1f^T once per point instead of once per grouped entry.
+template <int C>
+__device__ __forceinline__ void bn_put_rowmajor(float* __restrict__ o, const float (&g)[C]) {
+#pragma unroll
+  for (int k = 0; k < C; k += 4) *reinterpret_cast<float4*>(o + k) = make_float4(g[k], g[k + 1], g[k + 2], g[k + 3]);
+}
+
+// gfeat[b][n][d] = sum_c G[b * N + n][c] W_1[c][3 + d] (fp32, c ascending): one thread per (point, d).
+template <int D, int C0, int C1>
+__global__ __launch_bounds__(256) void bn_feat_grad_kernel(const float* __restrict__ G, const float* __restrict__ p1,
+                                                           int64_t rows, float* __restrict__ gfeat) {
+  __shared__ float w[C1][D];
+  for (int i = threadIdx.x; i < C1 * D; i += 256) w[i / D][i % D] = p1[(i / D) * C0 + 3 + i % D];
+  __syncthreads();
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (t >= rows * D) return;
+  const int64_t r = t / D;
+  const int d = static_cast<int>(t % D);
+  const float* g = G + r * C1;
+  float acc = 0.0f;
+#pragma unroll 8
+  for (int c = 0; c < C1; ++c) acc = __fmaf_rn(g[c], w[c][d], acc);
+  gfeat[t] = acc;
+}
+
 // MODE: 0 = per-entry gradient rows + feature gradient; k in 1..L = the sums A_k, B_k.
 template <typename T, typename FT, int D, int C1, int C2, int C3, int MODE>
-__global__ __launch_bounds__(kBnThreads) void sa_bn_bwd_kernel(
+__global__ __launch_bounds__(kBnThreads) __attribute__((amdgpu_waves_per_eu(2))) void sa_bn_bwd_kernel(
     PointsView<T> pts, PointsView<T> ctr, int S, int B, BnFeat<FT> feat, const int32_t* __restrict__ count,
     const int32_t* __restrict__ list, int nsample, const float* __restrict__ pack, const float* __restrict__ zrows,
     const float* __restrict__ gout, float* __restrict__ gfeat, int64_t gfb, double* __restrict__ dpartial,
-    float* __restrict__ rows) {
+    float* __restrict__ rows, float* __restrict__ frows, uint32_t* __restrict__ fkeys, int nfeat) {
   using Tb = BnTable<D, C1, C2, C3>;
   constexpr int C0 = Tb::C0, CL = Tb::CL, L = Tb::L;
   constexpr bool FINAL = MODE == 0;
@@ -431,6 +473,17 @@ __global__ __launch_bounds__(kBnThreads) void sa_bn_bwd_kernel(
   const float* p3 = pack + Tb::O3;
   const float* pL = C3 > 0 ? p3 : p2;
   const float* vL = pL + CL * CINL;
+  // the layers' per-channel vectors (bias | scale | shift | mean | istd | A/M | B/M) in LDS: read
+  // as wave-uniform LDS loads, not hoisted into (spilled) SGPRs
+  __shared__ float svec[7 * (C1 + C2 + (C3 > 0 ? C3 : 1))];
+  float* sv1 = svec;
+  float* sv2 = sv1 + 7 * C1;
+  float* sv3 = sv2 + 7 * C2;
+  for (int i = tid; i < 7 * C1; i += kBnThreads) sv1[i] = p1[C1 * C0 + i];
+  for (int i = tid; i < 7 * C2; i += kBnThreads) sv2[i] = p2[C2 * C1 + i];
+  if constexpr (C3 > 0)
+    for (int i = tid; i < 7 * C3; i += kBnThreads) sv3[i] = p3[C3 * C2 + i];
+  __syncthreads();
   const int cL = lane < CL ? lane : 0;
   const float scL = vL[CL + cL], shL = vL[2 * CL + cL], muL = vL[3 * CL + cL], isL = vL[4 * CL + cL];
   const int64_t M = (static_cast<int64_t>(B) * S * nsample + 63) & ~static_cast<int64_t>(63);  // padded
@@ -519,37 +572,49 @@ __global__ __launch_bounds__(kBnThreads) void sa_bn_bwd_kernel(
       }
       if constexpr (C3 > 0) {
         float g2[C2], g1[C1];
-        bn_bwd_top<C2, C3, FINAL>(z3r, M, e, act, p3, s_arg[wave], s_rg[wave], r, r < cnt, g2, gz3r);
+        bn_bwd_top<C2, C3, FINAL>(z3r, M, e, act, p3, sv3, s_arg[wave], s_rg[wave], r, r < cnt, g2, gz3r);
         if constexpr (MODE == 2) {
-          bn_bwd_sums<C1, C2, TW>(z2r, M, e, act, p2, g2, tl, lane, rn, s1, s2);
+          bn_bwd_sums<C1, C2, TW>(z2r, M, e, act, sv2, g2, tl, lane, rn, s1, s2);
           continue;
         }
         if constexpr (FINAL) {
-          if (act) bn_put_h<C1, C2>(z2r, M, e, p2, ha3r);
+          if (act) bn_put_h<C1, C2>(z2r, M, e, sv2, ha3r);
         }
-        bn_bwd_mid<C1, C2, FINAL>(z2r, M, e, act, p2, g2, g1, gz2r);
+        bn_bwd_mid<C1, C2, FINAL>(z2r, M, e, act, p2, sv2, g2, g1, gz2r);
         if constexpr (MODE == 1) {
-          bn_bwd_sums<C0, C1, TW>(z1r, M, e, act, p1, g1, tl, lane, rn, s1, s2);
+          bn_bwd_sums<C0, C1, TW>(z1r, M, e, act, sv1, g1, tl, lane, rn, s1, s2);
           continue;
         }
         if constexpr (FINAL) {
-          if (act) bn_put_h<C0, C1>(z1r, M, e, p1, ha2r);
-          bn_bwd_first<C0, C1>(z1r, e, act, p1, g1, gz1r);
-          if constexpr (D > 0)
+          if (act) bn_put_h<C0, C1>(z1r, M, e, sv1, ha2r);
+          bn_bwd_first<C0, C1>(z1r, e, act, sv1, g1, gz1r);
+          if constexpr (D == 32 || D == 64) {
+            if (frows) {
+              if (act) fkeys[e] = static_cast<uint32_t>(static_cast<int64_t>(b) * nfeat + n);
+              if (act) bn_put_rowmajor<C1>(frows + e * C1, g1);
+            }
+          } else if constexpr (D > 0) {
             if (gfeat) bn_scatter_feat<D, C0, C1, TW>(g1, tl, p1, lane, rn, n, act, gfeat + b * gfb);
+          }
         }
       } else {
         float g1[C1];
-        bn_bwd_top<C1, C2, FINAL>(z2r, M, e, act, p2, s_arg[wave], s_rg[wave], r, r < cnt, g1, gz2r);
+        bn_bwd_top<C1, C2, FINAL>(z2r, M, e, act, p2, sv2, s_arg[wave], s_rg[wave], r, r < cnt, g1, gz2r);
         if constexpr (MODE == 1) {
-          bn_bwd_sums<C0, C1, TW>(z1r, M, e, act, p1, g1, tl, lane, rn, s1, s2);
+          bn_bwd_sums<C0, C1, TW>(z1r, M, e, act, sv1, g1, tl, lane, rn, s1, s2);
           continue;
         }
         if constexpr (FINAL) {
-          if (act) bn_put_h<C0, C1>(z1r, M, e, p1, ha2r);
-          bn_bwd_first<C0, C1>(z1r, e, act, p1, g1, gz1r);
-          if constexpr (D > 0)
+          if (act) bn_put_h<C0, C1>(z1r, M, e, sv1, ha2r);
+          bn_bwd_first<C0, C1>(z1r, e, act, sv1, g1, gz1r);
+          if constexpr (D == 32 || D == 64) {
+            if (frows) {
+              if (act) fkeys[e] = static_cast<uint32_t>(static_cast<int64_t>(b) * nfeat + n);
+              if (act) bn_put_rowmajor<C1>(frows + e * C1, g1);
+            }
+          } else if constexpr (D > 0) {
             if (gfeat) bn_scatter_feat<D, C0, C1, TW>(g1, tl, p1, lane, rn, n, act, gfeat + b * gfb);
+          }
         }
       }
     }
@@ -590,6 +655,22 @@ __global__ __launch_bounds__(1024) void bn_sum_kernel(const PT* __restrict__ par
     for (int k = 0; k < 16; ++k) t += sl[k][c];
     out[e] = static_cast<OT>(t);
   }
+}
+
+// segsum.hip
+int64_t segment_sum_workspace_bytes(int64_t E, int64_t nrows);
+int segment_sum(const uint32_t* keys, const float* contrib, int64_t E, int64_t nrows, int ncol, float* out, void* ws,
+                hipStream_t st);
+
+// Mode-0 feature-gradient workspace: keys (E u32) | rows (E x D fp32) | segment_sum's own.
+inline int64_t bn_align(int64_t x) { return (x + 255) / 256 * 256; }
+static void bn_feat_ws_layout(void* ws, int64_t E, int64_t npts, int C, uint32_t** keys, float** rows, float** G,
+                              void** seg) {
+  char* p = static_cast<char*>(ws);
+  *keys = reinterpret_cast<uint32_t*>(p);
+  *rows = reinterpret_cast<float*>(p + bn_align(E * 4));
+  *G = reinterpret_cast<float*>(p + bn_align(E * 4) + bn_align(E * C * 4));
+  *seg = p + bn_align(E * 4) + bn_align(E * C * 4) + bn_align(npts * C * 4);
 }
 
 static int bn_grid(int64_t total) {
@@ -635,10 +716,29 @@ static int launch_bwd(const BnArgs& a, const float* zrows, const float* gout, fl
   PointsView<T> pv{static_cast<const T*>(a.xyz), a.sb, a.sc, a.sn};
   PointsView<T> cv{static_cast<const T*>(a.ctr), a.cb, a.cc, a.cn};
   BnFeat<FT> fv{static_cast<const FT*>(a.feat), a.fb, a.fd, a.fn};
+  // mode 0, D = C1 = 32 / 64 with a feature gradient: per-entry gz_1 rows + keys in the workspace,
+  // the deterministic per-point segment sums, then W_1f^T per point (bn_feat_ws_layout)
+  constexpr bool kSeg = MODE == 0 && (D == 32 || D == 64) && C1 == D;
+  const int nfeat = D > 0 ? static_cast<int>(gfb / D) : 0;
+  const int64_t E = static_cast<int64_t>(a.B) * a.S * a.nsample;
+  uint32_t* fkeys = nullptr;
+  float* frows = nullptr;
+  void* segws = nullptr;
+  float* G = nullptr;
+  const int64_t npts = static_cast<int64_t>(a.B) * nfeat;
+  if (kSeg && gfeat) bn_feat_ws_layout(ws, E, npts, C1, &fkeys, &frows, &G, &segws);
   hipLaunchKernelGGL((sa_bn_bwd_kernel<T, FT, D, C1, C2, C3, MODE>), dim3(grid), dim3(kBnThreads), 0, a.st, pv, cv,
                      a.S, a.B, fv, a.count, a.list, a.nsample, a.pack, zrows, gout, gfeat, gfb,
-                     static_cast<double*>(ws), rows);
+                     static_cast<double*>(ws), rows, frows, fkeys, nfeat);
   if (int e = launch_status("dvcp_sa_bn_backward")) return e;
+  if constexpr (kSeg) {
+    if (gfeat) {
+      if (int e = segment_sum(fkeys, frows, E, npts, C1, G, segws, a.st)) return e;
+      hipLaunchKernelGGL((bn_feat_grad_kernel<D, 3 + D, C1>), dim3(ceil_div(npts * D, 256)), dim3(256), 0, a.st, G,
+                         a.pack, npts, gfeat);
+      return launch_status("dvcp_sa_bn_backward(feat)");
+    }
+  }
   if constexpr (MODE != 0) {
     constexpr int CM = MODE == 1 ? C1 : (MODE == 2 ? C2 : C3);
     hipLaunchKernelGGL((bn_sum_kernel<double, double>), dim3(ceil_div(2 * CM, 64)), dim3(1024), 0, a.st,
@@ -725,6 +825,14 @@ extern "C" int64_t dvcp_sa_bn_workspace_bytes(int B, int S, int nlayer, const in
   for (int l = 0; l < nlayer; ++l) cmax = std::max<int64_t>(cmax, chans[l + 1]);
   const int64_t nw = static_cast<int64_t>(dvcp::bn_grid(static_cast<int64_t>(B) * S)) * dvcp::kBnWaves;
   return nw * 2 * cmax * 8;
+}
+
+extern "C" int64_t dvcp_sa_bn_feat_workspace_bytes(int B, int S, int nsample, int N, int D) {
+  if (B < 0 || S < 0 || nsample < 0 || N < 0 || D < 0) return -1;
+  if (D != 32 && D != 64) return 0;  // other tables scatter with atomics (no workspace)
+  const int64_t E = static_cast<int64_t>(B) * S * nsample, npts = static_cast<int64_t>(B) * N;
+  const int64_t seg = dvcp::segment_sum_workspace_bytes(E, npts);  // (C1 = D for these tables)
+  return seg < 0 ? -1 : dvcp::bn_align(E * 4) + dvcp::bn_align(E * D * 4) + dvcp::bn_align(npts * D * 4) + seg;
 }
 
 extern "C" int64_t dvcp_sa_bn_rows_floats(int B, int S, int nsample, int nlayer, const int* chans) {

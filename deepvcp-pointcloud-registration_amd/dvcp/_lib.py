@@ -116,6 +116,8 @@ def load():
     lib.dvcp_sa_bn_workspace_bytes.restype = ctypes.c_int64
     lib.dvcp_sa_bn_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     lib.dvcp_sa_bn_rows_floats.restype = ctypes.c_int64
+    lib.dvcp_sa_bn_feat_workspace_bytes.restype = ctypes.c_int64
+    lib.dvcp_sa_bn_feat_workspace_bytes.argtypes = [ctypes.c_int] * 5
     lib.dvcp_sa_bn_rows_floats.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     lib.dvcp_sa_bn_zrows_floats.restype = ctypes.c_int64
     lib.dvcp_sa_bn_zrows_floats.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
@@ -138,7 +140,7 @@ def exported_symbols():
             "dvcp_dfe_tgt_backward_workspace_bytes",
             "dvcp_cpg_backward_workspace_bytes", "dvcp_sa_group_mlp_backward_workspace_bytes",
             "dvcp_fe_head_backward_workspace_bytes", "dvcp_sa_bn_workspace_bytes",
-            "dvcp_sa_bn_pack_floats", "dvcp_sa_bn_rows_floats", "dvcp_sa_bn_zrows_floats",
+            "dvcp_sa_bn_pack_floats", "dvcp_sa_bn_rows_floats", "dvcp_sa_bn_feat_workspace_bytes", "dvcp_sa_bn_zrows_floats",
             "dvcp_cpg1d_nparams"] + list(SIGNATURES)
 
 

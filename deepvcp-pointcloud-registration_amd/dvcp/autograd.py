@@ -166,9 +166,9 @@ def _scatter_rows(g, idx, n):
 
 class _FeatExtract(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, fe, pts, starts, wl, side_stream, *params):
+    def forward(ctx, fe, pts, starts, wl, side_stream, fps, *params):
         saved = {}
-        xyz, feat, score = fe.run(pts, starts, wl=wl, side_stream=side_stream, saved=saved)
+        xyz, feat, score = fe.run(pts, starts, wl=wl, side_stream=side_stream, saved=saved, fps=fps)
         ctx.fe, ctx.saved = fe, saved
         ctx.shapes = [(p.shape, p.dtype) for p in params]
         ctx.mark_non_differentiable(xyz)
@@ -181,7 +181,7 @@ class _FeatExtract(torch.autograd.Function):
         fe, saved = ctx.fe, ctx.saved
         grads = []
         if g_feat is None:
-            return (None,) * 5 + tuple(None for _ in ctx.shapes)
+            return (None,) * 6 + tuple(None for _ in ctx.shapes)
         B, S, _ = g_feat.shape
         gp_fc, g = ops.fe_head_backward(saved["f3"], fe.fc_params(), g_feat.reshape(B * S, 32))
         g = g.view(B, S, 64)
@@ -207,13 +207,14 @@ class _FeatExtract(torch.autograd.Function):
                 o += co * ci + 3 * co
         grads += [gp_fc[:32 * 64].view(32, 64), gp_fc[32 * 64:]]
         ctx.saved = None
-        out = [gr.to(dt) if ctx.needs_input_grad[5 + k] else None for k, (gr, (_, dt)) in enumerate(zip(grads, ctx.shapes))]
-        return (None, None, None, None, None, *out)
+        out = [gr.to(dt) if ctx.needs_input_grad[6 + k] else None for k, (gr, (_, dt)) in enumerate(zip(grads, ctx.shapes))]
+        return (None, None, None, None, None, None, *out)
 
 
-def feat_extraction(fe, pts, starts, wl=None, side_stream=None):
-    """FE1.run differentiable in FE1's parameters (BN in FE1's mode): -> (xyz, feat, score)."""
-    return _FeatExtract.apply(fe, pts, starts, wl, side_stream, *_fe_params(fe))
+def feat_extraction(fe, pts, starts, wl=None, side_stream=None, fps=None):
+    """FE1.run differentiable in FE1's parameters (BN in FE1's mode): -> (xyz, feat, score).
+    ``fps``: the FPS chain launched ahead (FE1.launch_fps)."""
+    return _FeatExtract.apply(fe, pts, starts, wl, side_stream, fps, *_fe_params(fe))
 
 
 def dfe_rows(X, dfe_module):

@@ -66,6 +66,14 @@ class DeepVCP(nn.Module):
             cache[key] = torch.cuda.Stream(device=dev)
         return cache[key]
 
+    def _fps_stream(self, dev):
+        """A second stream per calling stream, for an FPS chain launched ahead (FE1.launch_fps)."""
+        cache = self.__dict__.setdefault("_dvcp_fps_streams", {})
+        key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+        if key not in cache:
+            cache[key] = torch.cuda.Stream(device=dev)
+        return cache[key]
+
     def _training_mode(self):
         """(train_head, train_fe) for this forward (train.py:105-125).  Autograd records through
         the head (DFE, CPG) when it is enabled and any head or extractor parameter requires
@@ -110,8 +118,8 @@ class DeepVCP(nn.Module):
         starts = starts.to(dev, non_blocking=True)
         side = self._side_stream(dev)
         if train_fe:  # differentiable in FE1's parameters (autograd.feat_extraction)
-            def run(pts, st, wl=None):
-                return autograd.feat_extraction(self.FE1, pts, st, wl=wl, side_stream=side)
+            def run(pts, st, wl=None, fps=None):
+                return autograd.feat_extraction(self.FE1, pts, st, wl=wl, side_stream=side, fps=fps)
         else:
             run = self.FE1.run
         if src_pts.shape == tgt_pts.shape and src_pts.dtype == tgt_pts.dtype and not self.FE1.training:
@@ -127,8 +135,11 @@ class DeepVCP(nn.Module):
             score = score2[:B]
         else:
             if train_fe:
+                # two passes (batch statistics per call); the target's serial FPS chain, which
+                # needs only its coordinates, runs on its own stream under the source's layers
+                tgt_fps = self.FE1.launch_fps(tgt_pts, starts[4:7], self._fps_stream(dev))
                 src_xyz, src_feat, score = run(src_pts, starts[0:3], wl=self.WL)
-                tgt_xyz, tgt_feat, _ = run(tgt_pts, starts[4:7])
+                tgt_xyz, tgt_feat, _ = run(tgt_pts, starts[4:7], fps=tgt_fps)
             else:
                 src_xyz, src_feat, score = run(src_pts, starts[0:3], wl=self.WL, side_stream=side)
                 tgt_xyz, tgt_feat, _ = run(tgt_pts, starts[4:7], side_stream=side)

@@ -39,7 +39,27 @@ class feat_extraction_layer(nn.Module):
         return cached_pack(self, "head" if wl is None else "head_wl", linear_tensors(*lins),
                            lambda: linear_pack(*lins))
 
-    def run(self, pts, starts=None, wl=None, side_stream=None, saved=None):
+    def launch_fps(self, pts, starts, stream):
+        """The serial FPS chain of ``run`` (it depends on the coordinates alone) enqueued on
+        ``stream``, for ``run(..., fps=...)``: a caller with two clouds starts the second cloud's
+        chain while the first one's layers run (extract_features in training mode).  ->
+        (indices, centres, events recorded on ``stream``)."""
+        xyz = pts[:, :3, :] if self.use_normal else pts
+        idxs, centres, events = [], [], []
+        stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(stream):
+            prev = xyz
+            for sa, st in zip((self.sa1, self.sa2, self.sa3), starts):
+                i, c = ops.fps(prev, sa.npoint, st.to(prev.device), pdim=2)
+                idxs.append(i)
+                centres.append(c)
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                events.append(ev)
+                prev = c
+        return idxs, centres, events
+
+    def run(self, pts, starts=None, wl=None, side_stream=None, saved=None, fps=None):
         """Fused forward.  starts: (3, B) FPS start indices (drawn like the reference if None).
         Returns xyz (B, 3, S) contiguous, feat (B, S, 32), score (B, S) when ``wl`` is given.
         ``saved`` (a dict): filled with what the backward needs (dvcp/autograd.py feat_extraction):
@@ -67,16 +87,23 @@ class feat_extraction_layer(nn.Module):
         layers = (self.sa1, self.sa2, self.sa3)
         main = torch.cuda.current_stream()
         side = side_stream if side_stream is not None else main
-        idxs, centres, events = [], [], []
-        prev = xyz
-        for sa, st in zip(layers, starts):
-            i, c = ops.fps(prev, sa.npoint, st.to(prev.device), pdim=2)
-            idxs.append(i)
-            centres.append(c)
-            ev = torch.cuda.Event()
-            ev.record(main)
-            events.append(ev)
-            prev = c
+        if fps is not None:  # launched ahead on another stream (launch_fps)
+            idxs, centres, events = fps
+            for i, c in zip(idxs, centres):  # (the side stream waits for each layer's event)
+                for t in (i, c):
+                    t.record_stream(main)
+                    t.record_stream(side)
+        else:
+            idxs, centres, events = [], [], []
+            prev = xyz
+            for sa, st in zip(layers, starts):
+                i, c = ops.fps(prev, sa.npoint, st.to(prev.device), pdim=2)
+                idxs.append(i)
+                centres.append(c)
+                ev = torch.cuda.Event()
+                ev.record(main)
+                events.append(ev)
+                prev = c
         # Inference folds the gathers of per-point layers into their consumers: the next layer's
         # MLP reads its features through the FPS indices (dvcp_sa_group_mlp_rows_ws) and the head
         # reads sa3's rows the same way (dvcp_fe_head_rows).  Training (``saved``) keeps the

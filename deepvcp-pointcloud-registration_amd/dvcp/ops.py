@@ -613,7 +613,16 @@ def sa_bn_backward(xyz, ctr, feat, count, lst, nsample, chans, pack, zrows, grad
     M = B * S * int(nsample)
     nrows = int(_lib.load().dvcp_sa_bn_rows_floats(B, S, int(nsample), len(chans) - 1, ch.data_ptr()))
     rows = torch.empty(max(nrows, 1), dtype=torch.float32, device=dev)
-    gF = torch.zeros(B, N, D, dtype=torch.float32, device=dev) if (want_feat_grad and D > 0) else None
+    gF = None
+    if want_feat_grad and D > 0:
+        if D in (32, 64):   # per-entry rows summed per point in entry order (deterministic)
+            fb = int(_lib.load().dvcp_sa_bn_feat_workspace_bytes(B, S, int(nsample), N, D))
+            if fb < 0:
+                raise RuntimeError("dvcp_sa_bn_feat_workspace_bytes: size query failed")
+            ws = torch.empty(max(1, (fb + 3) // 4), dtype=torch.float32, device=dev)
+            gF = torch.empty(B, N, D, dtype=torch.float32, device=dev)
+        else:
+            gF = torch.zeros(B, N, D, dtype=torch.float32, device=dev)
     call("dvcp_sa_bn_backward", *args, ptr(zrows), 0, ptr(g), ptr(gF), ptr(ws), None, ptr(rows), stream())
     Kc = 65536              # tables are 65536-entry chunks, channel-major inside (csrc/sa_bn.hip bn_at_rows)
     Mk = -(-M // Kc) * Kc

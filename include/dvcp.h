@@ -292,13 +292,17 @@ int dvcp_sa_group_mlp_backward(int dtype, const void* xyz, int64_t sb, int64_t s
  *   none); mode = 0 -> rows (dvcp_sa_bn_rows_floats floats): per layer l, dL/dz_l of every entry
  *   (C_l x M, channel-major) then the layer's input rows and a ones row (C_{l-1} + 1 x M), so
  *   [dW_l | db_l] = dz_l [h_{l-1}; 1]^T is a plain GEMM over the entries (the host runs it); and,
- *   if grad_feat is given (zeroed by the caller), dL/d feat (B x N x D fp32) through the grouping.
- *   grad_out: B x S x C_last fp32.  workspace: dvcp_sa_bn_workspace_bytes bytes.
+ *   if grad_feat is given, dL/d feat (B x N x D fp32) through the grouping: for D = 32 / 64
+ *   overwritten with per-point sums of per-entry rows taken in entry order (deterministic; mode-0
+ *   workspace: dvcp_sa_bn_feat_workspace_bytes(B, S, nsample, N, D) bytes), for other D
+ *   accumulated with float atomics (zero it first).
+ *   grad_out: B x S x C_last fp32.  workspace (modes >= 1): dvcp_sa_bn_workspace_bytes bytes.
  * Replaces the training-mode forward/backward of pointnet2_utils.py:176-202 (BatchNorm2d batch
  * statistics, running-stat update done by the host). */
 int64_t dvcp_sa_bn_pack_floats(int nlayer, const int* chans);
 int64_t dvcp_sa_bn_workspace_bytes(int B, int S, int nlayer, const int* chans);
 int64_t dvcp_sa_bn_rows_floats(int B, int S, int nsample, int nlayer, const int* chans);
+int64_t dvcp_sa_bn_feat_workspace_bytes(int B, int S, int nsample, int N, int D);
 int64_t dvcp_sa_bn_zrows_floats(int B, int S, int nsample, int nlayer, const int* chans);
 int dvcp_sa_bn_zrows(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
                      const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,

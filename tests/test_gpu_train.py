@@ -353,6 +353,9 @@ def test_sa_batch_stats_train_vs_oracle(cuda, table):
             o += n
     if gF is not None:
         errs["feat"] = _close(gF.permute(0, 2, 1), feat_o.grad, 1e-3, f"{table} feature gradient", check=False)
+        # the 32 / 64-channel tables sum per-entry rows per point in entry order: same bits again
+        _, gF2 = batchnorm.train_backward(mine, lay, G.permute(0, 2, 1).float().to(cuda), want_feat_grad=True)
+        assert torch.equal(gF2, gF), f"{table}: feature gradient differs between two runs"
     print(table, f"near-tie pairs left out: {int(near.sum())} of {near.numel()};",
           "relative gradient errors:", {k: f"{v[0]:.1e}" for k, v in errs.items()})
     bad = {k: f"{v[0]:.1e} > {v[1]}" for k, v in errs.items() if v[0] > v[1]}
