@@ -180,7 +180,7 @@ __global__ __launch_bounds__(1024) void dfe_bwd_sum_kernel(const float* __restri
 }
 
 template <int MODE, typename T>  // MODE 0: materialised rows X (R, 32, 35); 1: fused target rows
-__global__ __launch_bounds__(kDfeThreads) void dfe_bwd_kernel(const T* __restrict__ X, PointsView<T> ref,
+__global__ __launch_bounds__(kDfeThreads) __attribute__((amdgpu_waves_per_eu(2))) void dfe_bwd_kernel(const T* __restrict__ X, PointsView<T> ref,
                                                               const float* __restrict__ feat, int M,
                                                               const float* __restrict__ cand,
                                                               const float* __restrict__ dist,
@@ -269,14 +269,19 @@ __global__ __launch_bounds__(kDfeThreads) void dfe_bwd_kernel(const T* __restric
       float dx[35];
 #pragma unroll
       for (int i = 0; i < 35; ++i) dx[i] = 0.f;
-      bool any = false;
-      for (int ff = 0; ff < 32; ++ff) {
-        if (rsel[ql * 32 + ff] == j) {
-          const float gf = rg[ql * 32 + ff];
-          any = true;
+      // the channels routed to row j as a mask, then each lane walks only its own (about one per
+      // row; ascending, as before): a wave no longer steps through all 32 channels whenever one
+      // of its 64 rows takes each of them
+      uint32_t mine = 0u;
+#pragma unroll 8
+      for (int ff = 0; ff < 32; ++ff) mine |= rsel[ql * 32 + ff] == j ? (1u << ff) : 0u;
+      const bool any = mine != 0u;
+      while (mine != 0u) {
+        const int ff = __builtin_ctz(mine);
+        mine &= mine - 1u;
+        const float gf = rg[ql * 32 + ff];
 #pragma unroll
-          for (int i = 0; i < 35; ++i) dx[i] = __fmaf_rn(gf, Es[ff][i], dx[i]);
-        }
+        for (int i = 0; i < 35; ++i) dx[i] = __fmaf_rn(gf, Es[ff][i], dx[i]);
       }
       if constexpr (MODE == 0) {
         if (live)

@@ -112,16 +112,57 @@ __device__ __forceinline__ void bn_load_x(float (&x)[3 + D], PointsView<T> pts, 
   for (int d = 0; d < D; ++d) x[3 + d] = feat.at(b, d, n);
 }
 
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+}
+
+// Row layout of the z / gradient / input rows: 64-entry blocks, channel-major inside a block --
+// element (entry e, channel c) of a C-channel table at (e / 64) * C * 64 + c * 64 + e % 64 -- so a
+// wave's 64 consecutive entries of one channel are one 256-byte run and its whole chunk one
+// contiguous C x 256-byte region (tables are padded to a multiple of 64 entries).
+template <typename P>
+__device__ __forceinline__ P* bn_at(P* base, int C, int64_t e) {
+  return base + (e >> 6) * (static_cast<int64_t>(C) * 64) + (e & 63);
+}
+
+// The mode-0 gradient / input rows (the host's weight-gradient GEMM operands): 65536-entry
+// chunks, channel-major inside a chunk -- (e / 65536) * C * 65536 + c * 65536 + e % 65536 -- so
+// each chunk of a table is one (C x 65536) row-major GEMM operand (no layout copy on the host);
+// tables are padded to a multiple of 65536 entries.
+constexpr int kBnRowChunkLog = 16;
+constexpr int64_t kBnRowChunk = int64_t(1) << kBnRowChunkLog;
+__device__ __forceinline__ float* bn_at_rows(float* base, int C, int64_t e) {
+  return base + (e >> kBnRowChunkLog) * (static_cast<int64_t>(C) * kBnRowChunk) + (e & (kBnRowChunk - 1));
+}
+
+// z = W x + b stored to its row (channel-major), h = relu(z * scale + shift), channel by channel
+template <int CIN, int COUT>
+__device__ __forceinline__ void bn_layer_store(const float (&x)[CIN], float (&h)[COUT], const float* __restrict__ p,
+                                               float* __restrict__ zr, int64_t M, int64_t e) {
+  bn_matvec<CIN, COUT>(x, p, [&](int co, float acc, const float* q) {
+    const float z = acc + q[CIN * COUT + co];
+    bn_at(zr, COUT, e)[co * 64] = z;
+    const float y = z * q[CIN * COUT + COUT + co] + q[CIN * COUT + 2 * COUT + co];
+    h[co] = y > 0.0f ? y : 0.0f;
+  });
+}
+
 // ---- statistics pass ----------------------------------------------------------------------------
 template <typename T, typename FT, int D, int C1, int C2, int C3, int LAYER>
 __global__ __launch_bounds__(kBnThreads) void sa_bn_stats_kernel(PointsView<T> pts, PointsView<T> ctr, int S, int B,
                                                                  BnFeat<FT> feat, const int32_t* __restrict__ count,
                                                                  const int32_t* __restrict__ list, int nsample,
                                                                  const float* __restrict__ pack,
-                                                                 double* __restrict__ partial) {
+                                                                 double* __restrict__ partial,
+                                                                 float* __restrict__ zrows) {
   using Tb = BnTable<D, C1, C2, C3>;
   constexpr int C0 = Tb::C0;
   constexpr int CZ = LAYER == 1 ? C1 : (LAYER == 2 ? C2 : C3);
+  // the last layer's pass (every lower layer's batch statistics final) can also write every
+  // entry's z rows for the backward (zrows != null): the z-row pass of dvcp_sa_bn_zrows, fused
+  constexpr bool kLast = LAYER == (C3 > 0 ? 3 : 2);
+  const int64_t Mz = (static_cast<int64_t>(B) * S * nsample + 63) & ~static_cast<int64_t>(63);
   constexpr int G = kWave / CZ;  // slot groups (CZ divides 64)
   __shared__ float tile[kBnWaves][kWave][CZ + 1];
   __shared__ double red[kBnWaves][2][kWave];
@@ -147,7 +188,27 @@ __global__ __launch_bounds__(kBnThreads) void sa_bn_stats_kernel(PointsView<T> p
         float x[C0];
         bn_load_x<T, FT, D>(x, pts, feat, b, n, cx, cy, cz);
         float z[CZ];
-        if constexpr (LAYER == 1) {
+        const int64_t e = cs * nsample + r;
+        bool done = false;
+        if constexpr (kLast) {
+          if (zrows) {
+          done = true;
+          float h1[C1];
+          bn_layer_store<C0, C1>(x, h1, p1, zrows, Mz, e);
+          if constexpr (C3 > 0) {
+            float h2[C2];
+            bn_layer_store<C1, C2>(h1, h2, p2, zrows + C1 * Mz, Mz, e);
+            bn_rows_raw<C2, C3>(h2, z, p3);
+          } else {
+            bn_rows_raw<C1, C2>(h1, z, p2);
+          }
+          float* zl = zrows + (C3 > 0 ? (C1 + C2) : C1) * Mz;
+#pragma unroll
+          for (int k = 0; k < CZ; ++k) bn_at(zl, CZ, e)[k * 64] = z[k];
+          }
+        }
+        if (done) {
+        } else if constexpr (LAYER == 1) {
           bn_rows_raw<C0, C1>(x, z, p1);
         } else {
           float h1[C1];
@@ -190,42 +251,6 @@ __global__ __launch_bounds__(kBnThreads) void sa_bn_stats_kernel(PointsView<T> p
     o[lane] = a;
     o[CZ + lane] = q;
   }
-}
-
-__device__ __forceinline__ void wave_sync_lds() {
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-}
-
-// Row layout of the z / gradient / input rows: 64-entry blocks, channel-major inside a block --
-// element (entry e, channel c) of a C-channel table at (e / 64) * C * 64 + c * 64 + e % 64 -- so a
-// wave's 64 consecutive entries of one channel are one 256-byte run and its whole chunk one
-// contiguous C x 256-byte region (tables are padded to a multiple of 64 entries).
-template <typename P>
-__device__ __forceinline__ P* bn_at(P* base, int C, int64_t e) {
-  return base + (e >> 6) * (static_cast<int64_t>(C) * 64) + (e & 63);
-}
-
-// The mode-0 gradient / input rows (the host's weight-gradient GEMM operands): 65536-entry
-// chunks, channel-major inside a chunk -- (e / 65536) * C * 65536 + c * 65536 + e % 65536 -- so
-// each chunk of a table is one (C x 65536) row-major GEMM operand (no layout copy on the host);
-// tables are padded to a multiple of 65536 entries.
-constexpr int kBnRowChunkLog = 16;
-constexpr int64_t kBnRowChunk = int64_t(1) << kBnRowChunkLog;
-__device__ __forceinline__ float* bn_at_rows(float* base, int C, int64_t e) {
-  return base + (e >> kBnRowChunkLog) * (static_cast<int64_t>(C) * kBnRowChunk) + (e & (kBnRowChunk - 1));
-}
-
-// z = W x + b stored to its row (channel-major), h = relu(z * scale + shift), channel by channel
-template <int CIN, int COUT>
-__device__ __forceinline__ void bn_layer_store(const float (&x)[CIN], float (&h)[COUT], const float* __restrict__ p,
-                                               float* __restrict__ zr, int64_t M, int64_t e) {
-  bn_matvec<CIN, COUT>(x, p, [&](int co, float acc, const float* q) {
-    const float z = acc + q[CIN * COUT + co];
-    bn_at(zr, COUT, e)[co * 64] = z;
-    const float y = z * q[CIN * COUT + COUT + co] + q[CIN * COUT + 2 * COUT + co];
-    h[co] = y > 0.0f ? y : 0.0f;
-  });
 }
 
 // ---- forward rows -------------------------------------------------------------------------------
@@ -694,7 +719,7 @@ struct BnArgs {
 };
 
 template <typename T, typename FT, int D, int C1, int C2, int C3, int LAYER>
-static int launch_stats(const BnArgs& a, void* ws, double* sums) {
+static int launch_stats(const BnArgs& a, void* ws, double* sums, float* zrows) {
   constexpr int CZ = LAYER == 1 ? C1 : (LAYER == 2 ? C2 : C3);
   const int grid = bn_grid(static_cast<int64_t>(a.B) * a.S);
   PointsView<T> pv{static_cast<const T*>(a.xyz), a.sb, a.sc, a.sn};
@@ -702,7 +727,7 @@ static int launch_stats(const BnArgs& a, void* ws, double* sums) {
   BnFeat<FT> fv{static_cast<const FT*>(a.feat), a.fb, a.fd, a.fn};
   double* part = static_cast<double*>(ws);
   hipLaunchKernelGGL((sa_bn_stats_kernel<T, FT, D, C1, C2, C3, LAYER>), dim3(grid), dim3(kBnThreads), 0, a.st, pv,
-                     cv, a.S, a.B, fv, a.count, a.list, a.nsample, a.pack, part);
+                     cv, a.S, a.B, fv, a.count, a.list, a.nsample, a.pack, part, zrows);
   if (int e = launch_status("dvcp_sa_bn_stats")) return e;
   hipLaunchKernelGGL((bn_sum_kernel<double, double>), dim3(ceil_div(2 * CZ, 64)), dim3(1024), 0, a.st, part,
                      grid * kBnWaves, 2 * CZ, sums);
@@ -749,11 +774,11 @@ static int launch_bwd(const BnArgs& a, const float* zrows, const float* gout, fl
 }
 
 template <typename T, typename FT, int D, int C1, int C2, int C3>
-static int dispatch_stats(const BnArgs& a, int layer, void* ws, double* sums) {
-  if (layer == 1) return launch_stats<T, FT, D, C1, C2, C3, 1>(a, ws, sums);
-  if (layer == 2) return launch_stats<T, FT, D, C1, C2, C3, 2>(a, ws, sums);
+static int dispatch_stats(const BnArgs& a, int layer, void* ws, double* sums, float* zrows) {
+  if (layer == 1) return launch_stats<T, FT, D, C1, C2, C3, 1>(a, ws, sums, zrows);
+  if (layer == 2) return launch_stats<T, FT, D, C1, C2, C3, 2>(a, ws, sums, zrows);
   if constexpr (C3 > 0)
-    if (layer == 3) return launch_stats<T, FT, D, C1, C2, C3, 3>(a, ws, sums);
+    if (layer == 3) return launch_stats<T, FT, D, C1, C2, C3, 3>(a, ws, sums, zrows);
   set_error("dvcp_sa_bn_stats: layer %d out of range", layer);
   return DVCP_EINVAL;
 }
@@ -782,14 +807,14 @@ static int dispatch_bwd(const BnArgs& a, int mode, const float* zrows, const flo
 // Feature dtypes: fp64 only for the 3-channel normals table (ModelNet's double clouds); the
 // 32 / 64-channel tables read the previous layer's fp32 outputs.
 template <typename T, int DD, int A1, int A2, int A3>
-static int stats_ft(const BnArgs& a, bool ff64, int layer, void* ws, double* sums) {
+static int stats_ft(const BnArgs& a, bool ff64, int layer, void* ws, double* sums, float* zrows) {
   if constexpr (DD == 3) {
-    if (ff64) return dispatch_stats<T, double, DD, A1, A2, A3>(a, layer, ws, sums);
+    if (ff64) return dispatch_stats<T, double, DD, A1, A2, A3>(a, layer, ws, sums, zrows);
   } else if (DD > 0 && ff64) {
     set_error("dvcp_sa_bn_stats: fp64 features are taken for the 3-channel table only (D=%d)", DD);
     return DVCP_EINVAL;
   }
-  return dispatch_stats<T, float, DD, A1, A2, A3>(a, layer, ws, sums);
+  return dispatch_stats<T, float, DD, A1, A2, A3>(a, layer, ws, sums, zrows);
 }
 
 template <typename T, int DD, int A1, int A2, int A3>
@@ -865,12 +890,13 @@ extern "C" int dvcp_sa_bn_stats(int dtype, const void* xyz, int64_t sb, int64_t 
                                 int64_t cb, int64_t cc, int64_t cn, int S, int B, int feat_dtype, const void* feat,
                                 int64_t fb, int64_t fd, int64_t fn, int D, const int32_t* count, const int32_t* list,
                                 int nsample, int nlayer, const int* chans, const float* pack, int layer,
-                                void* workspace, double* sums, void* stream) {
+                                void* workspace, double* sums, float* zrows, void* stream) {
   if (int e = bn_check("dvcp_sa_bn_stats", dtype, xyz, ctr, N, S, B, feat_dtype, feat, D, count, list, nsample, nlayer,
                        chans, pack, workspace))
     return e;
   DVCP_REQUIRE(sums, "dvcp_sa_bn_stats: null sums");
   DVCP_REQUIRE(layer >= 1 && layer <= nlayer, "dvcp_sa_bn_stats: layer %d of %d", layer, nlayer);
+  DVCP_REQUIRE(!zrows || layer == nlayer, "dvcp_sa_bn_stats: z rows are written by the last layer's pass only");
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (B == 0 || S == 0) {
     if (hipMemsetAsync(sums, 0, 2 * chans[layer] * sizeof(double), st) != hipSuccess)
@@ -881,8 +907,8 @@ extern "C" int dvcp_sa_bn_stats(int dtype, const void* xyz, int64_t sb, int64_t 
   const bool f64 = dtype == DVCP_F64, ff64 = feat_dtype == DVCP_F64;
 #define DVCP_BN_S(DD, A1, A2, A3)                                                                           \
   if (D == DD && chans[1] == A1 && chans[2] == A2 && (nlayer == 2 ? 0 : chans[3]) == A3)                   \
-    return f64 ? dvcp::stats_ft<double, DD, A1, A2, A3>(a, ff64, layer, workspace, sums)                    \
-               : dvcp::stats_ft<float, DD, A1, A2, A3>(a, ff64, layer, workspace, sums);
+    return f64 ? dvcp::stats_ft<double, DD, A1, A2, A3>(a, ff64, layer, workspace, sums, zrows)             \
+               : dvcp::stats_ft<float, DD, A1, A2, A3>(a, ff64, layer, workspace, sums, zrows);
   DVCP_BN_TABLES(DVCP_BN_S)
 #undef DVCP_BN_S
   dvcp::set_error("dvcp_sa_bn_stats: unsupported table D=%d chans=%d,%d", D, chans[1], chans[2]);

@@ -69,7 +69,7 @@ SIGNATURES = {
                                    _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P],
     "dvcp_fe_head_backward": [_P, _I, _P, _P, _P, _P, _P, _P],
     "dvcp_sa_bn_stats": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _L, _L, _L, _I,
-                         _P, _P, _I, _I, _P, _P, _I, _P, _P, _P],
+                         _P, _P, _I, _I, _P, _P, _I, _P, _P, _P, _P],
     "dvcp_sa_bn_backward": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _L, _L, _L, _I,
                             _P, _P, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P],
     "dvcp_sa_bn_zrows": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _L, _L, _L, _I,

@@ -9,8 +9,9 @@ variance), once per FE1 call -- src and tgt are separate calls (deepVCP.py:29,72
 Forward (``train_forward``): one statistics pass per layer (dvcp_sa_bn_stats: fp64 sums of z and
 z^2, the layers below normalised by their batch statistics), then the eval kernel
 (dvcp_sa_group_mlp) with the batch statistics folded into its scale / shift.
-Backward (``train_backward``): every entry's conv outputs z_l are written once (dvcp_sa_bn_zrows,
-64-entry blocks, a few GB at C3 -- HBM is 288 GB), then torch's batch-norm backward,
+Backward (``train_backward``): every entry's conv outputs z_l, written once by the forward's last
+statistics pass (64-entry blocks, a few GB per call at C3 -- HBM is 288 GB -- held until the
+backward; dvcp_sa_bn_zrows recomputes them when absent), then torch's batch-norm backward,
     dz_l = scale_l (dy_l - mean(dy_l) - xhat_l mean(dy_l xhat_l)),
 whose mean terms make every entry's gradient non-zero: sums of the top layer over the routed
 (arg-max) rows, one dense pass per lower layer for its sums, and a final dense pass for dW, db and
@@ -60,8 +61,12 @@ def train_forward(sa, xyz, ctr, feat, count, lst, ns):
             parts += [conv.weight.reshape(-1).float(), conv.bias.float(), one, zero, zero, one, zero, zero]
         pack = torch.cat(parts).contiguous()
         assert pack.numel() == total == ops.sa_bn_pack_floats(chans)
+        zrows = None
         for layer, (bn, (o, cin, cout)) in enumerate(zip(sa.mlp_bns, offs), 1):
-            sums = ops.sa_bn_stats(xyz, ctr, feat, count, lst, ns, chans, pack, layer)
+            if layer == len(offs):  # the last pass also writes every entry's z rows for the backward
+                sums, zrows = ops.sa_bn_stats(xyz, ctr, feat, count, lst, ns, chans, pack, layer, want_zrows=True)
+            else:
+                sums = ops.sa_bn_stats(xyz, ctr, feat, count, lst, ns, chans, pack, layer)
             mean = sums[0] / M
             var = (sums[1] / M - mean * mean).clamp_min(0.0)
             istd = torch.rsqrt(var + bn.eps)
@@ -72,7 +77,7 @@ def train_forward(sa, xyz, ctr, feat, count, lst, ns):
             _update_running(bn, mean, var, M)
         fwd = torch.cat([pack[o:o + cout * cin + 3 * cout] for o, cin, cout in offs]).contiguous()
     out = ops.sa_group_mlp(xyz, ctr, feat, count, lst, ns, chans, fwd)
-    return out, dict(pack=pack, M=M)
+    return out, dict(pack=pack, M=M, zrows=zrows)
 
 
 def train_backward(sa, lay, g_out, want_feat_grad):
@@ -84,8 +89,11 @@ def train_backward(sa, lay, g_out, want_feat_grad):
     pack, M = st["pack"].clone(), st["M"]
     args = (lay["pts"], lay["ctr"], lay["feat"], lay["count"], lay["lst"], lay["ns"], chans)
     g = g_out.float().contiguous()
-    # every entry's conv outputs, with this batch's statistics (held only during this backward)
-    zrows = ops.sa_bn_zrows(*args, st["pack"])
+    # every entry's conv outputs with this batch's statistics: written by the forward's last
+    # statistics pass (held from the forward to here), else recomputed now
+    zrows = st.pop("zrows", None)
+    if zrows is None:
+        zrows = ops.sa_bn_zrows(*args, st["pack"])
     sums = [None] * len(offs)
     for k in range(len(offs), 0, -1):   # the top layer's sums first: each lower one needs those above
         s = ops.sa_bn_backward(*args, pack, zrows, g, k)

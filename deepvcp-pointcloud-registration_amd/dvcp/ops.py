@@ -572,17 +572,23 @@ def sa_bn_pack_floats(chans):
     return int(_lib.load().dvcp_sa_bn_pack_floats(len(chans) - 1, ch.data_ptr()))
 
 
-def sa_bn_stats(xyz, ctr, feat, count, lst, nsample, chans, pack, layer, xyz_pdim=2, feat_ddim=1, feat_pdim=2):
+def sa_bn_stats(xyz, ctr, feat, count, lst, nsample, chans, pack, layer, xyz_pdim=2, feat_ddim=1, feat_pdim=2,
+                want_zrows=False):
     """Training-mode BatchNorm statistics of the grouped MLP (pointnet2_utils.py:198 in train()):
     (2, C_layer) fp64 = per-channel sum z and sum z^2 of layer ``layer``'s conv output over all
-    B * S * nsample grouped entries, the layers below it normalised by ``pack``."""
+    B * S * nsample grouped entries, the layers below it normalised by ``pack``.  ``want_zrows``
+    (last layer only): also -> every entry's z rows, as ``sa_bn_zrows`` returns them."""
     args, ws, (B, N, S, D), ch = _bn_common(xyz, ctr, feat, count, lst, nsample, chans, pack, xyz_pdim, feat_ddim,
                                             feat_pdim)
     sums = torch.empty(2, chans[layer], dtype=torch.float64, device=xyz.device)
+    zrows = None
+    if want_zrows:
+        n = int(_lib.load().dvcp_sa_bn_zrows_floats(B, S, int(nsample), len(chans) - 1, ch.data_ptr()))
+        zrows = torch.empty(max(n, 1), dtype=torch.float32, device=xyz.device)
     macs = sum(a * b for a, b in zip(chans[:layer], chans[1:layer + 1]))
-    call("dvcp_sa_bn_stats", *args, int(layer), ptr(ws), ptr(sums), stream(),
+    call("dvcp_sa_bn_stats", *args, int(layer), ptr(ws), ptr(sums), ptr(zrows), stream(),
          work=(2.0 * macs * B * S * nsample, B * S * 4 * nsample + B * N * 4 * (3 + D)))
-    return sums
+    return (sums, zrows) if want_zrows else sums
 
 
 def sa_bn_zrows(xyz, ctr, feat, count, lst, nsample, chans, pack, xyz_pdim=2, feat_ddim=1, feat_pdim=2):

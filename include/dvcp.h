@@ -284,6 +284,8 @@ int dvcp_sa_group_mlp_backward(int dtype, const void* xyz, int64_t sb, int64_t s
  * batch-norm backward sums of layer l (zero until known).
  * dvcp_sa_bn_stats: sums (2 x C_layer fp64) = per-channel sum z and sum z^2 of the conv output of
  *   `layer` (1-based) over all M entries, the layers below it normalised by their pack entries.
+ *   zrows (optional, layer = nlayer only): also write dvcp_sa_bn_zrows's output (every lower
+ *   layer's statistics are final by then), so the backward needs no z-row pass of its own.
  * dvcp_sa_bn_zrows: zrows (dvcp_sa_bn_zrows_floats floats) = every entry's conv output z_l of
  *   every layer, channel-major (C_l x M per layer, entry e = centre * nsample + slot), with the
  *   pack's final batch statistics; the backward reads them instead of recomputing the MLP.
@@ -314,7 +316,7 @@ int dvcp_sa_bn_stats(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t
                      int feat_dtype, const void* feat, int64_t fb, int64_t fd, int64_t fn, int D,
                      const int32_t* count, const int32_t* list, int nsample, int nlayer,
                      const int* chans, const float* pack, int layer, void* workspace,
-                     double* sums, void* stream);
+                     double* sums, float* zrows, void* stream);
 int dvcp_sa_bn_backward(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
                         const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
                         int feat_dtype, const void* feat, int64_t fb, int64_t fd, int64_t fn,
