@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round-3 evidence: every GPU test, smoke, the C3 bench (with CPU baseline) + stage report,
+# rocprofv3 kernel stats isolated (one batch in flight) and at the default 10 lanes, then the PMC
+# passes (FETCH, WRITE, COMPUTE; tools/gpu_pmc.sh).
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
+tag=${1:-r3n}
+ROOT="$GRAFT_REPO_ROOT"
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rfs \
+  > gpurun_out/${tag}_pytest_gpu.log 2>&1
+rc=$?
+echo "PYTEST_EXIT $rc" >> gpurun_out/${tag}_pytest_gpu.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.log 2>&1 || exit $?
+timeout -k 10 400 python bench.py --stage-report > gpurun_out/${tag}_bench.log 2>&1 || exit $?
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/${tag}_iso" -o run \
+  -- python3 "$ROOT/bench.py" --no-cpu-baseline --inflight 1 --steps 6 --warmup 2 > "$ROOT/gpurun_out/${tag}_iso.log" 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/${tag}_p10" -o run \
+  -- python3 "$ROOT/bench.py" --no-cpu-baseline > "$ROOT/gpurun_out/${tag}_p10.log" 2>&1 || exit $?
+bash "$ROOT/tools/gpu_pmc.sh" "${tag}"
