@@ -103,6 +103,37 @@ __device__ __forceinline__ float box_box_lb2(float alx, float aly, float alz, fl
   return (gx * gx + gy * gy) + gz * gz;
 }
 
+// Tile boxes at half precision, rounded outward (largest half <= lo, smallest half >= hi; NaN
+// and +-inf pass through): 8 bytes per corner pair instead of 32, and box_box_lb2 over the widened
+// box is still a lower bound of every computed d2 in the tile (the gaps are monotone in the box).
+__device__ __forceinline__ uint32_t half_down(float x) {
+  const _Float16 h = static_cast<_Float16>(x);
+  uint32_t hb = __builtin_bit_cast(uint16_t, h);
+  if (static_cast<float>(h) > x) hb = (hb & 0x8000u) ? hb + 1u : (hb == 0u ? 0x8001u : hb - 1u);
+  return hb;
+}
+__device__ __forceinline__ uint32_t half_up(float x) {
+  const _Float16 h = static_cast<_Float16>(x);
+  uint32_t hb = __builtin_bit_cast(uint16_t, h);
+  if (static_cast<float>(h) < x) hb = (hb & 0x8000u) ? (hb == 0x8000u ? 0x0001u : hb - 1u) : hb + 1u;
+  return hb;
+}
+__device__ __forceinline__ float half_lo(uint32_t w) {
+  return static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(w & 0xFFFFu)));
+}
+__device__ __forceinline__ float half_hi(uint32_t w) {
+  return static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(w >> 16)));
+}
+// {lo.x | lo.y << 16, lo.z | hi.x << 16, hi.y | hi.z << 16}
+__device__ __forceinline__ uint3 pack_hbox(const float4& lo, const float4& hi) {
+  return make_uint3(half_down(lo.x) | (half_down(lo.y) << 16), half_down(lo.z) | (half_up(hi.x) << 16),
+                    half_up(hi.y) | (half_up(hi.z) << 16));
+}
+__device__ __forceinline__ float hbox_lb2(const uint3& h, float ax, float ay, float az, float bx, float by, float bz) {
+  return box_box_lb2(ax, ay, az, bx, by, bz, half_lo(h.x), half_hi(h.x), half_lo(h.y), half_hi(h.y), half_lo(h.z),
+                     half_hi(h.z));
+}
+
 template <int CTRL, int ROWS>
 __device__ __forceinline__ uint32_t dpp_max_u(uint32_t v) {
   return max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, ROWS, 0xF, false)));
@@ -406,7 +437,7 @@ __device__ __forceinline__ void key_ce(uint32_t& ah, uint32_t& al, uint32_t& bh,
 }
 
 template <int R>
-__global__ __launch_bounds__(kTiledThreads) void knn_sel_query_kernel(const float4* __restrict__ sorted,
+__global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3))) void knn_sel_query_kernel(const float4* __restrict__ sorted,
                                                                       const float4* __restrict__ tbox,
                                                                       const int32_t* __restrict__ qperm, int M,
                                                                       const void* __restrict__ qry_raw, int64_t qb,
@@ -424,11 +455,12 @@ __global__ __launch_bounds__(kTiledThreads) void knn_sel_query_kernel(const floa
     bx = slot % static_cast<int>(gridDim.x);
   }
   const int T = (M + kTile - 1) / kTile;
-  __shared__ float4 sbox[2 * kMaxTiles];
+  // 12 + 32 KB of LDS (half-precision boxes, candidate buffers): three workgroups per CU
+  __shared__ uint3 hbox[kMaxTiles];
   __shared__ uint2 sbuf[kTiledThreads / kWave][kSelBufN][kWave];  // lane-private candidate buffers
   {
     const float4* tbg = tbox + static_cast<int64_t>(b) * T * 2;
-    for (int i = threadIdx.x; i < 2 * T; i += kTiledThreads) sbox[i] = tbg[i];
+    for (int i = threadIdx.x; i < T; i += kTiledThreads) hbox[i] = pack_hbox(tbg[2 * i], tbg[2 * i + 1]);
     __syncthreads();
   }
   const int sq = (bx * (kTiledThreads / kWave) + wave) * kWave + lane;
@@ -461,8 +493,7 @@ __global__ __launch_bounds__(kTiledThreads) void knn_sel_query_kernel(const floa
   for (int r = 0; r < R; ++r) {
     const int t = r * 64 + lane;
     if (t < T) {
-      const float4 lo = sbox[2 * t], hi = sbox[2 * t + 1];
-      const float lb = box_box_lb2(wl[0], wl[1], wl[2], wh[0], wh[1], wh[2], lo.x, lo.y, lo.z, hi.x, hi.y, hi.z);
+      const float lb = hbox_lb2(hbox[t], wl[0], wl[1], wl[2], wh[0], wh[1], wh[2]);
       keys[r] = (__float_as_uint(lb) & ~kTileIdBits) | static_cast<uint32_t>(t);
     } else {
       keys[r] = 0xFFFFFFFFu;
@@ -541,31 +572,31 @@ __global__ __launch_bounds__(kTiledThreads) void knn_sel_query_kernel(const floa
       const uint32_t key = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(keys[pos >> 6]), pos & 63));
       if (__uint_as_float(key & ~kTileIdBits) > wkth) break;  // every later tile is farther
       const int t = static_cast<int>(key & kTileIdBits);
-      const float4 lo = sbox[2 * t], hi = sbox[2 * t + 1];
-      const float lbq = box_box_lb2(qx, qy, qz, qx, qy, qz, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z);
+      const float lbq = hbox_lb2(hbox[t], qx, qy, qz, qx, qy, qz);
       const bool act = live & (lbq <= kth);
       if (__ballot(act) == 0) continue;
       const const_float* tp = (const const_float*)(P + t * kTile);
       float c[4 * kTile];
 #pragma unroll
       for (int u = 0; u < 4 * kTile; ++u) c[u] = tp[u];
-      float d2v[kTile];
+      // d2 is recomputed wherever it is needed (the same expression, the same bits) instead of
+      // being held in 16 VGPRs across the merge and the appends
+      auto d2_of = [&](int j) {
+        const float dx = c[4 * j] - qx, dy = c[4 * j + 1] - qy, dz = c[4 * j + 2] - qz;
+        return (dx * dx + dy * dy) + dz * dz;
+      };
       uint32_t cm = 0;
       // Filter on the distance alone, d2 <= kf: a superset of the keys below the k-th key (a tie
       // with a higher index is appended too and dropped by the merge, which orders full keys);
       // kf is finite, so inf and NaN (padding) never pass, as in dvcp_knn.
       const float kf = fminf(kth, __builtin_bit_cast(float, 0x7F7FFFFFu));
 #pragma unroll
-      for (int j = 0; j < kTile; ++j) {
-        const float dx = c[4 * j] - qx, dy = c[4 * j + 1] - qy, dz = c[4 * j + 2] - qz;
-        d2v[j] = (dx * dx + dy * dy) + dz * dz;
-        cm |= (act && d2v[j] <= kf) ? (1u << j) : 0u;
-      }
+      for (int j = 0; j < kTile; ++j) cm |= (act && d2_of(j) <= kf) ? (1u << j) : 0u;
       if (wave_umax_i(static_cast<uint32_t>(fill + __popc(cm))) > static_cast<uint32_t>(kSelBufN)) {
         merge();  // room for the whole tile; then re-filter against the new k-th key
         const float kf2 = fminf(kth, __builtin_bit_cast(float, 0x7F7FFFFFu));
 #pragma unroll
-        for (int j = 0; j < kTile; ++j) cm &= d2v[j] <= kf2 ? ~0u : ~(1u << j);
+        for (int j = 0; j < kTile; ++j) cm &= d2_of(j) <= kf2 ? ~0u : ~(1u << j);
       }
       // appends: only the points some lane takes (wave-uniform loop over the union of the masks)
       uint32_t u = wave_or_u32(cm);
@@ -573,7 +604,8 @@ __global__ __launch_bounds__(kTiledThreads) void knn_sel_query_kernel(const floa
         const int j = __builtin_ctz(u);
         u &= u - 1;
         if ((cm >> j) & 1u) {
-          mybuf[fill][lane] = make_uint2(__float_as_uint(d2v[j]), __float_as_uint(tp[4 * j + 3]));
+          const float dx = tp[4 * j] - qx, dy = tp[4 * j + 1] - qy, dz = tp[4 * j + 2] - qz;
+          mybuf[fill][lane] = make_uint2(__float_as_uint((dx * dx + dy * dy) + dz * dz), __float_as_uint(tp[4 * j + 3]));
           ++fill;
         }
       }

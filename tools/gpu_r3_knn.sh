@@ -2,7 +2,7 @@
 # kNN parity tests + C3 micro-benchmark.
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
 tag=${1:-r3k}
-timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_forward.py -m gpu -v --timeout 200 \
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_e2e.py -m gpu -v --timeout 200 \
   --timeout-method thread -rfs -k "knn" > gpurun_out/${tag}_pytest.log 2>&1
 rc=$?
 echo "PYTEST_EXIT $rc" >> gpurun_out/${tag}_pytest.log
