@@ -563,26 +563,41 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
     fill = 0;
   };
 
-  const float4* P = uniform_ptr(sorted + static_cast<int64_t>(b) * T * kTile);
+  // The next tile in the sorted order is fetched one position ahead, one float per lane (a tile is
+  // 16 points x 4 floats = 64 floats: one coalesced 256-byte load), so its latency hides behind
+  // the current tile; its coordinates reach every lane by readlane (SGPR operands).
+  const float* P = reinterpret_cast<const float*>(sorted) + static_cast<int64_t>(b) * T * kTile * 4;
+  uint32_t key_next = T > 0 ? static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(keys[0]), 0)) : 0u;
+  float v_next = T > 0 ? P[static_cast<int64_t>(key_next & kTileIdBits) * (4 * kTile) + lane] : 0.f;
   // one flat loop over the sorted tile order (not unrolled over the key registers: the merge is
   // large, and the key register is a wave-uniform indexed read)
 #pragma unroll 1
   for (int pos = 0; pos < T; ++pos) {
     {
-      const uint32_t key = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(keys[pos >> 6]), pos & 63));
+      const uint32_t key = key_next;
+      const float v_cur = v_next;
+      if (pos + 1 < T) {
+        key_next = static_cast<uint32_t>(
+            __builtin_amdgcn_readlane(static_cast<int>(keys[(pos + 1) >> 6]), (pos + 1) & 63));
+        v_next = P[static_cast<int64_t>(key_next & kTileIdBits) * (4 * kTile) + lane];
+      }
       if (__uint_as_float(key & ~kTileIdBits) > wkth) break;  // every later tile is farther
       const int t = static_cast<int>(key & kTileIdBits);
       const float lbq = hbox_lb2(hbox[t], qx, qy, qz, qx, qy, qz);
       const bool act = live & (lbq <= kth);
       if (__ballot(act) == 0) continue;
-      const const_float* tp = (const const_float*)(P + t * kTile);
-      float c[4 * kTile];
+      auto bc = [&](int u) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v_cur), u)); };
+      float c[3 * kTile];
 #pragma unroll
-      for (int u = 0; u < 4 * kTile; ++u) c[u] = tp[u];
+      for (int j = 0; j < kTile; ++j) {
+        c[3 * j] = bc(4 * j);
+        c[3 * j + 1] = bc(4 * j + 1);
+        c[3 * j + 2] = bc(4 * j + 2);
+      }
       // d2 is recomputed wherever it is needed (the same expression, the same bits) instead of
       // being held in 16 VGPRs across the merge and the appends
       auto d2_of = [&](int j) {
-        const float dx = c[4 * j] - qx, dy = c[4 * j + 1] - qy, dz = c[4 * j + 2] - qz;
+        const float dx = c[3 * j] - qx, dy = c[3 * j + 1] - qy, dz = c[3 * j + 2] - qz;
         return (dx * dx + dy * dy) + dz * dz;
       };
       uint32_t cm = 0;
@@ -604,8 +619,8 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
         const int j = __builtin_ctz(u);
         u &= u - 1;
         if ((cm >> j) & 1u) {
-          const float dx = tp[4 * j] - qx, dy = tp[4 * j + 1] - qy, dz = tp[4 * j + 2] - qz;
-          mybuf[fill][lane] = make_uint2(__float_as_uint((dx * dx + dy * dy) + dz * dz), __float_as_uint(tp[4 * j + 3]));
+          const float dx = bc(4 * j) - qx, dy = bc(4 * j + 1) - qy, dz = bc(4 * j + 2) - qz;
+          mybuf[fill][lane] = make_uint2(__float_as_uint((dx * dx + dy * dy) + dz * dz), __float_as_uint(bc(4 * j + 3)));
           ++fill;
         }
       }
