@@ -28,7 +28,9 @@ constexpr int kBoxBatch = 1;          // tiles whose boxes are read (LDS) and te
 struct TiledLayout {
   float4* sorted;  // B x T*64: x, y, z, original index bits (padding: NaN, index 0x7FFFFFFF)
   float4* tbox;    // B x T x 2: {lo.xyz, _}, {hi.xyz, _}
-  int32_t* qperm;  // B x Q: query index by Morton position
+  int32_t* qperm;  // B x Q: query index by curve position
+  uint32_t* qbins;  // B x kSortBins: the queries' cell counts, then their running positions
+  uint32_t* qbox;   // B x 8: ~float_order(lo.xyz), float_order(hi.xyz) of the queries (atomicMax)
 };
 
 inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
@@ -42,7 +44,97 @@ inline TiledLayout tiled_layout(void* ws, int B, int M, int Q) {
   L.tbox = reinterpret_cast<float4*>(p);
   p += align256(32 * int64_t(B) * T);
   L.qperm = reinterpret_cast<int32_t*>(p);
+  p += align256(4 * int64_t(B) * Q);
+  L.qbins = reinterpret_cast<uint32_t*>(p);  // qbins and qbox are one zeroed range
+  L.qbox = L.qbins + int64_t(B) * kSortBins;
   return L;
+}
+inline int64_t tiled_zeroed_bytes(int B) { return 4 * int64_t(B) * (kSortBins + 8); }
+
+// The queries' curve order is a counting sort spread over many workgroups (kQSortItems queries
+// each; one workgroup per cloud took ~0.15 ms at C3's 85184 queries): bounding box by atomicMax
+// on order keys, per-workgroup LDS histograms added into the cloud's bins, one scan per cloud,
+// then a scatter by atomicAdd on the running positions (the order inside a cell is arbitrary:
+// the permutation only shapes the query waves, never a result).
+constexpr int kQSortItems = 8192;
+
+template <typename CT>
+__device__ __forceinline__ void qry_point(const PointsView<CT>& qry, int b, int i, float (&v)[3]) {
+#pragma unroll
+  for (int a = 0; a < 3; ++a) v[a] = static_cast<float>(qry.at(b, a, i));  // knn_cuda's .float()
+}
+
+__device__ __forceinline__ CurveGrid qry_grid(const uint32_t* qbox, int b) {
+  float lo[3], hi[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    lo[a] = float_unorder(~qbox[b * 8 + a]);
+    hi[a] = float_unorder(qbox[b * 8 + 3 + a]);
+  }
+  return curve_grid(lo, hi);
+}
+
+template <typename CT>
+__global__ __launch_bounds__(kBuildThreads) void knn_qbox_kernel(PointsView<CT> qry, int Q, uint32_t* qbox) {
+  const int b = blockIdx.y, lane = threadIdx.x & 63;
+  const int i0 = blockIdx.x * kQSortItems, i1 = min(Q, i0 + kQSortItems);
+  float lo[3], hi[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    lo[a] = __builtin_huge_valf();
+    hi[a] = -__builtin_huge_valf();
+  }
+  for (int i = i0 + threadIdx.x; i < i1; i += kBuildThreads) {
+    float v[3];
+    qry_point(qry, b, i, v);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {  // fminf / fmaxf: NaN coordinates are ignored, as block_bbox
+      lo[a] = fminf(lo[a], v[a]);
+      hi[a] = fmaxf(hi[a], v[a]);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    for (int off = 32; off > 0; off >>= 1) {
+      lo[a] = fminf(lo[a], __shfl_xor(lo[a], off, kWave));
+      hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], off, kWave));
+    }
+    if (lane == 0) {
+      atomicMax(&qbox[b * 8 + a], ~float_order(lo[a]));
+      atomicMax(&qbox[b * 8 + 3 + a], float_order(hi[a]));
+    }
+  }
+}
+
+template <typename CT>
+__global__ __launch_bounds__(kBuildThreads) void knn_qhist_kernel(PointsView<CT> qry, int Q, const uint32_t* qbox,
+                                                                  uint32_t* qbins) {
+  __shared__ uint32_t bins[kSortBins];
+  const int b = blockIdx.y;
+  const int i0 = blockIdx.x * kQSortItems, i1 = min(Q, i0 + kQSortItems);
+  for (int i = threadIdx.x; i < kSortBins; i += kBuildThreads) bins[i] = 0u;
+  __syncthreads();
+  const CurveGrid g = qry_grid(qbox, b);
+  for (int i = i0 + threadIdx.x; i < i1; i += kBuildThreads) {
+    float v[3];
+    qry_point(qry, b, i, v);
+    atomicAdd(&bins[curve_cell(g, v)], 1u);
+  }
+  __syncthreads();
+  uint32_t* gb = qbins + static_cast<int64_t>(b) * kSortBins;
+  for (int i = threadIdx.x; i < kSortBins; i += kBuildThreads)
+    if (bins[i] != 0u) atomicAdd(&gb[i], bins[i]);
+}
+
+__global__ __launch_bounds__(kBuildThreads) void knn_qscan_kernel(uint32_t* qbins) {
+  __shared__ uint32_t bins[kSortBins];
+  __shared__ uint32_t wsum[16];
+  uint32_t* gb = qbins + static_cast<int64_t>(blockIdx.x) * kSortBins;
+  for (int i = threadIdx.x; i < kSortBins; i += kBuildThreads) bins[i] = gb[i];
+  __syncthreads();
+  block_scan_bins(bins, wsum);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kSortBins; i += kBuildThreads) gb[i] = bins[i];
 }
 
 template <typename CT>
@@ -52,17 +144,25 @@ __global__ __launch_bounds__(kBuildThreads) void knn_tiled_build_kernel(PointsVi
   __shared__ uint32_t boxk[kMaxTiles][6];  // order-preserving float keys: lo.xyz (min), hi.xyz (max)
   __shared__ uint32_t wsum[16];
   __shared__ float red[2][3][16];
-  const int b = blockIdx.x, tid = threadIdx.x;
+  const int b = blockIdx.y, tid = threadIdx.x;
+  if (blockIdx.x > 0) {  // the queries' scatter into curve order (the scanned bins are running positions)
+    const int i0 = (blockIdx.x - 1) * kQSortItems, i1 = min(Q, i0 + kQSortItems);
+    const CurveGrid g = qry_grid(L.qbox, b);
+    uint32_t* gb = L.qbins + static_cast<int64_t>(b) * kSortBins;
+    int32_t* qp = L.qperm + static_cast<int64_t>(b) * Q;
+    for (int i = i0 + tid; i < i1; i += kBuildThreads) {
+      float v[3];
+      qry_point(qry, b, i, v);
+      qp[atomicAdd(&gb[curve_cell(g, v)], 1u)] = i;
+    }
+    return;
+  }
   const int T = (M + kTile - 1) / kTile;
   float4* so = L.sorted + static_cast<int64_t>(b) * T * kTile;
   // knn_cuda casts both inputs with .float()
   auto get_ref = [&](int i, float (&v)[3]) {
 #pragma unroll
     for (int a = 0; a < 3; ++a) v[a] = static_cast<float>(ref.at(b, a, i));
-  };
-  auto get_qry = [&](int i, float (&v)[3]) {
-#pragma unroll
-    for (int a = 0; a < 3; ++a) v[a] = static_cast<float>(qry.at(b, a, i));
   };
   for (int i = tid; i < T * 6; i += kBuildThreads) boxk[i / 6][i % 6] = (i % 6) < 3 ? 0xFFFFFFFFu : 0u;
   float lo[3], hi[3];
@@ -86,11 +186,6 @@ __global__ __launch_bounds__(kBuildThreads) void knn_tiled_build_kernel(PointsVi
     tb[0] = make_float4(float_unorder(boxk[t][0]), float_unorder(boxk[t][1]), float_unorder(boxk[t][2]), 0.f);
     tb[1] = make_float4(float_unorder(boxk[t][3]), float_unorder(boxk[t][4]), float_unorder(boxk[t][5]), 0.f);
   }
-  // queries: Morton order over their own bounding box
-  block_bbox(Q, get_qry, lo, hi, red);
-  int32_t* qp = L.qperm + static_cast<int64_t>(b) * Q;
-  morton_sort(
-      Q, get_qry, [&](int pos, int i, const float (&)[3]) { qp[pos] = i; }, lo, hi, bins, wsum);
 }
 
 // Lower bound of the computed d2 between a point in box [a_lo, a_hi] and a point in box
@@ -648,7 +743,7 @@ extern "C" int64_t dvcp_knn_tiled_workspace_bytes(int B, int M, int Q) {
   if (B < 0 || M < 0 || Q < 0) return -1;
   const int64_t T = dvcp::ceil_div(M, dvcp::kTile);
   return dvcp::align256(16 * int64_t(B) * T * dvcp::kTile) + dvcp::align256(32 * int64_t(B) * T) +
-         dvcp::align256(4 * int64_t(B) * Q);
+         dvcp::align256(4 * int64_t(B) * Q) + dvcp::align256(dvcp::tiled_zeroed_bytes(B));
 }
 
 static int knn_tiled_impl(int dtype, const void* ref, int64_t rb, int64_t rc, int64_t rn, int M, const void* qry,
@@ -661,14 +756,29 @@ static int knn_tiled_impl(int dtype, const void* ref, int64_t rb, int64_t rc, in
   if (B == 0 || Q == 0) return DVCP_OK;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const dvcp::TiledLayout L = dvcp::tiled_layout(workspace, B, M, Q);
-  if (dtype == DVCP_F32)
-    hipLaunchKernelGGL((dvcp::knn_tiled_build_kernel<float>), dim3(B), dim3(dvcp::kBuildThreads), 0, st,
-                       dvcp::PointsView<float>{static_cast<const float*>(ref), rb, rc, rn}, M,
-                       dvcp::PointsView<float>{static_cast<const float*>(qry), qb, qc, qn}, Q, L);
-  else
-    hipLaunchKernelGGL((dvcp::knn_tiled_build_kernel<double>), dim3(B), dim3(dvcp::kBuildThreads), 0, st,
-                       dvcp::PointsView<double>{static_cast<const double*>(ref), rb, rc, rn}, M,
-                       dvcp::PointsView<double>{static_cast<const double*>(qry), qb, qc, qn}, Q, L);
+  // queries: bounding box, cell counts, scan, then the scatter beside the reference build
+  if (hipMemsetAsync(L.qbins, 0, dvcp::tiled_zeroed_bytes(B), st) != hipSuccess) {
+    dvcp::set_error("dvcp_knn_tiled: memset failed");
+    return DVCP_EHIP;
+  }
+  const dim3 qgrid(dvcp::ceil_div(Q, dvcp::kQSortItems), B), bgrid(1 + qgrid.x, B);
+  if (dtype == DVCP_F32) {
+    const dvcp::PointsView<float> qv{static_cast<const float*>(qry), qb, qc, qn};
+    hipLaunchKernelGGL((dvcp::knn_qbox_kernel<float>), qgrid, dim3(dvcp::kBuildThreads), 0, st, qv, Q, L.qbox);
+    hipLaunchKernelGGL((dvcp::knn_qhist_kernel<float>), qgrid, dim3(dvcp::kBuildThreads), 0, st, qv, Q, L.qbox,
+                       L.qbins);
+    hipLaunchKernelGGL(dvcp::knn_qscan_kernel, dim3(B), dim3(dvcp::kBuildThreads), 0, st, L.qbins);
+    hipLaunchKernelGGL((dvcp::knn_tiled_build_kernel<float>), bgrid, dim3(dvcp::kBuildThreads), 0, st,
+                       dvcp::PointsView<float>{static_cast<const float*>(ref), rb, rc, rn}, M, qv, Q, L);
+  } else {
+    const dvcp::PointsView<double> qv{static_cast<const double*>(qry), qb, qc, qn};
+    hipLaunchKernelGGL((dvcp::knn_qbox_kernel<double>), qgrid, dim3(dvcp::kBuildThreads), 0, st, qv, Q, L.qbox);
+    hipLaunchKernelGGL((dvcp::knn_qhist_kernel<double>), qgrid, dim3(dvcp::kBuildThreads), 0, st, qv, Q, L.qbox,
+                       L.qbins);
+    hipLaunchKernelGGL(dvcp::knn_qscan_kernel, dim3(B), dim3(dvcp::kBuildThreads), 0, st, L.qbins);
+    hipLaunchKernelGGL((dvcp::knn_tiled_build_kernel<double>), bgrid, dim3(dvcp::kBuildThreads), 0, st,
+                       dvcp::PointsView<double>{static_cast<const double*>(ref), rb, rc, rn}, M, qv, Q, L);
+  }
   if (int e = dvcp::launch_status("dvcp_knn_tiled(build)")) return e;
   const int T = dvcp::ceil_div(M, dvcp::kTile);
   const int qf64 = dtype == DVCP_F64;

@@ -106,59 +106,75 @@ __device__ void block_bbox(int n, GET get, float (&lo)[3], float (&hi)[3], float
   __syncthreads();
 }
 
+// The 16^3 curve grid over a bounding box, and an item's 12-bit Hilbert cell in it.
+struct CurveGrid {
+  float lo[3], scale[3];
+};
+__device__ __forceinline__ CurveGrid curve_grid(const float (&lo)[3], const float (&hi)[3]) {
+  CurveGrid g;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    g.lo[a] = lo[a];
+    g.scale[a] = hi[a] > lo[a] ? 16.0f / (hi[a] - lo[a]) : 0.0f;
+  }
+  return g;
+}
+__device__ __forceinline__ uint32_t curve_cell(const CurveGrid& g, const float (&v)[3]) {
+  uint32_t q[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    int c = static_cast<int>((v[a] - g.lo[a]) * g.scale[a]);
+    q[a] = static_cast<uint32_t>(c < 0 ? 0 : (c > 15 ? 15 : c));
+  }
+  return hilbert3x4(q[0], q[1], q[2]);
+}
+
+// In-place exclusive scan of the kSortBins counts in bins (1024 threads).
+__device__ __forceinline__ void block_scan_bins(uint32_t* bins, uint32_t* wsum) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int PER = kSortBins / kBuildThreads;
+  uint32_t c[PER], s = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    c[k] = bins[tid * PER + k];
+    s += c[k];
+  }
+  uint32_t incl = s;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t u = __shfl_up(incl, off, kWave);
+    if (lane >= off) incl += u;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t run = incl - s;
+  for (int w = 0; w < wave; ++w) run += wsum[w];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    bins[tid * PER + k] = run;
+    run += c[k];
+  }
+}
+
 // Counting sort of n items by 12-bit Hilbert cell over [lo, hi]; emit(pos, i, v) for each item.
 template <typename GET, typename EMIT>
 __device__ void morton_sort(int n, GET get, EMIT emit, const float (&lo)[3], const float (&hi)[3], uint32_t* bins,
                             uint32_t* wsum) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  float scale[3];
-#pragma unroll
-  for (int a = 0; a < 3; ++a) scale[a] = hi[a] > lo[a] ? 16.0f / (hi[a] - lo[a]) : 0.0f;
-  auto cell = [&](const float (&v)[3]) -> uint32_t {
-    uint32_t q[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      int c = static_cast<int>((v[a] - lo[a]) * scale[a]);
-      q[a] = static_cast<uint32_t>(c < 0 ? 0 : (c > 15 ? 15 : c));
-    }
-    return hilbert3x4(q[0], q[1], q[2]);
-  };
+  const int tid = threadIdx.x;
+  const CurveGrid g = curve_grid(lo, hi);
   for (int i = tid; i < kSortBins; i += kBuildThreads) bins[i] = 0u;
   __syncthreads();
   for (int i = tid; i < n; i += kBuildThreads) {
     float v[3];
     get(i, v);
-    atomicAdd(&bins[cell(v)], 1u);
+    atomicAdd(&bins[curve_cell(g, v)], 1u);
   }
   __syncthreads();
-  {
-    constexpr int PER = kSortBins / kBuildThreads;
-    uint32_t c[PER], s = 0;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      c[k] = bins[tid * PER + k];
-      s += c[k];
-    }
-    uint32_t incl = s;
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t u = __shfl_up(incl, off, kWave);
-      if (lane >= off) incl += u;
-    }
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    uint32_t run = incl - s;
-    for (int w = 0; w < wave; ++w) run += wsum[w];
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      bins[tid * PER + k] = run;
-      run += c[k];
-    }
-  }
+  block_scan_bins(bins, wsum);
   __syncthreads();
   for (int i = tid; i < n; i += kBuildThreads) {
     float v[3];
     get(i, v);
-    emit(static_cast<int>(atomicAdd(&bins[cell(v)], 1u)), i, v);
+    emit(static_cast<int>(atomicAdd(&bins[curve_cell(g, v)], 1u)), i, v);
   }
   __syncthreads();
 }
