@@ -143,14 +143,26 @@ __global__ void bq_pack_kernel(PointsView<float> pts, int N, float4* __restrict_
   packed[static_cast<int64_t>(b) * np + n] = v;
 }
 
-// One workgroup per cloud: packed rows, point tiles with boxes, centre Hilbert permutation.
+// Two workgroups per cloud: packed rows and point tiles with boxes; the centres' Hilbert permutation.
 __global__ __launch_bounds__(kBuildThreads) void bq_build_kernel(PointsView<float> pts, int N, PointsView<float> ctr,
                                                                  int S, BqLayout L, int tiled) {
   __shared__ uint32_t bins[kSortBins];
   __shared__ uint32_t boxk[kBqMaxTiles][6];  // float_order keys: lo.xyz (min), hi.xyz (max)
   __shared__ uint32_t wsum[16];
   __shared__ float red[2][3][16];
-  const int b = blockIdx.x, tid = threadIdx.x;
+  const int b = blockIdx.y, tid = threadIdx.x;
+  auto get_ctr = [&](int i, float (&v)[3]) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) v[a] = ctr.at(b, a, i);
+  };
+  float lo[3], hi[3];
+  if (blockIdx.x == 1) {  // the centres' curve order, beside the point work of block 0
+    block_bbox(S, get_ctr, lo, hi, red);
+    int32_t* cp = L.cperm + static_cast<int64_t>(b) * S;
+    morton_sort(
+        S, get_ctr, [&](int pos, int i, const float (&)[3]) { cp[pos] = i; }, lo, hi, bins, wsum);
+    return;
+  }
   const int np = bq_padded_n(N);
   float4* pk = L.packed + static_cast<int64_t>(b) * np;
   for (int i = tid; i < np; i += kBuildThreads) {
@@ -169,11 +181,6 @@ __global__ __launch_bounds__(kBuildThreads) void bq_build_kernel(PointsView<floa
 #pragma unroll
     for (int a = 0; a < 3; ++a) v[a] = pts.at(b, a, i);
   };
-  auto get_ctr = [&](int i, float (&v)[3]) {
-#pragma unroll
-    for (int a = 0; a < 3; ++a) v[a] = ctr.at(b, a, i);
-  };
-  float lo[3], hi[3];
   block_bbox(N, get_pt, lo, hi, red);
   morton_sort(
       N, get_pt,
@@ -197,10 +204,6 @@ __global__ __launch_bounds__(kBuildThreads) void bq_build_kernel(PointsView<floa
     tb[0] = make_float4(float_unorder(boxk[t][0]), float_unorder(boxk[t][1]), float_unorder(boxk[t][2]), 0.f);
     tb[1] = make_float4(float_unorder(boxk[t][3]), float_unorder(boxk[t][4]), float_unorder(boxk[t][5]), 0.f);
   }
-  block_bbox(S, get_ctr, lo, hi, red);
-  int32_t* cp = L.cperm + static_cast<int64_t>(b) * S;
-  morton_sort(
-      S, get_ctr, [&](int pos, int i, const float (&)[3]) { cp[pos] = i; }, lo, hi, bins, wsum);
 }
 
 __global__ __launch_bounds__(256) void bq_wave_kernel(const float4* __restrict__ packed, int N, PointsView<float> ctr,
@@ -306,120 +309,186 @@ __global__ __launch_bounds__(256) void bq_tiled_kernel(BqLayout L, int N, Points
     cz = ctr.at(b, 2, s);
   }
   const float ssc = sumsq3(cx, cy, cz);
-  // wave box of the centres; a non-finite centre needs every point
   const bool fin = __builtin_isfinite(cx) && __builtin_isfinite(cy) && __builtin_isfinite(cz);
   const float inf = __builtin_huge_valf();
-  const float wlx = wave_fmin(live ? (fin ? cx : -inf) : inf), whx = wave_fmax(live ? (fin ? cx : inf) : -inf);
-  const float wly = wave_fmin(live ? (fin ? cy : -inf) : inf), why = wave_fmax(live ? (fin ? cy : inf) : -inf);
-  const float wlz = wave_fmin(live ? (fin ? cz : -inf) : inf), whz = wave_fmax(live ? (fin ? cz : inf) : -inf);
-  const float ssc_max = wave_fmax(live && fin ? ssc : 0.0f);
-
-  uint32_t* mybm = bm[wave];
-  for (int i = lane; i < NW; i += 64) mybm[i] = 0u;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  const float4* tb = L.tbox + static_cast<int64_t>(b) * T * 2;
-  const float4* so = L.sorted + static_cast<int64_t>(b) * T * kBqTile;
-  for (int t0 = 0; t0 < T; t0 += 64) {
-    const int t = t0 + lane;
-    bool cand = false;
-    if (t < T) {
-      const float4 lo = tb[2 * t], hi = tb[2 * t + 1];
-      const float gx = bq_gap(lo.x, hi.x, wlx, whx), gy = bq_gap(lo.y, hi.y, wly, why), gz = bq_gap(lo.z, hi.z, wlz, whz);
-      const float lb2 = (gx * gx + gy * gy) + gz * gz;
-      cand = !(lb2 > bq_prune_thr(r2, ssc_max, box_ss_max(lo.x, lo.y, lo.z, hi.x, hi.y, hi.z)));
-    }
-    uint64_t mask = __ballot(cand);
-    while (mask) {
-      // up to four candidate tiles per pass, their loads in flight together
-      int tt[4];
+  // Lane groups.  A run of 64 curve-consecutive centres can straddle a jump of the curve (a few
+  // lanes' centres far from the rest): its box, and so the candidate union every lane scans, is
+  // then many times that of either part, and such waves set the kernel's duration (C3: median
+  // wave ~60 us, the slowest ~300 us with 10x the median's candidates, all in clouds with
+  // outliers).  The wave therefore looks for the best single cut of its lane range (the split
+  // minimising the summed r-expanded box volumes, by prefix and suffix box scans), keeps it when
+  // it saves 30 %, and tries once more inside each part: up to four lane groups, each running the
+  // bitmap pass and the scan for its own box while the other lanes idle.  A centre's list
+  // depends only on its own tests, so the grouping never changes a result.
+  int cut1 = -1, cut2 = -1, cut3 = -1;
+  if (__ballot(live && !fin) == 0) {  // (a non-finite centre needs every point anyway)
+    const float rr2 = 2.0f * sqrtf(r2);
+    const bool bl = live;
+    auto box_vol = [&](const float (&lo)[3], const float (&hi)[3]) {
+      return !(hi[0] >= lo[0]) ? 0.0f : ((hi[0] - lo[0] + rr2) * (hi[1] - lo[1] + rr2)) * (hi[2] - lo[2] + rr2);
+    };
+    // the best single cut of lanes [a, e): the first lane of the second part, or -1
+    auto best_cut = [&](int a, int e) -> int {
+      const bool in = bl && lane >= a && lane < e;
+      const float c3[3] = {cx, cy, cz};
+      float plo[3], phi[3], slo[3], shi[3];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        tt[u] = mask ? t0 + __builtin_ctzll(mask) : -1;
-        mask &= mask - 1;
+      for (int d = 0; d < 3; ++d) {
+        plo[d] = slo[d] = in ? c3[d] : inf;
+        phi[d] = shi[d] = in ? c3[d] : -inf;
       }
-      float4 q[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) q[u] = so[max(tt[u], 0) * kBqTile + lane];
+      for (int off = 1; off < 64; off <<= 1) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int idx = __float_as_int(q[u].w);
-        const float gx = bq_gap(q[u].x, q[u].x, wlx, whx), gy = bq_gap(q[u].y, q[u].y, wly, why),
-                    gz = bq_gap(q[u].z, q[u].z, wlz, whz);
-        const float lb2 = (gx * gx + gy * gy) + gz * gz;
-        const float ssp = ((q[u].x * q[u].x + q[u].y * q[u].y) + q[u].z * q[u].z) * (1.0f + 0x1p-20f);
-        // NaN coordinates give NaN bounds, which are kept (never "> thr")
-        if (tt[u] >= 0 && idx < N && !(lb2 > bq_prune_thr(r2, ssc_max, ssp)))
-          atomicOr(&mybm[idx >> 5], 1u << (idx & 31));
+        for (int d = 0; d < 3; ++d) {
+          const float ul = __shfl_up(plo[d], off, kWave), uh = __shfl_up(phi[d], off, kWave);
+          const float dl = __shfl_down(slo[d], off, kWave), dh = __shfl_down(shi[d], off, kWave);
+          if (lane >= off) {
+            plo[d] = fminf(plo[d], ul);
+            phi[d] = fmaxf(phi[d], uh);
+          }
+          if (lane + off < 64) {
+            slo[d] = fminf(slo[d], dl);
+            shi[d] = fmaxf(shi[d], dh);
+          }
+        }
       }
+      const float vp = box_vol(plo, phi);  // lanes a..lane
+      const float vs = box_vol(slo, shi);  // lanes lane..e-1
+      const float vprev = __shfl_up(vp, 1, kWave);
+      const float whole = __shfl(vp, 63, kWave);
+      const float cost = (lane > a && lane < e) ? vprev + vs : inf;
+      float m = cost;
+      for (int off = 32; off > 0; off >>= 1) m = fminf(m, __shfl_xor(m, off, kWave));
+      if (!(m < 0.7f * whole)) return -1;
+      return static_cast<int>(__builtin_ctzll(__ballot(cost == m)));
+    };
+    cut1 = best_cut(0, 64);
+    if (cut1 > 0) {
+      cut2 = best_cut(0, cut1);
+      cut3 = best_cut(cut1, 64);
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-
+  const int ngroups = 1 + (cut1 >= 0) + (cut2 >= 0) + (cut3 >= 0);
+  const int gid = (cut2 >= 0 && lane >= cut2) + (cut1 >= 0 && lane >= cut1) + (cut3 >= 0 && lane >= cut3);
+  uint32_t* mybm = bm[wave];
+  const float4* tb = L.tbox + static_cast<int64_t>(b) * T * 2;
+  const float4* so = L.sorted + static_cast<int64_t>(b) * T * kBqTile;
   const float4* pk = L.packed + static_cast<int64_t>(b) * np;
   const int64_t row = (static_cast<int64_t>(b) * S + s) * nsample;
   int cnt = live ? 0 : nsample;
   int first = N;
   float4* mypt = cpt[wave];
   int32_t* myid = cid[wave];
-  for (int c0 = 0; c0 < NW; c0 += 64) {
-    const uint32_t word = (c0 + lane < NW) ? mybm[c0 + lane] : 0u;
-    const int pc = __builtin_popcount(word);
-    int incl = pc;
+  for (int g = 0; g < ngroups; ++g) {
+    const bool act = live && gid == g;
+    if (__ballot(act) == 0) continue;
+    // the group's box; a non-finite centre needs every point
+    const float wlx = wave_fmin(act ? (fin ? cx : -inf) : inf), whx = wave_fmax(act ? (fin ? cx : inf) : -inf);
+    const float wly = wave_fmin(act ? (fin ? cy : -inf) : inf), why = wave_fmax(act ? (fin ? cy : inf) : -inf);
+    const float wlz = wave_fmin(act ? (fin ? cz : -inf) : inf), whz = wave_fmax(act ? (fin ? cz : inf) : -inf);
+    const float ssc_max = wave_fmax(act && fin ? ssc : 0.0f);
+
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int i = lane; i < NW; i += 64) mybm[i] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int t0 = 0; t0 < T; t0 += 64) {
+      const int t = t0 + lane;
+      bool cand = false;
+      if (t < T) {
+        const float4 lo = tb[2 * t], hi = tb[2 * t + 1];
+        const float gx = bq_gap(lo.x, hi.x, wlx, whx), gy = bq_gap(lo.y, hi.y, wly, why), gz = bq_gap(lo.z, hi.z, wlz, whz);
+        const float lb2 = (gx * gx + gy * gy) + gz * gz;
+        cand = !(lb2 > bq_prune_thr(r2, ssc_max, box_ss_max(lo.x, lo.y, lo.z, hi.x, hi.y, hi.z)));
+      }
+      uint64_t mask = __ballot(cand);
+      while (mask) {
+        // up to four candidate tiles per pass, their loads in flight together
+        int tt[4];
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int u = __shfl_up(incl, off, kWave);
-      if (lane >= off) incl += u;
+        for (int u = 0; u < 4; ++u) {
+          tt[u] = mask ? t0 + __builtin_ctzll(mask) : -1;
+          mask &= mask - 1;
+        }
+        float4 q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) q[u] = so[max(tt[u], 0) * kBqTile + lane];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int idx = __float_as_int(q[u].w);
+          const float gx = bq_gap(q[u].x, q[u].x, wlx, whx), gy = bq_gap(q[u].y, q[u].y, wly, why),
+                      gz = bq_gap(q[u].z, q[u].z, wlz, whz);
+          const float lb2 = (gx * gx + gy * gy) + gz * gz;
+          const float ssp = ((q[u].x * q[u].x + q[u].y * q[u].y) + q[u].z * q[u].z) * (1.0f + 0x1p-20f);
+          // NaN coordinates give NaN bounds, which are kept (never "> thr")
+          if (tt[u] >= 0 && idx < N && !(lb2 > bq_prune_thr(r2, ssc_max, ssp)))
+            atomicOr(&mybm[idx >> 5], 1u << (idx & 31));
+        }
+      }
     }
-    const int total = __shfl(incl, 63, kWave);
-    const int excl = incl - pc;
-    for (int base = 0; base < total; base += kBqCap) {
-      // this round's candidates (positions [base, base + kBqCap) in index order): indices first,
-      // then the points gathered cooperatively (several loads in flight per lane)
-      int p = excl;
-      uint32_t wd = word;
-      while (wd && p < base + kBqCap) {
-        const int bit = __builtin_ctz(wd);
-        wd &= wd - 1;
-        if (p >= base) myid[p - base] = (c0 + lane) * 32 + bit;
-        ++p;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+
+    for (int c0 = 0; c0 < NW; c0 += 64) {
+      const uint32_t word = (c0 + lane < NW) ? mybm[c0 + lane] : 0u;
+      const int pc = __builtin_popcount(word);
+      int incl = pc;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int u = __shfl_up(incl, off, kWave);
+        if (lane >= off) incl += u;
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      const int nc = min(kBqCap, total - base);
+      const int total = __shfl(incl, 63, kWave);
+      const int excl = incl - pc;
+      for (int base = 0; base < total; base += kBqCap) {
+        // this round's candidates (positions [base, base + kBqCap) in index order): indices first,
+        // then the points gathered cooperatively (several loads in flight per lane)
+        int p = excl;
+        uint32_t wd = word;
+        while (wd && p < base + kBqCap) {
+          const int bit = __builtin_ctz(wd);
+          wd &= wd - 1;
+          if (p >= base) myid[p - base] = (c0 + lane) * 32 + bit;
+          ++p;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const int nc = min(kBqCap, total - base);
 #pragma unroll
-      for (int u = 0; u < kBqCap / 64; ++u) {
-        const int j = u * 64 + lane;
-        if (j < nc) mypt[j] = pk[myid[j]];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      for (int j0 = 0; j0 < nc; j0 += 64) {
-        const int je = min(nc, j0 + 64);
-        for (int j1 = j0; j1 < je; j1 += 8) {
-          float4 q[8];
+        for (int u = 0; u < kBqCap / 64; ++u) {
+          const int j = u * 64 + lane;
+          if (j < nc) mypt[j] = pk[myid[j]];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (int j0 = 0; j0 < nc; j0 += 64) {
+          const int je = min(nc, j0 + 64);
+          for (int j1 = j0; j1 < je; j1 += 8) {
+            float4 q[8];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) q[u] = mypt[j1 + u];  // j1 + 7 < kBqCap
+            for (int u = 0; u < 8; ++u) q[u] = mypt[j1 + u];  // j1 + 7 < kBqCap
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const float d2 = expansion_d2(dot3_blas(cx, cy, cz, q[u].x, q[u].y, q[u].z), ssc, q[u].w);
-            if ((j1 + u < je) & !(d2 > r2) & (cnt < nsample)) {
-              const int n = myid[j1 + u];
-              first = cnt == 0 ? n : first;
-              if (list) list[row + cnt] = n;
-              if (padded) padded[row + cnt] = n;
-              ++cnt;
+            for (int u = 0; u < 8; ++u) {
+              const float d2 = expansion_d2(dot3_blas(cx, cy, cz, q[u].x, q[u].y, q[u].z), ssc, q[u].w);
+              if (act & (j1 + u < je) & !(d2 > r2) & (cnt < nsample)) {
+                const int n = myid[j1 + u];
+                first = cnt == 0 ? n : first;
+                if (list) list[row + cnt] = n;
+                if (padded) padded[row + cnt] = n;
+                ++cnt;
+              }
             }
           }
+          if (__ballot(act && cnt < nsample) == 0) goto group_done;
         }
-        if (__ballot(cnt < nsample) == 0) goto done;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      __builtin_amdgcn_wave_barrier();
     }
+  group_done:;
   }
-done:
   if (!live) return;
   if (count) count[static_cast<int64_t>(b) * S + s] = cnt;
   if (padded)
@@ -450,7 +519,7 @@ static int launch_bq(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
     if (workspace) {
       const BqLayout L = bq_layout(workspace, B, N, S);
       const int tiled = N <= kBqMaxTiles * kBqTile;
-      hipLaunchKernelGGL(bq_build_kernel, dim3(B), dim3(kBuildThreads), 0, st, pv, N, cv, S, L, tiled);
+      hipLaunchKernelGGL(bq_build_kernel, dim3(tiled ? 2 : 1, B), dim3(kBuildThreads), 0, st, pv, N, cv, S, L, tiled);
       if (int e = launch_status("dvcp_ball_query(build)")) return e;
       if (tiled)
         hipLaunchKernelGGL(N <= kBqSmallTiles * kBqTile ? bq_tiled_kernel<kBqSmallTiles> : bq_tiled_kernel<kBqMaxTiles>,
