@@ -205,17 +205,51 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
     q0 = static_cast<int64_t>(blockIdx.x) * kMfmaWaves + wave;
     qs = static_cast<int64_t>(gridDim.x) * kMfmaWaves;
   }
-  for (int64_t ql = q0; ql < total; ql += qs) {
-    const int64_t q = xcd ? (xo + 8 * (ql / S)) * static_cast<int64_t>(S) + ql % S : ql;
-    // centre in curve order when `order` is given: consecutive waves then gather the U / point
-    // rows of one spatial neighbourhood, which stay in L2 instead of being fetched again
-    const int b = static_cast<int>(q / S);
-    const int c = order ? order[q] : static_cast<int>(q % S);
-    const int64_t fc = static_cast<int64_t>(b) * S + c;
-    int rows = count[fc];
-    rows = rows < 1 ? 1 : (rows > nsample ? nsample : rows);
-    const int32_t* lst = list + fc * nsample;
-    const T cx = ctr.at(b, 0, c), cy = ctr.at(b, 1, c), cz = ctr.at(b, 2, c);
+  // The wave's centres are ql = q0, q0 + qs, ...: their metadata (order, count, centre) is
+  // loaded 64 centres at a time, one per lane, and read back by readlane, so a centre's first
+  // tile waits only for its list entries (fetched one tile ahead) and its U rows.
+  auto lane_bcast = [](auto v, int j) {
+    if constexpr (sizeof(v) == 8) {
+      const int64_t u = __builtin_bit_cast(int64_t, v);
+      const int lo = __builtin_amdgcn_readlane(static_cast<int>(u & 0xFFFFFFFF), j);
+      const int hi = __builtin_amdgcn_readlane(static_cast<int>(u >> 32), j);
+      return __builtin_bit_cast(decltype(v), (static_cast<int64_t>(hi) << 32) | static_cast<uint32_t>(lo));
+    } else {
+      return __builtin_bit_cast(decltype(v), __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), j));
+    }
+  };
+  for (int64_t qc = q0; qc < total; qc += 64 * qs) {
+    const int64_t qm = qc + lane * qs;
+    int m_b = 0, m_rows = 1;
+    int64_t m_fc = 0;
+    T m_cx = T(0), m_cy = T(0), m_cz = T(0);
+    if (qm < total) {
+      const int64_t q = xcd ? (xo + 8 * (qm / S)) * static_cast<int64_t>(S) + qm % S : qm;
+      // centre in curve order when `order` is given: consecutive waves then gather the U / point
+      // rows of one spatial neighbourhood, which stay in L2 instead of being fetched again
+      m_b = static_cast<int>(q / S);
+      const int c = order ? order[q] : static_cast<int>(q % S);
+      m_fc = static_cast<int64_t>(m_b) * S + c;
+      const int r = count[m_fc];
+      m_rows = r < 1 ? 1 : (r > nsample ? nsample : r);
+      m_cx = ctr.at(m_b, 0, c);
+      m_cy = ctr.at(m_b, 1, c);
+      m_cz = ctr.at(m_b, 2, c);
+    }
+    const int ncen = static_cast<int>(min<int64_t>(64, (total - qc + qs - 1) / qs));
+    // list entry of this lane's point in the next tile to run (centre j, tile n0)
+    auto list_entry = [&](int j, int n0) {
+      const int64_t fcj = lane_bcast(m_fc, j);
+      const int rj = lane_bcast(m_rows, j);
+      const int row = n0 + r32;
+      return list[fcj * nsample + (row < rj ? row : 0)];
+    };
+    int n_next = list_entry(0, 0);
+  for (int j = 0; j < ncen; ++j) {
+    const int b = lane_bcast(m_b, j);
+    const int64_t fc = lane_bcast(m_fc, j);
+    const int rows = lane_bcast(m_rows, j);
+    const T cx = lane_bcast(m_cx, j), cy = lane_bcast(m_cy, j), cz = lane_bcast(m_cz, j);
     float mx[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) mx[ct] = 0.0f;  // post-ReLU values are >= +0
@@ -227,8 +261,11 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
       int zo = 0;
       asm volatile("" : "+v"(zo));
       // B fragment of layer 1: this lane's point (r32) and its half of the input channels
-      const int row = n0 + r32;
-      const int n = lst[row < rows ? row : 0];
+      const int n = n_next;
+      if (n0 + 32 < rows)
+        n_next = list_entry(j, n0 + 32);
+      else if (j + 1 < ncen)
+        n_next = list_entry(j + 1, 0);
       f32x16 acc1[MT];
       if constexpr (PRE) {
         // accumulators start from U[n] (channels (r&3) + 8(r>>2) + 4h of each 32-channel tile)
@@ -322,6 +359,7 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
       const float m = fmaxf(mx[ct], __shfl_xor(mx[ct], 32, kWave));
       if (h == 0) out[fc * C2 + 32 * ct + r32] = m;
     }
+  }
   }
 }
 

@@ -44,7 +44,8 @@ def main():
             ms = e0.elapsed_time(e1) / reps
             rows = count.clamp(1, ns).sum().item()
             macs = sum(a * b for a, b in zip(sa.chans[:-1], sa.chans[1:]))
-            print(f"sa{li + 1}: {ms:.4f} ms/call  rows {rows}  {2 * macs * rows / ms / 1e9:.1f} TFLOP/s", flush=True)
+            print(f"sa{li + 1}: {ms:.4f} ms/call  rows {rows}  {2 * macs * rows / ms / 1e9:.1f} TFLOP/s  "
+                  f"checksum {out.double().sum().item():.12e}", flush=True)
             if sa.npoint >= n_l:
                 out = torch.gather(out, 1, i.unsqueeze(-1).expand(-1, -1, out.shape[2]))
             pts_l, f = c, out.permute(0, 2, 1)
