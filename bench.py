@@ -55,6 +55,7 @@ import torch.distributed as dist  # noqa: E402
 
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
 PEAK_FP32_TFLOPS = 157.3   # fp32 vector = fp32 MFMA dense rate
+PEAK_BF16_TFLOPS = 16 * PEAK_FP32_TFLOPS   # bf16 MFMA dense rate (the SA layer 2's split pieces)
 PEAK_HBM_GBS = 8000.0
 N_CU = 256
 
@@ -249,7 +250,8 @@ def _per_kernel(log):
     out = {}
     for name, e0, e1, w in log:
         d = out.setdefault(name, {"n": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0, "exec_flops": 0.0,
-                                  "mfma_flops": 0.0, "exec_known": True, "wgs": None, "steps": 0})
+                                  "mfma_flops": 0.0, "bf16_alg": 0.0, "bf16_hw": 0.0, "exec_known": True,
+                                  "wgs": None, "steps": 0})
         d["n"] += 1
         d["ms"] += e0.elapsed_time(e1)
         w = tuple(w or ()) + (None,) * 5
@@ -261,9 +263,12 @@ def _per_kernel(log):
         if ex is None:
             d["exec_known"] = False
         else:
-            tot, mf = (ex, 0.0) if isinstance(ex, (int, float)) else ex
+            ex = (ex,) if isinstance(ex, (int, float)) else tuple(ex)
+            tot, mf, b_alg, b_hw = ex + (0.0,) * (4 - len(ex))
             d["exec_flops"] += tot
             d["mfma_flops"] += mf
+            d["bf16_alg"] += b_alg
+            d["bf16_hw"] += b_hw
         if w[3] is not None:
             d["wgs"] = w[3]
             d["steps"] += w[4]
@@ -304,7 +309,9 @@ def stage_roofline(iso, iso_steps, ms_step):
         t_byte = v["bytes"] / iso_steps / (PEAK_HBM_GBS * 1e9) * 1e3
         t_ref = v["flops"] / iso_steps / (PEAK_FP32_TFLOPS * 1e12) * 1e3
         known = v["exec_known"] and v["exec_flops"] > 0
-        t_exec = v["exec_flops"] / iso_steps / (PEAK_FP32_TFLOPS * 1e12) * 1e3 if known else None
+        # executed work at its pipe's peak: the bf16 pieces of the SA layer 2 at the bf16 MFMA rate
+        t_exec = ((v["exec_flops"] - v["bf16_alg"]) / (PEAK_FP32_TFLOPS * 1e12)
+                  + v["bf16_hw"] / (PEAK_BF16_TFLOPS * 1e12)) / iso_steps * 1e3 if known else None
         t_work = t_exec if known else t_ref
         ceil, bound = (t_work, "fp32") if t_work >= t_byte else (t_byte, "hbm")
         if bound == "fp32" and known and v["mfma_flops"] > 0.5 * v["exec_flops"]:
@@ -325,7 +332,8 @@ def stage_roofline(iso, iso_steps, ms_step):
         if st["frac_of_ceiling"] is not None and st["frac_of_ceiling"] > 1.0:
             st["ceiling_note"] = "ceiling above the measured time: the counted work exceeds what the kernel runs"
         stages[k] = st
-    roof = {"formula": "sum_s max(bytes_s / 8 TB/s, executed flops_s / 157.3 TF/s) / ms_per_step; "
+    roof = {"formula": "sum_s max(bytes_s / 8 TB/s, executed flops_s / 157.3 TF/s (the SA layer 2's bf16 split "
+                       "pieces at 2516.8 TF/s)) / ms_per_step; "
                        "stages without an executed count use their reference-graph flops",
             "ceiling_device_ms_per_step": round(ideal_dev, 4), "measured_device_ms_per_step_isolated": round(meas_dev, 4),
             "ms_per_step": round(ms_step, 4), "achieved_frac": round(ideal_dev / ms_step, 4),
@@ -349,7 +357,11 @@ def dominant_roofline(live, iso, stages, pmc):
     if st["bound"] == "hbm":
         achieved, peak, unit = v["bytes"] / v["n"] / (launch_ms * 1e-3) / 1e9, PEAK_HBM_GBS, "GB/s"
     else:
-        achieved, peak, unit = flops / v["n"] / (launch_ms * 1e-3) / 1e12, PEAK_FP32_TFLOPS * share, "TFLOP/s"
+        # the peak of this kernel's pipe mix: fp32 work at 157.3 TF/s, the bf16 pieces of the SA
+        # layer 2 (6 bf16 products per fp32-equivalent product) at the bf16 MFMA rate
+        t_peak = (flops - v["bf16_alg"]) / PEAK_FP32_TFLOPS + v["bf16_hw"] / PEAK_BF16_TFLOPS if known else None
+        peak_eff = flops / t_peak if t_peak else PEAK_FP32_TFLOPS
+        achieved, peak, unit = flops / v["n"] / (launch_ms * 1e-3) / 1e12, peak_eff * share, "TFLOP/s"
     w = live.get(name)
     p = pmc.get(name, {})
     return {"bound": "hbm" if st["bound"] == "hbm" else "mfma",
@@ -364,7 +376,9 @@ def dominant_roofline(live, iso, stages, pmc):
             "note": "dominant = largest device time per step (duration x CU share), one batch in flight; "
                     "achieved = executed flops (reference-graph flops if not counted) per launch / average "
                     "isolated launch time; peak = fp32 157.3 TF/s x the grid's CU share (fp32 MFMA = fp32 "
-                    "VALU rate on gfx950) or 8 TB/s; traffic = PMC HBM bytes per launch"}
+                    "VALU rate on gfx950; for the SA tables the fp32-equivalent rate of their pipe mix: the "
+                    "layer-2 split pieces at the 2516.8 TF/s bf16 MFMA rate, 6 per fp32-equivalent product) "
+                    "or 8 TB/s; traffic = PMC HBM bytes per launch"}
 
 
 def fps_roofline(live, iso, floor_us, pmc):

@@ -517,6 +517,12 @@ constexpr int kSelMin = 16;
 constexpr int kSelMaxScans = 8;  // rescans per round before the fallback (a guard)
 constexpr int kSelAccept = 64;   // centres accepted per round at most
 
+// this lane's index, computed where it is used (an opaque v_mbcnt pair the compiler cannot hoist)
+__device__ __forceinline__ int fresh_lane() {
+  int r;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(r));
+  return r;
+}
 __device__ __forceinline__ int sel_shift(uint32_t range) {  // smallest s with (range >> s) < kSelBins
   return range < kSelBins ? 0 : (32 - __clz(range)) - 8;
 }
@@ -534,6 +540,10 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
                                                                  unsigned long long* __restrict__ prof) {
   constexpr int W = THREADS / kWave;
   static_assert(PPT <= 32 && kSelMax == 128 && (THREADS == 512 || THREADS == 1024), "layout");
+  // group lanes: lane l holds the box and exact maximum of the wave's group p = l % GP, replicated
+  // over the QC = 64 / GP lane blocks, so one update test covers QC (centre, group) pairs per group
+  constexpr int GP = PPT <= 2 ? 2 : PPT <= 4 ? 4 : PPT <= 8 ? 8 : PPT <= 16 ? 16 : 32;
+  constexpr int QC = kWave / GP;
   __shared__ uint32_t bins[kMortonBins];  // setup; then the list's values [0, kSelCap) and positions
   __shared__ uint16_t perm[THREADS * PPT];
   __shared__ T red[2][3][W];
@@ -548,20 +558,24 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
   __shared__ int prank[W][kSelMax];  // per wave's i-range: count of preceding candidates | touched << 16
   __shared__ float wtf[W], wT[W];
   __shared__ uint32_t wpid[W];
+  __shared__ T acx[kSelAccept], acy[kSelAccept], acz[kSelAccept];  // the round's accepted centres, rank order
+  __shared__ T gbox[W][6][GP];  // group boxes, read back per round by the update (not held in VGPRs)
   __shared__ uint32_t na_cnt, cand_fill;
   float* lv = reinterpret_cast<float*>(bins);
   uint32_t* lpos = bins + kSelCap;
 
-  const int b = blockIdx.x, tid = threadIdx.x, lane_outer = tid & 63, lane = lane_outer, wave = tid >> 6;
+  const int b = blockIdx.x, tid = threadIdx.x, lane_outer = tid & 63, lane = lane_outer;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: its LDS addresses stay in SGPRs
   fps_morton_sort<T, THREADS>(pts, b, N, bins, perm, red, wsum);
 
   T px[PPT], py[PPT], pz[PPT];
   float dmin[PPT];
-  T gb[6], wb[6];  // lane p < PPT: box of group (wave, p); the wave's box (uniform)
+  T gb[6];  // lane l: box of group (wave, l % GP)
+  const int gl = lane & (GP - 1);  // this lane's group
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
-    gb[a] = wb[a] = static_cast<T>(__builtin_huge_val());
-    gb[3 + a] = wb[3 + a] = -static_cast<T>(__builtin_huge_val());
+    gb[a] = static_cast<T>(__builtin_huge_val());
+    gb[3 + a] = -static_cast<T>(__builtin_huge_val());
   }
 #pragma unroll 1
   for (int p = 0; p < PPT; ++p) {
@@ -583,21 +597,21 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
         l[a] = ol < l[a] ? ol : l[a];
         h[a] = oh > h[a] ? oh : h[a];
       }
-      wb[a] = l[a] < wb[a] ? l[a] : wb[a];
-      wb[3 + a] = h[a] > wb[3 + a] ? h[a] : wb[3 + a];
-      gb[a] = lane == p ? l[a] : gb[a];
-      gb[3 + a] = lane == p ? h[a] : gb[3 + a];
+      gb[a] = gl == p ? l[a] : gb[a];
+      gb[3 + a] = gl == p ? h[a] : gb[3 + a];
     }
   }
+  const bool grp = gl < PPT && (gl * W + wave) * kWave < N;  // lane l: a non-empty group
+  if (lane < GP) {
 #pragma unroll
-  for (int a = 0; a < 6; ++a) wb[a] = readfirstlane_t(wb[a]);
-  const bool grp = lane < PPT && (lane * W + wave) * kWave < N;  // lane p: a non-empty group
+    for (int a = 0; a < 6; ++a) gbox[wave][a][lane] = gb[a];
+  }
 
   int64_t* oi = out_idx + static_cast<int64_t>(b) * npoint;
   T* ox = out_xyz ? out_xyz + static_cast<int64_t>(b) * 3 * npoint : nullptr;
   int64_t cur = start[b];
   if (cur < 0 || cur >= N) cur = 0;  // host validates; keep the kernel in bounds regardless
-  float gub, wub, vmax;
+  float gub, vmax;
   {
     const T cx = pts.at(b, 0, cur), cy = pts.at(b, 1, cur), cz = pts.at(b, 2, cur);
     if (tid == 0) {
@@ -619,10 +633,9 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
 #pragma unroll 1
     for (int p = 0; p < PPT; ++p) {
       const float gm = wave_fmax_nn(fmaxf(dmin[p], 0.f));
-      gub = lane == p ? gm : gub;
+      gub = gl == p ? gm : gub;
     }
     gub = grp ? gub : -1.0f;
-    wub = wave_fmax_nn(fmaxf(gub, 0.f));
     m = wave_fmax_nn(fmaxf(m, 0.f));
     if (lane == 0) wtf[wave] = m;
   }
@@ -651,20 +664,15 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
     }
   };
   while (step < npoint) {
-    // The lane index laundered through an empty asm once per round: the round's LDS addresses are
-    // then recomputed from it (a few VALU ops) instead of being hoisted out of the loop as ~40
-    // lane-dependent constants, which at 1024 threads (128 VGPRs) were spilled to scratch.
-    int lane_r = lane_outer;
-    asm volatile("" : "+v"(lane_r));
-    const int lane = lane_r;
+    // The lane index is re-materialised (v_mbcnt in a volatile asm, fresh_lane) at the start of
+    // each scan and of the update: the round's LDS addresses are then recomputed from it (a few
+    // VALU ops) instead of being hoisted out of the loop as ~40 lane-dependent constants, and no
+    // lane register stays live across the round -- at 1024 threads (128 VGPRs) both were spilled.
     ++n_round;
     int kstar = 0;
-    uint64_t acc0 = 0, acc1 = 0;  // accepted candidates (slots 0-63, 64-127)
     bool raised = false;
     for (int scan = 0;; ++scan) {
-      int lane_s = lane_outer;  // laundered again per scan (see the round loop)
-      asm volatile("" : "+v"(lane_s));
-      const int lane = lane_s;
+      const int lane = fresh_lane();  // (see the round loop)
       ++n_scan;
       tick(-1);
       // ---- 1. scan: list the points above f, histogram their float bits over (f, vmax] ----------
@@ -805,7 +813,8 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
       if (mode == 2) {
         // ---- fallback: one exact argmax (value desc, original index asc) over every point ------
         ++n_fallback;
-        float bv = -1.0f;
+        float bv = -1.0f;  // opaque: the max over dmin is formed here, not hoisted out of the scan loop
+        asm volatile("" : "+v"(bv));
 #pragma unroll
         for (int p = 0; p < PPT; ++p) bv = fmaxf(bv, dmin[p]);
         bv = wave_fmax_nn(fmaxf(bv, 0.f));
@@ -833,9 +842,9 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
         for (int w = 1; w < W; ++w) gp = min(gp, wpid[w]);
         if (tid == 0) {
           const T gx = pts.at(b, 0, gp), gy = pts.at(b, 1, gp), gz = pts.at(b, 2, gp);
-          cxx[0] = gx;
-          cyy[0] = gy;
-          czz[0] = gz;
+          acx[0] = gx;
+          acy[0] = gy;
+          acz[0] = gz;
           oi[step] = static_cast<int64_t>(gp);
           if (ox) {
             ox[step] = gx;
@@ -845,8 +854,6 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
         }
         lds_barrier();
         kstar = 1;
-        acc0 = 1ull;
-        acc1 = 0ull;
         vmax = gmax;  // every value is <= gmax; the new centre's drops to 0
         break;
       }
@@ -883,10 +890,8 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
       float Tb = wT[0];
 #pragma unroll
       for (int w = 1; w < W; ++w) Tb = fmaxf(Tb, wT[w]);
-      if (tid == 0) {
-        na_cnt = 0u;
-        cand_fill = 0u;
-      }
+      if (tid == 0) na_cnt = 0u;  // (two waves: two 32-bit stores, not one 64-bit pair held across rounds)
+      if (tid == kWave) cand_fill = 0u;
       for (int i = tid; i < kSelBins; i += THREADS) hist[i] = 0u;
       tick(1);
       // ---- 4. rank and prefix test in one pass over candidate pairs ----------------------------
@@ -903,7 +908,9 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
           const int p0 = cpid[j0], p1 = cpid[j1];
           const T x0 = cxx[j0], y0 = cyy[j0], z0 = czz[j0];
           const T x1 = cxx[j1], y1 = cyy[j1], z1 = czz[j1];
-#pragma unroll
+          // rolled at PPT 16 x 1024 threads (128 VGPRs): one batch of four candidates live at a time
+          constexpr int kPairUnroll = PPT >= 16 && THREADS == 1024 ? 1 : kSelMax / W / 4;
+#pragma unroll kPairUnroll
           for (int c4 = 0; c4 < kSelMax / W / 4; ++c4) {
             const int i0 = i_lo + 4 * c4;
             if (i0 >= cnt) break;  // wave-uniform
@@ -963,8 +970,17 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
       }
       kstar = static_cast<int>(min(min(wave_umin(failr), static_cast<uint32_t>(cnt)),
                                    static_cast<uint32_t>(kSelAccept)));
-      acc0 = __ballot(rk[0] < kstar);
-      acc1 = __ballot(rk[1] < kstar);
+      // the accepted centres in rank order, for the update: every wave writes the same values
+      // (its own reads below follow its own writes in LDS order)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int jj = hh * 64 + lane;
+        if (rk[hh] < kstar) {
+          acx[rk[hh]] = cxx[jj];
+          acy[rk[hh]] = cyy[jj];
+          acz[rk[hh]] = czz[jj];
+        }
+      }
       // upper bound of every running minimum after this round: T, and the listed not accepted
       float vm = Tb;
 #pragma unroll
@@ -992,27 +1008,26 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
     }
     // ---- the update: apply the accepted centres ----------------------------------------------
     tick(-1);
+    // Lane l tests its group l % GP against centre c0 + l / GP: QC (centre, group) pairs per group
+    // lane and wave instruction (one centre per instruction left 64 - PPT lanes idle, and the
+    // update was bound by those box tests: 16 waves x ~26 centres per round on 4 SIMDs).
+    const int lane = fresh_lane();
     uint32_t dirty = 0u;
+    T gbl[6];
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      const uint64_t am = hh ? acc1 : acc0;
-      if (!am) continue;
-      const int i = hh * 64 + lane;
-      const bool live = (am >> lane) & 1ull;
-      const T mx = live ? cxx[i] : static_cast<T>(0), my = live ? cyy[i] : static_cast<T>(0),
-              mz = live ? czz[i] : static_cast<T>(0);
-      uint64_t rel = __ballot(live && !(box_lb2(mx, my, mz, wb) >= static_cast<T>(wub)));
-      while (rel) {
-        const int k = __ffsll(static_cast<long long>(rel)) - 1;
-        rel &= rel - 1;
-        const T cx = readlane_t(mx, k), cy = readlane_t(my, k), cz = readlane_t(mz, k);
-        uint32_t m = static_cast<uint32_t>(__ballot(grp && !(box_lb2(cx, cy, cz, gb) >= static_cast<T>(gub))));
-        dirty |= m;
-        while (m) {  // touched slots only; p is wave-uniform -> indexed register access
-          const int p = __ffs(m) - 1;
-          m &= m - 1;
-          dmin[p] = fps_update<T>(dmin[p], px[p], py[p], pz[p], cx, cy, cz);
-        }
+    for (int a = 0; a < 6; ++a) gbl[a] = gbox[wave][a][lane & (GP - 1)];
+    for (int c0 = 0; c0 < kstar; c0 += QC) {
+      const int cq = c0 + static_cast<int>(static_cast<unsigned>(lane) / GP);
+      const int ci = cq < kstar ? cq : kstar - 1;
+      const T cx = acx[ci], cy = acy[ci], cz = acz[ci];
+      uint64_t m = __ballot(cq < kstar && grp && !(box_lb2(cx, cy, cz, gbl) >= static_cast<T>(gub)));
+      while (m) {  // touched (centre, slot) pairs; p is wave-uniform -> indexed register access
+        const int k = __ffsll(static_cast<long long>(m)) - 1;
+        m &= m - 1;
+        const int p = k & (GP - 1);
+        dirty |= 1u << p;
+        const T sx = readlane_t(cx, k), sy = readlane_t(cy, k), sz = readlane_t(cz, k);
+        dmin[p] = fps_update<T>(dmin[p], px[p], py[p], pz[p], sx, sy, sz);
       }
     }
     // re-reduce the touched groups whose maximum point dropped (values only drop: a group keeps
@@ -1023,10 +1038,9 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
       const float gp = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gub), p));
       if (!__ballot(dmin[p] == gp)) {
         const float gm = wave_fmax_nn(fmaxf(dmin[p], 0.f));
-        gub = lane == p ? gm : gub;
+        gub = (lane & (GP - 1)) == p ? gm : gub;
       }
     }
-    wub = wave_fmax_nn(fmaxf(gub, 0.f));
     tick(4);
     step += kstar;
   }

@@ -17,14 +17,58 @@
 // [0, 0, 0, f(D/2) .. f(D-1)], so each half loads one contiguous, 16-B aligned feature run.
 // Bias is the accumulator's initial value; BN (eval) is y = acc * scale + shift with scale/shift
 // folded on the host side of the kernel (scale, shift of dvcp_sa_group_mlp's params); ReLU.
-// The MFMA is a k-ordered fp32 fma chain (exact fp32 products and sums), so the result differs
-// from the row-per-thread kernel only in summation order.
+// Layer 1 runs on the fp32 MFMA (a k-ordered fp32 fma chain).  Layer 2 (~95 % of the flops) runs
+// on the bf16 matrix cores, which are 16x the fp32 MFMA rate, with fp32 accuracy kept by a three-way
+// split (DVCP_SA_SPLIT3, default on): every fp32 operand is the exact sum of three bf16 pieces
+// x = x0 + x1 + x2 (each residual of a round-to-nearest bf16 conversion is exact in fp32), and
+//   a.b ~ a0 b0 + (a0 b1 + a1 b0) + (a0 b2 + a1 b1 + a2 b0)
+// drops only the terms a1 b2, a2 b1, a2 b2 (<= 2^-24 |a||b| together, the size of one fp32
+// rounding of the product); the bf16 x bf16 products are exact in the fp32 accumulator.  Six
+// v_mfma_f32_32x32x16_bf16 (32 cycles each) replace eight v_mfma_f32_32x32x2_f32 (64 cycles each)
+// per 16 channels of k, so layer 2 costs 3/8 of the fp32 MFMA time.  The result differs from
+// the fp32 chain by summation order and the dropped terms, within the fp32 tolerances of the
+// parity tests (tests/test_gpu_kernels.py: rtol = atol = 1e-5; the split's own error against an
+// fp64 evaluation is checked beside the fp32 path's in test_sa_split3_accuracy).
 #include "common.h"
 #include "morton.h"
 
 namespace dvcp {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+#ifndef DVCP_SA_SPLIT3
+#define DVCP_SA_SPLIT3 1
+#endif
+
+// x = x0 + x1 + x2 exactly (bf16 pieces of eight fp32 values; see the header)
+struct Split3 {
+  bf16x8 p0, p1, p2;
+};
+__device__ __forceinline__ Split3 split3(const float (&x)[8]) {
+  Split3 s;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 b0 = static_cast<__bf16>(x[j]);
+    const float r1 = x[j] - static_cast<float>(b0);
+    const __bf16 b1 = static_cast<__bf16>(r1);
+    const float r2 = r1 - static_cast<float>(b1);
+    s.p0[j] = b0;
+    s.p1[j] = b1;
+    s.p2[j] = static_cast<__bf16>(r2);
+  }
+  return s;
+}
+// acc += a.b over one 16-deep k-step, the six significant piece products, smallest first
+__device__ __forceinline__ f32x16 mfma_split3(const Split3& a, const bf16x8& b0, const bf16x8& b1, const bf16x8& b2,
+                                             f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p2, b0, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p1, b1, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p0, b2, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p1, b0, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p0, b1, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p0, b0, acc, 0, 0, 0);
+}
 
 constexpr int kMfmaWaves = 4;  // centres in flight per workgroup (one per SIMD)
 
@@ -34,17 +78,22 @@ struct SaMfmaShape {
   static constexpr int KS = 3 + D / 2;  // k-steps of layer 1
   static constexpr int MT = C1 / 32;    // layer-1 output tiles
   static constexpr int CT = C2 / 32;    // layer-2 output tiles
-  static constexpr int K2 = MT * 16;    // k-steps of layer 2
+  static constexpr int K2 = MT * 16;    // k-steps of layer 2 (fp32 32x32x2)
+  static constexpr int KB = MT * 2;     // k-steps of layer 2 (bf16 32x32x16, split3)
   static_assert(D % 8 == 0 && C1 % 32 == 0 && C2 % 32 == 0, "MFMA tiling");
 };
 
 // LDS image of the weights in fragment order (staged once per workgroup).
-template <int D, int C1, int C2>
+template <int D, int C1, int C2, bool PRE>
 struct SaMfmaLds {
   using S = SaMfmaShape<D, C1, C2>;
-  float w1[S::MT][S::KS][64];   // A fragment of layer 1: [tile][k-step][lane]
-  float wx[S::MT][2][64];       // decomposed layer 1: xyz columns only, k-steps (x|y), (z|0)
-  float w2[S::CT][S::K2][64];   // B fragment of layer 2: [tile][k-step][lane]
+  float w1[PRE ? 1 : S::MT][S::KS][64];  // A fragment of layer 1: [tile][k-step][lane] (not PRE)
+  float wx[S::MT][2][64];                // decomposed layer 1: xyz columns only, k-steps (x|y), (z|0)
+#if DVCP_SA_SPLIT3
+  bf16x8 w2s[S::CT][S::KB][3][64];       // B fragment of layer 2 as three bf16 pieces: [tile][k-step][piece][lane]
+#else
+  float w2[S::CT][S::K2][64];            // B fragment of layer 2: [tile][k-step][lane]
+#endif
   float b1[S::MT][2][16];       // layer-1 bias / BN scale / BN shift by [tile][lane half][register]
   float s1[S::MT][2][16];
   float t1[S::MT][2][16];
@@ -143,7 +192,7 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
     float* __restrict__ out, int xcd) {
   using Sh = SaMfmaShape<D, C1, C2>;
   constexpr int C0 = Sh::C0, KS = Sh::KS, MT = Sh::MT, CT = Sh::CT;
-  __shared__ SaMfmaLds<D, C1, C2> L;
+  __shared__ SaMfmaLds<D, C1, C2, PRE> L;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
 
   // ---- stage the weights (params: W1, b1, scale1, shift1, W2, b2, scale2, shift2) ---------
@@ -155,22 +204,40 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
   const float* pb2 = W2 + C2 * C1;
   const float* ps2 = pb2 + C2;
   const float* pt2 = ps2 + C2;
-  for (int i = tid; i < MT * KS * 64; i += blockDim.x) {
-    const int l = i % 64, s = (i / 64) % KS, mt = i / (64 * KS);
-    const int ch = sa_in_channel<D>(s, l >> 5);
-    L.w1[mt][s][l] = ch < 0 ? 0.0f : W1[(32 * mt + (l & 31)) * C0 + ch];
-  }
+  if (!PRE)
+    for (int i = tid; i < MT * KS * 64; i += blockDim.x) {
+      const int l = i % 64, s = (i / 64) % KS, mt = i / (64 * KS);
+      const int ch = sa_in_channel<D>(s, l >> 5);
+      L.w1[mt][s][l] = ch < 0 ? 0.0f : W1[(32 * mt + (l & 31)) * C0 + ch];
+    }
   if (PRE)
     for (int i = tid; i < MT * 2 * 64; i += blockDim.x) {
       const int l = i % 64, s = (i / 64) % 2, mt = i / 128;
       const int ch = s == 0 ? (l >> 5) : ((l >> 5) == 0 ? 2 : -1);
       L.wx[mt][s][l] = ch < 0 ? 0.0f : W1[(32 * mt + (l & 31)) * C0 + ch] * ps1[32 * mt + (l & 31)];
     }
+#if DVCP_SA_SPLIT3
+  // k-step s, lane half hh, element j <-> layer-1 channel 32 (s / 2) + acc_row(8 (s % 2) + j, hh): the
+  // layer-1 accumulator registers 8 (s % 2) .. + 7 of tile s / 2 are the A fragment as they stand
+  for (int i = tid; i < CT * Sh::KB * 64; i += blockDim.x) {
+    const int l = i % 64, s = (i / 64) % Sh::KB, ct = i / (64 * Sh::KB);
+    const int o = 32 * ct + (l & 31);
+    float w[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      w[j] = W2[o * C1 + 32 * (s / 2) + acc_row(8 * (s % 2) + j, l >> 5)] * (PRE ? ps2[o] : 1.0f);
+    const Split3 ws = split3(w);
+    L.w2s[ct][s][0][l] = ws.p0;
+    L.w2s[ct][s][1][l] = ws.p1;
+    L.w2s[ct][s][2][l] = ws.p2;
+  }
+#else
   for (int i = tid; i < CT * Sh::K2 * 64; i += blockDim.x) {
     const int l = i % 64, kk = (i / 64) % Sh::K2, ct = i / (64 * Sh::K2);
     const int mt = kk / 16, r = kk % 16;
     L.w2[ct][kk][l] = W2[(32 * ct + (l & 31)) * C1 + 32 * mt + acc_row(r, l >> 5)] * (PRE ? ps2[32 * ct + (l & 31)] : 1.0f);
   }
+#endif
   for (int i = tid; i < MT * 32; i += blockDim.x) {
     const int r = i % 16, hh = (i / 16) % 2, mt = i / 32;
     const int c = 32 * mt + acc_row(r, hh);
@@ -332,6 +399,19 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
       for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc2[ct][r] = b2[ct];
+#if DVCP_SA_SPLIT3
+#pragma unroll
+      for (int s = 0; s < Sh::KB; ++s) {
+        float x[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = acc1[s / 2][8 * (s % 2) + j];
+        const Split3 a = split3(x);
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+          acc2[ct] = mfma_split3(a, L.w2s[ct][s][0][lane + zo], L.w2s[ct][s][1][lane + zo], L.w2s[ct][s][2][lane + zo],
+                                 acc2[ct]);
+      }
+#else
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -339,6 +419,7 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
 #pragma unroll
           for (int ct = 0; ct < CT; ++ct)
             acc2[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(acc1[mt][r], L.w2[ct][mt * 16 + r][lane + zo], acc2[ct], 0, 0, 0);
+#endif
       // BN + ReLU, then max over this tile's points (registers).  PRE: BN is folded, and
       // max_i relu(v_i) = relu(max_i v_i), so the ReLU is the +0 the running max starts from.
 #pragma unroll

@@ -134,7 +134,8 @@ def sa_group_mlp_rows(xyz, ctr, feat, rows, count, lst, nsample, chans, params, 
     return out
 
 
-MFMA_F32_32X32X2_FLOPS = 2 * 32 * 32 * 2   # one v_mfma_f32_32x32x2_f32
+MFMA_F32_32X32X2_FLOPS = 2 * 32 * 32 * 2     # one v_mfma_f32_32x32x2_f32
+MFMA_BF16_32X32X16_FLOPS = 2 * 32 * 32 * 16  # one v_mfma_f32_32x32x16_bf16
 
 
 def _sa_exec_flops(chans, B, N, S, nsample, count):
@@ -144,19 +145,22 @@ def _sa_exec_flops(chans, B, N, S, nsample, count):
     * two-layer MFMA tables (sa2 35-32-64, sa3 67-64-64; csrc/sa_mlp_mfma.hip): layer 1 is split
       into the per-point pass sa_pre_kernel (VALU, 2 D C1 per input point) and, per 32-row tile of
       a centre's distinct hits (ceil(clamp(count, 1, ns) / 32) tiles; padded lanes of a tile
-      execute like real ones), 2 MT + MT 16 CT v_mfma_f32_32x32x2_f32 (xyz k-steps + layer 2);
+      execute like real ones), 2 MT v_mfma_f32_32x32x2_f32 (xyz k-steps) and layer 2 as MT 2 CT
+      16-deep k-steps of six v_mfma_f32_32x32x16_bf16 (the fp32-accurate three-way bf16 split);
     * other tables (sa1, csrc/sa_mlp.hip, VALU): one row per distinct hit, clamp(count, 0, ns)
       rows x 2 sum(C_l C_l+1).
-    Returns a callable -> (executed flops, of which MFMA flops)."""
+    Returns a callable -> (executed fp32-equivalent flops, of which on the matrix cores, of which
+    on the bf16 pipe as fp32-equivalent flops, the bf16 pipe's own flops (6 x those))."""
     if len(chans) == 3 and chans[0] - 3 in (32, 64):
         D, C1, C2 = chans[0] - 3, chans[1], chans[2]
         mt, ct = C1 // 32, C2 // 32
-        per_tile = (2 * mt + mt * 16 * ct) * MFMA_F32_32X32X2_FLOPS
+        xyz_tile = 2 * mt * MFMA_F32_32X32X2_FLOPS
+        l2_tile = 2 * mt * ct * MFMA_BF16_32X32X16_FLOPS  # = 2 x 32 rows x C1 x C2
 
         def f():
             tiles = float(((count.clamp(1, nsample).long() + 31) // 32).sum())
-            mfma = tiles * per_tile
-            return 2.0 * B * N * D * C1 + mfma, mfma
+            mfma = tiles * (xyz_tile + l2_tile)
+            return 2.0 * B * N * D * C1 + mfma, mfma, tiles * l2_tile, 6.0 * tiles * l2_tile
         return f
     macs = sum(a * b for a, b in zip(chans[:-1], chans[1:]))
 

@@ -384,6 +384,55 @@ def test_set_abstraction_vs_oracle(cuda, normals, layout, B):
         torch.testing.assert_close(G_f.cpu(), O_f, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("table", [1, 2])
+def test_sa_split3_accuracy(cuda, table):
+    """The two-layer MFMA tables run layer 2 as a three-way bf16 split on the bf16 matrix cores
+    (csrc/sa_mlp_mfma.hip).  On the same groups (the GPU ball query's lists) its error against an
+    fp64 evaluation of pointnet2_utils.py:195-200 must be of the size of an fp32 evaluation's error
+    (torch fp32 on the CPU, the reference's own arithmetic), and within the fp32 tolerance of it."""
+    import copy
+    import oracle as O
+    import dvcp.pointnet2_utils as P
+    from dvcp import ops
+    from tests_helpers import randomize_bn
+    g = torch.Generator().manual_seed(211 + table)
+    cfg = O.fe_config(use_normal=False, npoint=2000)[table]
+    B, N, S, ns, r = 2, 6000, 2000, cfg["nsample"], cfg["radius"]
+    D = cfg["in_channel"] - 3
+    torch.manual_seed(11)
+    mine = P.PointNetSetAbstraction(**cfg).eval()
+    randomize_bn(mine)
+    side = r * (4.19 * N / (0.75 * ns)) ** (1.0 / 3.0)  # ~3/4 of nsample hits per ball
+    xyz = ((torch.rand(B, 3, N, generator=g, dtype=torch.float64) - 0.5) * side).float()
+    feats = torch.randn(B, N, D, generator=g)           # point-major rows, as the forward stores them
+    gx, gf = xyz.to(cuda), feats.to(cuda)
+    ctr = gx[:, :, :S].contiguous()
+    mine_g = copy.deepcopy(mine).to(cuda)
+    count, lst, _ = ops.ball_query(gx, ctr, r, ns, pdim=2, cdim_pts=2)
+    out = ops.sa_group_mlp(gx, ctr, gf.transpose(1, 2), count, lst, ns, mine_g.chans, mine_g.packed_params(),
+                           xyz_pdim=2, feat_ddim=1, feat_pdim=2).cpu()           # (B, S, C2)
+    cnt = count.cpu().long().clamp(1, ns)
+    idx = lst.cpu().long()
+    idx = torch.where(torch.arange(ns).view(1, 1, ns) < cnt.unsqueeze(-1), idx, idx[:, :, :1])  # :104 padding
+    bi = torch.arange(B).view(B, 1, 1)
+    gxyz = xyz.transpose(1, 2)[bi, idx] - xyz.transpose(1, 2)[:, :S].unsqueeze(2)  # fp32 differences
+    rows = torch.cat([gxyz, feats[bi, idx]], dim=-1).permute(0, 3, 2, 1)             # (B, C0, ns, S)
+
+    def mlp(m, x):
+        for conv, bn in zip(m.mlp_convs, m.mlp_bns):
+            x = torch.relu(bn(conv(x)))
+        return torch.max(x, 2)[0].transpose(1, 2)
+    with torch.no_grad():
+        ref64 = mlp(copy.deepcopy(mine).double(), rows.double())
+        ref32 = mlp(mine, rows)
+    err_gpu = float((out.double() - ref64).abs().max())
+    err_f32 = float((ref32.double() - ref64).abs().max())
+    scale = float(ref64.abs().max())
+    print(f"sa table {table}: max |gpu - fp64| {err_gpu:.3e}, max |fp32 cpu - fp64| {err_f32:.3e}, |ref| {scale:.3f}")
+    assert err_gpu <= 4.0 * err_f32 + 1e-7 * scale
+    torch.testing.assert_close(out, ref32, rtol=1e-5, atol=1e-5)
+
+
 def _sa_oracle(ref, xyz, feats, start):
     import oracle as O
     orig = O.ref_r.farthest_point_sample
