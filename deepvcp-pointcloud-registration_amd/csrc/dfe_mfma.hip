@@ -24,6 +24,39 @@
 namespace dvcp {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+#ifndef DVCP_DFE_SPLIT3
+#define DVCP_DFE_SPLIT3 1
+#endif
+
+// x = x0 + x1 + x2 exactly in three bf16 pieces; a.b from the six significant piece products
+// (the fp32-accurate split of sa_mlp_mfma.hip, whose header gives the error bound)
+struct DfeSplit3 {
+  bf16x8 p0, p1, p2;
+};
+__device__ __forceinline__ DfeSplit3 dfe_split3(const float (&x)[8]) {
+  DfeSplit3 s;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 b0 = static_cast<__bf16>(x[j]);
+    const float r1 = x[j] - static_cast<float>(b0);
+    const __bf16 b1 = static_cast<__bf16>(r1);
+    s.p0[j] = b0;
+    s.p1[j] = b1;
+    s.p2[j] = static_cast<__bf16>(r1 - static_cast<float>(b1));
+  }
+  return s;
+}
+__device__ __forceinline__ f32x16 dfe_mfma_split3(const DfeSplit3& a, const bf16x8& b0, const bf16x8& b1,
+                                                 const bf16x8& b2, f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p2, b0, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p1, b1, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p0, b2, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p1, b0, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p0, b1, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p0, b0, acc, 0, 0, 0);
+}
 
 constexpr int kDfeMfmaWaves = 4;
 constexpr int kDfeKS = 19;  // layer-1 k-steps: 3 + 32/2
@@ -145,6 +178,10 @@ __global__ __launch_bounds__(kDfeMfmaWaves * kWave) void dfe_tgt_mfma_kernel(
 // roundings of intermediates, one of E); tests hold it to the same 1e-5 bound.
 //   H = X . E^T:  A = X (lane: row j, k-half), B = E^T fragment (lane: output channel, k-half)
 //   -> output channel on lanes, rows in registers, max over rows = registers + one lane swap.
+// DVCP_DFE_SPLIT3 (default): the xyz columns take two fp32 MFMA k-steps ((x|y), (z|0)) and the 32
+// feature columns two 16-deep bf16 k-steps of the fp32-accurate three-way split (lane half h's
+// features 16h + 8t .. + 7 in k-step t): 2 x 64 + 12 x 32 = 512 MFMA cycles per candidate instead
+// of 19 x 64 = 1216.
 // dist_sum: 32 fp32 distances summed in fp64 are exact whenever they span less than 2^24 (24-bit
 // mantissas, 5 bits of carry, 53-bit accumulator), so a butterfly sum equals the reference's
 // ordered sum; w_j = dist_j / dist_sum in fp64 is then bit-identical.
@@ -153,7 +190,12 @@ constexpr int kDfe1Waves = 4;
 struct Dfe1Lds {
   double p[32][35];      // W2 . W1 (fp64), prologue only
   double pb[32];         // W2 . b1 + b2
+#if DVCP_DFE_SPLIT3
+  float ex[2][64];          // E's xyz columns as fp32 B fragments: k-steps (x|y), (z|0)
+  bf16x8 es[2][3][64];      // E's feature columns as bf16 pieces: [k-step][piece][lane]
+#else
   float e[kDfeKS][64];   // E as the B fragment: [k-step][lane]
+#endif
   float eb[32];          // e
   float w[kDfe1Waves][32];  // per-wave w_j of the current candidate (fp64 quotient rounded to fp32)
 };
@@ -188,14 +230,34 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
   }
   __syncthreads();
   // E = W3 P in fragment order, e = W3 pb + b3
+  auto e_entry = [&](int o, int ch) {
+    double acc = 0.0;
+    for (int a = 0; a < 32; ++a) acc = __fma_rn(static_cast<double>(W3[o * 32 + a]), L.p[a][ch], acc);
+    return static_cast<float>(acc);
+  };
+#if DVCP_DFE_SPLIT3
+  for (int i = tid; i < 2 * 64; i += blockDim.x) {
+    const int l = i % 64, s = i / 64, hh = l >> 5, o = l & 31;
+    const int ch = s == 0 ? hh : (hh == 0 ? 2 : -1);
+    L.ex[s][l] = ch < 0 ? 0.0f : e_entry(o, ch);
+  }
+  for (int i = tid; i < 2 * 64; i += blockDim.x) {
+    const int l = i % 64, t = i / 64, hh = l >> 5, o = l & 31;
+    float w[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = e_entry(o, 3 + 16 * hh + 8 * t + j);
+    const DfeSplit3 ws = dfe_split3(w);
+    L.es[t][0][l] = ws.p0;
+    L.es[t][1][l] = ws.p1;
+    L.es[t][2][l] = ws.p2;
+  }
+#else
   for (int i = tid; i < kDfeKS * 64; i += blockDim.x) {
     const int l = i % 64, s = i / 64, hh = l >> 5, o = l & 31;
     const int ch = s < 3 ? (hh == 0 ? s : -1) : 3 + hh * 16 + (s - 3);
-    double acc = 0.0;
-    if (ch >= 0)
-      for (int a = 0; a < 32; ++a) acc = __fma_rn(static_cast<double>(W3[o * 32 + a]), L.p[a][ch], acc);
-    L.e[s][l] = static_cast<float>(acc);
+    L.e[s][l] = ch < 0 ? 0.0f : e_entry(o, ch);
   }
+#endif
   for (int o = tid; o < 32; o += blockDim.x) {
     double acc = 0.0;
     for (int a = 0; a < 32; ++a) acc = __fma_rn(static_cast<double>(W3[o * 32 + a]), L.pb[a], acc);
@@ -276,9 +338,18 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
   auto embed = [&](int gg, const Gathered& G) {
     float x[kDfeKS];
     // candidates_grouped_local = tgt_pts_picked - candidate (point dtype, then .float()); half 1: 0
+#if DVCP_DFE_SPLIT3
+    const float ddx = static_cast<float>(G.px - static_cast<T>(G.cx));
+    const float ddy = static_cast<float>(G.py - static_cast<T>(G.cy));
+    const float ddz = static_cast<float>(G.pz - static_cast<T>(G.cz));
+    x[0] = h == 0 ? ddx : ddy;  // the fp32 k-steps (x|y), (z|0)
+    x[1] = h == 0 ? ddz : 0.0f;
+    x[2] = 0.0f;
+#else
     x[0] = h == 0 ? static_cast<float>(G.px - static_cast<T>(G.cx)) : 0.0f;
     x[1] = h == 0 ? static_cast<float>(G.py - static_cast<T>(G.cy)) : 0.0f;
     x[2] = h == 0 ? static_cast<float>(G.pz - static_cast<T>(G.cz)) : 0.0f;
+#endif
     // the wave's own w row, read back as 16-byte broadcasts
     __builtin_amdgcn_wave_barrier();
     const float4* wr = reinterpret_cast<const float4*>(&L.w[wave][16 * h]);
@@ -310,8 +381,20 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
     f32x16 a;
 #pragma unroll
     for (int r = 0; r < 16; ++r) a[r] = eb;
+#if DVCP_DFE_SPLIT3
+    a = __builtin_amdgcn_mfma_f32_32x32x2f32(x[0], L.ex[0][lane + zo], a, 0, 0, 0);
+    a = __builtin_amdgcn_mfma_f32_32x32x2f32(x[1], L.ex[1][lane + zo], a, 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float f8[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f8[j] = x[3 + 8 * t + j];
+      a = dfe_mfma_split3(dfe_split3(f8), L.es[t][0][lane + zo], L.es[t][1][lane + zo], L.es[t][2][lane + zo], a);
+    }
+#else
 #pragma unroll
     for (int s = 0; s < kDfeKS; ++s) a = __builtin_amdgcn_mfma_f32_32x32x2f32(x[s], L.e[s][lane + zo], a, 0, 0, 0);
+#endif
     float m = a[0];
 #pragma unroll
     for (int r = 1; r < 16; ++r) m = fmaxf(m, a[r]);
