@@ -204,7 +204,7 @@ struct Dfe1Lds {
 // half the gathered bytes; each row is widened to fp32 before the weighting, which then runs in
 // fp32 exactly as for a float table holding the same values).
 template <typename T, typename FT = float>
-__global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
+__global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per_eu(3))) void dfe_tgt_mfma1_kernel(
     PointsView<T> ref, const FT* __restrict__ feat, int M, const float* __restrict__ cand,
     const float* __restrict__ dist, const int32_t* __restrict__ idx, int Q, int B, const float* __restrict__ params,
     float* __restrict__ out, int xcd) {
@@ -379,8 +379,10 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
     int zo = 0;  // opaque zero: E fragments are re-read from LDS per candidate, not hoisted
     asm volatile("" : "+v"(zo));
     f32x16 a;
+    // split path: zero-started accumulators (inline-constant C) and e added once to the row
+    // maximum, max_j fl(h_j + e) = fl(max_j h_j + e) (rounding is monotone)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) a[r] = eb;
+    for (int r = 0; r < 16; ++r) a[r] = DVCP_DFE_SPLIT3 ? 0.0f : eb;
 #if DVCP_DFE_SPLIT3
     a = __builtin_amdgcn_mfma_f32_32x32x2f32(x[0], L.ex[0][lane + zo], a, 0, 0, 0);
     a = __builtin_amdgcn_mfma_f32_32x32x2f32(x[1], L.ex[1][lane + zo], a, 0, 0, 0);
@@ -399,6 +401,7 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) void dfe_tgt_mfma1_kernel(
 #pragma unroll
     for (int r = 1; r < 16; ++r) m = fmaxf(m, a[r]);
     m = fmaxf(m, __shfl_xor(m, 32, kWave));
+    if (DVCP_DFE_SPLIT3) m += eb;
     if (h == 0) out[static_cast<int64_t>(glob(gg)) * 32 + r32] = m;
     __builtin_amdgcn_wave_barrier();  // the w row is rewritten for the next candidate
   };

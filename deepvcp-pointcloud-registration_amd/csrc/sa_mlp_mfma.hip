@@ -185,7 +185,7 @@ __global__ __launch_bounds__(kBuildThreads) void sa_order_kernel(PointsView<T> c
 }
 
 template <typename T, int D, int C1, int C2, bool PRE>
-__global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
+__global__ __launch_bounds__(kMfmaWaves * kWave) __attribute__((amdgpu_waves_per_eu(3))) void sa_mlp_mfma_kernel(
     PointsView<T> pts, PointsView<T> ctr, int S, int B, const float* __restrict__ feat, int64_t fb, int64_t fn,
     const int32_t* __restrict__ count, const int32_t* __restrict__ list, int nsample,
     const float* __restrict__ params, const float* __restrict__ U, int64_t ub, const int32_t* __restrict__ order,
@@ -317,9 +317,13 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
     const int64_t fc = lane_bcast(m_fc, j);
     const int rows = lane_bcast(m_rows, j);
     const T cx = lane_bcast(m_cx, j), cy = lane_bcast(m_cy, j), cz = lane_bcast(m_cz, j);
+    // PRE with the split layer 2 (BZ): the accumulators start from zero (an inline-constant C
+    // operand, no 32 register moves per tile) and the bias is added once to the maximum:
+    // max_i fl(a_i + b) = fl(max_i a_i + b) (rounding is monotone), then the ReLU.
+    constexpr bool BZ = PRE && DVCP_SA_SPLIT3;
     float mx[CT];
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) mx[ct] = 0.0f;  // post-ReLU values are >= +0
+    for (int ct = 0; ct < CT; ++ct) mx[ct] = BZ ? -__builtin_huge_valf() : 0.0f;  // else post-ReLU values are >= +0
 
     for (int n0 = 0; n0 < rows; n0 += 32) {
       // An opaque zero added to every LDS weight index: the fragments are re-read per tile
@@ -398,7 +402,7 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc2[ct][r] = b2[ct];
+        for (int r = 0; r < 16; ++r) acc2[ct][r] = BZ ? 0.0f : b2[ct];
 #if DVCP_SA_SPLIT3
 #pragma unroll
       for (int s = 0; s < Sh::KB; ++s) {
@@ -437,7 +441,8 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa_mlp_mfma_kernel(
     // the two lane halves hold different points of the same channel
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
-      const float m = fmaxf(mx[ct], __shfl_xor(mx[ct], 32, kWave));
+      float m = fmaxf(mx[ct], __shfl_xor(mx[ct], 32, kWave));
+      if (BZ) m = fmaxf(m + b2[ct], 0.0f);
       if (h == 0) out[fc * C2 + 32 * ct + r32] = m;
     }
   }
