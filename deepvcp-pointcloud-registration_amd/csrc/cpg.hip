@@ -9,9 +9,9 @@
 // target block is loaded once into registers; the cost volume is built in LDS one 8-channel
 // quarter at a time with a zero halo (13^3 cells, 70 KB) next to conv1's weights ([ci][tap][co],
 // 55 KB); conv1 runs on the matrix cores (see below), accumulating the quarters in registers;
-// its output (haloed) then replaces volume and weights in LDS for conv2, which runs the same way
-// with its 4 output channels padded to 16; conv2's haloed output feeds conv3 (VALU, maskless),
-// and the softmax and weighted mean finish in registers.
+// its output (haloed) then replaces volume and weights in LDS for conv2 (VALU: its 4 output
+// channels would fill a quarter of an MFMA tile); conv2's haloed output feeds conv3 (VALU,
+// maskless), and the softmax and weighted mean finish in registers.
 #include "common.h"
 #include "cpg_grid.h"
 
@@ -37,7 +37,6 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
                                                           const float* __restrict__ params, float* __restrict__ vcp,
                                                           float* __restrict__ weight) {
   __shared__ __attribute__((aligned(16))) float big[kCpgBigF];
-  __shared__ __attribute__((aligned(16))) float w2[16 * 27 * 4];  // conv2 W [ci][tap][co]
   __shared__ float w3[4 * 27];
   __shared__ float bias[16 + 4 + 1];
   __shared__ float sv[32];
@@ -66,10 +65,6 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
   for (int i = tid; i < 16 * 32 * 27; i += kCpgThreads) {  // torch (co, ci, kd, kh, kw)
     const int co = i / (32 * 27), r = i % (32 * 27);
     w1[r * 16 + co] = P1[i];
-  }
-  for (int i = tid; i < 4 * 16 * 27; i += kCpgThreads) {
-    const int co = i / (16 * 27), r = i % (16 * 27);
-    w2[r * 4 + co] = P2[i];
   }
   if (tid < 4 * 27) w3[tid] = P3[tid];
   if (tid < 16) bias[tid] = P1[16 * 32 * 27 + tid];
@@ -158,35 +153,50 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
   }
   __syncthreads();
 
-  // conv2 (16 -> 4) the same way, output channels padded to the MFMA's 16 columns
+  // conv2 (16 -> 4) on VALU, one voxel per thread: a 16-column MFMA tile would leave 12 of its
+  // 16 output columns empty (4x the MFMA time of the useful work).  W2[co][ci][tap] comes through
+  // the scalar cache (wave-uniform), one tap plane (4 x 9 weights) at a time.
+  int hv[kCpgV];
 #pragma unroll
-  for (int i = 0; i < kTW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int v = 0; v < kCpgV; ++v) hv[v] = cpg_halo(gv[v] < C ? gv[v] : 0, dG, dGG, PG, PGG);
+  float o2[kCpgV][4];
+#pragma unroll
+  for (int v = 0; v < kCpgV; ++v)
+#pragma unroll
+    for (int co = 0; co < 4; ++co) o2[v][co] = 0.f;
 #pragma unroll 1
-  for (int t = 0; t < 27; ++t) {
-    const int off = (t / 9 - 1) * PGG + ((t / 3) % 3 - 1) * PG + (t % 3 - 1);
+  for (int ci = 0; ci < 16; ++ci) {
+    const float* xin = out1 + ci * PV;
 #pragma unroll
-    for (int cg = 0; cg < 4; ++cg) {
-      const int ci = 4 * cg + kg;
-      const float bw = l16 < 4 ? w2[(ci * 27 + t) * 4 + l16] : 0.f;
-      const float* vin = out1 + ci * PV + off;
+    for (int kd = 0; kd < 3; ++kd) {
+      // (an opaque zero ordered after the running sums keeps all 108 weights of the channel from
+      // being loaded into SGPRs at once)
+      int zw = 0;
+      asm volatile("" : "+s"(zw) : "v"(o2[0][0]));
+      const float* w2c = P2 + ci * 27 + 9 * kd + zw;
 #pragma unroll
-      for (int i = 0; i < kTW; ++i)
-        if (wave + kW * i < NT)
-          acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(vin[vx[i]], bw, acc[i], 0, 0, 0);
+      for (int t9 = 0; t9 < 9; ++t9) {
+        const int t = 9 * kd + t9;
+        const int off = (t / 9 - 1) * PGG + ((t / 3) % 3 - 1) * PG + (t % 3 - 1);
+#pragma unroll
+        for (int v = 0; v < kCpgV; ++v) {
+          if (v == 0 || gv[v] < C) {  // (v = 0: every thread, C >= 1024 or a clamped in-range cell)
+            const float x = xin[hv[v] + off];
+#pragma unroll
+            for (int co = 0; co < 4; ++co) o2[v][co] = __fmaf_rn(w2c[co * 16 * 27 + t9], x, o2[v][co]);
+          }
+        }
+      }
     }
   }
-  __syncthreads();
+  __syncthreads();  // every conv1 output read; out2 overwrites them
   for (int i = tid; i < 4 * PV; i += kCpgThreads) out2[i] = 0.f;
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < kTW; ++i) {
-    const int t = wave + kW * i;
+  for (int v = 0; v < kCpgV; ++v)
+    if (gv[v] < C)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int g = 16 * t + 4 * kg + r;
-      if (t < NT && g < C && l16 < 4) out2[l16 * PV + cpg_halo(g, dG, dGG, PG, PGG)] = acc[i][r] + bias[16 + l16];
-    }
-  }
+      for (int co = 0; co < 4; ++co) out2[co * PV + hv[v]] = o2[v][co] + bias[16 + co];
   __syncthreads();
 
   // conv3: 4 -> 1, one voxel per thread (haloed input: no masks)
@@ -194,15 +204,13 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
   float lmax = -__builtin_huge_valf();
 #pragma unroll
   for (int v = 0; v < kCpgV; ++v) {
-    const int g = gv[v] < C ? gv[v] : 0;
-    const int hv = cpg_halo(g, dG, dGG, PG, PGG);
     float a = 0.f;
 #pragma unroll
     for (int ci = 0; ci < 4; ++ci)
 #pragma unroll
       for (int t = 0; t < 27; ++t) {
         const int off = (t / 9 - 1) * PGG + ((t / 3) % 3 - 1) * PG + (t % 3 - 1);
-        a = __fmaf_rn(w3[ci * 27 + t], out2[ci * PV + hv + off], a);
+        a = __fmaf_rn(w3[ci * 27 + t], out2[ci * PV + hv[v] + off], a);
       }
     lg[v] = a + bias[20];
     if (gv[v] < C) lmax = fmaxf(lmax, lg[v]);
