@@ -619,10 +619,18 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
   float wkth = wave_max_nonneg(kth);
   int fill = 0;
   uint2(*mybuf)[kWave] = sbuf[wave];
+#ifdef DVCP_KNN_DIAG  // per-wave counters (diagnostic builds only; written over lane 0's distances)
+  uint64_t dg_t0 = __builtin_readcyclecounter(), dg_merge_clk = 0;
+  int dg_scanned = 0, dg_active = 0, dg_merges = 0, dg_appends = 0;
+#endif
 
   auto merge = [&]() {
     const int n = static_cast<int>(wave_umax_i(static_cast<uint32_t>(fill)));  // wave-uniform
     if (n == 0) return;
+#ifdef DVCP_KNN_DIAG
+    const uint64_t dg_m0 = __builtin_readcyclecounter();
+    ++dg_merges;
+#endif
     uint32_t bh[kSelBufN], bl[kSelBufN];
 #pragma unroll
     for (int i = 0; i < kSelBufN; ++i) {
@@ -666,11 +674,18 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
     kth = __uint_as_float(static_cast<uint32_t>(kkey >> 32));
     wkth = wave_max_nonneg(kth);
     fill = 0;
+#ifdef DVCP_KNN_DIAG
+    dg_merge_clk += __builtin_readcyclecounter() - dg_m0;
+#endif
   };
 
   // The next tile in the sorted order is fetched one position ahead, one float per lane (a tile is
   // 16 points x 4 floats = 64 floats: one coalesced 256-byte load), so its latency hides behind
   // the current tile; its coordinates reach every lane by readlane (SGPR operands).
+  // (Per-wave counters, DVCP_KNN_DIAG, C3: ~185 tiles pass the wave's bound, ~32 of them have a
+  // lane within its own k-th distance, 11 merges = 20-24 % of the wave's clock.  Loading only the
+  // tiles some lane needs, found by a look-ahead test, was slower: 0.97 -> 1.11 ms per call,
+  // profiles/round3/r3x_knn_diag_*.log.)
   const float* P = reinterpret_cast<const float*>(sorted) + static_cast<int64_t>(b) * T * kTile * 4;
   uint32_t key_next = T > 0 ? static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(keys[0]), 0)) : 0u;
   float v_next = T > 0 ? P[static_cast<int64_t>(key_next & kTileIdBits) * (4 * kTile) + lane] : 0.f;
@@ -690,7 +705,13 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
       const int t = static_cast<int>(key & kTileIdBits);
       const float lbq = hbox_lb2(hbox[t], qx, qy, qz, qx, qy, qz);
       const bool act = live & (lbq <= kth);
+#ifdef DVCP_KNN_DIAG
+      ++dg_scanned;
+#endif
       if (__ballot(act) == 0) continue;
+#ifdef DVCP_KNN_DIAG
+      ++dg_active;
+#endif
       auto bc = [&](int u) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v_cur), u)); };
       float c[3 * kTile];
 #pragma unroll
@@ -724,6 +745,9 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
         const int j = __builtin_ctz(u);
         u &= u - 1;
         if ((cm >> j) & 1u) {
+#ifdef DVCP_KNN_DIAG
+          ++dg_appends;
+#endif
           const float dx = bc(4 * j) - qx, dy = bc(4 * j + 1) - qy, dz = bc(4 * j + 2) - qz;
           mybuf[fill][lane] = make_uint2(__float_as_uint((dx * dx + dy * dy) + dz * dz), __float_as_uint(bc(4 * j + 3)));
           ++fill;
@@ -732,8 +756,26 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
     }
   }
   merge();
+#ifdef DVCP_KNN_DIAG
+  const uint64_t dg_total = __builtin_readcyclecounter() - dg_t0;
+  uint32_t app_sum = static_cast<uint32_t>(dg_appends);
+  for (int off = 32; off > 0; off >>= 1) app_sum += __shfl_xor(app_sum, off, kWave);
+#endif
   if (!live) return;
   const int64_t o = (static_cast<int64_t>(b) * Q + q) * k;
+#ifdef DVCP_KNN_DIAG
+  if (lane == 0 && dist && k == 32) {
+    dist[o + 0] = static_cast<float>(dg_scanned);
+    dist[o + 1] = static_cast<float>(dg_active);
+    dist[o + 2] = static_cast<float>(dg_merges);
+    dist[o + 3] = static_cast<float>(app_sum);
+    dist[o + 4] = static_cast<float>(dg_total);
+    dist[o + 5] = static_cast<float>(dg_merge_clk);
+    dist[o + 6] = static_cast<float>(T);
+    dist[o + 31] = -12345.0f;
+    return;
+  }
+#endif
 #pragma unroll
   for (int t = 0; t < KT; ++t) {
     if (t < k) {

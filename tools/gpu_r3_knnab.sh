@@ -1,0 +1,20 @@
+#!/bin/bash
+# kNN parity tests on the in-tree library (B), the kNN micro-benchmark and per-wave diagnostics
+# (dvcp/libdvcp_hip_D.so), then the C3 bench alternating dvcp/libdvcp_hip_A.so (A) and B.
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
+tag=${1:-knnab}
+L=deepvcp-pointcloud-registration_amd/dvcp
+timeout -k 10 400 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread -rfs -k "knn or c3 or dfe" \
+  > gpurun_out/${tag}_pytest.log 2>&1 || exit $?
+timeout -k 10 120 python tools/knn_bench.py > gpurun_out/${tag}_knnbench.log 2>&1 || exit $?
+cp $L/libdvcp_hip.so /tmp/libdvcp_hip_B.so
+cp $L/libdvcp_hip_D.so $L/libdvcp_hip.so
+timeout -k 10 120 python tools/knn_diag.py > gpurun_out/${tag}_diag.log 2>&1 || { cp /tmp/libdvcp_hip_B.so $L/libdvcp_hip.so; exit 1; }
+for i in 1 2; do
+  for v in A B; do
+    if [ $v = A ]; then cp $L/libdvcp_hip_A.so $L/libdvcp_hip.so; else cp /tmp/libdvcp_hip_B.so $L/libdvcp_hip.so; fi
+    echo "== $v run $i" >> gpurun_out/${tag}_bench.log
+    timeout -k 10 200 python bench.py --steps 30 --warmup 5 --no-cpu-baseline >> gpurun_out/${tag}_bench.log 2>&1 || exit $?
+  done
+done
+cp /tmp/libdvcp_hip_B.so $L/libdvcp_hip.so
