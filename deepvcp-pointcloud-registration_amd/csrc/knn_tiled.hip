@@ -563,6 +563,7 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
   // 12 + 32 KB of LDS (half-precision boxes, candidate buffers): three workgroups per CU
   __shared__ uint3 hbox[kMaxTiles];
   __shared__ uint2 sbuf[kTiledThreads / kWave][kSelBufN][kWave];  // lane-private candidate buffers
+  __shared__ float4 stile[kTiledThreads / kWave][kTile];            // the wave's current tile (appends)
   {
     const float4* tbg = tbox + static_cast<int64_t>(b) * T * 2;
     for (int i = threadIdx.x; i < T; i += kTiledThreads) hbox[i] = pack_hbox(tbg[2 * i], tbg[2 * i + 1]);
@@ -739,19 +740,27 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
 #pragma unroll
         for (int j = 0; j < kTile; ++j) cm &= d2_of(j) <= kf2 ? ~0u : ~(1u << j);
       }
-      // appends: only the points some lane takes (wave-uniform loop over the union of the masks)
-      uint32_t u = wave_or_u32(cm);
-      while (u != 0) {
-        const int j = __builtin_ctz(u);
-        u &= u - 1;
-        if ((cm >> j) & 1u) {
+      // appends: each lane walks its own mask, reading its points from the wave's copy of the tile
+      // in LDS (the wave loops max-over-lanes popc(mask) times instead of over the union of the
+      // masks with four readlanes per point); the same d2 expression, the same bits
+      if (__ballot(cm != 0) != 0) {  // wave-uniform: every lane writes its float of the tile
+        reinterpret_cast<float*>(stile[wave])[lane] = v_cur;
+        __builtin_amdgcn_wave_barrier();
+        uint32_t my = cm;
+        while (__ballot(my != 0) != 0) {
+          if (my != 0) {
+            const int j = __builtin_ctz(my);
+            my &= my - 1;
 #ifdef DVCP_KNN_DIAG
-          ++dg_appends;
+            ++dg_appends;
 #endif
-          const float dx = bc(4 * j) - qx, dy = bc(4 * j + 1) - qy, dz = bc(4 * j + 2) - qz;
-          mybuf[fill][lane] = make_uint2(__float_as_uint((dx * dx + dy * dy) + dz * dz), __float_as_uint(bc(4 * j + 3)));
-          ++fill;
+            const float4 pt = stile[wave][j];
+            const float dx = pt.x - qx, dy = pt.y - qy, dz = pt.z - qz;
+            mybuf[fill][lane] = make_uint2(__float_as_uint((dx * dx + dy * dy) + dz * dz), __float_as_uint(pt.w));
+            ++fill;
+          }
         }
+        __builtin_amdgcn_wave_barrier();  // (the next active tile rewrites stile)
       }
     }
   }
