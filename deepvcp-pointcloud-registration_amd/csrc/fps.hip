@@ -555,7 +555,10 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
   __shared__ __attribute__((aligned(16))) T cxx[kSelMax];
   __shared__ __attribute__((aligned(16))) T cyy[kSelMax];
   __shared__ __attribute__((aligned(16))) T czz[kSelMax];
-  __shared__ int prank[W][kSelMax];  // per wave's i-range: count of preceding candidates | touched << 16
+  // per candidate, summed over the waves' i-ranges by LDS atomics: count of preceding candidates
+  // (bits 0-15) + count of waves with a toucher (bits 16+); phase 5 reads one word per candidate
+  // instead of one per wave (it ran on every wave, 4 per SIMD, with W reads each)
+  __shared__ uint32_t srank[kSelMax];
   __shared__ float wtf[W], wT[W];
   __shared__ uint32_t wpid[W];
   __shared__ T acx[kSelAccept], acy[kSelAccept], acz[kSelAccept];  // the round's accepted centres, rank order
@@ -886,6 +889,7 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
       tl = wave_fmax_nn(tl);
       if (lane == 0) wT[wave] = tl;
       if (na < 4u * kSelTarget) f *= 0.85f;  // next round: keep a few hundred points above the floor
+      if (wave * kWave < kSelMax) srank[wave * kWave + lane] = 0u;  // (read last by the previous round)
       lds_barrier();
       float Tb = wT[0];
 #pragma unroll
@@ -941,8 +945,10 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
             }
           }
         }
-        prank[wave][lane] = r0 | (t0 << 16);
-        prank[wave][lane + kWave] = r1 | (t1 << 16);
+        if (i_lo < cnt) {  // wave-uniform
+          if (r0 | t0) atomicAdd(&srank[lane], static_cast<uint32_t>(r0 | (t0 << 16)));
+          if (r1 | t1) atomicAdd(&srank[lane + kWave], static_cast<uint32_t>(r1 | (t1 << 16)));
+        }
       }
       lds_barrier();
       tick(2);
@@ -955,14 +961,9 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
         const int jj = hh * 64 + lane;
         rk[hh] = 0x7FFFFFFF;
         if (jj < cnt) {
-          int r = 0, tor = 0;
-#pragma unroll
-          for (int w = 0; w < W; ++w) {
-            const int e = prank[w][jj];
-            r += e & 0xFFFF;
-            tor |= e;
-          }
-          const bool touched = (tor >> 16) != 0;
+          const uint32_t e = srank[jj];
+          const int r = static_cast<int>(e & 0xFFFFu);
+          const bool touched = (e >> 16) != 0u;
           rk[hh] = r;
           const bool fail = r >= left || (r > 0 && (touched || !(cvv[jj] > Tb)));
           failr = fail ? min(failr, static_cast<uint32_t>(r)) : failr;

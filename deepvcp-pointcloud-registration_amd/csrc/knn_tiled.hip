@@ -530,6 +530,12 @@ __global__ __launch_bounds__(kTiledThreads) void knn_tiled_query_kernel(const fl
 // point appended, and a point is only left out when its key is not below a k-th key that is at
 // least the true one (filters and pruning use the last merged, i.e. a stale-high, k-th key).
 constexpr int kSelBufN = 16;
+// DVCP_KNN_LAZY (default): a tile's 256 bytes are loaded once some lane is known to need it.  The
+// alternative prefetch one sorted position ahead made every scanned tile wait for its successor's
+// load at the loop latch (the register copy), ~660 clk per skipped tile (DVCP_KNN_DIAG).
+#ifndef DVCP_KNN_LAZY
+#define DVCP_KNN_LAZY 1
+#endif
 
 __device__ __forceinline__ void key_ce(uint32_t& ah, uint32_t& al, uint32_t& bh, uint32_t& bl, bool asc) {
   const uint64_t a = (static_cast<uint64_t>(ah) << 32) | al, b = (static_cast<uint64_t>(bh) << 32) | bl;
@@ -621,7 +627,8 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
   int fill = 0;
   uint2(*mybuf)[kWave] = sbuf[wave];
 #ifdef DVCP_KNN_DIAG  // per-wave counters (diagnostic builds only; written over lane 0's distances)
-  uint64_t dg_t0 = __builtin_readcyclecounter(), dg_merge_clk = 0;
+  uint64_t dg_t0 = __builtin_readcyclecounter(), dg_merge_clk = 0, dg_skip_clk = 0, dg_prev = 0;
+  int dg_kind = -1;  // the previous iteration: 0 skipped, 1 processed
   int dg_scanned = 0, dg_active = 0, dg_merges = 0, dg_appends = 0;
 #endif
 
@@ -689,19 +696,35 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
   // profiles/round3/r3x_knn_diag_*.log.)
   const float* P = reinterpret_cast<const float*>(sorted) + static_cast<int64_t>(b) * T * kTile * 4;
   uint32_t key_next = T > 0 ? static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(keys[0]), 0)) : 0u;
+#if !DVCP_KNN_LAZY
   float v_next = T > 0 ? P[static_cast<int64_t>(key_next & kTileIdBits) * (4 * kTile) + lane] : 0.f;
+#endif
   // one flat loop over the sorted tile order (not unrolled over the key registers: the merge is
   // large, and the key register is a wave-uniform indexed read)
 #pragma unroll 1
   for (int pos = 0; pos < T; ++pos) {
+#ifdef DVCP_KNN_DIAG
+    {
+      const uint64_t now = __builtin_readcyclecounter();
+      if (dg_kind == 0) dg_skip_clk += now - dg_prev;
+      dg_prev = now;
+      dg_kind = 0;
+    }
+#endif
     {
       const uint32_t key = key_next;
+#if DVCP_KNN_LAZY
+      if (pos + 1 < T)
+        key_next = static_cast<uint32_t>(
+            __builtin_amdgcn_readlane(static_cast<int>(keys[(pos + 1) >> 6]), (pos + 1) & 63));
+#else
       const float v_cur = v_next;
       if (pos + 1 < T) {
         key_next = static_cast<uint32_t>(
             __builtin_amdgcn_readlane(static_cast<int>(keys[(pos + 1) >> 6]), (pos + 1) & 63));
         v_next = P[static_cast<int64_t>(key_next & kTileIdBits) * (4 * kTile) + lane];
       }
+#endif
       if (__uint_as_float(key & ~kTileIdBits) > wkth) break;  // every later tile is farther
       const int t = static_cast<int>(key & kTileIdBits);
       const float lbq = hbox_lb2(hbox[t], qx, qy, qz, qx, qy, qz);
@@ -712,6 +735,10 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
       if (__ballot(act) == 0) continue;
 #ifdef DVCP_KNN_DIAG
       ++dg_active;
+      dg_kind = 1;
+#endif
+#if DVCP_KNN_LAZY
+      const float v_cur = P[static_cast<int64_t>(t) * (4 * kTile) + lane];
 #endif
       auto bc = [&](int u) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v_cur), u)); };
       float c[3 * kTile];
@@ -780,7 +807,7 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
     dist[o + 3] = static_cast<float>(app_sum);
     dist[o + 4] = static_cast<float>(dg_total);
     dist[o + 5] = static_cast<float>(dg_merge_clk);
-    dist[o + 6] = static_cast<float>(T);
+    dist[o + 6] = static_cast<float>(dg_skip_clk);
     dist[o + 31] = -12345.0f;
     return;
   }

@@ -28,13 +28,15 @@ def main():
     torch.cuda.synchronize()
     d = dist.cpu().numpy().reshape(-1, 32)
     rows = d[d[:, 31] == -12345.0][:, :7]
-    names = ["scanned", "active", "merges", "appends", "clk", "merge_clk", "T"]
+    names = ["scanned", "active", "merges", "appends", "clk", "merge_clk", "skip_clk"]
     print(f"waves {len(rows)}")
     for i, n in enumerate(names):
         v = rows[:, i]
         print(f"{n:10s} mean {v.mean():12.1f}  p50 {np.percentile(v, 50):12.1f}  p90 {np.percentile(v, 90):12.1f}  "
               f"max {v.max():12.1f}  sum {v.sum():14.1f}")
     print(f"merge share of wave clk {rows[:, 5].sum() / rows[:, 4].sum():.3f}")
+    print(f"skipped-tile share of wave clk {rows[:, 6].sum() / rows[:, 4].sum():.3f}, "
+          f"clk per skipped tile {rows[:, 6].sum() / (rows[:, 0].sum() - rows[:, 1].sum()):.1f}")
     print(f"appends per active tile per lane {rows[:, 3].sum() / rows[:, 1].sum() / 64:.3f}")
     # by distance of the wave's first query from the cloud centre
     q = qry.cpu().numpy().reshape(-1, 3)
