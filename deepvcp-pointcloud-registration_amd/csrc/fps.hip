@@ -559,7 +559,10 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
   // (bits 0-15) + count of waves with a toucher (bits 16+); phase 5 reads one word per candidate
   // instead of one per wave (it ran on every wave, 4 per SIMD, with W reads each)
   __shared__ uint32_t srank[kSelMax];
-  __shared__ float wtf[W], wT[W];
+  __shared__ float wtf[W];
+  // T_f and T (non-negative floats as bits) reduced over the waves by LDS atomicMax: every wave
+  // reads one word instead of W
+  __shared__ uint32_t tf_max, tb_max;
   __shared__ uint32_t wpid[W];
   __shared__ T acx[kSelAccept], acy[kSelAccept], acz[kSelAccept];  // the round's accepted centres, rank order
   __shared__ T gbox[W][6][GP];  // group boxes, read back per round by the update (not held in VGPRs)
@@ -646,6 +649,8 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
   if (tid == 0) {
     na_cnt = 0u;
     cand_fill = 0u;
+    tf_max = 0u;
+    tb_max = 0u;
   }
   lds_barrier();
   vmax = wtf[0];
@@ -720,14 +725,12 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
         }
       }
       tf = wave_fmax_nn(tf);
-      if (lane == 0) wtf[wave] = tf;
+      if (lane == 0) atomicMax(&tf_max, __float_as_uint(tf));
       lds_barrier();
       tick(0);
       // ---- 2. decide (every wave computes the same decision from LDS) -------------------------
       const uint32_t na = na_cnt;
-      float Tf = wtf[0];
-#pragma unroll
-      for (int w = 1; w < W; ++w) Tf = fmaxf(Tf, wtf[w]);
+      const float Tf = __uint_as_float(tf_max);
       // suffix counts: lane l holds bins 4l .. 4l+3; suf(k) = hits in bins >= k
       uint32_t h[4], hs[4];
 #pragma unroll
@@ -809,7 +812,10 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
       if (mode == 1) {  // rescan: everyone has read hist / na / wtf; clear them
         lds_barrier();
         for (int i = tid; i < kSelBins; i += THREADS) hist[i] = 0u;
-        if (tid == 0) na_cnt = 0u;
+        if (tid == 0) {
+          na_cnt = 0u;
+          tf_max = 0u;
+        }
         lds_barrier();
         continue;
       }
@@ -824,7 +830,10 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
         lds_barrier();  // (wtf / hist reads above are done)
         if (lane == 0) wtf[wave] = bv;
         for (int i = tid; i < kSelBins; i += THREADS) hist[i] = 0u;
-        if (tid == 0) na_cnt = 0u;
+        if (tid == 0) {
+          na_cnt = 0u;
+          tf_max = 0u;
+        }
         lds_barrier();
         float gmax = wtf[0];
 #pragma unroll
@@ -887,14 +896,15 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
         }
       }
       tl = wave_fmax_nn(tl);
-      if (lane == 0) wT[wave] = tl;
+      if (lane == 0) atomicMax(&tb_max, __float_as_uint(tl));
       if (na < 4u * kSelTarget) f *= 0.85f;  // next round: keep a few hundred points above the floor
       if (wave * kWave < kSelMax) srank[wave * kWave + lane] = 0u;  // (read last by the previous round)
       lds_barrier();
-      float Tb = wT[0];
-#pragma unroll
-      for (int w = 1; w < W; ++w) Tb = fmaxf(Tb, wT[w]);
-      if (tid == 0) na_cnt = 0u;  // (two waves: two 32-bit stores, not one 64-bit pair held across rounds)
+      const float Tb = __uint_as_float(tb_max);
+      if (tid == 0) {  // (T_f was read by every wave before this barrier)
+        na_cnt = 0u;
+        tf_max = 0u;
+      }
       if (tid == kWave) cand_fill = 0u;
       for (int i = tid; i < kSelBins; i += THREADS) hist[i] = 0u;
       tick(1);
@@ -953,6 +963,7 @@ __global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, 
       lds_barrier();
       tick(2);
       // ---- 5. k = the smallest rank that fails; accepted = ranks < k (every wave, redundantly) ----
+      if (tid == 0) tb_max = 0u;  // every wave read T before the phase-4 barrier
       const int left = npoint - step;
       int rk[2];
       uint32_t failr = 0xFFFFFFFFu;
