@@ -18,6 +18,34 @@
 namespace dvcp {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// DVCP_CPG_SPLIT3 (default): conv1 on the bf16 matrix cores (v_mfma_f32_16x16x32_bf16) with the
+// fp32-accurate three-way split of sa_mlp_mfma.hip: each 8-channel quarter of the cost volume is
+// stored in LDS as three bf16 piece images ([piece][cell][8 channels], 16 B per cell and piece,
+// split once when the volume is built) and each quarter's weights as three B-fragment images; a
+// k-step covers 4 taps x 8 channels (K = 32), 7 k-steps per quarter (taps 0..26 + one zero tap),
+// six bf16 MFMAs (16 cycles) each, instead of 27 x 2 fp32 16x16x4 MFMAs (32 cycles) per quarter.
+#ifndef DVCP_CPG_SPLIT3
+#define DVCP_CPG_SPLIT3 1
+#endif
+
+// x = x0 + x1 + x2 exactly (bf16 pieces, as sa_mlp_mfma.hip's split3)
+__device__ __forceinline__ void cpg_split3(float x, __bf16& p0, __bf16& p1, __bf16& p2) {
+  p0 = static_cast<__bf16>(x);
+  const float r1 = x - static_cast<float>(p0);
+  p1 = static_cast<__bf16>(r1);
+  p2 = static_cast<__bf16>(r1 - static_cast<float>(p1));
+}
+__device__ __forceinline__ f32x4 cpg_mfma_split3(const bf16x8& a0, const bf16x8& a1, const bf16x8& a2,
+                                                const bf16x8& b0, const bf16x8& b1, const bf16x8& b2, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b0, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b2, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b0, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b1, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc, 0, 0, 0);
+}
 
 constexpr int kCpgThreads = 1024;  // 16 waves: four per SIMD (LDS allows one workgroup per CU)
 constexpr int kCpgMaxC = 1331;
@@ -41,8 +69,10 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
   __shared__ float bias[16 + 4 + 1];
   __shared__ float sv[32];
   __shared__ float red[32];
+#if !DVCP_CPG_SPLIT3
   float* vol = big;            // conv1 input: a haloed 8-channel quarter of the cost volume
   float* w1 = big + kCpgVolF;  // conv1 W [ci][tap][co]
+#endif
   float* out1 = big;           // after conv1: its output, haloed [co][cell] (16 x PV)
   float* out2 = big;           // after conv2: its output, haloed [co][cell] (4 x PV)
 
@@ -61,11 +91,13 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
     const int e = u * kCpgThreads + tid;  // memory order (c, f)
     tv[u] = e < 32 * C ? T[(e % 32) * t_f + (e / 32) * t_c] : 0.f;
   }
+#if !DVCP_CPG_SPLIT3
 #pragma unroll 6
   for (int i = tid; i < 16 * 32 * 27; i += kCpgThreads) {  // torch (co, ci, kd, kh, kw)
     const int co = i / (32 * 27), r = i % (32 * 27);
     w1[r * 16 + co] = P1[i];
   }
+#endif
   if (tid < 4 * 27) w3[tid] = P3[tid];
   if (tid < 16) bias[tid] = P1[16 * 32 * 27 + tid];
   if (tid < 4) bias[16 + tid] = P2[4 * 16 * 27 + tid];
@@ -87,16 +119,87 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
   constexpr int kTW = (kT + kW - 1) / kW;           // per wave
   const int lane = tid & 63, wave = tid >> 6, kg = lane >> 4, l16 = lane & 15;
   const int NT = (C + 15) / 16;
-  int vx[kTW];  // haloed address of the lane's voxel per tile (a border cell past the end)
+  int vx[kTW];  // haloed address of the lane's voxel per tile (voxel 0's cell past the end: every
+                // tap of a padding row stays inside the volume; its output row is discarded)
 #pragma unroll
   for (int i = 0; i < kTW; ++i) {
     const int g = 16 * (wave + kW * i) + l16;
-    vx[i] = g < C ? cpg_halo(g, dG, dGG, PG, PGG) : 0;
+    vx[i] = cpg_halo(g < C ? g : 0, dG, dGG, PG, PGG);
   }
   f32x4 acc[kTW];
 #pragma unroll
   for (int i = 0; i < kTW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+#if DVCP_CPG_SPLIT3
+  {
+    uint4* vsp = reinterpret_cast<uint4*>(big);                    // [piece][cell]: 8 bf16 channels
+    uint4* w1p = vsp + 3 * PV;                                     // [k-step][piece][lane]
+    static_assert(3 * kCpgPV * 16 + 7 * 3 * 64 * 16 <= kCpgBigF * 4, "split images must fit the area");
+#pragma unroll 1
+    for (int q = 0; q < 32 / kCpgQ; ++q) {
+      __syncthreads();
+      for (int i = tid; i < 3 * PV; i += kCpgThreads) vsp[i] = make_uint4(0u, 0u, 0u, 0u);
+      // this quarter's conv1 weights: k-step s, lane (co = l & 15, tap 4 s + (l >> 4)), channel j
+      for (int i = tid; i < 7 * 64; i += kCpgThreads) {
+        const int l = i & 63, st = i >> 6, co = l & 15, tap = 4 * st + (l >> 4);
+        bf16x8 b0, b1, b2;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const float w = tap < 27 ? P1[(co * 32 + kCpgQ * q + jj) * 27 + tap] : 0.0f;
+          __bf16 x0, x1, x2;
+          cpg_split3(w, x0, x1, x2);
+          b0[jj] = x0;
+          b1[jj] = x1;
+          b2[jj] = x2;
+        }
+        w1p[(st * 3 + 0) * 64 + l] = __builtin_bit_cast(uint4, b0);
+        w1p[(st * 3 + 1) * 64 + l] = __builtin_bit_cast(uint4, b1);
+        w1p[(st * 3 + 2) * 64 + l] = __builtin_bit_cast(uint4, b2);
+      }
+      __syncthreads();
+      // cost volume quarter as bf16 pieces (see the fp32 path below for the Q11 index map)
+      int zo = 0;
+      asm volatile("" : "+v"(zo));
+      const int f0 = tid & 31;
+      const int l0 = f0 * C + (tid >> 5) + zo;
+      uint16_t* vh = reinterpret_cast<uint16_t*>(vsp);
+#pragma unroll
+      for (int u = 0; u < kCpgE; ++u) {
+        const int e = u * kCpgThreads + tid;
+        const int l = l0 + (kCpgThreads / 32) * u;
+        const int g = l >> 5, fp = l & 31;
+        if (e < 32 * C && (fp >> 3) == q) {
+          const float d = sv[fp] - tv[u];
+          __bf16 x0, x1, x2;
+          cpg_split3(d * d, x0, x1, x2);
+          const int c8 = cpg_halo(g, dG, dGG, PG, PGG) * 8 + (fp & 7);
+          vh[c8] = __builtin_bit_cast(uint16_t, x0);
+          vh[8 * PV + c8] = __builtin_bit_cast(uint16_t, x1);
+          vh[16 * PV + c8] = __builtin_bit_cast(uint16_t, x2);
+        }
+      }
+      __syncthreads();
+#pragma unroll 1
+      for (int st = 0; st < 7; ++st) {
+        // lane's tap 4 st + kg (tap 27: zero weights, any in-range cell)
+        const int tap = 4 * st + kg;
+        const int off = tap < 27 ? (tap / 9 - 1) * PGG + ((tap / 3) % 3 - 1) * PG + (tap % 3 - 1) : 0;
+        const bf16x8 b0 = __builtin_bit_cast(bf16x8, w1p[(st * 3 + 0) * 64 + lane + zo]);
+        const bf16x8 b1 = __builtin_bit_cast(bf16x8, w1p[(st * 3 + 1) * 64 + lane + zo]);
+        const bf16x8 b2 = __builtin_bit_cast(bf16x8, w1p[(st * 3 + 2) * 64 + lane + zo]);
+#pragma unroll
+        for (int i = 0; i < kTW; ++i)
+          if (wave + kW * i < NT) {  // wave-uniform
+            const int cell = vx[i] + off;
+            const bf16x8 a0 = __builtin_bit_cast(bf16x8, vsp[cell]);
+            const bf16x8 a1 = __builtin_bit_cast(bf16x8, vsp[PV + cell]);
+            const bf16x8 a2 = __builtin_bit_cast(bf16x8, vsp[2 * PV + cell]);
+            acc[i] = cpg_mfma_split3(a0, a1, a2, b0, b1, b2, acc[i]);
+          }
+      }
+    }
+  }
+#else
 #pragma unroll 1
   for (int q = 0; q < 32 / kCpgQ; ++q) {
     __syncthreads();
@@ -137,6 +240,7 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
       }
     }
   }
+#endif
   __syncthreads();
   // conv1 output -> out1 (haloed, zero border); accumulator register r of lane l is voxel
   // 16 t + 4 (l >> 4) + r, output channel l & 15
