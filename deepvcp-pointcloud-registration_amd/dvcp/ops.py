@@ -327,10 +327,25 @@ def dfe_tgt(ref_xyz, ref_feat, cand, dist, idx, params, ref_pdim=2, literal=Fals
     call(name, dtype_code(ref_xyz), ptr(ref_xyz), rb, rc, rn, M, ptr(feat_c), ptr(cand_c), ptr(dist_c),
          ptr(idx_c), B, Q, ptr(params), ptr(out), stream(),
          work=(2.0 * 3168 * 32 * B * Q, B * (M * (12 + row) + Q * (12 + 32 * 8 + 128)),
-               # executed: one v_mfma_f32_32x32x2_f32 per k-step per candidate (35 input channels
-               # padded to 19 k-steps; literal: + 16 + 16 for fc2, fc3)
-               ((51 if literal else 19) * MFMA_F32_32X32X2_FLOPS * float(B * Q),) * 2))
+               _dfe_tgt_exec(literal, float(B * Q))))
     return out
+
+
+def _dfe_tgt_exec(literal, cands):
+    """Executed MFMA work of the target DFE (csrc/dfe_mfma.hip), as bench.py's 4-tuple (fp32-equivalent
+    flops, of which on the matrix cores, of which on the bf16 pipe, the bf16 pipe's own flops).
+    Literal (Q14) path: 51 v_mfma_f32_32x32x2_f32 per candidate (fc1's 35 inputs in 19 k-steps, 16 +
+    16 for fc2, fc3).  Collapsed path: the xyz columns in 2 fp32 k-steps and the 32 feature columns
+    in 2 split-3 bf16 k-steps (six v_mfma_f32_32x32x16_bf16 each)."""
+    if literal:
+        f = 51 * MFMA_F32_32X32X2_FLOPS * cands
+        return f, f
+    bf = 2 * MFMA_BF16_32X32X16_FLOPS * cands
+    f = 2 * MFMA_F32_32X32X2_FLOPS * cands + bf
+    return f, f, bf, 6.0 * bf
+
+
+MFMA_BF16_16X16X32_FLOPS = 2 * 16 * 16 * 32  # one v_mfma_f32_16x16x32_bf16
 
 
 def cpg(src, tgt, cand, G, params, want_weight=False):
@@ -349,10 +364,17 @@ def cpg(src, tgt, cand, G, params, want_weight=False):
     call("dvcp_cpg", ptr(srcc), ptr(tgt), tgt.stride(1), tgt.stride(2), tgt.stride(3), ptr(candc), B * K, int(G),
          ptr(params), ptr(vcp), ptr(w), stream(),
          work=(2.0 * 27 * (32 * 16 + 16 * 4 + 4) * B * K * C, B * K * (128 + C * (128 + 12) + 12),
-               # executed (reference graph; halo padding of the implicit GEMM not counted), of which
-               # conv1 runs on v_mfma_f32_16x16x4_f32
-               (2.0 * 27 * (32 * 16 + 16 * 4 + 4) * B * K * C, 2.0 * 27 * 32 * 16 * B * K * C)))
+               _cpg_exec(B * K, C)))
     return (vcp, w) if want_weight else vcp
+
+
+def _cpg_exec(P, C):
+    """Executed work of the CPG forward (csrc/cpg.hip) as bench.py's 4-tuple: conv1 on
+    v_mfma_f32_16x16x32_bf16 with the split-3 (per 16-voxel tile and 8-channel quarter, 7 k-steps of
+    4 taps: one zero tap of padding), conv2 and conv3 on VALU (reference-graph flops)."""
+    conv1 = float(P) * (-(-C // 16)) * 4 * 7 * MFMA_BF16_16X16X32_FLOPS
+    rest = 2.0 * 27 * (16 * 4 + 4) * P * C
+    return conv1 + rest, conv1, conv1, 6.0 * conv1
 
 
 def rigid_transform(x, y):
