@@ -114,6 +114,129 @@ __global__ __launch_bounds__(1024) void topk_kernel(const float* __restrict__ sc
   }
 }
 
+// Top-K by radix select (default): the K-th largest 64-bit key (float order of the score << 32 |
+// ~index: value descending, ties -> lower index, exactly the argmax rounds' order) is found 8 bits
+// at a time below the keys' common prefix (LDS histogram, one wave picks the digit), then the K
+// keys at or above it are gathered and each one's output position is its count of larger keys.
+// ~3 barriers per pass and a few passes instead of K block-argmax rounds.
+constexpr int kTopkMaxK = 1024;
+
+template <int PPT>
+__global__ __launch_bounds__(1024) void topk_select_kernel(const float* __restrict__ score, int S, int K,
+                                                           int64_t* __restrict__ out) {
+  constexpr int NT = 1024;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ uint32_t hist[256];
+  __shared__ uint64_t red[2][NT / kWave];
+  __shared__ uint64_t cand[kTopkMaxK];
+  __shared__ uint32_t sel[2], ncand;
+  uint64_t key[PPT];
+  uint64_t kmax = 0ull, kmin = ~0ull;
+#pragma unroll
+  for (int p = 0; p < PPT; ++p) {
+    const int n = tid + p * NT;
+    key[p] = n < S ? ((static_cast<uint64_t>(float_order(score[static_cast<int64_t>(b) * S + n])) << 32) |
+                      static_cast<uint64_t>(0xFFFFFFFFu - static_cast<uint32_t>(n)))
+                   : 0ull;  // below every real key (their low word is > 0)
+    if (n < S) {
+      kmax = key[p] > kmax ? key[p] : kmax;
+      kmin = key[p] < kmin ? key[p] : kmin;
+    }
+  }
+  // common prefix of the real keys: the radix passes start at their first differing bit
+  kmax = wave_max_u64(kmax);
+  kmin = ~wave_max_u64(~kmin);
+  if (lane == 0) {
+    red[0][wave] = kmax;
+    red[1][wave] = ~kmin;
+  }
+  if (tid == 0) ncand = 0u;
+  lds_barrier();
+  uint64_t hi = red[0][0], lo_n = red[1][0];
+#pragma unroll
+  for (int w = 1; w < NT / kWave; ++w) {
+    hi = red[0][w] > hi ? red[0][w] : hi;
+    lo_n = red[1][w] > lo_n ? red[1][w] : lo_n;
+  }
+  const uint64_t lo = ~lo_n;
+  const int top = hi == lo ? 0 : 63 - __clzll(static_cast<long long>(hi ^ lo));  // highest differing bit
+  uint64_t prefix = hi & ~((top >= 63) ? ~0ull : ((2ull << top) - 1ull));       // bits above `top`
+  uint64_t pmask = (top >= 63) ? 0ull : ~((2ull << top) - 1ull);
+  uint32_t need = static_cast<uint32_t>(K);
+  int shift = top + 1;  // bits [shift, 64) are fixed in prefix
+#pragma unroll 1
+  while (shift > 0) {
+    const int w = shift >= 8 ? 8 : shift;
+    shift -= w;
+    for (int i = tid; i < 256; i += NT) hist[i] = 0u;
+    lds_barrier();
+    const uint32_t dm = (1u << w) - 1u;
+#pragma unroll
+    for (int p = 0; p < PPT; ++p)
+      if ((key[p] & pmask) == prefix) atomicAdd(&hist[static_cast<uint32_t>(key[p] >> shift) & dm], 1u);
+    lds_barrier();
+    if (wave == 0) {
+      // digits from the top: the digit d where the count of larger digits is < need <= count of
+      // digits >= d.  Lane l holds digits 255 - 4l .. 252 - 4l (descending).
+      uint32_t c[4], run = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        c[j] = hist[255 - (4 * lane + j)];
+        run += c[j];
+      }
+      uint32_t incl = run;  // inclusive prefix over lanes (descending digit order)
+#pragma unroll
+      for (int off = 1; off < kWave; off <<= 1) {
+        const uint32_t u = __shfl_up(incl, off, kWave);
+        if (lane >= off) incl += u;
+      }
+      uint32_t before = incl - run;  // keys with larger digits in lower lanes
+      int dsel = -1;
+      uint32_t above = 0, cnt_d = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (dsel < 0 && before + c[j] >= need) {
+          dsel = 255 - (4 * lane + j);
+          above = before;
+          cnt_d = c[j];
+        }
+        before += c[j];
+      }
+      const uint64_t hit = __ballot(dsel >= 0);
+      const int src = __ffsll(static_cast<long long>(hit)) - 1;
+      const int d = __shfl(dsel, src, kWave);
+      const uint32_t ab = __shfl(above, src, kWave), cd = __shfl(cnt_d, src, kWave);
+      if (lane == 0) {
+        sel[0] = static_cast<uint32_t>(d);
+        sel[1] = (need - ab) | (cd == need - ab ? 0x80000000u : 0u);  // all keys of digit d are taken
+      }
+    }
+    lds_barrier();
+    prefix |= static_cast<uint64_t>(sel[0]) << shift;
+    pmask |= static_cast<uint64_t>(dm) << shift;
+    const uint32_t sv = sel[1];
+    need = sv & 0x7FFFFFFFu;
+    if (sv & 0x80000000u) break;  // every key matching the prefix is in the top K (uniform)
+  }
+  // the top K: keys above the prefix range, and every key in it (count == need)
+#pragma unroll
+  for (int p = 0; p < PPT; ++p) {
+    const uint64_t km = key[p] & pmask;
+    if (key[p] != 0ull && km >= prefix) {
+      const uint32_t i = atomicAdd(&ncand, 1u);
+      if (i < static_cast<uint32_t>(kTopkMaxK)) cand[i] = key[p];
+    }
+  }
+  lds_barrier();
+  const int nc = min(static_cast<int>(ncand), K);
+  for (int i = tid; i < nc; i += NT) {
+    const uint64_t ki = cand[i];
+    int r = 0;
+    for (int j = 0; j < nc; ++j) r += cand[j] > ki ? 1 : 0;
+    out[static_cast<int64_t>(b) * K + r] = key_index(ki);
+  }
+}
+
 }  // namespace dvcp
 
 extern "C" int dvcp_fe_head(const float* x, int P, const float* params, float* feat, float* score, void* stream) {
@@ -150,7 +273,10 @@ extern "C" int dvcp_topk(const float* score, int B, int S, int K, int64_t* idx, 
   const int ppt = dvcp::ceil_div(S, 1024);
 #define DVCP_TOPK(P)                                                                                   \
   if (ppt <= P) {                                                                                      \
-    hipLaunchKernelGGL((dvcp::topk_kernel<P>), dim3(B), dim3(1024), 0, st, score, S, K, idx);          \
+    if (K <= dvcp::kTopkMaxK)                                                                          \
+      hipLaunchKernelGGL((dvcp::topk_select_kernel<P>), dim3(B), dim3(1024), 0, st, score, S, K, idx); \
+    else                                                                                               \
+      hipLaunchKernelGGL((dvcp::topk_kernel<P>), dim3(B), dim3(1024), 0, st, score, S, K, idx);        \
     return dvcp::launch_status("dvcp_topk");                                                           \
   }
   DVCP_TOPK(1)
