@@ -513,6 +513,40 @@ def test_topk(cuda):
     assert ops.topk(tied.to(cuda), 4).cpu().tolist() == [[1, 2, 4, 3]]  # value desc, index asc
 
 
+@pytest.mark.parametrize("case", ["all_equal", "few_values", "negative", "k_eq_s", "k1", "ragged", "k256"])
+def test_topk_radix_select_cases(cuda, case):
+    """The radix-select top-k (head_topk.hip) against value-descending, index-ascending order:
+    massive ties (the select runs into the index bits), mixed signs, K = S, K = 1, S not a
+    multiple of the workgroup, C5's K = 256."""
+    import numpy as np
+    from dvcp import ops
+    g = torch.Generator().manual_seed(118)
+    B, S, K = 3, 10000, 64
+    if case == "all_equal":
+        s = torch.full((B, S), 0.75)
+    elif case == "few_values":
+        s = torch.randint(0, 5, (B, S), generator=g).float() * 0.25
+    elif case == "negative":
+        s = torch.randn(B, S, generator=g)
+    elif case == "k_eq_s":
+        S = K = 700
+        s = torch.rand(B, S, generator=g)
+    elif case == "k1":
+        K = 1
+        s = torch.rand(B, S, generator=g)
+    elif case == "ragged":
+        S, K = 3333, 50
+        s = torch.randint(0, 40, (B, S), generator=g).float()
+    else:
+        S, K = 16384, 256
+        s = torch.rand(B, S, generator=g)
+    got = ops.topk(s.to(cuda), K).cpu().numpy()
+    for b in range(B):
+        v = s[b].numpy()
+        want = np.lexsort((np.arange(S), -v))[:K]  # value descending, then index ascending
+        assert np.array_equal(got[b], want), case
+
+
 # ------------------------------------------------------------------------------ DFE / CPG
 def test_dfe_vs_oracle(cuda):
     import oracle as O
