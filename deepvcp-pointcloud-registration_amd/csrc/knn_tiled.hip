@@ -536,6 +536,12 @@ constexpr int kSelBufN = 16;
 #ifndef DVCP_KNN_LAZY
 #define DVCP_KNN_LAZY 1
 #endif
+// DVCP_KNN_SLOAD: an active tile's 16 points reach the wave as scalar loads (the tile index is
+// wave-uniform, the tile is read-only here) instead of one vector load and 48 readlanes; the
+// appends, which index the tile per lane, load their LDS copy from L2 when a lane needs one.
+#ifndef DVCP_KNN_SLOAD
+#define DVCP_KNN_SLOAD 0
+#endif
 
 __device__ __forceinline__ void key_ce(uint32_t& ah, uint32_t& al, uint32_t& bh, uint32_t& bl, bool asc) {
   const uint64_t a = (static_cast<uint64_t>(ah) << 32) | al, b = (static_cast<uint64_t>(bh) << 32) | bl;
@@ -737,17 +743,30 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
       ++dg_active;
       dg_kind = 1;
 #endif
+      float c[3 * kTile];
+#if DVCP_KNN_LAZY && DVCP_KNN_SLOAD
+      {
+        const float4* Pt = reinterpret_cast<const float4*>(P) + static_cast<int64_t>(t) * kTile;
+#pragma unroll
+        for (int j = 0; j < kTile; ++j) {
+          const float4 pj = Pt[j];
+          c[3 * j] = pj.x;
+          c[3 * j + 1] = pj.y;
+          c[3 * j + 2] = pj.z;
+        }
+      }
+#else
 #if DVCP_KNN_LAZY
       const float v_cur = P[static_cast<int64_t>(t) * (4 * kTile) + lane];
 #endif
       auto bc = [&](int u) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v_cur), u)); };
-      float c[3 * kTile];
 #pragma unroll
       for (int j = 0; j < kTile; ++j) {
         c[3 * j] = bc(4 * j);
         c[3 * j + 1] = bc(4 * j + 1);
         c[3 * j + 2] = bc(4 * j + 2);
       }
+#endif
       // d2 is recomputed wherever it is needed (the same expression, the same bits) instead of
       // being held in 16 VGPRs across the merge and the appends
       auto d2_of = [&](int j) {
@@ -771,7 +790,11 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
       // in LDS (the wave loops max-over-lanes popc(mask) times instead of over the union of the
       // masks with four readlanes per point); the same d2 expression, the same bits
       if (__ballot(cm != 0) != 0) {  // wave-uniform: every lane writes its float of the tile
+#if DVCP_KNN_LAZY && DVCP_KNN_SLOAD
+        reinterpret_cast<float*>(stile[wave])[lane] = P[static_cast<int64_t>(t) * (4 * kTile) + lane];
+#else
         reinterpret_cast<float*>(stile[wave])[lane] = v_cur;
+#endif
         __builtin_amdgcn_wave_barrier();
         uint32_t my = cm;
         while (__ballot(my != 0) != 0) {
