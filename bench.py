@@ -58,6 +58,14 @@ PEAK_FP32_TFLOPS = 157.3   # fp32 vector = fp32 MFMA dense rate
 PEAK_BF16_TFLOPS = 16 * PEAK_FP32_TFLOPS   # bf16 MFMA dense rate (the SA layer 2's split pieces)
 PEAK_HBM_GBS = 8000.0
 N_CU = 256
+# flops counted per unit of the distance-scan kernels (dvcp/ops.py): one (query, point) evaluation =
+# 3 sub + 3 mul + 2 add + 1 compare = 9; SURVEY.md 8(d) prices it at ~8 (no compare), i.e. 8/9 of
+# the reported achieved rate
+FLOP_CONVENTION = {
+    "dvcp_knn_tiled": "9 flop per (query, reference point) pair of the reference's brute-force graph: 3 sub, "
+                      "3 mul, 2 add, 1 compare (SURVEY 8(d) counts ~8 without the compare: x 8/9)",
+    "dvcp_ball_query_ws": "9 flop per (centre, point) pair of the reference's dense graph (as the kNN)",
+}
 
 
 def parse():
@@ -86,6 +94,9 @@ def parse():
     p.add_argument("--iso-steps", type=int, default=3,
                    help="steps timed per kernel with one batch in flight (stage roofline)")
     p.add_argument("--cpu-pairs", type=int, default=3, help="C3 pairs timed for the CPU baseline (median)")
+    p.add_argument("--detail-json", default=None,
+                   help="also write the full record (per-stage roofline, live launch times) to this file; it "
+                        "always goes to stderr as one 'bench-detail' JSON line")
     a = p.parse_args()
     c5 = a.config == "c5"
     a.batch = a.batch if a.batch is not None else (2 if c5 else 8)
@@ -238,9 +249,41 @@ def main():
             for k, v in stages.items():
                 print(f"{k:28s} {v}", file=sys.stderr)
             print(json.dumps(step_roof), file=sys.stderr)
-        print(json.dumps(out), flush=True)
+        # the full record to stderr (and --detail-json); stdout gets ONE compact headline line that
+        # a log tail keeps whole (value, latency, roofline, cpu_baseline, parity, errors)
+        print("bench-detail " + json.dumps(out), file=sys.stderr, flush=True)
+        if args.detail_json:
+            with open(args.detail_json, "w") as fh:
+                json.dump(out, fh, indent=1)
+        print(json.dumps(headline(out)), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+                 "vs_baseline", "dtype", "data", "config", "latency_ms_single_batch", "roofline", "cpu_baseline",
+                 "parity", "registration_error_vs_gt")
+
+
+def headline(out):
+    """The stdout line: the contract's fields plus latency, roofline, cpu_baseline, parity and the
+    registration error, each trimmed of its long notes; the FPS chain and the step roofline as
+    one-number summaries (the full objects are in the stderr 'bench-detail' line)."""
+    h = {k: out[k] for k in HEADLINE_KEYS if k in out}
+    h["roofline"] = {k: v for k, v in out["roofline"].items() if k not in ("note", "pmc", "work_basis")}
+    if out["roofline"].get("pmc"):
+        h["roofline"]["pmc"] = {k: v for k, v in out["roofline"]["pmc"].items() if k != "note"}
+    if "cpu_baseline" in out:
+        h["cpu_baseline"] = {k: out["cpu_baseline"][k] for k in ("value", "unit", "cores", "kind", "sample", "cpu_model")}
+    if "parity" in out:
+        h["parity"] = {k: v for k, v in out["parity"].items() if not k.endswith("_note")}
+    if "registration_error_vs_gt" in out:
+        h["registration_error_vs_gt"] = {k: v for k, v in out["registration_error_vs_gt"].items() if k != "note"}
+    fr = out.get("fps_roofline") or {}
+    h["fps"] = {k: fr.get(k) for k in ("us_per_centre", "step_floor_us", "frac_of_step_floor", "avg_launch_ms_isolated")}
+    h["step_roofline_frac"] = out["step_roofline"]["achieved_frac"]
+    h["hbm_fraction_step"] = out["hbm_fraction_step"]
+    return h
 
 
 def _per_kernel(log):
@@ -364,8 +407,10 @@ def dominant_roofline(live, iso, stages, pmc):
         achieved, peak, unit = flops / v["n"] / (launch_ms * 1e-3) / 1e12, peak_eff * share, "TFLOP/s"
     w = live.get(name)
     p = pmc.get(name, {})
-    return {"bound": "hbm" if st["bound"] == "hbm" else "mfma",
-            "pipe": {"mfma": "mfma", "fp32": "valu", "hbm": "hbm"}[st["bound"]],
+    return {"bound": {"mfma": "mfma", "fp32": "valu", "hbm": "hbm"}[st["bound"]],
+            "bound_note": "the stage's own bound: mfma (matrix cores), valu (fp32 vector ALU; on gfx950 its peak "
+                          "equals the fp32 MFMA rate, 157.3 TF/s) or hbm",
+            "flop_convention": FLOP_CONVENTION.get(name, "executed flops as counted by dvcp/ops.py"),
             "kernel": name, "achieved": round(achieved, 3), "peak": round(peak, 3), "unit": unit,
             "frac": round(achieved / peak, 4), "traffic": p.get("hbm_bytes_per_launch"),
             "work_basis": st["work_basis"], "flops_per_launch": flops / v["n"],

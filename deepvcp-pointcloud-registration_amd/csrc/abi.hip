@@ -28,4 +28,6 @@ int launch_status(const char* what) {
 
 extern "C" const char* dvcp_last_error(void) { return dvcp::g_err; }
 
-extern "C" int dvcp_abi_version(void) { return 1; }
+// 2: dvcp_paper_pose gained inlier_ratio, dvcp_sa_bn_stats gained zrows, dvcp_fps_split_probe gained out_xyz
+// (round 3); a consumer built against an older header must fail cleanly, not pass shifted pointers.
+extern "C" int dvcp_abi_version(void) { return DVCP_ABI_VERSION; }

@@ -458,9 +458,16 @@ extern "C" int64_t dvcp_dfe_tgt_backward_workspace_bytes(int B, int Q, int M, in
 static int dfe_backward_launch(int mode, int dtype, const void* X, const void* ref_xyz, int64_t rb, int64_t rc,
                                int64_t rn, int M, const float* ref_feat, const float* cand, const float* dist,
                                const int32_t* idx, int Q, int64_t R, const float* params, const float* grad_out,
-                               float* ws, float* grad_params, float* gX, float* gF_out, hipStream_t st) {
-  if (R <= 0) {  // no rows: zero gradients
+                               float* ws, float* grad_params, float* gX, float* gF_out, int rows_out, hipStream_t st) {
+  if (R <= 0) {  // no rows: zero gradients (the target-feature gradient too: no entry routes to any row)
     hipLaunchKernelGGL(dvcp::dfe_bwd_finish_kernel, dim3(1), dim3(1024), 0, st, nullptr, params, grad_params);
+    if (gF_out && M > 0 && rows_out > 0) {
+      const hipError_t e = hipMemsetAsync(gF_out, 0, static_cast<size_t>(rows_out) * M * 32 * sizeof(float), st);
+      if (e != hipSuccess) {
+        dvcp::set_error("dvcp_dfe_tgt_backward: hipMemsetAsync: %s", hipGetErrorString(e));
+        return DVCP_EHIP;
+      }
+    }
     return dvcp::launch_status("dvcp_dfe_backward");
   }
   const int nblk = static_cast<int>(dfe_bwd_blocks(R));
@@ -508,7 +515,7 @@ extern "C" int dvcp_dfe_backward(int x_dtype, const void* X, int64_t R, const fl
                                  float* ws, float* grad_params, float* grad_X, void* stream) {
   DVCP_REQUIRE(params && grad_params && (R <= 0 || (X && grad_out && ws)), "dvcp_dfe_backward: null pointer");
   return dfe_backward_launch(0, x_dtype, X, nullptr, 0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, 1, R, params,
-                             grad_out, ws, grad_params, grad_X, nullptr, static_cast<hipStream_t>(stream));
+                             grad_out, ws, grad_params, grad_X, nullptr, 0, static_cast<hipStream_t>(stream));
 }
 
 extern "C" int dvcp_dfe_tgt_backward(int dtype, const void* ref_xyz, int64_t rb, int64_t rc, int64_t rn, int M,
@@ -519,7 +526,11 @@ extern "C" int dvcp_dfe_tgt_backward(int dtype, const void* ref_xyz, int64_t rb,
   DVCP_REQUIRE(B == 0 || Q == 0 || (ref_xyz && ref_feat && cand && dist && idx && grad_out && ws),
                "dvcp_dfe_tgt_backward: null pointer");
   DVCP_REQUIRE(M > 0 && B >= 0 && Q >= 0, "dvcp_dfe_tgt_backward: bad sizes");
+  // the feature gradient's segment sums use int entry counts and u32 row keys (include/dvcp.h)
+  DVCP_REQUIRE(!grad_ref_feat || (static_cast<int64_t>(B) * Q * 32 < (int64_t(1) << 31) &&
+                                  static_cast<int64_t>(B) * M < (int64_t(1) << 31)),
+               "dvcp_dfe_tgt_backward: B*Q*32 and B*M must stay below 2^31 (B=%d Q=%d M=%d)", B, Q, M);
   return dfe_backward_launch(1, dtype, nullptr, ref_xyz, rb, rc, rn, M, ref_feat, cand, dist, idx, Q > 0 ? Q : 1,
-                             static_cast<int64_t>(B) * Q, params, grad_out, ws, grad_params, nullptr, grad_ref_feat,
+                             static_cast<int64_t>(B) * Q, params, grad_out, ws, grad_params, nullptr, grad_ref_feat, B,
                              static_cast<hipStream_t>(stream));
 }

@@ -137,7 +137,7 @@ __global__ __launch_bounds__(1024) void topk_select_kernel(const float* __restri
     const int n = tid + p * NT;
     key[p] = n < S ? ((static_cast<uint64_t>(float_order(score[static_cast<int64_t>(b) * S + n])) << 32) |
                       static_cast<uint64_t>(0xFFFFFFFFu - static_cast<uint32_t>(n)))
-                   : 0ull;  // below every real key (their low word is > 0)
+                   : 0ull;  // padding (n >= S): excluded by index from the histograms and the gather
     if (n < S) {
       kmax = key[p] > kmax ? key[p] : kmax;
       kmin = key[p] < kmin ? key[p] : kmin;
@@ -173,7 +173,8 @@ __global__ __launch_bounds__(1024) void topk_select_kernel(const float* __restri
     const uint32_t dm = (1u << w) - 1u;
 #pragma unroll
     for (int p = 0; p < PPT; ++p)
-      if ((key[p] & pmask) == prefix) atomicAdd(&hist[static_cast<uint32_t>(key[p] >> shift) & dm], 1u);
+      if (tid + p * NT < S && (key[p] & pmask) == prefix)  // padding slots never vote (any score may
+        atomicAdd(&hist[static_cast<uint32_t>(key[p] >> shift) & dm], 1u);  // share their key's top bits)
     lds_barrier();
     if (wave == 0) {
       // digits from the top: the digit d where the count of larger digits is < need <= count of
@@ -222,7 +223,7 @@ __global__ __launch_bounds__(1024) void topk_select_kernel(const float* __restri
 #pragma unroll
   for (int p = 0; p < PPT; ++p) {
     const uint64_t km = key[p] & pmask;
-    if (key[p] != 0ull && km >= prefix) {
+    if (tid + p * NT < S && km >= prefix) {
       const uint32_t i = atomicAdd(&ncand, 1u);
       if (i < static_cast<uint32_t>(kTopkMaxK)) cand[i] = key[p];
     }

@@ -13,7 +13,9 @@ from .get_cat_feat_src import Get_Cat_Feat_Src  # noqa: F401
 from .get_cat_feat_tgt import Get_Cat_Feat_Tgt  # noqa: F401
 from .knn import KNN  # noqa: F401
 from . import paper  # noqa: F401
-from .metrics import registration_errors  # noqa: F401
+# the reference harness's registration error (train.py:112-120, :156-164; C8 fixed): per pair on the
+# GPU (dvcp_registration_error), so a multi-GPU job all-gathers it with the poses
+from .ops import registration_error as registration_errors  # noqa: F401
 from .datasets import KITTIDataset, ModelNet40Dataset  # noqa: F401
 from .voxelize import voxelize, voxelize_point  # noqa: F401
 from .weighting_layer import weighting_layer  # noqa: F401

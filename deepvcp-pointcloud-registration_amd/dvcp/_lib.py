@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdvcp_hip.so")
 
 F32, F64 = 0, 1
+ABI_VERSION = 2   # include/dvcp.h DVCP_ABI_VERSION
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _L = ctypes.c_int64
@@ -93,6 +94,9 @@ def load():
     lib.dvcp_last_error.argtypes = []
     lib.dvcp_abi_version.restype = ctypes.c_int
     lib.dvcp_abi_version.argtypes = []
+    if lib.dvcp_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"dvcp: {LIB_PATH} has ABI version {lib.dvcp_abi_version()}, this package expects "
+                           f"{ABI_VERSION}: rebuild it (make -j16 in deepvcp-pointcloud-registration_amd/)")
     lib.dvcp_knn_grid_workspace_bytes.restype = ctypes.c_int64
     lib.dvcp_knn_grid_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
     lib.dvcp_knn_tiled_workspace_bytes.restype = ctypes.c_int64

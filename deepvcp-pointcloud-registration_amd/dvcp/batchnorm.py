@@ -46,9 +46,17 @@ def _update_running(bn, mean, var, M):
         bn.running_var.mul_(1.0 - f).add_(unbiased.to(bn.running_var.dtype), alpha=f)
 
 
-def train_forward(sa, xyz, ctr, feat, count, lst, ns):
+# z rows kept from the forward for the backward only up to this size per layer call (bytes); above
+# it the backward recomputes them (dvcp_sa_bn_zrows), trading one pass for the memory.
+ZROWS_KEEP_MAX_BYTES = 16 << 30
+
+
+def train_forward(sa, xyz, ctr, feat, count, lst, ns, keep_zrows=False):
     """pointnet2_utils.py:195-200 with ``sa`` in training mode, on (B, 3, N) points, (B, 3, S)
-    centres and (B, D, N) features.  Returns (out (B, S, C_last) fp32, state for the backward)."""
+    centres and (B, D, N) features.  Returns (out (B, S, C_last) fp32, state for the backward).
+    ``keep_zrows``: a backward will run (the autograd path), so the last statistics pass also
+    writes every entry's z rows for it (within ZROWS_KEEP_MAX_BYTES); a train-mode forward with no
+    backward (no_grad, frozen extractor) allocates none."""
     chans = sa.chans
     offs, total = _layer_offsets(chans)
     dev = xyz.device
@@ -62,8 +70,9 @@ def train_forward(sa, xyz, ctr, feat, count, lst, ns):
         pack = torch.cat(parts).contiguous()
         assert pack.numel() == total == ops.sa_bn_pack_floats(chans)
         zrows = None
+        keep = keep_zrows and ops.sa_bn_zrows_bytes(B, S, ns, chans) <= ZROWS_KEEP_MAX_BYTES
         for layer, (bn, (o, cin, cout)) in enumerate(zip(sa.mlp_bns, offs), 1):
-            if layer == len(offs):  # the last pass also writes every entry's z rows for the backward
+            if keep and layer == len(offs):  # the last pass also writes every entry's z rows
                 sums, zrows = ops.sa_bn_stats(xyz, ctr, feat, count, lst, ns, chans, pack, layer, want_zrows=True)
             else:
                 sums = ops.sa_bn_stats(xyz, ctr, feat, count, lst, ns, chans, pack, layer)

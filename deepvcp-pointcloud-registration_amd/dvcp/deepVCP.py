@@ -104,7 +104,7 @@ class DeepVCP(nn.Module):
         del S3
         return torch.stack([torch.randint(0, n, (B,), dtype=torch.long) for n in sizes])
 
-    def extract_features(self, src_pts, tgt_pts, starts=None, train_fe=False):
+    def extract_features(self, src_pts, tgt_pts, starts=None, train_fe=False, trace=None):
         """The feature-extractor half of forward (deepVCP.py:29,72 -- FE1 on both clouds, the
         weighting layer's scores): a dict the head half (``forward_head``) consumes.  It depends on
         no trainable head parameter, so with the extractor frozen a training loop can run it for
@@ -121,7 +121,10 @@ class DeepVCP(nn.Module):
             def run(pts, st, wl=None, fps=None):
                 return autograd.feat_extraction(self.FE1, pts, st, wl=wl, side_stream=side, fps=fps)
         else:
-            run = self.FE1.run
+            lt = trace.setdefault("fe_layers", []) if trace is not None else None
+
+            def run(pts, st, wl=None, side_stream=None):
+                return self.FE1.run(pts, st, wl=wl, side_stream=side_stream, layer_trace=lt)
         if src_pts.shape == tgt_pts.shape and src_pts.dtype == tgt_pts.dtype and not self.FE1.training:
             # src and tgt share FE1's weights and eval-mode FE is per cloud: one 2B-cloud pass
             # (in training mode each call normalises with its own batch statistics: two passes)
@@ -159,8 +162,8 @@ class DeepVCP(nn.Module):
         ``return_weights``: also return the key points' weighting-layer scores (B, K), the
         weights of the paper's weighted pose solve (dvcp.paper)."""
         train_head, train_fe = self._training_mode()
-        feats = self.extract_features(src_pts, tgt_pts, starts, train_fe=train_fe)
         tr = {} if (return_weights and trace is None) else trace
+        feats = self.extract_features(src_pts, tgt_pts, starts, train_fe=train_fe, trace=trace)
         keypts, vcp = self._head(feats, R_init, train_head, tr, keypoint_idx)
         if not return_weights:
             return keypts, vcp

@@ -59,7 +59,7 @@ class feat_extraction_layer(nn.Module):
                 prev = c
         return idxs, centres, events
 
-    def run(self, pts, starts=None, wl=None, side_stream=None, saved=None, fps=None):
+    def run(self, pts, starts=None, wl=None, side_stream=None, saved=None, fps=None, layer_trace=None):
         """Fused forward.  starts: (3, B) FPS start indices (drawn like the reference if None).
         Returns xyz (B, 3, S) contiguous, feat (B, S, 32), score (B, S) when ``wl`` is given.
         ``saved`` (a dict): filled with what the backward needs (dvcp/autograd.py feat_extraction):
@@ -74,7 +74,11 @@ class feat_extraction_layer(nn.Module):
 
         In training mode (``self.training``) the set-abstraction BatchNorms use batch statistics
         over this call's grouped entries and update their running statistics (dvcp/batchnorm.py);
-        every layer is then evaluated on its FPS centres (the statistics are over the centres)."""
+        every layer is then evaluated on its FPS centres (the statistics are over the centres).
+
+        ``layer_trace`` (a list, parity tests): gets one dict per layer -- its FPS indices ``idx``,
+        the ball query's distinct-hit ``count`` / ``lst`` and ``per_point`` (lists are then per
+        point, to be read through ``idx``; else per FPS centre)."""
         train_bn = self.training
         B, _, N = pts.shape
         if self.use_normal:
@@ -127,7 +131,8 @@ class feat_extraction_layer(nn.Module):
                 count, lst, _ = ops.ball_query(pts_l, ctr_l, sa.radius, ns, pdim=2, cdim_pts=2)
                 bn_state = None
                 if train_bn:
-                    res, bn_state = batchnorm.train_forward(sa, pts_l, ctr_l, f, count, lst, ns)
+                    res, bn_state = batchnorm.train_forward(sa, pts_l, ctr_l, f, count, lst, ns,
+                                                            keep_zrows=saved is not None)
                 elif f_rows is not None:
                     res = ops.sa_group_mlp_rows(pts_l, ctr_l, f_rows[0], f_rows[1], count, lst, ns, sa.chans,
                                                 sa.packed_params())
@@ -145,6 +150,8 @@ class feat_extraction_layer(nn.Module):
                         out = torch.gather(res, 1, i.unsqueeze(-1).expand(-1, -1, res.shape[2]))
                 else:
                     out = res
+                if layer_trace is not None:
+                    layer_trace.append(dict(idx=i, count=count, lst=lst, per_point=per_point, n=n_l))
                 if saved is not None:
                     saved.setdefault("layers", []).append(dict(pts=pts_l, ctr=ctr_l, feat=f, count=count, lst=lst,
                                                                ns=ns, idx=i, per_point=per_point, bn=bn_state))

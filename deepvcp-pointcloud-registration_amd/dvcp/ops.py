@@ -617,6 +617,12 @@ def sa_bn_stats(xyz, ctr, feat, count, lst, nsample, chans, pack, layer, xyz_pdi
     return (sums, zrows) if want_zrows else sums
 
 
+def sa_bn_zrows_bytes(B, S, nsample, chans):
+    """Size of ``sa_bn_zrows``'s output for this grouping (bytes)."""
+    ch = torch.tensor(list(chans), dtype=torch.int32)
+    return 4 * int(_lib.load().dvcp_sa_bn_zrows_floats(B, S, int(nsample), len(chans) - 1, ch.data_ptr()))
+
+
 def sa_bn_zrows(xyz, ctr, feat, count, lst, nsample, chans, pack, xyz_pdim=2, feat_ddim=1, feat_pdim=2):
     """Every grouped entry's conv outputs z_l of every layer with the batch statistics in ``pack``:
     flat fp32, per layer (M / 64, C_l, 64) blocks (what dvcp_sa_bn_backward reads)."""

@@ -34,6 +34,9 @@ extern "C" {
 #define DVCP_EINVAL (-1)    /* bad argument / unsupported shape */
 #define DVCP_EHIP (-2)      /* HIP launch error */
 
+/* Bumped on every incompatible signature change; dvcp/_lib.py refuses a library whose version differs. */
+#define DVCP_ABI_VERSION 2
+
 const char* dvcp_last_error(void);
 int dvcp_abi_version(void);
 

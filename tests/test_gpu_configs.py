@@ -152,6 +152,73 @@ def test_c5_fp16_features_vs_fp32(cuda):
     torch.testing.assert_close(t1, t0, rtol=0, atol=1e-3)
 
 
+def test_c5_head_stage_decoupled_vs_oracle(cuda):
+    """C5's head at full size, stage-decoupled: the GPU's feature extractor on
+    a 65536-point pair, its K = 256 key points moved by R_init, then every head stage against the
+    oracle fed the SAME inputs:
+    * candidate grid (voxelize.py:19-83) of all 256 key points: exact;
+    * kNN (get_cat_feat_tgt.py:44-52) of all 340,736 candidates, run at full size: indices and
+      distances bit-exact on a 16-key-point slice (21,296 queries, the oracle's chunked brute force);
+    * the fused target gather + DFE (get_cat_feat_tgt.py:54-96 + deep_feat_embedding.py:47-60) on
+      the fp32 table, and on BASELINE's fp16 table against the oracle on the same rounded values:
+      within 1e-5;
+    * the source DFE (all key points) within 1e-5;
+    * CPG (cpg.py:27-60) on the oracle's own DFE outputs for the slice: vcp within 1e-5."""
+    import oracle as O
+    import dvcp
+    from dvcp import ops
+    from dvcp.synthetic import make_pairs, randomize_bn
+    B, N, K, r, s = 1, 65536, 256, 2.0, 0.4
+    G = int((2 * r) / s + 1)
+    src, tgt, R_gt, _ = make_pairs(B, N, seed=557)
+    torch.manual_seed(0)
+    mine = dvcp.DeepVCP(use_normal=False, K=K, r=r, s=s).eval().to(cuda)
+    randomize_bn(mine)
+    starts = mine.draw_starts(B, N, N)
+    with torch.no_grad():
+        f = mine.extract_features(src.to(cuda), tgt.to(cuda), starts)
+        top = ops.topk(f["score"], K)
+        keypts, src_cat, moved = ops.src_keypoints(f["src_xyz"], f["src_feat"], top, f["starts"][3], R_gt.to(cuda))
+        src_dfe = ops.dfe(src_cat, mine.DFE.packed_params())
+        cand, _ = ops.voxelize(moved, r, s, G, pdim=1)
+        qry = cand.view(B, K * G ** 3, 3)
+        dist, idx, _ = ops.knn(f["tgt_xyz"], qry, 32, ref_pdim=2, qry_pdim=1, want_idx64=False)
+        tgt_dfe = ops.dfe_tgt(f["tgt_xyz"], f["tgt_feat"], qry, dist, idx, mine.DFE.packed_params(), ref_pdim=2)
+        tgt_dfe16 = ops.dfe_tgt(f["tgt_xyz"], f["tgt_feat"].half(), qry, dist, idx, mine.DFE.packed_params(),
+                                ref_pdim=2)
+    torch.cuda.synchronize()
+    dfe_o, cpg_o = O.feat_embedding_layer(), O.cpg()
+    dfe_o.load_state_dict({k: v.cpu() for k, v in mine.DFE.state_dict().items()})
+    cpg_o.load_state_dict({k: v.cpu() for k, v in mine.cpg.state_dict().items()})
+    cand_o = O.voxelize(moved.cpu(), r, s)
+    assert torch.equal(cand.cpu(), cand_o)
+    with torch.no_grad():
+        src_dfe_o = dfe_o(src_cat.cpu(), src=True)
+    torch.testing.assert_close(src_dfe.cpu(), src_dfe_o, rtol=1e-5, atol=1e-5)
+    tx, tf = f["tgt_xyz"].transpose(1, 2).cpu(), f["tgt_feat"].cpu()
+    sl = slice(120, 136)                                   # 16 key points of 256
+    C = G ** 3
+    kp_sl = keypts[:, sl].cpu()
+    wants = []
+    for table, got_dfe in ((tf, tgt_dfe), (tf.half().float(), tgt_dfe16)):
+        with torch.no_grad(), O.tracing() as trace:
+            cat_o = O.Get_Cat_Feat_Tgt()(cand_o[:, sl], kp_sl, tx, table)
+            want_dfe = dfe_o(cat_o, src=False)
+            del cat_o
+        d = dict(trace)
+        q = slice(sl.start * C, sl.stop * C)
+        assert torch.equal(idx[:, q].cpu().long(), d["knn_idx"]), "C5 kNN indices differ from the oracle"
+        assert torch.equal(dist[:, q].cpu(), d["knn_dist"]), "C5 kNN distances differ from the oracle"
+        torch.testing.assert_close(got_dfe[:, q].cpu().view(want_dfe.shape), want_dfe, rtol=1e-5, atol=1e-5)
+        wants.append(want_dfe)
+    # CPG on the oracle's own stage inputs (the fp32 table's DFE of the slice)
+    with torch.no_grad():
+        vcp_o = cpg_o(src_dfe_o[:, sl].unsqueeze(2), wants[0].permute(0, 1, 3, 2), cand_o[:, sl], r, s)
+        vcp = ops.cpg(src_dfe_o[:, sl].to(cuda), wants[0].to(cuda).permute(0, 1, 3, 2), cand_o[:, sl].to(cuda), G,
+                      mine.cpg.packed_params())
+    torch.testing.assert_close(vcp.cpu(), vcp_o, rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("dtype,N,npoint,B", [(torch.float32, 40000, 3000, 3), (torch.float64, 20000, 2000, 2)])
 def test_split_fps_vs_oracle(cuda, dtype, N, npoint, B):
     """The split FPS (S workgroups per cloud, ragged last chunk, several clouds per launch) is

@@ -93,26 +93,26 @@ def _oracle_threads():
     return max(1, min(n, 16))
 
 
-def test_e2e_c3_batch8_lanes(cuda):
-    """BASELINE C3 as bench.py runs it: B = 8 pairs, N = 16384, K = 64, r = 2.0, s = 0.4, FE
-    npoint 10000, with two more 8-pair batches in flight on their own streams.  Checked:
-    * the lane-0 batch run concurrently equals the same batch run alone (bit for bit);
-    * pairs 0 and 7 against the live oracle, each end to end with the GPU's OWN top-k: FE
-      geometry exact, top-k per rank (tests_helpers.topk_parity), key points exact, candidates
-      exact, vcp within 1e-5 and R, t within the north_star's 1e-4.  Should a near-tie block
-      reorder the top-k, the pair is re-run from the oracle's top-k at full size and R, t
-      must still be within 1e-4 (asserted, never skipped)."""
+C3_B = 8
+
+
+@pytest.fixture(scope="module")
+def c3_lanes(cuda):
+    """BASELINE C3 as bench.py runs it: B = 8 pairs, N = 16384, K = 64, r = 2.0, s = 0.4, FE npoint
+    10000, with two more 8-pair batches in flight on their own streams.  The lane-0 batch (with its
+    stage trace: FE layers' FPS indices and ball-query lists, features, scores, top-k, candidates,
+    kNN) and the same batch run alone."""
     import oracle as O
     import dvcp
     from dvcp.synthetic import condition_weights, make_pairs, randomize_bn
-    B, N, K, r, s = 8, 16384, 64, 2.0, 0.4
+    B, N, K, r, s = C3_B, 16384, 64, 2.0, 0.4
     lanes_data = [make_pairs(B, N, seed=777 + 101 * lane) for lane in range(3)]
     torch.manual_seed(0)
     ref = O.DeepVCP(use_normal=False, K=K, r=r, s=s).eval()
     randomize_bn(ref)
     mine = dvcp.DeepVCP(use_normal=False, K=K, r=r, s=s).eval().to(cuda)
     mine.load_state_dict(ref.state_dict())
-    src, tgt, R_gt, t_gt = lanes_data[0]
+    src = lanes_data[0][0]
     with torch.no_grad():
         _, calib, _ = mine.FE1.run(src[:1].to(cuda))
     condition_weights(ref, feats=calib)     # separated key-point scores (dvcp/synthetic.py)
@@ -137,44 +137,92 @@ def test_e2e_c3_batch8_lanes(cuda):
         torch.cuda.synchronize()
         alone = run(0)
         torch.cuda.synchronize()
-    for a, b in zip(outs[0], alone):
+    return dict(ref=ref, mine=mine, data=lanes_data[0], starts=starts[0], trace=tr, outs=outs, alone=alone,
+                K=K)
+
+
+def test_e2e_c3_lanes_equal_alone(c3_lanes):
+    """The lane-0 batch run alongside two other batches equals the same batch run alone, bit for bit."""
+    for a, b in zip(c3_lanes["outs"][0], c3_lanes["alone"]):
         assert torch.equal(a, b), "a batch run alongside others differs from the same batch run alone"
-    kp, vcp, loss, R, t = (x.cpu() for x in outs[0])
 
+
+@pytest.mark.parametrize("b", range(C3_B))
+def test_e2e_c3_pair_vs_oracle(cuda, c3_lanes, b):
+    """Every pair of the C3 batch against the live oracle (REF-R, oracle/ref_r.py), stage by stage
+    with the GPU's OWN outputs of the batched run:
+    * all 7 FPS index sequences bit-exact (src / tgt sa1-sa3 at 16384 -> 10000 -> 10000 -> 10000);
+    * the six FE ball-query lists (pointnet2_utils.py:87-107, padded form) -- exact except rows
+      whose differing points sit within 4 ulp of r^2 (BLAS rounding of square_distance; counted);
+    * FE geometry exact, FE features (src and tgt) within rtol 1e-4;
+    * top-k per rank (tests_helpers.topk_parity), key points and candidates exact;
+    * the kNN (get_cat_feat_tgt.py:44-52) of all 85184 candidates: indices AND distances bit-exact;
+    * target DFE features within rtol 1e-4, vcp within 1e-5, R, t within the north_star's 1e-4.
+    Should a near-tie block reorder the top-k, the back half (key points, candidates, kNN, DFE,
+    vcp, R, t) is re-run from the oracle's top-k at full size and checked the same way."""
+    import oracle as O
+    from tests_helpers import ball_rows_mismatch_ok, padded_ball_rows
+    c = c3_lanes
+    ref, mine, K, tr = c["ref"], c["mine"], c["K"], c["trace"]
+    src, tgt, R_gt, t_gt = c["data"]
+    starts = c["starts"]
+    kp, vcp, loss, R, t = (x.cpu() for x in c["outs"][0])
+    B = src.shape[0]
     torch.set_num_threads(_oracle_threads())
-    for b in (0, B - 1):
-        with torch.no_grad(), O.fps_starts([x[b:b + 1] for x in starts[0]]), O.tracing() as trace:
-            kp_o, vcp_o = ref(src[b:b + 1], tgt[b:b + 1], R_gt[b:b + 1], torch.zeros(1, 3))
-            loss_o, R_o, t_o = O.deepVCP_loss(kp_o, vcp_o, R_gt[b:b + 1], t_gt[b:b + 1], 0.5)
-        d = dict(trace)
-        fe_x = [v for n, v in trace if n == "fe_xyz"]
-        assert torch.equal(tr["src_xyz"][b:b + 1].transpose(1, 2).cpu(), fe_x[0])
-        assert torch.equal(tr["tgt_xyz"][b:b + 1].transpose(1, 2).cpu(), fe_x[1])
-        want = d["wl_score"][..., 0]
-        torch.testing.assert_close(tr["score"][b:b + 1].cpu(), want, rtol=1e-3, atol=1e-5)
-        exact, n_amb = topk_parity(tr["topk"][b:b + 1], tr["score"][b:b + 1], d["topk_idx"], want, K)
-        print(f"C3 pair {b}: GPU top-k == oracle top-k: {exact} ({n_amb} near-tie rank boundaries), "
-              f"max|dR| {float((R[b] - R_o[0]).abs().max()):.2e}, max|dt| {float((t[b] - t_o[0]).abs().max()):.2e}")
-        if exact:
-            assert torch.equal(kp[b:b + 1], kp_o)
-            assert torch.equal(tr["cand"][b:b + 1].cpu(), d["candidates"])
-            torch.testing.assert_close(vcp[b:b + 1], vcp_o, rtol=1e-5, atol=1e-5)
-            torch.testing.assert_close(R[b:b + 1], R_o, rtol=0, atol=1e-4)
-            torch.testing.assert_close(t[b:b + 1], t_o, rtol=0, atol=1e-4)
-        else:
-            one = tuple(x[b:b + 1].to(cuda) for x in lanes_data[0])
-            with torch.no_grad():
-                kp1, vcp1, _, R1, t1 = _run_pair(mine, one, [x[b:b + 1] for x in starts[0]], d["topk_idx"])
-            assert torch.equal(kp1.cpu(), kp_o)
-            torch.testing.assert_close(vcp1.cpu(), vcp_o, rtol=1e-5, atol=1e-5)
-            torch.testing.assert_close(R1.cpu(), R_o, rtol=0, atol=1e-4)
-            torch.testing.assert_close(t1.cpu(), t_o, rtol=0, atol=1e-4)
+    with torch.no_grad(), O.fps_starts([x[b:b + 1] for x in starts]), O.tracing() as trace:
+        kp_o, vcp_o = ref(src[b:b + 1], tgt[b:b + 1], R_gt[b:b + 1], torch.zeros(1, 3))
+        loss_o, R_o, t_o = O.deepVCP_loss(kp_o, vcp_o, R_gt[b:b + 1], t_gt[b:b + 1], 0.5)
+    d = dict(trace)
+    fps_o = [v for n, v in trace if n == "fps_idx"]    # src sa1-3, key points, tgt sa1-3
+    ball_o = [v for n, v in trace if n == "ball_idx"]
+    feat_o = [v for n, v in trace if n == "fe_feat"]
+    fe_x = [v for n, v in trace if n == "fe_xyz"]
+    radii = [mine.FE1.sa1.radius, mine.FE1.sa2.radius, mine.FE1.sa3.radius]
+    n_boundary = 0
+    for side, (row, o0, cloud) in enumerate(((b, 0, src), (B + b, 4, tgt))):
+        pts = cloud[b].t().contiguous()                       # (N, 3)
+        for lvl, layer in enumerate(tr["fe_layers"]):
+            fidx = fps_o[o0 + lvl][0]
+            assert torch.equal(layer["idx"][row].cpu(), fidx), (side, lvl)
+            ctr = pts[fidx]
+            got = padded_ball_rows(layer, row)
+            n_boundary += ball_rows_mismatch_ok(pts[None], ctr[None], got[None], ball_o[o0 + lvl], radii[lvl])
+            pts = ctr
+    assert torch.equal(tr["src_xyz"][b:b + 1].transpose(1, 2).cpu(), fe_x[0])
+    assert torch.equal(tr["tgt_xyz"][b:b + 1].transpose(1, 2).cpu(), fe_x[1])
+    torch.testing.assert_close(tr["src_feat"][b:b + 1].cpu(), feat_o[0], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(tr["tgt_feat"][b:b + 1].cpu(), feat_o[1], rtol=1e-4, atol=1e-5)
+    want = d["wl_score"][..., 0]
+    torch.testing.assert_close(tr["score"][b:b + 1].cpu(), want, rtol=1e-3, atol=1e-5)
+    exact, n_amb = topk_parity(tr["topk"][b:b + 1], tr["score"][b:b + 1], d["topk_idx"], want, K)
+    print(f"C3 pair {b}: 7 FPS exact, {n_boundary} ball rows differing only at r^2 rounding; GPU top-k == oracle "
+          f"top-k: {exact} ({n_amb} near-tie rank boundaries), max|dR| {float((R[b] - R_o[0]).abs().max()):.2e}, "
+          f"max|dt| {float((t[b] - t_o[0]).abs().max()):.2e}")
+    if exact:
+        back = dict(kp=kp[b:b + 1], vcp=vcp[b:b + 1], R=R[b:b + 1], t=t[b:b + 1], cand=tr["cand"][b:b + 1],
+                    knn_idx=tr["knn_idx"][b:b + 1], knn_dist=tr["knn_dist"][b:b + 1], tgt_dfe=tr["tgt_dfe"][b:b + 1])
+    else:   # near-tie block reordered: the back half from the oracle's top-k
+        one = tuple(x[b:b + 1].to(cuda) for x in c["data"])
+        tr1 = {}
+        with torch.no_grad():
+            kp1, vcp1, _, R1, t1 = _run_pair(mine, one, [x[b:b + 1] for x in starts], d["topk_idx"], trace=tr1)
+        back = dict(kp=kp1, vcp=vcp1, R=R1, t=t1, cand=tr1["cand"], knn_idx=tr1["knn_idx"], knn_dist=tr1["knn_dist"],
+                    tgt_dfe=tr1["tgt_dfe"])
+    back = {k: v.cpu() for k, v in back.items()}
+    assert torch.equal(back["kp"], kp_o)
+    assert torch.equal(back["cand"], d["candidates"])
+    assert torch.equal(back["knn_idx"].long(), d["knn_idx"]), "kNN indices differ from the oracle"
+    assert torch.equal(back["knn_dist"], d["knn_dist"]), "kNN distances differ from the oracle"
+    torch.testing.assert_close(back["tgt_dfe"].reshape(d["tgt_dfe"].shape), d["tgt_dfe"], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(back["vcp"], vcp_o, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(back["R"], R_o, rtol=0, atol=1e-4)
+    torch.testing.assert_close(back["t"], t_o, rtol=0, atol=1e-4)
 
 
-def _run_pair(model, data, starts, keypoint_idx):
+def _run_pair(model, data, starts, keypoint_idx, trace=None):
     import dvcp
     s_, g_, R_, t_ = data
-    kp, vcp = model(s_, g_, R_, torch.zeros(1, 3), starts=torch.stack(starts), keypoint_idx=keypoint_idx)
+    kp, vcp = model(s_, g_, R_, torch.zeros(1, 3), starts=torch.stack(starts), keypoint_idx=keypoint_idx, trace=trace)
     loss, R, t = dvcp.deepVCP_loss(kp, vcp, R_, t_, 0.5)
     return kp, vcp, loss, R, t
 

@@ -513,7 +513,8 @@ def test_topk(cuda):
     assert ops.topk(tied.to(cuda), 4).cpu().tolist() == [[1, 2, 4, 3]]  # value desc, index asc
 
 
-@pytest.mark.parametrize("case", ["all_equal", "few_values", "negative", "k_eq_s", "k1", "ragged", "k256"])
+@pytest.mark.parametrize("case", ["all_equal", "few_values", "negative", "k_eq_s", "k1", "ragged", "k256",
+                                  "neg_inf_ragged"])
 def test_topk_radix_select_cases(cuda, case):
     """The radix-select top-k (head_topk.hip) against value-descending, index-ascending order:
     massive ties (the select runs into the index bits), mixed signs, K = S, K = 1, S not a
@@ -537,6 +538,13 @@ def test_topk_radix_select_cases(cuda, case):
     elif case == "ragged":
         S, K = 3333, 50
         s = torch.randint(0, 40, (B, S), generator=g).float()
+    elif case == "neg_inf_ragged":
+        # K = S, S not a multiple of 1024, scores of both signs and -inf: the K-th key's top byte
+        # is the padding slots' (0), which must still never be selected
+        S = K = 1500
+        s = torch.randn(B, S, generator=g)
+        s[:, ::3] = -float("inf")
+        s[1, 5:9] = -3.0e38
     else:
         S, K = 16384, 256
         s = torch.rand(B, S, generator=g)

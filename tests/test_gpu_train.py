@@ -520,6 +520,17 @@ def test_backward_entry_points_empty_inputs(cuda):
                                       torch.zeros(0, 2, dtype=torch.float64, device=dev),
                                       torch.ones((), dtype=torch.float64, device=dev), 0.5)
     assert g.shape == (0, 3, 64)
+    # target DFE with no query (Q = 0, B > 0): the feature gradient is all zeros, not uninitialised
+    B, M = 2, 500
+    ref_xyz = torch.rand(B, 3, M, device=dev)
+    feat = torch.rand(B, M, 32, device=dev)
+    for _ in range(2):   # the second call gets the caching allocator's reused (dirty) block
+        junk = torch.full((B, M, 32), float("nan"), device=dev)
+        del junk
+        gp, gF = ops.dfe_tgt_backward(ref_xyz, feat, torch.zeros(B, 0, 3, device=dev),
+                                      torch.zeros(B, 0, 32, device=dev), torch.zeros(B, 0, 32, dtype=torch.int32, device=dev),
+                                      params, torch.zeros(B, 0, 32, device=dev), want_feat_grad=True)
+        assert gF.shape == (B, M, 32) and not gF.any() and not gp.any()
 
 
 def test_cpg_backward_rejects_bad_grid(cuda):
@@ -676,3 +687,30 @@ def test_direct_module_calls_keep_or_refuse_gradients(cuda):
     with torch.no_grad():
         new_xyz, out = sa.eval()(x, None)
     assert out.shape == (2, 32, 256)
+
+
+def test_train_mode_forward_without_backward_keeps_no_zrows(cuda, monkeypatch):
+    """Batch-statistics forward with no backward to follow (under no_grad): no statistics pass is
+    asked for the per-entry z rows (several GB per layer at C3); with autograd the last pass of
+    every layer writes them for the backward."""
+    import dvcp
+    from dvcp import ops
+    from dvcp.synthetic import make_pairs
+    asked = []
+    real = ops.sa_bn_stats
+
+    def spy(*a, **k):
+        asked.append(bool(k.get("want_zrows", False)))
+        return real(*a, **k)
+
+    monkeypatch.setattr(ops, "sa_bn_stats", spy)
+    src, _, _, _ = make_pairs(2, 2048, seed=96)
+    torch.manual_seed(0)
+    fe = dvcp.feat_extraction_layer(use_normal=False, npoint=256).to(cuda).train()
+    with torch.no_grad():
+        fe(src.to(cuda))
+    assert asked and not any(asked)
+    asked.clear()
+    _, feat = fe(src.to(cuda))
+    assert sum(asked) == 3          # one z-row pass per set-abstraction layer
+    feat.sum().backward()

@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-3 evidence: every GPU test, smoke, the C3 bench (with CPU baseline) + stage report,
-# rocprofv3 kernel stats isolated (one batch in flight) and at the default 10 lanes, then the PMC
-# passes (FETCH, WRITE, COMPUTE; tools/gpu_pmc.sh).
+# Round evidence on one GPU box: every GPU test, smoke, the C3 bench (with the CPU baseline and the
+# per-stage report), rocprofv3 kernel statistics with one batch in flight (iso) and at the bench's
+# default lanes (p10), then the PMC passes (tools/gpu_pmc.sh).  Usage: tools/gpu_evidence.sh <tag>
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
-tag=${1:-r3n}
+tag=${1:-ev}
 ROOT="$GRAFT_REPO_ROOT"
-timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rfs \
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rfs \
   > gpurun_out/${tag}_pytest_gpu.log 2>&1
 rc=$?
 echo "PYTEST_EXIT $rc" >> gpurun_out/${tag}_pytest_gpu.log
