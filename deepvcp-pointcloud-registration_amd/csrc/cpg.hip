@@ -47,6 +47,15 @@ __device__ __forceinline__ f32x4 cpg_mfma_split3(const bf16x8& a0, const bf16x8&
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc, 0, 0, 0);
 }
 
+// DVCP_CPG_DIAG (diagnostic builds only): wave 0 of each workgroup records the shader clock at the
+// phase boundaries and writes the deltas over the key point's softmax weights (tools/cpg_diag.py).
+#ifdef DVCP_CPG_DIAG
+#define DVCP_CPG_TICK(k) \
+  if (tid == 0) dg[k] = __builtin_readcyclecounter();
+#else
+#define DVCP_CPG_TICK(k)
+#endif
+
 constexpr int kCpgThreads = 1024;  // 16 waves: four per SIMD (LDS allows one workgroup per CU)
 constexpr int kCpgMaxC = 1331;
 constexpr int kCpgMaxG = 11;
@@ -59,6 +68,25 @@ constexpr int kCpgBigF = 16 * kCpgPV;  // quarter volume + conv1 weights, later 
 constexpr int kCpgE = (32 * kCpgMaxC + kCpgThreads - 1) / kCpgThreads;  // target values per thread
 static_assert(kCpgVolF + kCpgW1F <= kCpgBigF, "quarter volume + conv1 weights must fit the area");
 
+// Each 8-channel quarter of the cost volume takes the target values l = 32 g + f' with f' in the
+// quarter (Q11: l = f C + c).  QBAL (every residue c mod 32 has exactly 8 channels f per quarter,
+// cpg_balanced(C): G = 11 and G = 6, the forward's grids): each thread loads, per quarter, the
+// values of that quarter (wave w, step u: rows c = 8 (16 u + w) + lane / 8, the (lane % 8)-th f of
+// the row in the quarter), so every lane builds cost cells in every quarter; otherwise a thread's
+// values all fall in one quarter (their l mod 32 is the same) and three quarters of the lanes idle
+// through each quarter's build.
+__host__ __device__ inline bool cpg_balanced(int C) {
+  const int m = C & 31;
+  for (int cr = 0; cr < 32; ++cr) {
+    int n[4] = {0, 0, 0, 0};
+    for (int f = 0; f < 32; ++f) ++n[((m * f + cr) & 31) >> 3];
+    if (n[0] != 8 || n[1] != 8 || n[2] != 8 || n[3] != 8) return false;
+  }
+  return true;
+}
+constexpr int kCpgBalU = (kCpgMaxC + 127) / 128;  // QBAL load steps (128 rows per step)
+
+template <bool QBAL>
 __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restrict__ src, const float* __restrict__ tgt,
                                                           int64_t t_p, int64_t t_f, int64_t t_c,
                                                           const float* __restrict__ cand, int G,
@@ -77,6 +105,12 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
   float* out2 = big;           // after conv2: its output, haloed [co][cell] (4 x PV)
 
   const int p = blockIdx.x, tid = threadIdx.x;
+#ifdef DVCP_CPG_DIAG
+  uint64_t dg[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dg[i] = 0;
+#endif
+  DVCP_CPG_TICK(0)
   const int C = G * G * G, GG = G * G;
   const int PG = G + 2, PGG = PG * PG, PV = PG * PGG;
   const FastDiv dG(G), dGG(GG);
@@ -85,11 +119,33 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
   const float* P3 = P2 + 4 * 16 * 27 + 4;
   // the whole (C, 32) target block of this key point, coalesced, all loads in flight
   const float* T = tgt + static_cast<int64_t>(p) * t_p;
-  float tv[kCpgE];
+  __shared__ uint8_t fsel[32][4][8];  // QBAL: the j-th channel f of residue c mod 32 in quarter q
+  constexpr int kTv = QBAL ? 4 * kCpgBalU : kCpgE;
+  float tv[kTv];
+  if constexpr (QBAL) {
+    if (tid < 128) {
+      const int cr = tid >> 2, q = tid & 3, m = C & 31;
+      int j = 0;
+      for (int f = 0; f < 32; ++f)
+        if ((((m * f + cr) & 31) >> 3) == q) fsel[cr][q][j++] = static_cast<uint8_t>(f);
+    }
+    __syncthreads();
+    const int wv = tid >> 6, ln = tid & 63;
 #pragma unroll
-  for (int u = 0; u < kCpgE; ++u) {
-    const int e = u * kCpgThreads + tid;  // memory order (c, f)
-    tv[u] = e < 32 * C ? T[(e % 32) * t_f + (e / 32) * t_c] : 0.f;
+    for (int u = 0; u < kCpgBalU; ++u) {
+      const int c = 8 * (16 * u + wv) + (ln >> 3);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int f = fsel[c & 31][q][ln & 7];
+        tv[q * kCpgBalU + u] = c < C ? T[f * t_f + c * t_c] : 0.f;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < kCpgE; ++u) {
+      const int e = u * kCpgThreads + tid;  // memory order (c, f)
+      tv[u] = e < 32 * C ? T[(e % 32) * t_f + (e / 32) * t_c] : 0.f;
+    }
   }
 #if !DVCP_CPG_SPLIT3
 #pragma unroll 6
@@ -104,6 +160,7 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
   if (tid == 0) bias[20] = P3[4 * 27];
   if (tid < 32) sv[tid] = src[static_cast<int64_t>(p) * 32 + tid];
 
+  DVCP_CPG_TICK(1)
   // per-thread voxels (conv3, softmax)
   int gv[kCpgV];
 #pragma unroll
@@ -138,6 +195,7 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
 #pragma unroll 1
     for (int q = 0; q < 32 / kCpgQ; ++q) {
       __syncthreads();
+      DVCP_CPG_TICK(2 + 3 * q)
       for (int i = tid; i < 3 * PV; i += kCpgThreads) vsp[i] = make_uint4(0u, 0u, 0u, 0u);
       // this quarter's conv1 weights: k-step s, lane (co = l & 15, tap 4 s + (l >> 4)), channel j
       for (int i = tid; i < 7 * 64; i += kCpgThreads) {
@@ -157,28 +215,47 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
         w1p[(st * 3 + 2) * 64 + l] = __builtin_bit_cast(uint4, b2);
       }
       __syncthreads();
+      DVCP_CPG_TICK(3 + 3 * q)
       // cost volume quarter as bf16 pieces (see the fp32 path below for the Q11 index map)
       int zo = 0;
       asm volatile("" : "+v"(zo));
-      const int f0 = tid & 31;
-      const int l0 = f0 * C + (tid >> 5) + zo;
       uint16_t* vh = reinterpret_cast<uint16_t*>(vsp);
-#pragma unroll
-      for (int u = 0; u < kCpgE; ++u) {
-        const int e = u * kCpgThreads + tid;
-        const int l = l0 + (kCpgThreads / 32) * u;
+      auto put = [&](int l, float t) {  // cost cell of target value l (Q11), as three bf16 pieces
         const int g = l >> 5, fp = l & 31;
-        if (e < 32 * C && (fp >> 3) == q) {
-          const float d = sv[fp] - tv[u];
-          __bf16 x0, x1, x2;
-          cpg_split3(d * d, x0, x1, x2);
-          const int c8 = cpg_halo(g, dG, dGG, PG, PGG) * 8 + (fp & 7);
-          vh[c8] = __builtin_bit_cast(uint16_t, x0);
-          vh[8 * PV + c8] = __builtin_bit_cast(uint16_t, x1);
-          vh[16 * PV + c8] = __builtin_bit_cast(uint16_t, x2);
+        const float d = sv[fp] - t;
+        __bf16 x0, x1, x2;
+        cpg_split3(d * d, x0, x1, x2);
+        const int c8 = cpg_halo(g, dG, dGG, PG, PGG) * 8 + (fp & 7);
+        vh[c8] = __builtin_bit_cast(uint16_t, x0);
+        vh[8 * PV + c8] = __builtin_bit_cast(uint16_t, x1);
+        vh[16 * PV + c8] = __builtin_bit_cast(uint16_t, x2);
+      };
+      if constexpr (QBAL) {
+        // this quarter's values, one per step, every lane (no divergence but the tail rows)
+        const int wv = tid >> 6, ln = tid & 63;
+#pragma unroll
+        for (int u = 0; u < kCpgBalU; ++u) {
+          const int c = 8 * (16 * u + wv) + (ln >> 3) + zo;
+          if (c < C) {
+            const int f = fsel[c & 31][q][ln & 7];
+            float t = tv[0];
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) t = qq == q ? tv[qq * kCpgBalU + u] : t;  // (q is uniform)
+            put(f * C + c, t);
+          }
+        }
+      } else {
+        const int f0 = tid & 31;
+        const int l0 = f0 * C + (tid >> 5) + zo;
+#pragma unroll
+        for (int u = 0; u < kCpgE; ++u) {
+          const int e = u * kCpgThreads + tid;
+          const int l = l0 + (kCpgThreads / 32) * u;
+          if (e < 32 * C && ((l & 31) >> 3) == q) put(l, tv[u]);
         }
       }
       __syncthreads();
+      DVCP_CPG_TICK(4 + 3 * q)
 #pragma unroll 1
       for (int st = 0; st < 7; ++st) {
         // lane's tap 4 st + kg (tap 27: zero weights, any in-range cell)
@@ -242,6 +319,7 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
   }
 #endif
   __syncthreads();
+  DVCP_CPG_TICK(14)
   // conv1 output -> out1 (haloed, zero border); accumulator register r of lane l is voxel
   // 16 t + 4 (l >> 4) + r, output channel l & 15
   for (int i = tid; i < 16 * PV; i += kCpgThreads) out1[i] = 0.f;
@@ -260,6 +338,7 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
   // conv2 (16 -> 4) on VALU, one voxel per thread: a 16-column MFMA tile would leave 12 of its
   // 16 output columns empty (4x the MFMA time of the useful work).  W2[co][ci][tap] comes through
   // the scalar cache (wave-uniform), one tap plane (4 x 9 weights) at a time.
+  DVCP_CPG_TICK(15)
   int hv[kCpgV];
 #pragma unroll
   for (int v = 0; v < kCpgV; ++v) hv[v] = cpg_halo(gv[v] < C ? gv[v] : 0, dG, dGG, PG, PGG);
@@ -294,6 +373,9 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
     }
   }
   __syncthreads();  // every conv1 output read; out2 overwrites them
+#ifdef DVCP_CPG_DIAG
+  uint64_t dg_c2 = __builtin_readcyclecounter();
+#endif
   for (int i = tid; i < 4 * PV; i += kCpgThreads) out2[i] = 0.f;
   __syncthreads();
 #pragma unroll
@@ -348,6 +430,22 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
   sx = block_sum(sx, red);
   sy = block_sum(sy, red);
   sz = block_sum(sz, red);
+#ifdef DVCP_CPG_DIAG
+  if (tid == 0 && weight) {  // phase deltas: [load, q0 zero, q0 build, q0 mfma, ..., out1, conv2, rest]
+    const uint64_t end = __builtin_readcyclecounter();
+    float* o = weight + static_cast<int64_t>(p) * C;
+    o[0] = static_cast<float>(dg[1] - dg[0]);
+    for (int q = 0; q < 4; ++q) {
+      o[1 + 3 * q] = static_cast<float>(dg[3 + 3 * q] - dg[2 + 3 * q]);
+      o[2 + 3 * q] = static_cast<float>(dg[4 + 3 * q] - dg[3 + 3 * q]);
+      o[3 + 3 * q] = static_cast<float>((q < 3 ? dg[5 + 3 * q] : dg[14]) - dg[4 + 3 * q]);
+    }
+    o[13] = static_cast<float>(dg[15] - dg[14]);
+    o[14] = static_cast<float>(dg_c2 - dg[15]);
+    o[15] = static_cast<float>(end - dg_c2);
+    o[16] = static_cast<float>(end - dg[0]);
+  }
+#endif
   if (tid == 0) {
     vcp[static_cast<int64_t>(p) * 3 + 0] = sx / sw;
     vcp[static_cast<int64_t>(p) * 3 + 1] = sy / sw;
@@ -362,7 +460,11 @@ extern "C" int dvcp_cpg(const float* src, const float* tgt, int64_t t_p, int64_t
   DVCP_REQUIRE(src && tgt && cand && params && vcp, "dvcp_cpg: null pointer");
   DVCP_REQUIRE(G >= 1 && G * G * G <= dvcp::kCpgMaxC, "dvcp_cpg: grid side G=%d unsupported (C <= 1331)", G);
   if (P <= 0) return DVCP_OK;
-  hipLaunchKernelGGL(dvcp::cpg_kernel, dim3(P), dim3(dvcp::kCpgThreads), 0, static_cast<hipStream_t>(stream), src, tgt,
-                     t_p, t_f, t_c, cand, G, params, vcp, weight);
+  if (dvcp::cpg_balanced(G * G * G))
+    hipLaunchKernelGGL(dvcp::cpg_kernel<true>, dim3(P), dim3(dvcp::kCpgThreads), 0, static_cast<hipStream_t>(stream),
+                       src, tgt, t_p, t_f, t_c, cand, G, params, vcp, weight);
+  else
+    hipLaunchKernelGGL(dvcp::cpg_kernel<false>, dim3(P), dim3(dvcp::kCpgThreads), 0, static_cast<hipStream_t>(stream),
+                       src, tgt, t_p, t_f, t_c, cand, G, params, vcp, weight);
   return dvcp::launch_status("dvcp_cpg");
 }

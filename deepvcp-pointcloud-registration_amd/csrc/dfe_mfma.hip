@@ -187,6 +187,17 @@ __global__ __launch_bounds__(kDfeMfmaWaves * kWave) void dfe_tgt_mfma_kernel(
 // ordered sum; w_j = dist_j / dist_sum in fp64 is then bit-identical.
 constexpr int kDfe1Waves = 4;
 
+// v + (v moved by the DPP pattern CTRL), fp64 (the two halves moved separately)
+template <int CTRL>
+__device__ __forceinline__ double dpp_add_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return v + __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
 struct Dfe1Lds {
   double p[32][35];      // W2 . W1 (fp64), prologue only
   double pb[32];         // W2 . b1 + b2
@@ -197,7 +208,7 @@ struct Dfe1Lds {
   float e[kDfeKS][64];   // E as the B fragment: [k-step][lane]
 #endif
   float eb[32];          // e
-  float w[kDfe1Waves][32];  // per-wave w_j of the current candidate (fp64 quotient rounded to fp32)
+  float w[kDfe1Waves][2][32];  // per-wave w rows of two consecutive candidates (fp64 quotient rounded to fp32)
 };
 
 // FT: the feature table's element type -- float, or _Float16 (the C5 "fp16 features" storage:
@@ -277,9 +288,10 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
   // multiple of 8): workgroups are dispatched to the 8 XCDs round robin (blockIdx % 8), so the
   // workgroups of XCD x take the candidates of pairs x, x+8, ...; each pair's gathered feature
   // table then lives in one XCD's L2 instead of being fetched into all eight.
-  int total, stride, g, xo = 0;
+  int total, stride, g, xo = 0, P = 1;
   if (xcd) {
     xo = static_cast<int>(blockIdx.x) & 7;
+    P = 8;
     total = ((B - xo + 7) / 8) * Q;
     stride = static_cast<int>(gridDim.x >> 3) * kDfe1Waves;
     g = static_cast<int>(blockIdx.x >> 3) * kDfe1Waves + __builtin_amdgcn_readfirstlane(wave);
@@ -289,25 +301,45 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
     g = static_cast<int>(blockIdx.x) * kDfe1Waves + __builtin_amdgcn_readfirstlane(wave);
   }
   if (g >= total) return;
-  auto glob = [&](int li) -> int {  // local candidate index -> global (b * Q + q)
-    if (!xcd) return li;
-    const int pl = li / Q;
-    return (xo + 8 * pl) * Q + (li - pl * Q);
+  // Local candidate index li = pl * Q + q -> pair b = xo + P * pl and global candidate b * Q + q,
+  // tracked incrementally per pipeline slot (wave-uniform, no integer division per candidate);
+  // indices past the end clamp to the last candidate (loads stay in bounds, results unused).
+  struct Cand {
+    int li, pl, q;
   };
-  auto load_row = [&](int gg, float& dj, int& n) {
-    const int gc = glob(gg < total ? gg : total - 1);
+  auto cand_at = [&](int li) {
+    Cand c;
+    c.li = li;
+    c.pl = li / Q;  // once per slot at the start
+    c.q = li - c.pl * Q;
+    return c;
+  };
+  const int st_pl = stride / Q, st_q = stride - st_pl * Q;
+  auto advance = [&](Cand& c) {  // branch-free (scalar selects): li += stride
+    c.li += stride;
+    c.q += st_q;
+    c.pl += st_pl;
+    const bool wrap = c.q >= Q;
+    c.q = wrap ? c.q - Q : c.q;
+    c.pl = wrap ? c.pl + 1 : c.pl;
+  };
+  const Cand last = cand_at(total - 1);
+  auto pair_of = [&](const Cand& c) { return xo + P * (c.li < total ? c.pl : last.pl); };
+  auto glob_of = [&](const Cand& c) { return pair_of(c) * Q + (c.li < total ? c.q : last.q); };
+  auto load_row = [&](const Cand& c, float& dj, int& n) {
+    const int gc = glob_of(c);
     dj = dist[static_cast<int64_t>(gc) * 32 + r32];
     n = idx[static_cast<int64_t>(gc) * 32 + r32];
   };
   struct Gathered {
     float4 f[4];
-    uint4 hf[2];  // fp16 table: the row's 16 halves of this lane half, widened in embed
+    uint4 hf[2];  // fp16 table: the row's 16 halves of this lane half, widened in prep
     T px, py, pz;
     float cx, cy, cz;
   };
-  auto gather = [&](int gg, int nraw, Gathered& G) {
-    const int gc = glob(gg < total ? gg : total - 1);
-    const int bb = gc / Q;
+  auto gather = [&](const Cand& c, int nraw, Gathered& G) {
+    const int bb = pair_of(c);
+    const int gc = bb * Q + (c.li < total ? c.q : last.q);
     const int n = nraw < 0 ? 0 : (nraw >= M ? M - 1 : nraw);
     if constexpr (sizeof(FT) == 4) {
       const float4* fr = reinterpret_cast<const float4*>(feat + (static_cast<int64_t>(bb) * M + n) * 32 + 16 * h);
@@ -325,34 +357,36 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
     G.cy = cand[static_cast<int64_t>(gc) * 3 + 1];
     G.cz = cand[static_cast<int64_t>(gc) * 3 + 2];
   };
-  // get_cat_feat_tgt.py:57-58 (lanes 32..63 mirror lanes 0..31): the w row of a candidate.
-  // w = dist / dist_sum is formed in fp64 like the reference and rounded once to fp32; the
-  // feature product below is then one fp32 multiply (the reference rounds the fp64 product to
+  // get_cat_feat_tgt.py:57-58 (lanes 32..63 mirror lanes 0..31): the w row of a candidate, into
+  // the wave's LDS row `buf` (two rows: a candidate's row is written while the previous one may
+  // still be read).  w = dist / dist_sum is formed in fp64 like the reference and rounded once to
+  // fp32; the feature product is then one fp32 multiply (the reference rounds the fp64 product to
   // fp32 at the DFE input: the two differ by at most one fp32 ulp of the input).
-  auto weights = [&](float dj) {
-    double dsum = static_cast<double>(dj);
-#pragma unroll
-    for (int off = 16; off > 0; off >>= 1) dsum += __shfl_xor(dsum, off, kWave);
-    L.w[wave][r32] = static_cast<float>(static_cast<double>(dj) / dsum);  // both lane halves write the same value
+  auto weights = [&](float dj, int buf) {
+    // sum of the 32 distances: quad and row rotations by DPP (no LDS round trips), then the two
+    // 16-lane row totals of the lower half read back and added (the upper half mirrors it)
+    double v = static_cast<double>(dj);
+    v = dpp_add_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+    v = dpp_add_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+    v = dpp_add_f64<0x124>(v);  // row_ror:4
+    v = dpp_add_f64<0x128>(v);  // row_ror:8
+    const double dsum = readlane_f64(v, 15) + readlane_f64(v, 31);
+    L.w[wave][buf][r32] = static_cast<float>(static_cast<double>(dj) / dsum);  // both halves write the same value
   };
-  auto embed = [&](int gg, const Gathered& G) {
-    float x[kDfeKS];
+  // A operands of a candidate: the xyz k-steps ((dx|dy), (dz|0)) and the 32 weighted features as
+  // split-3 bf16 pieces (lane half h: features 16h .. 16h + 15, k-step t: 16h + 8t ..)
+  struct Prepared {
+    float x0, x1;
+    DfeSplit3 s[2];
+  };
+  auto prep = [&](const Gathered& G, int buf, Prepared& X) {
     // candidates_grouped_local = tgt_pts_picked - candidate (point dtype, then .float()); half 1: 0
-#if DVCP_DFE_SPLIT3
     const float ddx = static_cast<float>(G.px - static_cast<T>(G.cx));
     const float ddy = static_cast<float>(G.py - static_cast<T>(G.cy));
     const float ddz = static_cast<float>(G.pz - static_cast<T>(G.cz));
-    x[0] = h == 0 ? ddx : ddy;  // the fp32 k-steps (x|y), (z|0)
-    x[1] = h == 0 ? ddz : 0.0f;
-    x[2] = 0.0f;
-#else
-    x[0] = h == 0 ? static_cast<float>(G.px - static_cast<T>(G.cx)) : 0.0f;
-    x[1] = h == 0 ? static_cast<float>(G.py - static_cast<T>(G.cy)) : 0.0f;
-    x[2] = h == 0 ? static_cast<float>(G.pz - static_cast<T>(G.cz)) : 0.0f;
-#endif
-    // the wave's own w row, read back as 16-byte broadcasts
-    __builtin_amdgcn_wave_barrier();
-    const float4* wr = reinterpret_cast<const float4*>(&L.w[wave][16 * h]);
+    X.x0 = h == 0 ? ddx : ddy;
+    X.x1 = h == 0 ? ddz : 0.0f;
+    const float4* wr = reinterpret_cast<const float4*>(&L.w[wave][buf][16 * h]);
     float4 fv[4];
     if constexpr (sizeof(FT) == 4) {
 #pragma unroll
@@ -368,64 +402,94 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
         fv[v].w = static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(hi >> 16)));
       }
     }
+    float x[16];
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const float4 w4 = wr[v];
-      x[3 + 4 * v] = fv[v].x * w4.x;
-      x[4 + 4 * v] = fv[v].y * w4.y;
-      x[5 + 4 * v] = fv[v].z * w4.z;
-      x[6 + 4 * v] = fv[v].w * w4.w;
+      x[4 * v] = fv[v].x * w4.x;
+      x[4 * v + 1] = fv[v].y * w4.y;
+      x[4 * v + 2] = fv[v].z * w4.z;
+      x[4 * v + 3] = fv[v].w * w4.w;
     }
-    int zo = 0;  // opaque zero: E fragments are re-read from LDS per candidate, not hoisted
-    asm volatile("" : "+v"(zo));
-    f32x16 a;
-    // split path: zero-started accumulators (inline-constant C) and e added once to the row
-    // maximum, max_j fl(h_j + e) = fl(max_j h_j + e) (rounding is monotone)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) a[r] = DVCP_DFE_SPLIT3 ? 0.0f : eb;
-#if DVCP_DFE_SPLIT3
-    a = __builtin_amdgcn_mfma_f32_32x32x2f32(x[0], L.ex[0][lane + zo], a, 0, 0, 0);
-    a = __builtin_amdgcn_mfma_f32_32x32x2f32(x[1], L.ex[1][lane + zo], a, 0, 0, 0);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       float f8[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f8[j] = x[3 + 8 * t + j];
-      a = dfe_mfma_split3(dfe_split3(f8), L.es[t][0][lane + zo], L.es[t][1][lane + zo], L.es[t][2][lane + zo], a);
+      for (int j = 0; j < 8; ++j) f8[j] = x[8 * t + j];
+      X.s[t] = dfe_split3(f8);
     }
-#else
+  };
+  // H = X E^T on the matrix cores; zero-started accumulators, e added once to the row maximum:
+  // max_j fl(h_j + e) = fl(max_j h_j + e) (rounding is monotone)
+  auto mfma = [&](const Prepared& X) {
+    int zo = 0;  // opaque zero: E fragments are re-read from LDS per candidate, not hoisted
+    asm volatile("" : "+v"(zo));
+    f32x16 a;
 #pragma unroll
-    for (int s = 0; s < kDfeKS; ++s) a = __builtin_amdgcn_mfma_f32_32x32x2f32(x[s], L.e[s][lane + zo], a, 0, 0, 0);
-#endif
+    for (int r = 0; r < 16; ++r) a[r] = 0.0f;
+    a = __builtin_amdgcn_mfma_f32_32x32x2f32(X.x0, L.ex[0][lane + zo], a, 0, 0, 0);
+    a = __builtin_amdgcn_mfma_f32_32x32x2f32(X.x1, L.ex[1][lane + zo], a, 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      a = dfe_mfma_split3(X.s[t], L.es[t][0][lane + zo], L.es[t][1][lane + zo], L.es[t][2][lane + zo], a);
+    return a;
+  };
+  auto finish = [&](const Cand& cg, const f32x16& a) {
     float m = a[0];
 #pragma unroll
     for (int r = 1; r < 16; ++r) m = fmaxf(m, a[r]);
     m = fmaxf(m, __shfl_xor(m, 32, kWave));
-    if (DVCP_DFE_SPLIT3) m += eb;
-    if (h == 0) out[static_cast<int64_t>(glob(gg)) * 32 + r32] = m;
-    __builtin_amdgcn_wave_barrier();  // the w row is rewritten for the next candidate
+    m += eb;
+    if (h == 0) out[static_cast<int64_t>(glob_of(cg)) * 32 + r32] = m;
   };
-  float djA, djB;
-  int nA, nB;
-  Gathered GA, GB;
-  load_row(g, djA, nA);
-  load_row(g + stride, djB, nB);
-  gather(g, nA, GA);
-  for (;;) {
-    // slot A holds candidate g (gathered), slot B the row of g + stride
-    weights(djA);
-    load_row(g + 2 * stride, djA, nA);
-    gather(g + stride, nB, GB);
-    embed(g, GA);
-    g += stride;
-    if (g >= total) break;
-    weights(djB);
-    load_row(g + 2 * stride, djB, nB);
-    gather(g + stride, nA, GA);
-    embed(g, GB);
-    g += stride;
-    if (g >= total) break;
+  // Software pipeline, one candidate per step: step c issues candidate c's MFMA chain and, in the
+  // same basic block, the independent VALU work of candidate c + 1 (its w row, its operands), which
+  // the scheduler places between the MFMAs; kNN rows are loaded six candidates ahead (they come
+  // from HBM / the infinity cache), gathered rows two ahead of their use.  Slots: rows U & 7,
+  // gathered rows and operands U & 1 (unrolled by 8, so every slot index is a constant).
+  float dj[8];
+  int nn[8];
+  Gathered G[2];
+  Prepared X[2];
+  Cand t0 = cand_at(g), t2 = cand_at(g + 2 * stride), t6 = cand_at(g + 6 * stride);
+  {
+    Cand r = t0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      load_row(r, dj[i], nn[i]);
+      advance(r);
+    }
+    Cand c1 = t0;
+    advance(c1);
+    gather(t0, nn[0], G[0]);
+    gather(c1, nn[1], G[1]);
+    weights(dj[0], 0);
+    prep(G[0], 0, X[0]);
   }
+#define DVCP_DFE_STEP(U)                                              \
+  {                                                                   \
+    const f32x16 acc = mfma(X[(U)&1]);                                \
+    weights(dj[((U) + 1) & 7], ((U) + 1) & 1);                        \
+    prep(G[((U) + 1) & 1], ((U) + 1) & 1, X[((U) + 1) & 1]);          \
+    load_row(t6, dj[((U) + 6) & 7], nn[((U) + 6) & 7]);               \
+    gather(t2, nn[((U) + 2) & 7], G[(U)&1]);                          \
+    finish(t0, acc);                                                  \
+    advance(t0);                                                      \
+    advance(t2);                                                      \
+    advance(t6);                                                      \
+    if (t0.li >= total) break;                                        \
+  }
+  for (;;) {
+    DVCP_DFE_STEP(0)
+    DVCP_DFE_STEP(1)
+    DVCP_DFE_STEP(2)
+    DVCP_DFE_STEP(3)
+    DVCP_DFE_STEP(4)
+    DVCP_DFE_STEP(5)
+    DVCP_DFE_STEP(6)
+    DVCP_DFE_STEP(7)
+  }
+#undef DVCP_DFE_STEP
 }
 
 template <typename T>

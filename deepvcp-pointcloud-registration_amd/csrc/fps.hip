@@ -532,8 +532,16 @@ __device__ __forceinline__ float prev_float(float v) {  // largest float below v
 // wave-wide max / min of non-negative floats (as ordered bits)
 __device__ __forceinline__ float wave_fmax_nn(float v) { return float_unorder_fps(wave_umax(float_order(v))); }
 
+// Up to 10 points per lane at 1024 threads (sa2 / sa3 of C3: 10000 points) the kernel fits in 96
+// VGPRs (5 waves per SIMD worth), so a fifth wave of up to 128 VGPRs -- a set-abstraction MFMA
+// table, a ball query -- can share the FPS workgroup's CU: the chain's four waves per SIMD spend
+// ~97 % of their time waiting on barriers and LDS (VALUBusy ~3 %, profiles/pmc_summary.json).
+template <int PPT, int THREADS>
+constexpr int fps_select_waves_per_eu() { return PPT <= 10 && THREADS == 1024 ? 5 : 1; }
+
 template <typename T, int PPT, bool TIMING = false, int THREADS = kFpsThreads>
-__global__ __launch_bounds__(THREADS) void fps_select_kernel(PointsView<T> pts, int N, int npoint,
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(fps_select_waves_per_eu<PPT, THREADS>())))
+void fps_select_kernel(PointsView<T> pts, int N, int npoint,
                                                                  const int64_t* __restrict__ start,
                                                                  int64_t* __restrict__ out_idx,
                                                                  T* __restrict__ out_xyz,

@@ -530,11 +530,13 @@ __global__ __launch_bounds__(kTiledThreads) void knn_tiled_query_kernel(const fl
 // point appended, and a point is only left out when its key is not below a k-th key that is at
 // least the true one (filters and pruning use the last merged, i.e. a stale-high, k-th key).
 constexpr int kSelBufN = 16;
-// DVCP_KNN_LAZY (default): a tile's 256 bytes are loaded once some lane is known to need it.  The
-// alternative prefetch one sorted position ahead made every scanned tile wait for its successor's
-// load at the loop latch (the register copy), ~660 clk per skipped tile (DVCP_KNN_DIAG).
-#ifndef DVCP_KNN_LAZY
-#define DVCP_KNN_LAZY 1
+// A tile's 256 bytes are loaded once some lane is known to need it (prefetching one sorted position
+// ahead made every scanned tile wait for its successor's load at the loop latch, ~660 clk per
+// skipped tile under DVCP_KNN_DIAG; round 3).
+// DVCP_KNN_CHUNK (default): the sorted order is scanned 64 positions at a time behind a
+// tile-parallel prefilter against lane-group boxes (see the scan below).
+#ifndef DVCP_KNN_CHUNK
+#define DVCP_KNN_CHUNK 1
 #endif
 // DVCP_KNN_SLOAD: an active tile's 16 points reach the wave as scalar loads (the tile index is
 // wave-uniform, the tile is read-only here) instead of one vector load and 48 readlanes; the
@@ -542,6 +544,24 @@ constexpr int kSelBufN = 16;
 #ifndef DVCP_KNN_SLOAD
 #define DVCP_KNN_SLOAD 0
 #endif
+
+// (d2, index) keys packed into doubles of [1, 2) (see knn_sel_query_kernel): 14 index bits
+constexpr double kKeyEmpty = __builtin_bit_cast(double, 0x3FF0000000000000ull | (0x7F800000ull << 14) | 0x3FFFull);
+__device__ __forceinline__ double key_pack(float d2, uint32_t index) {
+  return __builtin_bit_cast(double, 0x3FF0000000000000ull | (static_cast<uint64_t>(__float_as_uint(d2)) << 14) |
+                                        static_cast<uint64_t>(index & 0x3FFFu));
+}
+__device__ __forceinline__ float key_d2(double kd) {
+  return __uint_as_float(static_cast<uint32_t>((__builtin_bit_cast(uint64_t, kd) >> 14) & 0x7FFFFFFFull));
+}
+__device__ __forceinline__ int key_index(double kd) {
+  return static_cast<int>(__builtin_bit_cast(uint64_t, kd) & 0x3FFFull);
+}
+__device__ __forceinline__ void key_ce_f64(double& a, double& b, bool asc) {
+  const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);
+  a = asc ? lo : hi;
+  b = asc ? hi : lo;
+}
 
 __device__ __forceinline__ void key_ce(uint32_t& ah, uint32_t& al, uint32_t& bh, uint32_t& bl, bool asc) {
   const uint64_t a = (static_cast<uint64_t>(ah) << 32) | al, b = (static_cast<uint64_t>(bh) << 32) | bl;
@@ -574,7 +594,7 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
   const int T = (M + kTile - 1) / kTile;
   // 12 + 32 KB of LDS (half-precision boxes, candidate buffers): three workgroups per CU
   __shared__ uint3 hbox[kMaxTiles];
-  __shared__ uint2 sbuf[kTiledThreads / kWave][kSelBufN][kWave];  // lane-private candidate buffers
+  __shared__ double sbuf[kTiledThreads / kWave][kSelBufN][kWave];  // lane-private candidate buffers (packed keys)
   __shared__ float4 stile[kTiledThreads / kWave][kTile];            // the wave's current tile (appends)
   {
     const float4* tbg = tbox + static_cast<int64_t>(b) * T * 2;
@@ -619,19 +639,18 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
   }
   wave_bitonic<R>(keys);
 
-  uint32_t th[KT], tl[KT];  // this lane's 32 smallest keys so far, ascending
+  // This lane's 32 smallest keys so far, ascending.  A key (d2, index) is packed into the mantissa
+  // of a double in [1, 2): bits 0x3FF0'0000'0000'0000 | d2_bits << 14 | index (M <= 16384: 14 index
+  // bits; non-negative d2 bits order like the values), so doubles order exactly like the keys and
+  // a compare-exchange is one v_min_f64 + one v_max_f64 instead of a 64-bit compare and four selects.
+  double tk[KT];
 #pragma unroll
-  for (int t = 0; t < KT; ++t) {
-    th[t] = 0x7F800000u;
-    tl[t] = ~0u;
-  }
-  constexpr uint64_t kEmpty = (static_cast<uint64_t>(0x7F800000u) << 32) | 0xFFFFFFFFu;
-  const int kq = k - 1;  // wave-uniform: th[kq], tl[kq] are indexed register reads
-  uint64_t kkey = live ? kEmpty : 0ull;  // dead lanes never take a point
-  float kth = live ? __builtin_huge_valf() : 0.0f;
+  for (int t = 0; t < KT; ++t) tk[t] = kKeyEmpty;
+  const int kq = k - 1;  // wave-uniform
+  float kth = live ? __builtin_huge_valf() : 0.0f;  // dead lanes never take a point
   float wkth = wave_max_nonneg(kth);
   int fill = 0;
-  uint2(*mybuf)[kWave] = sbuf[wave];
+  double(*mybuf)[kWave] = sbuf[wave];
 #ifdef DVCP_KNN_DIAG  // per-wave counters (diagnostic builds only; written over lane 0's distances)
   uint64_t dg_t0 = __builtin_readcyclecounter(), dg_merge_clk = 0, dg_skip_clk = 0, dg_prev = 0;
   int dg_kind = -1;  // the previous iteration: 0 skipped, 1 processed
@@ -645,15 +664,13 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
     const uint64_t dg_m0 = __builtin_readcyclecounter();
     ++dg_merges;
 #endif
-    uint32_t bh[kSelBufN], bl[kSelBufN];
+    double bk[kSelBufN];
 #pragma unroll
     for (int i = 0; i < kSelBufN; ++i) {
-      bh[i] = 0x7F800000u;
-      bl[i] = ~0u;
+      bk[i] = kKeyEmpty;
       if (i < n) {
-        const uint2 e = mybuf[i][lane];
-        bh[i] = i < fill ? e.x : bh[i];
-        bl[i] = i < fill ? e.y : bl[i];
+        const double e = mybuf[i][lane];
+        bk[i] = i < fill ? e : bk[i];
       }
     }
     // bitonic sort of the 16 buffered keys, ascending
@@ -664,28 +681,26 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
 #pragma unroll
         for (int i = 0; i < kSelBufN; ++i) {
           const int l = i ^ j;
-          if (l > i) key_ce(bh[i], bl[i], bh[l], bl[l], (i & kk) == 0);
+          if (l > i) key_ce_f64(bk[i], bk[l], (i & kk) == 0);
         }
     // C[i] = min(top[i], buf[31 - i]) (buf[16..31] = empty): bitonic, the 32 smallest keys
 #pragma unroll
-    for (int i = KT - kSelBufN; i < KT; ++i) {
-      const int jb = KT - 1 - i;
-      const uint64_t a = (static_cast<uint64_t>(th[i]) << 32) | tl[i];
-      const uint64_t c = (static_cast<uint64_t>(bh[jb]) << 32) | bl[jb];
-      const bool lt = c < a;
-      th[i] = lt ? bh[jb] : th[i];
-      tl[i] = lt ? bl[jb] : tl[i];
-    }
+    for (int i = KT - kSelBufN; i < KT; ++i) tk[i] = __builtin_fmin(tk[i], bk[KT - 1 - i]);
     // bitonic merge, ascending
 #pragma unroll
     for (int j = KT >> 1; j > 0; j >>= 1)
 #pragma unroll
       for (int i = 0; i < KT; ++i) {
         const int l = i ^ j;
-        if (l > i) key_ce(th[i], tl[i], th[l], tl[l], true);
+        if (l > i) key_ce_f64(tk[i], tk[l], true);
       }
-    kkey = live ? ((static_cast<uint64_t>(th[kq]) << 32) | tl[kq]) : 0ull;
-    kth = __uint_as_float(static_cast<uint32_t>(kkey >> 32));
+    // the k-th key (a dynamically indexed double array would not stay in registers)
+    double kk_ = tk[KT - 1];
+    if (kq != KT - 1) {  // wave-uniform; the forward's k = 32 never takes it
+#pragma unroll
+      for (int t = 0; t < KT - 1; ++t) kk_ = t == kq ? tk[t] : kk_;
+    }
+    kth = live ? key_d2(kk_) : 0.0f;
     wkth = wave_max_nonneg(kth);
     fill = 0;
 #ifdef DVCP_KNN_DIAG
@@ -693,20 +708,174 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
 #endif
   };
 
-  // The next tile in the sorted order is fetched one position ahead, one float per lane (a tile is
-  // 16 points x 4 floats = 64 floats: one coalesced 256-byte load), so its latency hides behind
-  // the current tile; its coordinates reach every lane by readlane (SGPR operands).
+  // A needed tile is one coalesced 256-byte load (16 points x 4 floats: one float per lane) whose
+  // coordinates reach every lane by readlane (SGPR operands).
   // (Per-wave counters, DVCP_KNN_DIAG, C3: ~185 tiles pass the wave's bound, ~32 of them have a
   // lane within its own k-th distance, 11 merges = 20-24 % of the wave's clock.  Loading only the
   // tiles some lane needs, found by a look-ahead test, was slower: 0.97 -> 1.11 ms per call,
   // profiles/round3/r3x_knn_diag_*.log.)
   const float* P = reinterpret_cast<const float*>(sorted) + static_cast<int64_t>(b) * T * kTile * 4;
-  uint32_t key_next = T > 0 ? static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(keys[0]), 0)) : 0u;
-#if !DVCP_KNN_LAZY
-  float v_next = T > 0 ? P[static_cast<int64_t>(key_next & kTileIdBits) * (4 * kTile) + lane] : 0.f;
+  // Visit the tile of sorted key `key` (its bound already known not to exceed wkth): the per-lane
+  // test, then the distances, the filter and the appends.
+  auto visit = [&](uint32_t key) {
+    const int t = static_cast<int>(key & kTileIdBits);
+    const float lbq = hbox_lb2(hbox[t], qx, qy, qz, qx, qy, qz);
+    const bool act = live & (lbq <= kth);
+#ifdef DVCP_KNN_DIAG
+    ++dg_scanned;
 #endif
+    if (__ballot(act) == 0) return;
+#ifdef DVCP_KNN_DIAG
+    ++dg_active;
+    dg_kind = 1;
+#endif
+    float c[3 * kTile];
+#if DVCP_KNN_SLOAD
+    {
+      const float4* Pt = reinterpret_cast<const float4*>(P) + static_cast<int64_t>(t) * kTile;
+#pragma unroll
+      for (int j = 0; j < kTile; ++j) {
+        const float4 pj = Pt[j];
+        c[3 * j] = pj.x;
+        c[3 * j + 1] = pj.y;
+        c[3 * j + 2] = pj.z;
+      }
+    }
+#else
+    const float v_cur = P[static_cast<int64_t>(t) * (4 * kTile) + lane];
+    auto bc = [&](int u) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v_cur), u)); };
+#pragma unroll
+    for (int j = 0; j < kTile; ++j) {
+      c[3 * j] = bc(4 * j);
+      c[3 * j + 1] = bc(4 * j + 1);
+      c[3 * j + 2] = bc(4 * j + 2);
+    }
+#endif
+    // d2 is recomputed wherever it is needed (the same expression, the same bits) instead of
+    // being held in 16 VGPRs across the merge and the appends
+    auto d2_of = [&](int j) {
+      const float dx = c[3 * j] - qx, dy = c[3 * j + 1] - qy, dz = c[3 * j + 2] - qz;
+      return (dx * dx + dy * dy) + dz * dz;
+    };
+    uint32_t cm = 0;
+    // Filter on the distance alone, d2 <= kf: a superset of the keys below the k-th key (a tie
+    // with a higher index is appended too and dropped by the merge, which orders full keys);
+    // kf is finite, so inf and NaN (padding) never pass, as in dvcp_knn.
+    const float kf = fminf(kth, __builtin_bit_cast(float, 0x7F7FFFFFu));
+#pragma unroll
+    for (int j = 0; j < kTile; ++j) cm |= (act && d2_of(j) <= kf) ? (1u << j) : 0u;
+    if (wave_umax_i(static_cast<uint32_t>(fill + __popc(cm))) > static_cast<uint32_t>(kSelBufN)) {
+      merge();  // room for the whole tile; then re-filter against the new k-th key
+      const float kf2 = fminf(kth, __builtin_bit_cast(float, 0x7F7FFFFFu));
+#pragma unroll
+      for (int j = 0; j < kTile; ++j) cm &= d2_of(j) <= kf2 ? ~0u : ~(1u << j);
+    }
+    // appends: each lane walks its own mask, reading its points from the wave's copy of the tile
+    // in LDS (the wave loops max-over-lanes popc(mask) times instead of over the union of the
+    // masks with four readlanes per point); the same d2 expression, the same bits
+    if (__ballot(cm != 0) != 0) {  // wave-uniform: every lane writes its float of the tile
+#if DVCP_KNN_SLOAD
+      reinterpret_cast<float*>(stile[wave])[lane] = P[static_cast<int64_t>(t) * (4 * kTile) + lane];
+#else
+      reinterpret_cast<float*>(stile[wave])[lane] = v_cur;
+#endif
+      __builtin_amdgcn_wave_barrier();
+      uint32_t my = cm;
+      while (__ballot(my != 0) != 0) {
+        if (my != 0) {
+          const int j = __builtin_ctz(my);
+          my &= my - 1;
+#ifdef DVCP_KNN_DIAG
+          ++dg_appends;
+#endif
+          const float4 pt = stile[wave][j];
+          const float dx = pt.x - qx, dy = pt.y - qy, dz = pt.z - qz;
+          mybuf[fill][lane] = key_pack((dx * dx + dy * dy) + dz * dz, __float_as_uint(pt.w));
+          ++fill;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();  // (the next active tile rewrites stile)
+    }
+  };
+
+#if DVCP_KNN_CHUNK
+  // Chunked scan.  The sorted order is taken 64 positions at a time, one position per lane, and a
+  // tile-parallel prefilter drops the positions no query can need: lane i tests its tile's box
+  // against the boxes of the wave's kKnnSub lane groups (16 Hilbert-consecutive queries each) with
+  // each group's largest k-th distance.  A position survives when some group's bound reaches its
+  // k-th distance; only survivors get the per-lane test (visit).  The group bounds come from k-th
+  // distances read at chunk start: merges only lower them, so a stale bound keeps a superset and
+  // the scan stays exact; the stop rule is re-checked at every surviving position.
+  constexpr int kKnnSub = 4, kSubLanes = kWave / kKnnSub;
+  float gl[3] = {wl[0], wl[1], wl[2]}, gh[3] = {wh[0], wh[1], wh[2]};  // (overwritten below)
+  {
+    float a[3] = {live ? qx : __builtin_huge_valf(), live ? qy : __builtin_huge_valf(),
+                  live ? qz : __builtin_huge_valf()};
+    float z[3] = {live ? qx : -__builtin_huge_valf(), live ? qy : -__builtin_huge_valf(),
+                  live ? qz : -__builtin_huge_valf()};
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax)
+#pragma unroll
+      for (int off = kSubLanes / 2; off > 0; off >>= 1) {
+        a[ax] = fminf(a[ax], __shfl_xor(a[ax], off, kWave));
+        z[ax] = fmaxf(z[ax], __shfl_xor(z[ax], off, kWave));
+      }
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax) {
+      gl[ax] = a[ax];
+      gh[ax] = z[ax];
+    }
+  }
+  // every group's box, in LDS (read back as broadcasts per chunk: 24 wave-uniform values held in
+  // registers across the scan would spill)
+  __shared__ float4 sgbox[kTiledThreads / kWave][kKnnSub][2];
+  if ((lane & (kSubLanes - 1)) == 0) {
+    sgbox[wave][lane / kSubLanes][0] = make_float4(gl[0], gl[1], gl[2], 0.0f);
+    sgbox[wave][lane / kSubLanes][1] = make_float4(gh[0], gh[1], gh[2], 0.0f);
+  }
+  __builtin_amdgcn_wave_barrier();
+  bool stop = false;
+#pragma unroll 1
+  for (int base = 0; base < T && !stop; base += kWave) {
+    uint32_t mykey = keys[base >> 6];  // lane i: sorted position base + i (re-read below, not held)
+    const bool inr = base + lane < T;
+    const float klb = __uint_as_float(mykey & ~kTileIdBits);
+    const uint64_t over = __ballot(!inr || klb > wkth);
+    const int lim = over ? __builtin_ctzll(over) : kWave;  // positions past lim are never needed
+    // the groups' k-th distances (largest per group) as of now
+    float gk = kth;
+#pragma unroll
+    for (int off = kSubLanes / 2; off > 0; off >>= 1) gk = fmaxf(gk, __shfl_xor(gk, off, kWave));
+    float gks[kKnnSub];
+#pragma unroll
+    for (int g = 0; g < kKnnSub; ++g) gks[g] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gk), g * kSubLanes));
+    const int tt = inr ? static_cast<int>(mykey & kTileIdBits) : 0;
+    const uint3 hb = hbox[tt < T ? tt : 0];
+    const float blx = half_lo(hb.x), bly = half_hi(hb.x), blz = half_lo(hb.y);
+    const float bhx = half_hi(hb.y), bhy = half_lo(hb.z), bhz = half_hi(hb.z);
+    bool pass = false;
+#pragma unroll
+    for (int g = 0; g < kKnnSub; ++g) {
+      const float4 lo = sgbox[wave][g][0], hi = sgbox[wave][g][1];
+      pass |= box_box_lb2(lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, blx, bly, blz, bhx, bhy, bhz) <= gks[g];
+    }
+    uint64_t cand = __ballot(pass && inr) & (lim >= kWave ? ~0ull : ((1ull << lim) - 1ull));
+    if (lim < kWave) stop = true;
+    while (cand) {
+      const int i = __builtin_ctzll(cand);
+      cand &= cand - 1ull;
+      const uint32_t key = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(keys[base >> 6]), i));
+      if (__uint_as_float(key & ~kTileIdBits) > wkth) {  // every later tile is farther
+        stop = true;
+        break;
+      }
+      visit(key);
+    }
+  }
+#else
   // one flat loop over the sorted tile order (not unrolled over the key registers: the merge is
   // large, and the key register is a wave-uniform indexed read)
+  uint32_t key_next = T > 0 ? static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(keys[0]), 0)) : 0u;
 #pragma unroll 1
   for (int pos = 0; pos < T; ++pos) {
 #ifdef DVCP_KNN_DIAG
@@ -717,103 +886,13 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
       dg_kind = 0;
     }
 #endif
-    {
-      const uint32_t key = key_next;
-#if DVCP_KNN_LAZY
-      if (pos + 1 < T)
-        key_next = static_cast<uint32_t>(
-            __builtin_amdgcn_readlane(static_cast<int>(keys[(pos + 1) >> 6]), (pos + 1) & 63));
-#else
-      const float v_cur = v_next;
-      if (pos + 1 < T) {
-        key_next = static_cast<uint32_t>(
-            __builtin_amdgcn_readlane(static_cast<int>(keys[(pos + 1) >> 6]), (pos + 1) & 63));
-        v_next = P[static_cast<int64_t>(key_next & kTileIdBits) * (4 * kTile) + lane];
-      }
-#endif
-      if (__uint_as_float(key & ~kTileIdBits) > wkth) break;  // every later tile is farther
-      const int t = static_cast<int>(key & kTileIdBits);
-      const float lbq = hbox_lb2(hbox[t], qx, qy, qz, qx, qy, qz);
-      const bool act = live & (lbq <= kth);
-#ifdef DVCP_KNN_DIAG
-      ++dg_scanned;
-#endif
-      if (__ballot(act) == 0) continue;
-#ifdef DVCP_KNN_DIAG
-      ++dg_active;
-      dg_kind = 1;
-#endif
-      float c[3 * kTile];
-#if DVCP_KNN_LAZY && DVCP_KNN_SLOAD
-      {
-        const float4* Pt = reinterpret_cast<const float4*>(P) + static_cast<int64_t>(t) * kTile;
-#pragma unroll
-        for (int j = 0; j < kTile; ++j) {
-          const float4 pj = Pt[j];
-          c[3 * j] = pj.x;
-          c[3 * j + 1] = pj.y;
-          c[3 * j + 2] = pj.z;
-        }
-      }
-#else
-#if DVCP_KNN_LAZY
-      const float v_cur = P[static_cast<int64_t>(t) * (4 * kTile) + lane];
-#endif
-      auto bc = [&](int u) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v_cur), u)); };
-#pragma unroll
-      for (int j = 0; j < kTile; ++j) {
-        c[3 * j] = bc(4 * j);
-        c[3 * j + 1] = bc(4 * j + 1);
-        c[3 * j + 2] = bc(4 * j + 2);
-      }
-#endif
-      // d2 is recomputed wherever it is needed (the same expression, the same bits) instead of
-      // being held in 16 VGPRs across the merge and the appends
-      auto d2_of = [&](int j) {
-        const float dx = c[3 * j] - qx, dy = c[3 * j + 1] - qy, dz = c[3 * j + 2] - qz;
-        return (dx * dx + dy * dy) + dz * dz;
-      };
-      uint32_t cm = 0;
-      // Filter on the distance alone, d2 <= kf: a superset of the keys below the k-th key (a tie
-      // with a higher index is appended too and dropped by the merge, which orders full keys);
-      // kf is finite, so inf and NaN (padding) never pass, as in dvcp_knn.
-      const float kf = fminf(kth, __builtin_bit_cast(float, 0x7F7FFFFFu));
-#pragma unroll
-      for (int j = 0; j < kTile; ++j) cm |= (act && d2_of(j) <= kf) ? (1u << j) : 0u;
-      if (wave_umax_i(static_cast<uint32_t>(fill + __popc(cm))) > static_cast<uint32_t>(kSelBufN)) {
-        merge();  // room for the whole tile; then re-filter against the new k-th key
-        const float kf2 = fminf(kth, __builtin_bit_cast(float, 0x7F7FFFFFu));
-#pragma unroll
-        for (int j = 0; j < kTile; ++j) cm &= d2_of(j) <= kf2 ? ~0u : ~(1u << j);
-      }
-      // appends: each lane walks its own mask, reading its points from the wave's copy of the tile
-      // in LDS (the wave loops max-over-lanes popc(mask) times instead of over the union of the
-      // masks with four readlanes per point); the same d2 expression, the same bits
-      if (__ballot(cm != 0) != 0) {  // wave-uniform: every lane writes its float of the tile
-#if DVCP_KNN_LAZY && DVCP_KNN_SLOAD
-        reinterpret_cast<float*>(stile[wave])[lane] = P[static_cast<int64_t>(t) * (4 * kTile) + lane];
-#else
-        reinterpret_cast<float*>(stile[wave])[lane] = v_cur;
-#endif
-        __builtin_amdgcn_wave_barrier();
-        uint32_t my = cm;
-        while (__ballot(my != 0) != 0) {
-          if (my != 0) {
-            const int j = __builtin_ctz(my);
-            my &= my - 1;
-#ifdef DVCP_KNN_DIAG
-            ++dg_appends;
-#endif
-            const float4 pt = stile[wave][j];
-            const float dx = pt.x - qx, dy = pt.y - qy, dz = pt.z - qz;
-            mybuf[fill][lane] = make_uint2(__float_as_uint((dx * dx + dy * dy) + dz * dz), __float_as_uint(pt.w));
-            ++fill;
-          }
-        }
-        __builtin_amdgcn_wave_barrier();  // (the next active tile rewrites stile)
-      }
-    }
+    const uint32_t key = key_next;
+    if (pos + 1 < T)
+      key_next = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(keys[(pos + 1) >> 6]), (pos + 1) & 63));
+    if (__uint_as_float(key & ~kTileIdBits) > wkth) break;  // every later tile is farther
+    visit(key);
   }
+#endif
   merge();
 #ifdef DVCP_KNN_DIAG
   const uint64_t dg_total = __builtin_readcyclecounter() - dg_t0;
@@ -838,9 +917,9 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
 #pragma unroll
   for (int t = 0; t < KT; ++t) {
     if (t < k) {
-      const bool ok = ((static_cast<uint64_t>(th[t]) << 32) | tl[t]) != kEmpty;  // fewer than k finite points
-      const float d2 = __uint_as_float(th[t]);
-      const int i = static_cast<int>(tl[t]);
+      const bool ok = tk[t] != kKeyEmpty;  // fewer than k finite points
+      const float d2 = key_d2(tk[t]);
+      const int i = key_index(tk[t]);
       if (dist) dist[o + t] = ok ? sqrt_rn(d2) : __builtin_huge_valf();
       if (idx) idx[o + t] = ok ? i : -1;
       if (idx64) idx64[o + t] = ok ? i : -1;

@@ -2,8 +2,9 @@
 test_gpu_e2e.py's):
 
 * C2 -- ModelNet40-like, 32 pairs x 2048 points with normals (C_in = 6, fp64), K = 32: the whole
-  batch in one forward; every pair equals its own single-pair run (pairs are independent in
-  eval mode), and pair 0 matches the oracle (key points exact, R, t within 1e-4).
+  batch in one forward; pairs 0, 13 and 31 each equal their own single-pair run (pairs are
+  independent in eval mode) and match the oracle (key points exact, R, t within
+  1e-4).
 * C5 -- synthetic 65536-point clouds, K = 256: the first FPS (65536 -> 10000, the dense kernel
   above the register-resident limit) is bit-exact against the oracle, and the full forward +
   pose solve runs with its structural properties intact, with the reference's fp32 features and
@@ -31,15 +32,14 @@ def _calibrated_pair(use_normal, K, r, s, src0, fe_npoint=10000):
     return ref, mine
 
 
-def test_c2_modelnet_batch32(cuda):
-    """C2 in one batch; pair 0 end to end against the oracle with the GPU's own top-k, checked
-    rank by rank (tests_helpers.topk_parity).  Should a near-tie block reorder the top-k, pair 0
-    is re-run from the oracle's top-k and key points, R, t must still match: the R, t <= 1e-4
-    check is asserted on every path, never skipped."""
-    import oracle as O
+C2_PAIRS = (0, 13, 31)
+
+
+@pytest.fixture(scope="module")
+def c2_batch(cuda):
+    """C2 in one batch (32 ModelNet-like pairs with normals, fp64, N = 2048, K = 32)."""
     import dvcp
     from dvcp.synthetic import make_pairs
-    from tests_helpers import topk_parity
     B, N, K, r, s = 32, 2048, 32, 1.0, 0.4
     src, tgt, R_gt, t_gt = make_pairs(B, N, normals=True, seed=202)   # fp64, C_in = 6
     ref, mine = _calibrated_pair(True, K, r, s, src[:1])
@@ -49,36 +49,58 @@ def test_c2_modelnet_batch32(cuda):
     with torch.no_grad():
         kp, vcp = mine(src.to(cuda), tgt.to(cuda), R_gt.to(cuda), torch.zeros(1, 3), starts=starts, trace=tr)
         loss, R, t = dvcp.deepVCP_loss(kp, vcp, R_gt.to(cuda), t_gt.to(cuda), 0.5)
-    assert kp.shape == (B, K, 3) and vcp.shape == (B, K, 3)
-    # pairs are independent: each equals its own single-pair run (same FPS starts)
-    for b in (0, 13, 31):
-        with torch.no_grad():
-            kp1, vcp1 = mine(src[b:b + 1].to(cuda), tgt[b:b + 1].to(cuda), R_gt[b:b + 1].to(cuda),
-                             torch.zeros(1, 3), starts=starts[:, b:b + 1])
-            _, R1, t1 = dvcp.deepVCP_loss(kp1, vcp1, R_gt[b:b + 1].to(cuda), t_gt[b:b + 1].to(cuda), 0.5)
-        assert torch.equal(kp1[0], kp[b]), b
-        torch.testing.assert_close(vcp1[0], vcp[b], rtol=0, atol=1e-6)
-        torch.testing.assert_close(R1[0], R[b], rtol=0, atol=1e-9)
-        torch.testing.assert_close(t1[0], t[b], rtol=0, atol=1e-9)
-    # pair 0 against the oracle
-    with torch.no_grad(), O.fps_starts(list(starts[:, :1])), O.tracing() as trace:
-        kp_o, vcp_o = ref(src[:1], tgt[:1], R_gt[:1], torch.zeros(1, 3))
-        _, R_o, t_o = O.deepVCP_loss(kp_o, vcp_o, R_gt[:1], t_gt[:1], 0.5)
+    assert kp.shape == (B, K, 3) and vcp.shape == (B, K, 3) and torch.isfinite(loss)
+    return dict(ref=ref, mine=mine, data=(src, tgt, R_gt, t_gt), starts=starts, trace=tr, out=(kp, vcp, R, t), K=K)
+
+
+@pytest.mark.parametrize("b", C2_PAIRS)
+def test_c2_pair_equals_single_pair_run(cuda, c2_batch, b):
+    """Pairs are independent: pair b of the batch equals its own single-pair run."""
+    import dvcp
+    c = c2_batch
+    src, tgt, R_gt, t_gt = c["data"]
+    kp, vcp, R, t = c["out"]
+    with torch.no_grad():
+        kp1, vcp1 = c["mine"](src[b:b + 1].to(cuda), tgt[b:b + 1].to(cuda), R_gt[b:b + 1].to(cuda),
+                              torch.zeros(1, 3), starts=c["starts"][:, b:b + 1])
+        _, R1, t1 = dvcp.deepVCP_loss(kp1, vcp1, R_gt[b:b + 1].to(cuda), t_gt[b:b + 1].to(cuda), 0.5)
+    assert torch.equal(kp1[0], kp[b]), b
+    torch.testing.assert_close(vcp1[0], vcp[b], rtol=0, atol=1e-6)
+    torch.testing.assert_close(R1[0], R[b], rtol=0, atol=1e-9)
+    torch.testing.assert_close(t1[0], t[b], rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("b", C2_PAIRS)
+def test_c2_pair_vs_oracle(cuda, c2_batch, b):
+    """Pair b of the C2 batch end to end against the oracle with the GPU's own top-k, checked rank
+    by rank (tests_helpers.topk_parity).  Should a near-tie block reorder the top-k, the pair is
+    re-run from the oracle's top-k and key points, R, t must still match: the R, t <= 1e-4 check is
+    asserted on every path, never skipped."""
+    import oracle as O
+    import dvcp
+    from tests_helpers import topk_parity
+    c = c2_batch
+    src, tgt, R_gt, t_gt = c["data"]
+    kp, vcp, R, t = c["out"]
+    tr, K, starts = c["trace"], c["K"], c["starts"]
+    sl = slice(b, b + 1)
+    with torch.no_grad(), O.fps_starts(list(starts[:, sl])), O.tracing() as trace:
+        kp_o, vcp_o = c["ref"](src[sl], tgt[sl], R_gt[sl], torch.zeros(1, 3))
+        _, R_o, t_o = O.deepVCP_loss(kp_o, vcp_o, R_gt[sl], t_gt[sl], 0.5)
     d = dict(trace)
     want = d["wl_score"][..., 0]
-    exact, n_amb = topk_parity(tr["topk"][:1], tr["score"][:1], d["topk_idx"], want, K)
-    print(f"C2 pair 0: GPU top-k == oracle top-k: {exact} ({n_amb} near-tie rank boundaries)")
+    exact, n_amb = topk_parity(tr["topk"][sl], tr["score"][sl], d["topk_idx"], want, K)
+    print(f"C2 pair {b}: GPU top-k == oracle top-k: {exact} ({n_amb} near-tie rank boundaries)")
     if exact:
-        kp0, R0, t0 = kp[:1], R[:1], t[:1]
+        kp0, R0, t0 = kp[sl], R[sl], t[sl]
     else:   # a near-tie block reordered: the back half from the oracle's top-k
         with torch.no_grad():
-            kp0, vcp0 = mine(src[:1].to(cuda), tgt[:1].to(cuda), R_gt[:1].to(cuda), torch.zeros(1, 3),
-                             starts=starts[:, :1], keypoint_idx=d["topk_idx"])
-            _, R0, t0 = dvcp.deepVCP_loss(kp0, vcp0, R_gt[:1].to(cuda), t_gt[:1].to(cuda), 0.5)
+            kp0, vcp0 = c["mine"](src[sl].to(cuda), tgt[sl].to(cuda), R_gt[sl].to(cuda), torch.zeros(1, 3),
+                                  starts=starts[:, sl], keypoint_idx=d["topk_idx"])
+            _, R0, t0 = dvcp.deepVCP_loss(kp0, vcp0, R_gt[sl].to(cuda), t_gt[sl].to(cuda), 0.5)
     assert torch.equal(kp0.cpu(), kp_o.to(kp0.dtype))
     torch.testing.assert_close(R0.cpu(), R_o, rtol=0, atol=1e-4)
     torch.testing.assert_close(t0.cpu(), t_o, rtol=0, atol=1e-4)
-    assert torch.isfinite(loss)
 
 
 def test_c5_first_fps_full_size_vs_oracle(cuda):

@@ -56,3 +56,20 @@ for lvl in range(3):
         else:
             same = torch.equal(w, cat)
         print(f"layer {lvl} {nm:5s} shards-equal {same}")
+
+# the same batch after the caching allocator's free blocks were filled with garbage (NaN / 0xFF):
+# a kernel that read memory it never wrote would now differ
+junk = []
+for mb in (4096, 2048, 1024, 512, 256, 128, 64, 32, 16, 8, 4, 2, 1):
+    for _ in range(8):
+        t = torch.empty(mb << 18, dtype=torch.float32, device=dev)
+        t.fill_(float("nan"))
+        junk.append(t)
+        u = torch.empty(mb << 18, dtype=torch.int32, device=dev)
+        u.fill_(-1)
+        junk.append(u)
+del junk, t, u
+dirty = run(0, P)
+for k in keys:
+    same = torch.equal(whole[k], dirty[k])
+    print(f"{k:10s} after-garbage-equal {same}")

@@ -25,7 +25,8 @@ def main():
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     reps = 10
     outs = {}
-    for method in ("tiled_insert", "tiled", "tiled_insert", "tiled"):
+    methods = ("tiled",) if "--fast" in sys.argv else ("tiled_insert", "tiled", "tiled_insert", "tiled")
+    for method in methods:
         for _ in range(3):
             dist, idx, _ = ops.knn(ref, qry, 32, ref_pdim=2, qry_pdim=1, want_idx64=False, method=method)
         torch.cuda.synchronize()
@@ -38,8 +39,9 @@ def main():
         print(f"knn {method}: {e0.elapsed_time(e1) / reps:.4f} ms/call (build + query)  queries "
               f"{qry.shape[0] * qry.shape[1]}  checksum {dist.double().sum().item():.6e} {idx.long().sum().item()}",
               flush=True)
-    same = all(torch.equal(a, b) for a, b in zip(outs["tiled"], outs["tiled_insert"]))
-    print(f"knn tiled == tiled_insert: {same}", flush=True)
+    if "tiled_insert" in outs:
+        same = all(torch.equal(a, b) for a, b in zip(outs["tiled"], outs["tiled_insert"]))
+        print(f"knn tiled == tiled_insert: {same}", flush=True)
 
     # the target-side deep feature embedding on these neighbour lists (features random)
     import dvcp
