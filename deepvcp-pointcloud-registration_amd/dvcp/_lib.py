@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdvcp_hip.so")
 
 F32, F64 = 0, 1
-ABI_VERSION = 2   # include/dvcp.h DVCP_ABI_VERSION
+ABI_VERSION = 3   # include/dvcp.h DVCP_ABI_VERSION
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _L = ctypes.c_int64
@@ -75,6 +75,9 @@ SIGNATURES = {
                             _P, _P, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P],
     "dvcp_sa_bn_zrows": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _L, _L, _L, _I,
                          _P, _P, _I, _I, _P, _P, _P, _P],
+    "dvcp_sa_bnm_pre": [_P, _L, _L, _I, _I, _I, _I, _I, _P, _P, _P],
+    "dvcp_sa_bnm_pass": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _P, _L, _L, _I, _P, _P, _I, _I, _I,
+                         _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
 }
 
 _lib = None
@@ -94,7 +97,10 @@ def load():
     lib.dvcp_last_error.argtypes = []
     lib.dvcp_abi_version.restype = ctypes.c_int
     lib.dvcp_abi_version.argtypes = []
-    if lib.dvcp_abi_version() != ABI_VERSION:
+    # DVCP_SKIP_ABI=1: the A/B harness (tools/gpu_ab_micro.sh) loading an older build for the entry
+    # points it times; entry points that build lacks are left undeclared
+    skip = os.environ.get("DVCP_SKIP_ABI") == "1"
+    if lib.dvcp_abi_version() != ABI_VERSION and not skip:
         raise RuntimeError(f"dvcp: {LIB_PATH} has ABI version {lib.dvcp_abi_version()}, this package expects "
                            f"{ABI_VERSION}: rebuild it (make -j16 in deepvcp-pointcloud-registration_amd/)")
     lib.dvcp_knn_grid_workspace_bytes.restype = ctypes.c_int64
@@ -129,7 +135,14 @@ def load():
     lib.dvcp_cpg1d_nparams.argtypes = []
     lib.dvcp_sa_bn_pack_floats.restype = ctypes.c_int64
     lib.dvcp_sa_bn_pack_floats.argtypes = [ctypes.c_int, ctypes.c_void_p]
+    if hasattr(lib, "dvcp_sa_bnm_supported") or not skip:
+        lib.dvcp_sa_bnm_supported.restype = ctypes.c_int
+        lib.dvcp_sa_bnm_supported.argtypes = [ctypes.c_int] * 3
+        lib.dvcp_sa_bnm_workspace_bytes.restype = ctypes.c_int64
+        lib.dvcp_sa_bnm_workspace_bytes.argtypes = [ctypes.c_int] * 8
     for name, args in SIGNATURES.items():
+        if skip and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = ctypes.c_int
         fn.argtypes = args
@@ -145,7 +158,7 @@ def exported_symbols():
             "dvcp_cpg_backward_workspace_bytes", "dvcp_sa_group_mlp_backward_workspace_bytes",
             "dvcp_fe_head_backward_workspace_bytes", "dvcp_sa_bn_workspace_bytes",
             "dvcp_sa_bn_pack_floats", "dvcp_sa_bn_rows_floats", "dvcp_sa_bn_feat_workspace_bytes", "dvcp_sa_bn_zrows_floats",
-            "dvcp_cpg1d_nparams"] + list(SIGNATURES)
+            "dvcp_cpg1d_nparams", "dvcp_sa_bnm_supported", "dvcp_sa_bnm_workspace_bytes"] + list(SIGNATURES)
 
 
 # When a list, every entry-point call appends (name, start_event, end_event, work) recorded on

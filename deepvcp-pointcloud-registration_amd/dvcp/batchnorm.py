@@ -6,6 +6,11 @@ batch over all B * S * nsample grouped entries (BatchNorm2d over (B, H, W); the 
 the ball query are entries like any other) and updates the running statistics (momentum, unbiased
 variance), once per FE1 call -- src and tgt are separate calls (deepVCP.py:29,72).
 
+The two-layer tables (sa2, sa3; fp32) run on the matrix cores (csrc/sa_bn_mfma.hip,
+``_train_forward_mfma`` / ``_train_backward_mfma``): every pass recomputes the MLP per 32-entry
+tile, nothing per entry is stored, and the weight gradients are MFMA products over the entries.
+The rest (sa1 3-16-16-32, fp64 inputs) takes the lane-per-entry passes below.
+
 Forward (``train_forward``): one statistics pass per layer (dvcp_sa_bn_stats: fp64 sums of z and
 z^2, the layers below normalised by their batch statistics), then the eval kernel
 (dvcp_sa_group_mlp) with the batch statistics folded into its scale / shift.
@@ -51,6 +56,73 @@ def _update_running(bn, mean, var, M):
 ZROWS_KEEP_MAX_BYTES = 16 << 30
 
 
+def _bnm_pack(sa, dev):
+    offs, total = _layer_offsets(sa.chans)
+    parts = []
+    for conv, (o, cin, cout) in zip(sa.mlp_convs, offs):
+        one, zero = torch.ones(cout, device=dev), torch.zeros(cout, device=dev)
+        parts += [conv.weight.reshape(-1).float(), conv.bias.float(), one, zero, zero, one, zero, zero]
+    pack = torch.cat(parts).contiguous()
+    assert pack.numel() == total == ops.sa_bn_pack_floats(sa.chans)
+    return pack, offs
+
+
+def _set_stats(pack, bn, o, cin, cout, sums, M):
+    """Batch mean / variance of one layer from its sums; scale, shift, mean, istd into the pack and
+    the running-statistics update."""
+    mean = sums[0] / M
+    var = (sums[1] / M - mean * mean).clamp_min(0.0)
+    istd = torch.rsqrt(var + bn.eps)
+    scale = bn.weight.double() * istd
+    shift = bn.bias.double() - mean * scale
+    v = o + cout * cin + cout
+    pack[v:v + 4 * cout] = torch.cat([scale, shift, mean, istd]).float()
+    _update_running(bn, mean, var, M)
+
+
+def _train_forward_mfma(sa, xyz, ctr, feat, count, lst, ns):
+    """The two-layer tables on the matrix cores (csrc/sa_bn_mfma.hip): the per-point half of layer 1
+    once, one statistics pass per layer, then the forward with its arg-max routing.  Nothing per
+    entry is kept for the backward; it recomputes the MLP."""
+    chans = sa.chans
+    B, S = ctr.shape[0], ctr.shape[2]
+    M = B * S * ns
+    with torch.no_grad():
+        pack, offs = _bnm_pack(sa, xyz.device)
+        U = ops.sa_bnm_pre(feat, chans, pack)
+        for layer, (bn, (o, cin, cout)) in enumerate(zip(sa.mlp_bns, offs), 1):
+            sums = ops.sa_bnm_stats(xyz, ctr, feat, count, lst, ns, chans, pack, U, layer)
+            _set_stats(pack, bn, o, cin, cout, sums, M)
+        fwd = ops.sa_bnm_forward(xyz, ctr, feat, count, lst, ns, chans, pack, U)
+    return fwd[0], dict(pack=pack, M=M, U=U, fwd=fwd, mfma=True)
+
+
+def _train_backward_mfma(sa, lay, g_out, want_feat_grad):
+    chans = sa.chans
+    offs, _ = _layer_offsets(chans)
+    st = lay["bn"]
+    pack, M, U, fwd = st["pack"].clone(), st["M"], st["U"], st["fwd"]
+    args = (lay["pts"], lay["ctr"], lay["feat"], lay["count"], lay["lst"], lay["ns"], chans)
+    g = g_out.float().contiguous()
+    out, _, zb = fwd
+    (o1, c0, c1), (o2, _, c2) = offs
+    # layer 2's sums over the routed rows (gy2 = g at each (centre, channel)'s arg-max when the max
+    # is positive): A2 = sum gy2, B2 = sum gy2 xhat2
+    v2 = o2 + c2 * c1
+    mu2, is2 = pack[v2 + 3 * c2:v2 + 4 * c2], pack[v2 + 4 * c2:v2 + 5 * c2]
+    gy = torch.where(out > 0, g, torch.zeros_like(g)).double()
+    xh = ((zb - mu2) * is2).double()
+    s2 = torch.stack([gy.sum((0, 1)), (gy * xh).sum((0, 1))])
+    pack[v2 + 5 * c2:v2 + 7 * c2] = (s2 / M).reshape(-1).float()
+    s1 = ops.sa_bnm_backward(*args, pack, U, fwd, g, 1)
+    v1 = o1 + c1 * c0
+    pack[v1 + 5 * c1:v1 + 7 * c1] = (s1 / M).reshape(-1).float()
+    grads, gF = ops.sa_bnm_backward(*args, pack, U, fwd, g, 0, want_feat_grad=want_feat_grad)
+    n1 = c1 * c0 + c1
+    parts = [grads[:n1], s1[1], s1[0], grads[n1:], s2[1], s2[0]]   # per layer dW, db, dgamma, dbeta
+    return torch.cat([p.float() for p in parts]), gF
+
+
 def train_forward(sa, xyz, ctr, feat, count, lst, ns, keep_zrows=False):
     """pointnet2_utils.py:195-200 with ``sa`` in training mode, on (B, 3, N) points, (B, 3, S)
     centres and (B, D, N) features.  Returns (out (B, S, C_last) fp32, state for the backward).
@@ -58,17 +130,13 @@ def train_forward(sa, xyz, ctr, feat, count, lst, ns, keep_zrows=False):
     writes every entry's z rows for it (within ZROWS_KEEP_MAX_BYTES); a train-mode forward with no
     backward (no_grad, frozen extractor) allocates none."""
     chans = sa.chans
-    offs, total = _layer_offsets(chans)
+    if ops.sa_bnm_usable(xyz, ctr, feat, chans):
+        return _train_forward_mfma(sa, xyz, ctr, feat, count, lst, ns)
     dev = xyz.device
     B, S = ctr.shape[0], ctr.shape[2]
     M = B * S * ns
-    parts = []
     with torch.no_grad():
-        for conv, (o, cin, cout) in zip(sa.mlp_convs, offs):
-            one, zero = torch.ones(cout, device=dev), torch.zeros(cout, device=dev)
-            parts += [conv.weight.reshape(-1).float(), conv.bias.float(), one, zero, zero, one, zero, zero]
-        pack = torch.cat(parts).contiguous()
-        assert pack.numel() == total == ops.sa_bn_pack_floats(chans)
+        pack, offs = _bnm_pack(sa, dev)
         zrows = None
         keep = keep_zrows and ops.sa_bn_zrows_bytes(B, S, ns, chans) <= ZROWS_KEEP_MAX_BYTES
         for layer, (bn, (o, cin, cout)) in enumerate(zip(sa.mlp_bns, offs), 1):
@@ -76,14 +144,7 @@ def train_forward(sa, xyz, ctr, feat, count, lst, ns, keep_zrows=False):
                 sums, zrows = ops.sa_bn_stats(xyz, ctr, feat, count, lst, ns, chans, pack, layer, want_zrows=True)
             else:
                 sums = ops.sa_bn_stats(xyz, ctr, feat, count, lst, ns, chans, pack, layer)
-            mean = sums[0] / M
-            var = (sums[1] / M - mean * mean).clamp_min(0.0)
-            istd = torch.rsqrt(var + bn.eps)
-            scale = bn.weight.double() * istd
-            shift = bn.bias.double() - mean * scale
-            v = o + cout * cin + cout
-            pack[v:v + 4 * cout] = torch.cat([scale, shift, mean, istd]).float()
-            _update_running(bn, mean, var, M)
+            _set_stats(pack, bn, o, cin, cout, sums, M)
         fwd = torch.cat([pack[o:o + cout * cin + 3 * cout] for o, cin, cout in offs]).contiguous()
     out = ops.sa_group_mlp(xyz, ctr, feat, count, lst, ns, chans, fwd)
     return out, dict(pack=pack, M=M, zrows=zrows)
@@ -92,6 +153,8 @@ def train_forward(sa, xyz, ctr, feat, count, lst, ns, keep_zrows=False):
 def train_backward(sa, lay, g_out, want_feat_grad):
     """Backward of ``train_forward``: (packed parameter gradient -- per layer dW, db, dgamma,
     dbeta -- and dL/d feat (B, N, D) fp32 or None)."""
+    if lay["bn"].get("mfma"):
+        return _train_backward_mfma(sa, lay, g_out, want_feat_grad)
     chans = sa.chans
     offs, _ = _layer_offsets(chans)
     st = lay["bn"]

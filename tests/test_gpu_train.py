@@ -292,18 +292,22 @@ def test_sa_backward_vs_oracle(cuda, table):
           "relative gradient errors:", {k: f"{v:.1e}" for k, v in errs.items()})
 
 
-@pytest.mark.parametrize("table", ["sa1", "sa1_normals", "sa1_normals_f64", "sa2", "sa3"])
+@pytest.mark.parametrize("table", ["sa1", "sa1_normals", "sa1_normals_f64", "sa2", "sa3", "sa2_rows", "sa3_rows"])
 def test_sa_batch_stats_train_vs_oracle(cuda, table):
     """pointnet2_utils.py:176-202 with the module in training mode (batch-statistics BatchNorm, as
     train.py's model.train()): the forward output, the running-statistics update and every conv /
     BN parameter gradient and the grouped-feature gradient against torch autograd through the
     oracle's PointNetSetAbstraction in train mode (fp32 like the reference).  (centre, channel)
     pairs whose two best rows tie within 1e-5 (fp64, batch statistics) get a zero output gradient
-    on both sides; the batch-norm mean terms still reach every entry."""
+    on both sides; the batch-norm mean terms still reach every entry.  ``*_rows``: the same case
+    with point-major feature rows (as the extractor passes them), which the two-layer tables run
+    on the matrix cores (csrc/sa_bn_mfma.hip) -- channel-first features take the VALU passes."""
     import oracle as O
     import dvcp
     from dvcp import batchnorm, ops
     from tests_helpers import randomize_bn
+    rows = table.endswith("_rows")
+    table = table.replace("_rows", "")
     g = torch.Generator().manual_seed(["sa1", "sa1_normals", "sa1_normals_f64", "sa2", "sa3"].index(table) + 400)
     cin, mlp, radius, ns, xyz, feat = _sa_case(table, g)
     B, _, N = xyz.shape
@@ -326,10 +330,13 @@ def test_sa_batch_stats_train_vs_oracle(cuda, table):
     (out_o * G).sum().backward()
 
     x, f = xyz.to(cuda), (None if feat is None else feat.to(cuda))
+    if rows:
+        f = feat.permute(0, 2, 1).contiguous().to(cuda).permute(0, 2, 1)
     ns_ = min(ns, N)
     _, ctr = ops.fps(x, S, start.to(cuda), pdim=2)
     count, lst, _ = ops.ball_query(x, ctr, radius, ns_, pdim=2, cdim_pts=2)
     out, st = batchnorm.train_forward(mine, x, ctr, f, count, lst, ns_)
+    assert bool(st.get("mfma")) == rows
     torch.testing.assert_close(out.permute(0, 2, 1).cpu(), out_o.detach(), rtol=1e-4, atol=1e-4)
     for i, (bm, br) in enumerate(zip(mine.mlp_bns, ref.mlp_bns)):
         torch.testing.assert_close(bm.running_mean.cpu(), br.running_mean, rtol=1e-4, atol=1e-6)
@@ -712,5 +719,7 @@ def test_train_mode_forward_without_backward_keeps_no_zrows(cuda, monkeypatch):
     assert asked and not any(asked)
     asked.clear()
     _, feat = fe(src.to(cuda))
-    assert sum(asked) == 3          # one z-row pass per set-abstraction layer
+    # sa1's z-row pass; sa2 / sa3 run on the matrix cores (csrc/sa_bn_mfma.hip), which recompute
+    # the MLP in the backward and keep nothing per entry
+    assert sum(asked) == 1
     feat.sum().backward()

@@ -13,9 +13,10 @@ for i in 1 2; do
   for v in $vs; do
     if [ $v = B ]; then cp /tmp/libdvcp_hip_B.so $L/libdvcp_hip.so; else cp $L/libdvcp_hip_$v.so $L/libdvcp_hip.so; fi
     echo "== $v run $i" >> gpurun_out/${tag}.log
-    timeout -k 10 200 python tools/knn_bench.py --fast >> gpurun_out/${tag}.log 2>&1 || exit $?
+    DVCP_SKIP_ABI=1 timeout -k 10 200 python tools/knn_bench.py --fast >> gpurun_out/${tag}.log 2>&1 || exit $?
   done
 done
 cp /tmp/libdvcp_hip_B.so $L/libdvcp_hip.so
+[ "$kexpr" = none ] && exit 0
 timeout -k 10 400 python -u -m pytest tests -m gpu -k "$kexpr" -q --timeout 300 --timeout-method thread -rfs \
   > gpurun_out/${tag}_pytest.log 2>&1
