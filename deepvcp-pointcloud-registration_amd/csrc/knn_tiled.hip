@@ -535,10 +535,10 @@ constexpr int kSelBufN = 16;
 // skipped tile under DVCP_KNN_DIAG; round 3).
 // DVCP_KNN_CHUNK (default): the sorted order is scanned 64 positions at a time behind a
 // tile-parallel prefilter against lane-group boxes (see the scan below).
-// DVCP_KNN_CHUNK == 2 (default): 64 positions at a time behind an exact tile-parallel per-lane
-// test; 1: behind a lane-group box prefilter; 0: one sorted position at a time.
+// (Round 4 measured an exact per-lane bulk test over each 64-position chunk -- every lane's tile
+// box against all 64 queries of the wave -- 0.92 against 0.75 ms per C3 batch: not kept.)
 #ifndef DVCP_KNN_CHUNK
-#define DVCP_KNN_CHUNK 2
+#define DVCP_KNN_CHUNK 1
 #endif
 // DVCP_KNN_SLOAD: an active tile's 16 points reach the wave as scalar loads (the tile index is
 // wave-uniform, the tile is read-only here) instead of one vector load and 48 readlanes; the
@@ -598,7 +598,6 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
   __shared__ uint3 hbox[kMaxTiles];
   __shared__ double sbuf[kTiledThreads / kWave][kSelBufN][kWave];  // lane-private candidate buffers (packed keys)
   __shared__ float4 stile[kTiledThreads / kWave][kTile];            // the wave's current tile (appends)
-  __shared__ float4 sqry[kTiledThreads / kWave][kWave];               // the wave's queries and k-th distances
   {
     const float4* tbg = tbox + static_cast<int64_t>(b) * T * 2;
     for (int i = threadIdx.x; i < T; i += kTiledThreads) hbox[i] = pack_hbox(tbg[2 * i], tbg[2 * i + 1]);
@@ -654,8 +653,6 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
   float wkth = wave_max_nonneg(kth);
   int fill = 0;
   double(*mybuf)[kWave] = sbuf[wave];
-  sqry[wave][lane] = make_float4(qx, qy, qz, live ? kth : -1.0f);
-  __builtin_amdgcn_wave_barrier();
 #ifdef DVCP_KNN_DIAG  // per-wave counters (diagnostic builds only; written over lane 0's distances)
   uint64_t dg_t0 = __builtin_readcyclecounter(), dg_merge_clk = 0, dg_skip_clk = 0, dg_prev = 0;
   int dg_kind = -1;  // the previous iteration: 0 skipped, 1 processed
@@ -707,7 +704,6 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
     }
     kth = live ? key_d2(kk_) : 0.0f;
     wkth = wave_max_nonneg(kth);
-    sqry[wave][lane].w = live ? kth : -1.0f;
     fill = 0;
 #ifdef DVCP_KNN_DIAG
     dg_merge_clk += __builtin_readcyclecounter() - dg_m0;
@@ -804,91 +800,7 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
     }
   };
 
-  // Visit a tile some lane needs (found by the bulk test below): the tile reaches the wave as one
-  // coalesced 256-byte load (one float per lane) copied to LDS, and each lane reads its 16 points
-  // back as broadcasts; then the distances, the filter and the appends.  No per-lane box test: a
-  // lane whose bound exceeds its k-th distance has every d2 above it, and the filter drops them.
-  auto visit2 = [&](uint32_t key) {
-    const int t = static_cast<int>(key & kTileIdBits);
-#ifdef DVCP_KNN_DIAG
-    ++dg_scanned;
-    ++dg_active;
-    dg_kind = 1;
-#endif
-    reinterpret_cast<float*>(stile[wave])[lane] = P[static_cast<int64_t>(t) * (4 * kTile) + lane];
-    __builtin_amdgcn_wave_barrier();
-    auto d2_of = [&](int j) {
-      const float4 pt = stile[wave][j];
-      const float dx = pt.x - qx, dy = pt.y - qy, dz = pt.z - qz;
-      return (dx * dx + dy * dy) + dz * dz;
-    };
-    uint32_t cm = 0;
-    const float kf = fminf(kth, __builtin_bit_cast(float, 0x7F7FFFFFu));
-#pragma unroll
-    for (int j = 0; j < kTile; ++j) cm |= (live && d2_of(j) <= kf) ? (1u << j) : 0u;
-    if (wave_umax_i(static_cast<uint32_t>(fill + __popc(cm))) > static_cast<uint32_t>(kSelBufN)) {
-      merge();  // room for the whole tile; then re-filter against the new k-th key
-      const float kf2 = fminf(kth, __builtin_bit_cast(float, 0x7F7FFFFFu));
-#pragma unroll
-      for (int j = 0; j < kTile; ++j) cm &= d2_of(j) <= kf2 ? ~0u : ~(1u << j);
-    }
-    uint32_t my = cm;
-    while (__ballot(my != 0) != 0) {
-      if (my != 0) {
-        const int j = __builtin_ctz(my);
-        my &= my - 1;
-#ifdef DVCP_KNN_DIAG
-        ++dg_appends;
-#endif
-        const float4 pt = stile[wave][j];
-        const float dx = pt.x - qx, dy = pt.y - qy, dz = pt.z - qz;
-        mybuf[fill][lane] = key_pack((dx * dx + dy * dy) + dz * dz, __float_as_uint(pt.w));
-        ++fill;
-      }
-    }
-    __builtin_amdgcn_wave_barrier();  // (the next tile rewrites stile)
-  };
-
-#if DVCP_KNN_CHUNK == 2
-  // Chunked scan with an exact bulk test.  The sorted order is taken 64 positions at a time, one
-  // position per lane; lane i tests its tile's box against every query of the wave (point-box bound
-  // against that query's k-th distance, the queries read back from LDS as broadcasts), so one pass
-  // of 64 x ~12 VALU finds the tiles some lane needs, instead of a per-lane test and a ballot per
-  // sorted position (~185 positions pass the wave's bound at C3, ~32 are needed).  k-th distances
-  // are those at chunk start: merges only lower them, so a stale one keeps a superset; the stop
-  // rule is re-checked at every needed position.
-  (void)visit;
-  bool stop = false;
-#pragma unroll 1
-  for (int base = 0; base < T && !stop; base += kWave) {
-    const uint32_t mykey = keys[base >> 6];  // lane i: sorted position base + i
-    const bool inr = base + lane < T;
-    const uint64_t over = __ballot(!inr || __uint_as_float(mykey & ~kTileIdBits) > wkth);
-    const int lim = over ? __builtin_ctzll(over) : kWave;  // positions past lim are never needed
-    const int tt = inr ? static_cast<int>(mykey & kTileIdBits) : 0;
-    const uint3 hb = hbox[tt < T ? tt : 0];
-    const float blx = half_lo(hb.x), bly = half_hi(hb.x), blz = half_lo(hb.y);
-    const float bhx = half_hi(hb.y), bhy = half_lo(hb.z), bhz = half_hi(hb.z);
-    bool pass = false;
-#pragma unroll 8
-    for (int l = 0; l < kWave; ++l) {
-      const float4 qq = sqry[wave][l];  // (x, y, z, k-th distance; -1 for a dead lane)
-      pass |= box_box_lb2(qq.x, qq.y, qq.z, qq.x, qq.y, qq.z, blx, bly, blz, bhx, bhy, bhz) <= qq.w;
-    }
-    uint64_t cand = __ballot(pass && inr) & (lim >= kWave ? ~0ull : ((1ull << lim) - 1ull));
-    if (lim < kWave) stop = true;
-    while (cand) {
-      const int i = __builtin_ctzll(cand);
-      cand &= cand - 1ull;
-      const uint32_t key = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(mykey), i));
-      if (__uint_as_float(key & ~kTileIdBits) > wkth) {  // every later tile is farther
-        stop = true;
-        break;
-      }
-      visit2(key);
-    }
-  }
-#elif DVCP_KNN_CHUNK
+#if DVCP_KNN_CHUNK
   // Chunked scan.  The sorted order is taken 64 positions at a time, one position per lane, and a
   // tile-parallel prefilter drops the positions no query can need: lane i tests its tile's box
   // against the boxes of the wave's kKnnSub lane groups (16 Hilbert-consecutive queries each) with
