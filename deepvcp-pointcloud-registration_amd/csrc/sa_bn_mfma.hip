@@ -53,7 +53,7 @@ constexpr int kBnmWaves = 4;
 constexpr int kBnmThreads = kBnmWaves * kWave;
 constexpr int kBnmMaxGrid = 1024;
 
-enum : int { kS1 = 1, kS2 = 2, kFwd = 3, kB1 = 4, kB0A = 5, kB0B = 6 };
+enum : int { kS1 = 1, kS2 = 2, kS3 = 8, kFwd = 3, kB1 = 4, kB0A = 5, kB0B = 6 };
 
 // x = p0 + p1 + p2 exactly (bf16 pieces of eight fp32 values)
 struct Pieces {
@@ -112,8 +112,8 @@ struct BnmArgs {
   const float* ctr;
   int64_t cb, cc, cn;
   int S, B, N, nsample;
-  const float* feat;  // (B, N, D): feat[b fb + n fn + d]
-  int64_t fb, fn;
+  const float* feat;  // feat[b fb + d fd + n fn] (the two-layer tables: fd = 1, 16-byte aligned rows)
+  int64_t fb, fd, fn;
   const int32_t* count;
   const int32_t* list;
   const float* pack;  // per layer W | bias | scale | shift | mean | istd | A/M | B/M
@@ -587,6 +587,436 @@ __global__ __launch_bounds__(kBnmThreads) __attribute__((amdgpu_waves_per_eu(PAS
   }
 }
 
+// ---- sa1: 3 [+3 normals] - 16 - 16 - 32 --------------------------------------------------------
+// The same scheme for the three-layer table.  The 16-channel layers fill half of a 32-row tile (the
+// other rows have zero weights and constants, so they stay zero), and a product over 16 channels
+// is one 16-deep k-step: in T register order k-step 0 (registers 0..7) holds channels 0..15 in
+// both lane halves.  Layer 1 (k = 3 or 6) is fp32 MFMA k-steps from the bias; there is no
+// per-point table.  Passes: S1..S3, FWD, B2 = A2, B2 (needs A3, B3 from the host), B1 = A1, B1,
+// B0 = every weight gradient (dW3 = gz3^T h2, dW2 = gz2^T h1 on the matrix cores, dW1 on VALU).
+// No feature gradient: the layer's input features are the data (normals) or absent.
+struct Bnm3Lds {
+  float wx[4][64];       // W1: k-steps (x | y), (z | 0), (nx | ny), (nz | 0); lane = c1 row
+  bf16x8 w2[3][64];      // W2: lane = c2 row, k = c1 (T order)
+  bf16x8 w2t[3][64];     // W2^T: lane = c1 row, k = c2
+  bf16x8 w3[3][64];      // W3: lane = c3 row, k = c2
+  bf16x8 w3t[2][3][64];  // W3^T: lane = c2 row, k = c3 (two k-steps)
+  float b1T[2][16], s1T[2][16], t1T[2][16];
+  float b2T[2][16], s2T[2][16], t2T[2][16];
+  float4 q2T[2][16];     // {s2, k2, mu2, ka2}
+  float b3T[2][16];
+  float4 q3T[2][16];     // {s3, k3, mu3, ka3}
+  int2 route[kBnmWaves][32];
+  float4 dtab[kBnmWaves][32];  // the tile's entries: (dx, dy, dz, -)
+  float4 ntab[kBnmWaves][32];  // the tile's entries: normals
+};
+
+// One layer's per-channel constants for channel c (zero beyond C): bias, BN scale / shift, mean,
+// istd, and the backward's k = -s b istd, ka = s a (a = A/M, b = B/M).
+struct BnmLayerC {
+  float b, s, t, mu, is, k, ka;
+};
+__device__ __forceinline__ BnmLayerC bnm_layer_c(const float* v, int C, int c) {
+  BnmLayerC q{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    q.b = v[c];
+    q.s = v[C + c];
+    q.t = v[2 * C + c];
+    q.mu = v[3 * C + c];
+    q.is = v[4 * C + c];
+    q.k = static_cast<float>(-(static_cast<double>(q.s) * v[6 * C + c] * q.is));
+    q.ka = static_cast<float>(static_cast<double>(q.s) * v[5 * C + c]);
+  }
+  return q;
+}
+
+enum : int { kB2 = 7 };  // three-layer backward sums of layer 2
+
+template <int D, int PASS>
+__global__ __launch_bounds__(kBnmThreads) __attribute__((amdgpu_waves_per_eu(PASS == kB0A ? 1 : 2))) void sa_bnm3_kernel(
+    BnmArgs a) {
+  constexpr int C0 = 3 + D, C1 = 16, C2 = 16, C3 = 32;
+  constexpr bool kRoute = PASS == kB2 || PASS == kB1 || PASS == kB0A;  // kB0A: every weight gradient
+  __shared__ Bnm3Lds L;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
+  const float* W1 = a.pack;
+  const float* v1 = W1 + C1 * C0;
+  const float* W2 = v1 + 7 * C1;
+  const float* v2 = W2 + C2 * C1;
+  const float* W3 = v2 + 7 * C2;
+  const float* v3 = W3 + C3 * C2;
+  for (int i = tid; i < 4 * 64; i += kBnmThreads) {
+    const int l = i % 64, st = i / 64, c1 = l & 31, hh = l >> 5;
+    int ch = st == 0 ? hh : (st == 1 ? (hh == 0 ? 2 : -1) : (st == 2 ? 3 + hh : (hh == 0 ? 5 : -1)));
+    if (ch >= C0) ch = -1;
+    L.wx[st][l] = (ch < 0 || c1 >= C1) ? 0.0f : W1[c1 * C0 + ch];
+  }
+  for (int l = tid; l < 64; l += kBnmThreads) {
+    const int row = l & 31, hh = l >> 5;
+    float w[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = row < C2 ? W2[row * C1 + arow(j, hh)] : 0.0f;
+    Pieces p = bnm_split(w);
+    L.w2[0][l] = p.p0, L.w2[1][l] = p.p1, L.w2[2][l] = p.p2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = row < C1 ? W2[arow(j, hh) * C1 + row] : 0.0f;
+    p = bnm_split(w);
+    L.w2t[0][l] = p.p0, L.w2t[1][l] = p.p1, L.w2t[2][l] = p.p2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = W3[row * C2 + arow(j, hh)];
+    p = bnm_split(w);
+    L.w3[0][l] = p.p0, L.w3[1][l] = p.p1, L.w3[2][l] = p.p2;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w[j] = row < C2 ? W3[arow(8 * k + j, hh) * C2 + row] : 0.0f;
+      p = bnm_split(w);
+      L.w3t[k][0][l] = p.p0, L.w3t[k][1][l] = p.p1, L.w3t[k][2][l] = p.p2;
+    }
+  }
+  for (int i = tid; i < 32; i += kBnmThreads) {
+    const int r = i % 16, hh = i / 16, c = arow(r, hh);
+    const BnmLayerC q1 = bnm_layer_c(v1, C1, c), q2 = bnm_layer_c(v2, C2, c), q3 = bnm_layer_c(v3, C3, c);
+    L.b1T[hh][r] = q1.b, L.s1T[hh][r] = q1.s, L.t1T[hh][r] = q1.t;
+    L.b2T[hh][r] = q2.b, L.s2T[hh][r] = q2.s, L.t2T[hh][r] = q2.t;
+    L.q2T[hh][r] = make_float4(q2.s, q2.k, q2.mu, q2.ka);
+    L.b3T[hh][r] = q3.b;
+    L.q3T[hh][r] = make_float4(q3.s, q3.k, q3.mu, q3.ka);
+  }
+  const BnmLayerC n1 = bnm_layer_c(v1, C1, r32), n2 = bnm_layer_c(v2, C2, r32), n3 = bnm_layer_c(v3, C3, r32);
+  __syncthreads();
+
+  constexpr int CS = PASS == kS3 ? C3 : 16;
+  double st1 = 0.0, st2 = 0.0;
+  f32x16 dw3, dw2;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dw3[r] = dw2[r] = 0.0f;
+  float db2 = 0.0f, db3 = 0.0f, dw1[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) dw1[k] = 0.0f;
+
+  const int ns = a.nsample;
+  const int64_t total = static_cast<int64_t>(a.B) * a.S;
+  for (int64_t fc = static_cast<int64_t>(blockIdx.x) * kBnmWaves + wave; fc < total;
+       fc += static_cast<int64_t>(gridDim.x) * kBnmWaves) {
+    const int b = static_cast<int>(fc / a.S), s = static_cast<int>(fc - static_cast<int64_t>(b) * a.S);
+    int rows = a.count[fc];
+    rows = rows < 1 ? 1 : (rows > ns ? ns : rows);
+    const int ghost = rows < ns ? 1 : 0;
+    const float gw = static_cast<float>(ns - rows);
+    const float cx = a.ctr[b * a.cb + s * a.cn], cy = a.ctr[b * a.cb + a.cc + s * a.cn],
+                cz = a.ctr[b * a.cb + 2 * a.cc + s * a.cn];
+    const int32_t* lst = a.list + fc * ns;
+    int argN = 0;
+    float gN = 0.0f;
+    if constexpr (kRoute) {
+      const int64_t o = fc * C3 + r32;
+      argN = a.arg[o];
+      gN = a.out[o] > 0.0f ? a.gout[o] : 0.0f;
+      if (h == 0) L.route[wave][r32] = make_int2(argN, __float_as_int(gN));
+    }
+    float best = -1.0f, bz = 0.0f;
+    int barg = 0;
+    const int ntiles = (rows + ghost + 31) / 32;
+    for (int t = 0; t < ntiles; ++t) {
+      __builtin_amdgcn_wave_barrier();
+      int zo = 0;
+      asm volatile("" : "+v"(zo));
+      const int n0 = 32 * t;
+      const int p = n0 + r32;
+      const int n = lst[p < rows ? p : 0];
+      const float dx = a.xyz[b * a.sb + n * a.sn] - cx;
+      const float dy = a.xyz[b * a.sb + a.sc + n * a.sn] - cy;
+      const float dz = a.xyz[b * a.sb + 2 * a.sc + n * a.sn] - cz;
+      float nx = 0.0f, ny = 0.0f, nz = 0.0f;
+      if constexpr (D == 3) {
+        const float* fr = a.feat + b * a.fb + static_cast<int64_t>(n) * a.fn;
+        nx = fr[0];
+        ny = fr[a.fd];
+        nz = fr[2 * a.fd];
+      }
+      const float x0 = h == 0 ? dx : dy, x1 = h == 0 ? dz : 0.0f;
+      const float x2 = h == 0 ? nx : ny, x3 = h == 0 ? nz : 0.0f;
+      if (h == 0) {
+        L.dtab[wave][r32] = make_float4(dx, dy, dz, 0.0f);
+        L.ntab[wave][r32] = make_float4(nx, ny, nz, 0.0f);
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      auto wt = [&](int r) {
+        const int pa = n0 + arow(r, h);
+        return pa < rows ? 1.0f : ((ghost && pa == rows) ? gw : 0.0f);
+      };
+      auto frag = [&](const bf16x8(&f)[3][64]) { return Pieces{f[0][lane + zo], f[1][lane + zo], f[2][lane + zo]}; };
+      auto piece = [&](const f32x16& v, int k) {
+        float x[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = v[8 * k + j];
+        return bnm_split(x);
+      };
+      auto z1_t = [&]() {
+        f32x16 z;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) z[r] = L.b1T[h][r + zo];
+        z = __builtin_amdgcn_mfma_f32_32x32x2f32(L.wx[0][lane + zo], x0, z, 0, 0, 0);
+        z = __builtin_amdgcn_mfma_f32_32x32x2f32(L.wx[1][lane + zo], x1, z, 0, 0, 0);
+        if constexpr (D == 3) {
+          z = __builtin_amdgcn_mfma_f32_32x32x2f32(L.wx[2][lane + zo], x2, z, 0, 0, 0);
+          z = __builtin_amdgcn_mfma_f32_32x32x2f32(L.wx[3][lane + zo], x3, z, 0, 0, 0);
+        }
+        return z;
+      };
+      auto z1_n = [&]() {
+        f32x16 z;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) z[r] = n1.b;
+        z = __builtin_amdgcn_mfma_f32_32x32x2f32(x0, L.wx[0][lane + zo], z, 0, 0, 0);
+        z = __builtin_amdgcn_mfma_f32_32x32x2f32(x1, L.wx[1][lane + zo], z, 0, 0, 0);
+        if constexpr (D == 3) {
+          z = __builtin_amdgcn_mfma_f32_32x32x2f32(x2, L.wx[2][lane + zo], z, 0, 0, 0);
+          z = __builtin_amdgcn_mfma_f32_32x32x2f32(x3, L.wx[3][lane + zo], z, 0, 0, 0);
+        }
+        return z;
+      };
+      auto sums = [&](const f32x16& z) {
+        float a1 = 0.0f, a2 = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float w = wt(r);
+          a1 += w * z[r];
+          a2 += w * (z[r] * z[r]);
+        }
+        st1 += a1;
+        st2 += a2;
+      };
+      if constexpr (PASS == kS1) {
+        sums(z1_n());
+        continue;
+      }
+      // h1 (T)
+      f32x16 h1T = z1_t();
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float y = h1T[r] * L.s1T[h][r + zo] + L.t1T[h][r + zo];
+        h1T[r] = y > 0.0f ? y : 0.0f;
+      }
+      const Pieces ph1 = piece(h1T, 0);
+      auto z2_n = [&]() {
+        f32x16 z;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) z[r] = n2.b;
+        return bnm_mfma6(ph1, frag(L.w2), z);
+      };
+      if constexpr (PASS == kS2) {
+        sums(z2_n());
+        continue;
+      }
+      f32x16 z2T;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) z2T[r] = L.b2T[h][r + zo];
+      z2T = bnm_mfma6(frag(L.w2), ph1, z2T);
+      f32x16 z2N;
+      if constexpr (PASS == kB2 || PASS == kB0A) z2N = z2_n();
+      f32x16 h2T;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float y = z2T[r] * L.s2T[h][r + zo] + L.t2T[h][r + zo];
+        h2T[r] = y > 0.0f ? y : 0.0f;
+      }
+      const Pieces ph2 = piece(h2T, 0);
+      if constexpr (PASS == kS3 || PASS == kFwd) {
+        f32x16 z3N;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) z3N[r] = n3.b;
+        z3N = bnm_mfma6(ph2, frag(L.w3), z3N);
+        if constexpr (PASS == kS3) {
+          sums(z3N);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int pa = n0 + arow(r, h);
+            const float y = z3N[r] * n3.s + n3.t;
+            const float hv = y > 0.0f ? y : 0.0f;
+            if (pa < rows && hv > best) {
+              best = hv;
+              barg = pa;
+              bz = z3N[r];
+            }
+          }
+        }
+        continue;
+      }
+      // ---- backward chain: gz3 (T) -> gh2 ----------------------------------------------------------
+      f32x16 g3T;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) g3T[r] = L.b3T[h][r + zo];
+      g3T = bnm_mfma6(frag(L.w3), ph2, g3T);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int2 rt = L.route[wave][arow(r, h) + zo];
+        const float4 q = L.q3T[h][r + zo];
+        const float gy = p == rt.x ? __int_as_float(rt.y) : 0.0f;
+        g3T[r] = (q.x * gy + q.y * (g3T[r] - q.z)) - q.w;  // gz3 (unweighted)
+      }
+      const Pieces pg0 = piece(g3T, 0), pg1 = piece(g3T, 1);
+      if constexpr (PASS == kB2) {
+        f32x16 gh2N;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) gh2N[r] = 0.0f;
+        gh2N = bnm_mfma6(pg0, frag(L.w3t[0]), gh2N);
+        gh2N = bnm_mfma6(pg1, frag(L.w3t[1]), gh2N);
+        float a1 = 0.0f, a2 = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float z = z2N[r], w = wt(r);
+          const float gy = z * n2.s + n2.t > 0.0f ? gh2N[r] : 0.0f;
+          a1 += w * gy;
+          a2 += w * (gy * ((z - n2.mu) * n2.is));
+        }
+        st1 += a1;
+        st2 += a2;
+        continue;
+      }
+      // gh2 (T) -> gz2 (T) -> gh1 (N)
+      f32x16 gz2T;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gz2T[r] = 0.0f;
+      gz2T = bnm_mfma6(frag(L.w3t[0]), pg0, gz2T);
+      gz2T = bnm_mfma6(frag(L.w3t[1]), pg1, gz2T);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float4 q = L.q2T[h][r + zo];
+        const float z = z2T[r];
+        const float gy = z * L.s2T[h][r + zo] + L.t2T[h][r + zo] > 0.0f ? gz2T[r] : 0.0f;
+        gz2T[r] = (q.x * gy + q.y * (z - q.z)) - q.w;
+      }
+      f32x16 gh1N;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gh1N[r] = 0.0f;
+      gh1N = bnm_mfma6(piece(gz2T, 0), frag(L.w2t), gh1N);
+      const f32x16 z1N = z1_n();
+      if constexpr (PASS == kB1) {
+        float a1 = 0.0f, a2 = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float z = z1N[r], w = wt(r);
+          const float gy = z * n1.s + n1.t > 0.0f ? gh1N[r] : 0.0f;
+          a1 += w * gy;
+          a2 += w * (gy * ((z - n1.mu) * n1.is));
+        }
+        st1 += a1;
+        st2 += a2;
+        continue;
+      }
+      // ---- every weight gradient (N layouts) -------------------------------------------------------
+      // dW3 += gz3^T h2
+      f32x16 g3N;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) g3N[r] = n3.b;
+      g3N = bnm_mfma6(ph2, frag(L.w3), g3N);
+      f32x16 h2N;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int pa = n0 + arow(r, h);
+        const float gy = pa == argN ? gN : 0.0f;
+        g3N[r] = wt(r) * ((n3.s * gy + n3.k * (g3N[r] - n3.mu)) - n3.ka);
+        db3 += g3N[r];
+        const float y = z2N[r] * n2.s + n2.t;
+        h2N[r] = y > 0.0f ? y : 0.0f;
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) dw3 = bnm_mfma6(piece(g3N, k), piece(h2N, k), dw3);
+      // dW2 += gz2^T h1 (gh2 in N layout)
+      f32x16 g2N;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) g2N[r] = 0.0f;
+      g2N = bnm_mfma6(pg0, frag(L.w3t[0]), g2N);
+      g2N = bnm_mfma6(pg1, frag(L.w3t[1]), g2N);
+      f32x16 h1N;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float z = z2N[r];
+        const float gy = z * n2.s + n2.t > 0.0f ? g2N[r] : 0.0f;
+        g2N[r] = wt(r) * ((n2.s * gy + n2.k * (z - n2.mu)) - n2.ka);
+        db2 += g2N[r];
+        const float y = z1N[r] * n1.s + n1.t;
+        h1N[r] = y > 0.0f ? y : 0.0f;
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) dw2 = bnm_mfma6(piece(g2N, k), piece(h1N, k), dw2);
+      // dW1, db1 (VALU; lane = c1)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float z = z1N[r];
+        const float gy = z * n1.s + n1.t > 0.0f ? gh1N[r] : 0.0f;
+        const float gz = wt(r) * ((n1.s * gy + n1.k * (z - n1.mu)) - n1.ka);
+        const float4 dq = L.dtab[wave][arow(r, h)];
+        dw1[0] += gz * dq.x;
+        dw1[1] += gz * dq.y;
+        dw1[2] += gz * dq.z;
+        if constexpr (D == 3) {
+          const float4 nq = L.ntab[wave][arow(r, h)];
+          dw1[3] += gz * nq.x;
+          dw1[4] += gz * nq.y;
+          dw1[5] += gz * nq.z;
+        }
+        dw1[6] += gz;
+      }
+    }
+    if constexpr (PASS == kFwd) {
+      const float ob = __shfl_xor(best, 32, kWave), oz = __shfl_xor(bz, 32, kWave);
+      const int oa = __shfl_xor(barg, 32, kWave);
+      if (ob > best || (ob == best && oa < barg)) {
+        best = ob;
+        barg = oa;
+        bz = oz;
+      }
+      if (h == 0) {
+        const int64_t o = fc * C3 + r32;
+        a.out[o] = best;
+        a.arg[o] = barg;
+        a.zbest[o] = bz;
+      }
+    }
+    if constexpr (kRoute) {
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+
+  const int64_t wg = static_cast<int64_t>(blockIdx.x) * kBnmWaves + wave;
+  if constexpr (PASS == kS1 || PASS == kS2 || PASS == kS3 || PASS == kB1 || PASS == kB2) {
+    double* o = static_cast<double*>(a.part) + (wg * 2 + h) * (2 * CS);
+    if (r32 < CS) {
+      o[r32] = st1;
+      o[CS + r32] = st2;
+    }
+  } else if constexpr (PASS == kB0A) {
+    constexpr int P1 = C1 * C0 + C1, P2 = C2 * C1 + C2, P3 = C3 * C2 + C3;
+    float* o = static_cast<float*>(a.part) + wg * (P1 + P2 + P3);
+    float d[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) d[k] = dw1[k] + __shfl_xor(dw1[k], 32, kWave);
+    const float e2 = db2 + __shfl_xor(db2, 32, kWave), e3 = db3 + __shfl_xor(db3, 32, kWave);
+    if (h == 0) {
+      if (r32 < C1) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) o[r32 * C0 + k] = d[k];
+#pragma unroll
+        for (int k = 0; k < D; ++k) o[r32 * C0 + 3 + k] = d[3 + k];
+        o[C1 * C0 + r32] = d[6];
+        o[P1 + C2 * C1 + r32] = e2;
+      }
+      o[P1 + P2 + C3 * C2 + r32] = e3;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = arow(r, h);
+      if (row < C2 && r32 < C1) o[P1 + row * C1 + r32] = dw2[r];
+      if (r32 < C2) o[P1 + P2 + row * C2 + r32] = dw3[r];
+    }
+  }
+}
+
 // U[b][n] = W1f f_n + b1 (fp32, features in ascending order from the bias): thread (point,
 // 4-channel group), the weights as [k][c] float4 rows in LDS.
 template <int D, int C1>
@@ -723,17 +1153,46 @@ int bnm_grid(int64_t centres) {
   return static_cast<int>(need < kBnmMaxGrid ? (need > 0 ? need : 1) : kBnmMaxGrid);
 }
 
-// Workspace: per-wave partials | dW1's xyz / bias sums (C1 x 4) and feature columns (C1 x D) |
-// keys | gz1 rows | per-point sums G | segsum's own.
+// The tables: two layers (D, C1, C2) = (32, 32, 64) / (64, 64, 64), three layers (D, 16, 16, 32)
+// with D = 0 / 3.
+struct BnmTable {
+  int nlayer, D, C1, C2, C3;
+};
+bool bnm_table(int nlayer, const int* chans, BnmTable* t) {
+  if (!chans) return false;
+  if (nlayer == 2) {
+    const int D = chans[0] - 3;
+    if (!((D == 32 && chans[1] == 32 && chans[2] == 64) || (D == 64 && chans[1] == 64 && chans[2] == 64))) return false;
+    *t = BnmTable{2, D, chans[1], chans[2], 0};
+    return true;
+  }
+  if (nlayer == 3) {
+    const int D = chans[0] - 3;
+    if (!((D == 0 || D == 3) && chans[1] == 16 && chans[2] == 16 && chans[3] == 32)) return false;
+    *t = BnmTable{3, D, 16, 16, 32};
+    return true;
+  }
+  return false;
+}
+int bnm_grads_floats(const BnmTable& t) {
+  const int C0 = 3 + t.D;
+  int n = t.C1 * C0 + t.C1 + t.C2 * t.C1 + t.C2;
+  if (t.nlayer == 3) n += t.C3 * t.C2 + t.C3;
+  return n;
+}
+
+// Workspace: per-wave partials | (two layers) dW1's xyz / bias sums (C1 x 4) and feature columns
+// (C1 x D) | (backward) keys | gz1 rows | per-point sums G | segsum's own.
 constexpr int kGtfBlocks = 512;
-int64_t bnm_part_bytes(int64_t centres, int D, int C1, int C2) {
+int64_t bnm_part_bytes(int64_t centres, const BnmTable& t) {
   const int64_t nw = static_cast<int64_t>(bnm_grid(centres)) * kBnmWaves;
-  const int64_t cmax = C1 > C2 ? C1 : C2;
+  const int64_t cmax = std::max(std::max(t.C1, t.C2), t.C3);
   int64_t b = nw * 2 * 2 * cmax * 8;
-  b = std::max<int64_t>(b, nw * (C2 * C1 + C2) * 4);
-  b = std::max<int64_t>(b, nw * 4 * C1 * 4);
-  b = std::max<int64_t>(b, static_cast<int64_t>(kGtfBlocks) * C1 * D * 4);
-  return bnm_align(b) + bnm_align(C1 * 4 * 4) + bnm_align(static_cast<int64_t>(C1) * D * 4);
+  if (t.nlayer == 3) return bnm_align(std::max<int64_t>(b, nw * bnm_grads_floats(t) * 4));
+  b = std::max<int64_t>(b, nw * (t.C2 * t.C1 + t.C2) * 4);
+  b = std::max<int64_t>(b, nw * 4 * t.C1 * 4);
+  b = std::max<int64_t>(b, static_cast<int64_t>(kGtfBlocks) * t.C1 * t.D * 4);
+  return bnm_align(b) + bnm_align(t.C1 * 4 * 4) + bnm_align(static_cast<int64_t>(t.C1) * t.D * 4);
 }
 int64_t bnm_feat_bytes(int64_t E, int64_t npts, int C1) {
   const int64_t seg = segment_sum_workspace_bytes(E, npts);
@@ -746,33 +1205,46 @@ int bnm_launch(const BnmArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((sa_bnm_kernel<D, C1, C2, PASS>), dim3(grid), dim3(kBnmThreads), 0, st, a);
   return launch_status("dvcp_sa_bnm_pass");
 }
+template <int D, int PASS>
+int bnm3_launch(const BnmArgs& a, hipStream_t st) {
+  const int grid = bnm_grid(static_cast<int64_t>(a.B) * a.S);
+  hipLaunchKernelGGL((sa_bnm3_kernel<D, PASS>), dim3(grid), dim3(kBnmThreads), 0, st, a);
+  return launch_status("dvcp_sa_bnm_pass");
+}
 
+int bnm_sums(const void* ws, int nw, int C, double* sums, hipStream_t st) {
+  hipLaunchKernelGGL((bnm_sum_kernel<double, double>), dim3(ceil_div(2 * C, 64)), dim3(1024), 0, st,
+                     static_cast<const double*>(ws), 2 * nw, 2 * C, sums);
+  return launch_status("dvcp_sa_bnm_pass(sum)");
+}
+
+// ABI pass codes: 1..3 statistics of layer l, 10 forward, 20 + l backward sums of layer l, 30 gradients
 template <int D, int C1, int C2>
-int bnm_pass(int pass, BnmArgs a, void* ws, double* sums, float* grads, float* gfeat, hipStream_t st) {
+int bnm_pass2(int pass, BnmArgs a, void* ws, double* sums, float* grads, float* gfeat, hipStream_t st) {
   const int64_t centres = static_cast<int64_t>(a.B) * a.S;
   const int nw = bnm_grid(centres) * kBnmWaves;
   a.part = ws;
-  if (pass == kS1 || pass == kS2 || pass == kB1) {
-    const int C = pass == kS2 ? C2 : C1;
-    int e = pass == kS1   ? bnm_launch<D, C1, C2, kS1>(a, st)
-            : pass == kS2 ? bnm_launch<D, C1, C2, kS2>(a, st)
-                          : bnm_launch<D, C1, C2, kB1>(a, st);
-    if (e) return e;
-    hipLaunchKernelGGL((bnm_sum_kernel<double, double>), dim3(ceil_div(2 * C, 64)), dim3(1024), 0, st,
-                       static_cast<const double*>(ws), 2 * nw, 2 * C, sums);
-    return launch_status("dvcp_sa_bnm_pass(sum)");
+  if (pass == 1 || pass == 2 || pass == 21) {
+    const int e = pass == 1 ? bnm_launch<D, C1, C2, kS1>(a, st)
+                            : (pass == 2 ? bnm_launch<D, C1, C2, kS2>(a, st) : bnm_launch<D, C1, C2, kB1>(a, st));
+    return e ? e : bnm_sums(ws, nw, pass == 2 ? C2 : C1, sums, st);
   }
-  if (pass == kFwd) return bnm_launch<D, C1, C2, kFwd>(a, st);
-  // pass 5: the gradients -- layer 2 (dW2 | db2); layer 1's xyz / bias columns and the per-entry
-  // gz1 rows; their per-point segment sums G; dW1's feature columns G^T F; the feature gradient
+  if (pass == 10) return bnm_launch<D, C1, C2, kFwd>(a, st);
+  if (pass != 30) {
+    set_error("dvcp_sa_bnm_pass: pass %d is not one of 1, 2, 10, 21, 30 for a two-layer table", pass);
+    return DVCP_EINVAL;
+  }
+  // the gradients -- layer 2 (dW2 | db2); layer 1's xyz / bias columns and the per-entry gz1 rows;
+  // their per-point segment sums G; dW1's feature columns G^T F; the feature gradient
   constexpr int C0 = 3 + D;
   constexpr int P1 = C1 * C0 + C1, P2 = C2 * C1 + C2;
+  const BnmTable tb{2, D, C1, C2, 0};
   if (int e = bnm_launch<D, C1, C2, kB0A>(a, st)) return e;
   hipLaunchKernelGGL((bnm_sum_kernel<float, float>), dim3(ceil_div(P2, 64)), dim3(1024), 0, st,
                      static_cast<const float*>(ws), nw, P2, grads + P1);
   if (int e = launch_status("dvcp_sa_bnm_pass(dW2)")) return e;
   const int64_t E = centres * a.nsample, npts = static_cast<int64_t>(a.B) * a.N;
-  const int64_t pb = bnm_part_bytes(centres, D, C1, C2);
+  const int64_t pb = bnm_part_bytes(centres, tb);
   char* w8 = static_cast<char*>(ws);
   float* xb = reinterpret_cast<float*>(w8 + pb - bnm_align(C1 * 4 * 4) - bnm_align(static_cast<int64_t>(C1) * D * 4));
   float* fw = reinterpret_cast<float*>(w8 + pb - bnm_align(static_cast<int64_t>(C1) * D * 4));
@@ -802,33 +1274,62 @@ int bnm_pass(int pass, BnmArgs a, void* ws, double* sums, float* grads, float* g
   return DVCP_OK;
 }
 
-bool bnm_table(int D, int C1, int C2) { return (D == 32 && C1 == 32 && C2 == 64) || (D == 64 && C1 == 64 && C2 == 64); }
+template <int D>
+int bnm_pass3(int pass, BnmArgs a, void* ws, double* sums, float* grads, hipStream_t st) {
+  const int nw = bnm_grid(static_cast<int64_t>(a.B) * a.S) * kBnmWaves;
+  a.part = ws;
+  int e = DVCP_OK, C = 16;
+  switch (pass) {
+    case 1: e = bnm3_launch<D, kS1>(a, st); break;
+    case 2: e = bnm3_launch<D, kS2>(a, st); break;
+    case 3: e = bnm3_launch<D, kS3>(a, st), C = 32; break;
+    case 10: return bnm3_launch<D, kFwd>(a, st);
+    case 21: e = bnm3_launch<D, kB1>(a, st); break;
+    case 22: e = bnm3_launch<D, kB2>(a, st); break;
+    case 30: {
+      if (int e2 = bnm3_launch<D, kB0A>(a, st)) return e2;
+      const int P = bnm_grads_floats(BnmTable{3, D, 16, 16, 32});
+      hipLaunchKernelGGL((bnm_sum_kernel<float, float>), dim3(ceil_div(P, 64)), dim3(1024), 0, st,
+                         static_cast<const float*>(ws), nw, P, grads);
+      return launch_status("dvcp_sa_bnm_pass(grads)");
+    }
+    default:
+      set_error("dvcp_sa_bnm_pass: pass %d is not one of 1, 2, 3, 10, 21, 22, 30 for a three-layer table", pass);
+      return DVCP_EINVAL;
+  }
+  return e ? e : bnm_sums(ws, nw, C, sums, st);
+}
 
 }  // namespace
 }  // namespace dvcp
 
-extern "C" int dvcp_sa_bnm_supported(int D, int C1, int C2) { return dvcp::bnm_table(D, C1, C2) ? 1 : 0; }
+extern "C" int dvcp_sa_bnm_supported(int nlayer, const int* chans) {
+  dvcp::BnmTable t;
+  return dvcp::bnm_table(nlayer, chans, &t) ? 1 : 0;
+}
 
-extern "C" int64_t dvcp_sa_bnm_workspace_bytes(int B, int S, int N, int nsample, int D, int C1, int C2,
+extern "C" int64_t dvcp_sa_bnm_workspace_bytes(int B, int S, int N, int nsample, int nlayer, const int* chans,
                                                int backward) {
-  if (B < 0 || S < 0 || N < 0 || nsample < 0 || !dvcp::bnm_table(D, C1, C2)) return -1;
+  dvcp::BnmTable t;
+  if (B < 0 || S < 0 || N < 0 || nsample < 0 || !dvcp::bnm_table(nlayer, chans, &t)) return -1;
   const int64_t centres = static_cast<int64_t>(B) * S;
-  const int64_t b = dvcp::bnm_part_bytes(centres, D, C1, C2);
-  if (!backward) return b;  // the statistics passes use the partials only
-  const int64_t f = dvcp::bnm_feat_bytes(centres * nsample, static_cast<int64_t>(B) * N, C1);
+  const int64_t b = dvcp::bnm_part_bytes(centres, t);
+  if (!backward || t.nlayer == 3) return b;  // only the two-layer gradients need the feature part
+  const int64_t f = dvcp::bnm_feat_bytes(centres * nsample, static_cast<int64_t>(B) * N, t.C1);
   return f < 0 ? -1 : b + f;
 }
 
-extern "C" int dvcp_sa_bnm_pre(const float* feat, int64_t fb, int64_t fn, int N, int B, int D, int C1, int C2,
+extern "C" int dvcp_sa_bnm_pre(const float* feat, int64_t fb, int64_t fn, int N, int B, int nlayer, const int* chans,
                                const float* pack, float* U, void* stream) {
+  dvcp::BnmTable t;
+  DVCP_REQUIRE(dvcp::bnm_table(nlayer, chans, &t) && t.nlayer == 2, "dvcp_sa_bnm_pre: not a two-layer table");
   DVCP_REQUIRE(feat && pack && U, "dvcp_sa_bnm_pre: null pointer");
-  DVCP_REQUIRE(dvcp::bnm_table(D, C1, C2), "dvcp_sa_bnm_pre: unsupported table D=%d %d-%d", D, C1, C2);
   DVCP_REQUIRE(N >= 0 && B >= 0 && fb % 4 == 0 && fn % 4 == 0, "dvcp_sa_bnm_pre: bad sizes / strides");
   DVCP_REQUIRE(reinterpret_cast<uintptr_t>(feat) % 16 == 0, "dvcp_sa_bnm_pre: feature rows must be 16-byte aligned");
   const int64_t rows = static_cast<int64_t>(B) * N;
   if (rows == 0) return DVCP_OK;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (D == 32)
+  if (t.D == 32)
     hipLaunchKernelGGL((dvcp::bnm_pre_kernel<32, 32>), dim3(dvcp::ceil_div(rows, 256 / 8)), dim3(256), 0, st, feat, fb,
                        fn, N, B, pack, U);
   else
@@ -839,39 +1340,47 @@ extern "C" int dvcp_sa_bnm_pre(const float* feat, int64_t fb, int64_t fn, int N,
 
 extern "C" int dvcp_sa_bnm_pass(int pass, const float* xyz, int64_t sb, int64_t sc, int64_t sn, int N, const float* ctr,
                                 int64_t cb, int64_t cc, int64_t cn, int S, int B, const float* feat, int64_t fb,
-                                int64_t fn, int D, const int32_t* count, const int32_t* list, int nsample, int C1,
-                                int C2, const float* pack, const float* U, const float* grad_out, int32_t* arg,
-                                float* out, float* zbest, void* workspace, double* sums, float* grads,
-                                float* grad_feat, void* stream) {
-  DVCP_REQUIRE(pass >= 1 && pass <= 5, "dvcp_sa_bnm_pass: pass %d (1..5)", pass);
-  DVCP_REQUIRE(dvcp::bnm_table(D, C1, C2), "dvcp_sa_bnm_pass: unsupported table D=%d %d-%d", D, C1, C2);
-  DVCP_REQUIRE(xyz && ctr && feat && count && list && pack && U, "dvcp_sa_bnm_pass: null input");
+                                int64_t fd, int64_t fn, int D, const int32_t* count, const int32_t* list, int nsample,
+                                int nlayer, const int* chans, const float* pack, const float* U,
+                                const float* grad_out, int32_t* arg, float* out, float* zbest, void* workspace,
+                                double* sums, float* grads, float* grad_feat, void* stream) {
+  dvcp::BnmTable t;
+  DVCP_REQUIRE(dvcp::bnm_table(nlayer, chans, &t) && t.D == D, "dvcp_sa_bnm_pass: unsupported table");
+  DVCP_REQUIRE(xyz && ctr && count && list && pack, "dvcp_sa_bnm_pass: null input");
+  DVCP_REQUIRE(D == 0 || feat, "dvcp_sa_bnm_pass: D=%d but feat is NULL", D);
+  DVCP_REQUIRE(t.nlayer == 3 || (U && fd == 1), "dvcp_sa_bnm_pass: two-layer tables need U and point-major rows");
   DVCP_REQUIRE(N > 0 && S >= 0 && B >= 0 && nsample > 0, "dvcp_sa_bnm_pass: bad sizes");
   DVCP_REQUIRE(static_cast<int64_t>(B) * S * nsample < (int64_t(1) << 31) &&
                    static_cast<int64_t>(B) * N < (int64_t(1) << 31),
                "dvcp_sa_bnm_pass: more than 2^31 entries / points");
-  DVCP_REQUIRE(pass == 3 || pass == 5 || sums, "dvcp_sa_bnm_pass: null sums");
-  DVCP_REQUIRE(pass != 3 || (arg && out && zbest), "dvcp_sa_bnm_pass: null forward outputs");
-  DVCP_REQUIRE(pass < 4 || (grad_out && arg && out), "dvcp_sa_bnm_pass: null gradient / routing");
-  DVCP_REQUIRE(pass != 5 || grads, "dvcp_sa_bnm_pass: null grads");
-  DVCP_REQUIRE(pass == 3 || workspace, "dvcp_sa_bnm_pass: null workspace");
+  const bool stats = (pass >= 1 && pass <= t.nlayer) || (pass > 20 && pass < 20 + t.nlayer);
+  DVCP_REQUIRE(stats || pass == 10 || pass == 30, "dvcp_sa_bnm_pass: bad pass %d", pass);
+  DVCP_REQUIRE(!stats || sums, "dvcp_sa_bnm_pass: null sums");
+  DVCP_REQUIRE(pass != 10 || (arg && out && zbest), "dvcp_sa_bnm_pass: null forward outputs");
+  DVCP_REQUIRE(pass < 20 || (grad_out && arg && out), "dvcp_sa_bnm_pass: null gradient / routing");
+  DVCP_REQUIRE(pass != 30 || grads, "dvcp_sa_bnm_pass: null grads");
+  DVCP_REQUIRE(pass == 10 || workspace, "dvcp_sa_bnm_pass: null workspace");
+  DVCP_REQUIRE(!grad_feat || t.nlayer == 2, "dvcp_sa_bnm_pass: no feature gradient for the three-layer table");
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (B == 0 || S == 0) {
-    if (pass == 1 || pass == 4)
-      if (hipMemsetAsync(sums, 0, 2 * C1 * sizeof(double), st) != hipSuccess) return dvcp::launch_status("dvcp_sa_bnm");
-    if (pass == 2)
-      if (hipMemsetAsync(sums, 0, 2 * C2 * sizeof(double), st) != hipSuccess) return dvcp::launch_status("dvcp_sa_bnm");
-    if (pass == 5) {
-      const int64_t P = static_cast<int64_t>(C1) * (3 + D) + C1 + static_cast<int64_t>(C2) * C1 + C2;
-      if (hipMemsetAsync(grads, 0, P * sizeof(float), st) != hipSuccess) return dvcp::launch_status("dvcp_sa_bnm");
+    const int cs[4] = {0, t.C1, t.C2, t.C3};
+    if (stats) {
+      const int C = cs[pass > 20 ? pass - 20 : pass];
+      if (hipMemsetAsync(sums, 0, 2 * C * sizeof(double), st) != hipSuccess) return dvcp::launch_status("dvcp_sa_bnm");
+    }
+    if (pass == 30) {
+      if (hipMemsetAsync(grads, 0, dvcp::bnm_grads_floats(t) * sizeof(float), st) != hipSuccess)
+        return dvcp::launch_status("dvcp_sa_bnm");
       if (grad_feat && hipMemsetAsync(grad_feat, 0, static_cast<int64_t>(B) * N * D * sizeof(float), st) != hipSuccess)
         return dvcp::launch_status("dvcp_sa_bnm");
     }
     return DVCP_OK;
   }
-  dvcp::BnmArgs a{xyz,     sb,    sc,      sn,    ctr,  cb,   cc,    cn,      S,       B,       N,
-                  nsample, feat,  fb,      fn,    count, list, pack, U,       grad_out, arg,   out,
-                  zbest,   nullptr, nullptr, nullptr};
-  if (D == 32) return dvcp::bnm_pass<32, 32, 64>(pass, a, workspace, sums, grads, grad_feat, st);
-  return dvcp::bnm_pass<64, 64, 64>(pass, a, workspace, sums, grads, grad_feat, st);
+  dvcp::BnmArgs a{xyz,   sb,   sc,   sn,  ctr,      cb,  cc,  cn,    S,       B,       N,      nsample, feat, fb,
+                  fd,    fn,   count, list, pack,   U,   grad_out, arg, out, zbest, nullptr, nullptr, nullptr};
+  if (t.nlayer == 3)
+    return D == 0 ? dvcp::bnm_pass3<0>(pass, a, workspace, sums, grads, st)
+                  : dvcp::bnm_pass3<3>(pass, a, workspace, sums, grads, st);
+  if (D == 32) return dvcp::bnm_pass2<32, 32, 64>(pass, a, workspace, sums, grads, grad_feat, st);
+  return dvcp::bnm_pass2<64, 64, 64>(pass, a, workspace, sums, grads, grad_feat, st);
 }

@@ -75,8 +75,8 @@ SIGNATURES = {
                             _P, _P, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P],
     "dvcp_sa_bn_zrows": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _L, _L, _L, _I,
                          _P, _P, _I, _I, _P, _P, _P, _P],
-    "dvcp_sa_bnm_pre": [_P, _L, _L, _I, _I, _I, _I, _I, _P, _P, _P],
-    "dvcp_sa_bnm_pass": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _P, _L, _L, _I, _P, _P, _I, _I, _I,
+    "dvcp_sa_bnm_pre": [_P, _L, _L, _I, _I, _I, _P, _P, _P, _P],
+    "dvcp_sa_bnm_pass": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _P, _L, _L, _L, _I, _P, _P, _I, _I, _P,
                          _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
 }
 
@@ -137,9 +137,9 @@ def load():
     lib.dvcp_sa_bn_pack_floats.argtypes = [ctypes.c_int, ctypes.c_void_p]
     if hasattr(lib, "dvcp_sa_bnm_supported") or not skip:
         lib.dvcp_sa_bnm_supported.restype = ctypes.c_int
-        lib.dvcp_sa_bnm_supported.argtypes = [ctypes.c_int] * 3
+        lib.dvcp_sa_bnm_supported.argtypes = [ctypes.c_int, ctypes.c_void_p]
         lib.dvcp_sa_bnm_workspace_bytes.restype = ctypes.c_int64
-        lib.dvcp_sa_bnm_workspace_bytes.argtypes = [ctypes.c_int] * 8
+        lib.dvcp_sa_bnm_workspace_bytes.argtypes = [ctypes.c_int] * 5 + [ctypes.c_void_p, ctypes.c_int]
     for name, args in SIGNATURES.items():
         if skip and not hasattr(lib, name):
             continue

@@ -6,10 +6,11 @@ batch over all B * S * nsample grouped entries (BatchNorm2d over (B, H, W); the 
 the ball query are entries like any other) and updates the running statistics (momentum, unbiased
 variance), once per FE1 call -- src and tgt are separate calls (deepVCP.py:29,72).
 
-The two-layer tables (sa2, sa3; fp32) run on the matrix cores (csrc/sa_bn_mfma.hip,
-``_train_forward_mfma`` / ``_train_backward_mfma``): every pass recomputes the MLP per 32-entry
-tile, nothing per entry is stored, and the weight gradients are MFMA products over the entries.
-The rest (sa1 3-16-16-32, fp64 inputs) takes the lane-per-entry passes below.
+The REF-R tables with fp32 inputs (sa1 3[+3]-16-16-32, sa2, sa3) run on the matrix cores
+(csrc/sa_bn_mfma.hip, ``_train_forward_mfma`` / ``_train_backward_mfma``): every pass recomputes
+the MLP per 32-entry tile, nothing per entry is stored, and the weight gradients are MFMA products
+over the entries.  The rest (fp64 inputs, channel-first feature tables) takes the lane-per-entry
+passes below.
 
 Forward (``train_forward``): one statistics pass per layer (dvcp_sa_bn_stats: fp64 sums of z and
 z^2, the layers below normalised by their batch statistics), then the eval kernel
@@ -81,15 +82,15 @@ def _set_stats(pack, bn, o, cin, cout, sums, M):
 
 
 def _train_forward_mfma(sa, xyz, ctr, feat, count, lst, ns):
-    """The two-layer tables on the matrix cores (csrc/sa_bn_mfma.hip): the per-point half of layer 1
-    once, one statistics pass per layer, then the forward with its arg-max routing.  Nothing per
-    entry is kept for the backward; it recomputes the MLP."""
+    """The REF-R tables on the matrix cores (csrc/sa_bn_mfma.hip): (two-layer tables) the
+    per-point half of layer 1 once, one statistics pass per layer, then the forward with its
+    arg-max routing.  Nothing per entry is kept for the backward; it recomputes the MLP."""
     chans = sa.chans
     B, S = ctr.shape[0], ctr.shape[2]
     M = B * S * ns
     with torch.no_grad():
         pack, offs = _bnm_pack(sa, xyz.device)
-        U = ops.sa_bnm_pre(feat, chans, pack)
+        U = ops.sa_bnm_pre(feat, chans, pack) if len(chans) == 3 else None
         for layer, (bn, (o, cin, cout)) in enumerate(zip(sa.mlp_bns, offs), 1):
             sums = ops.sa_bnm_stats(xyz, ctr, feat, count, lst, ns, chans, pack, U, layer)
             _set_stats(pack, bn, o, cin, cout, sums, M)
@@ -105,22 +106,32 @@ def _train_backward_mfma(sa, lay, g_out, want_feat_grad):
     args = (lay["pts"], lay["ctr"], lay["feat"], lay["count"], lay["lst"], lay["ns"], chans)
     g = g_out.float().contiguous()
     out, _, zb = fwd
-    (o1, c0, c1), (o2, _, c2) = offs
-    # layer 2's sums over the routed rows (gy2 = g at each (centre, channel)'s arg-max when the max
-    # is positive): A2 = sum gy2, B2 = sum gy2 xhat2
-    v2 = o2 + c2 * c1
-    mu2, is2 = pack[v2 + 3 * c2:v2 + 4 * c2], pack[v2 + 4 * c2:v2 + 5 * c2]
+    L = len(offs)
+    sums = [None] * L
+    # the last layer's sums over the routed rows (gy = g at each (centre, channel)'s arg-max when
+    # the max is positive): A = sum gy, B = sum gy xhat
+    o, cin, cout = offs[-1]
+    v = o + cout * cin
+    mu, istd = pack[v + 3 * cout:v + 4 * cout], pack[v + 4 * cout:v + 5 * cout]
     gy = torch.where(out > 0, g, torch.zeros_like(g)).double()
-    xh = ((zb - mu2) * is2).double()
-    s2 = torch.stack([gy.sum((0, 1)), (gy * xh).sum((0, 1))])
-    pack[v2 + 5 * c2:v2 + 7 * c2] = (s2 / M).reshape(-1).float()
-    s1 = ops.sa_bnm_backward(*args, pack, U, fwd, g, 1)
-    v1 = o1 + c1 * c0
-    pack[v1 + 5 * c1:v1 + 7 * c1] = (s1 / M).reshape(-1).float()
+    xh = ((zb - mu) * istd).double()
+    sums[-1] = torch.stack([gy.sum((0, 1)), (gy * xh).sum((0, 1))])
+    pack[v + 5 * cout:v + 7 * cout] = (sums[-1] / M).reshape(-1).float()
+    for k in range(L - 1, 0, -1):   # each lower layer's sums need those of the layers above
+        sums[k - 1] = ops.sa_bnm_backward(*args, pack, U, fwd, g, k)
+        o, cin, cout = offs[k - 1]
+        v = o + cout * cin
+        pack[v + 5 * cout:v + 7 * cout] = (sums[k - 1] / M).reshape(-1).float()
     grads, gF = ops.sa_bnm_backward(*args, pack, U, fwd, g, 0, want_feat_grad=want_feat_grad)
-    n1 = c1 * c0 + c1
-    parts = [grads[:n1], s1[1], s1[0], grads[n1:], s2[1], s2[0]]   # per layer dW, db, dgamma, dbeta
+    parts, i = [], 0
+    for (o, cin, cout), s in zip(offs, sums):   # per layer dW, db, dgamma, dbeta
+        parts += [grads[i:i + cout * cin + cout], s[1], s[0]]
+        i += cout * cin + cout
     return torch.cat([p.float() for p in parts]), gF
+
+
+# The matrix-core path for the tables it takes (tests switch it off to check the VALU passes).
+USE_MFMA = True
 
 
 def train_forward(sa, xyz, ctr, feat, count, lst, ns, keep_zrows=False):
@@ -130,7 +141,7 @@ def train_forward(sa, xyz, ctr, feat, count, lst, ns, keep_zrows=False):
     writes every entry's z rows for it (within ZROWS_KEEP_MAX_BYTES); a train-mode forward with no
     backward (no_grad, frozen extractor) allocates none."""
     chans = sa.chans
-    if ops.sa_bnm_usable(xyz, ctr, feat, chans):
+    if USE_MFMA and ops.sa_bnm_usable(xyz, ctr, feat, chans):
         return _train_forward_mfma(sa, xyz, ctr, feat, count, lst, ns)
     dev = xyz.device
     B, S = ctr.shape[0], ctr.shape[2]

@@ -678,30 +678,41 @@ def sa_bn_backward(xyz, ctr, feat, count, lst, nsample, chans, pack, zrows, grad
 
 
 def sa_bnm_usable(xyz, ctr, feat, chans):
-    """Whether the matrix-core training path (dvcp_sa_bnm_*) takes this grouping: the two-layer
-    tables sa2 / sa3 with fp32 points and fp32 point-major feature rows (16-byte aligned)."""
-    if len(chans) != 3 or feat is None or feat.dim() != 3:
+    """Whether the matrix-core training path (dvcp_sa_bnm_*) takes this grouping: the REF-R tables
+    (sa1 3[+3]-16-16-32, sa2, sa3) with fp32 points and features; the two-layer tables need
+    point-major feature rows (16-byte aligned)."""
+    ch = torch.tensor(list(chans), dtype=torch.int32)
+    if not _lib.load().dvcp_sa_bnm_supported(len(chans) - 1, ch.data_ptr()):
         return False
-    if xyz.dtype != torch.float32 or ctr.dtype != torch.float32 or feat.dtype != torch.float32:
+    if xyz.dtype != torch.float32 or ctr.dtype != torch.float32:
         return False
-    if feat.stride(1) != 1 or feat.stride(0) % 4 or feat.stride(2) % 4 or feat.data_ptr() % 16:
+    if feat is None:
+        return len(chans) == 4 and int(chans[0]) == 3
+    if feat.dtype != torch.float32 or feat.dim() != 3:
         return False
-    return bool(_lib.load().dvcp_sa_bnm_supported(int(chans[0]) - 3, int(chans[1]), int(chans[2])))
+    if len(chans) == 3 and (feat.stride(1) != 1 or feat.stride(0) % 4 or feat.stride(2) % 4 or feat.data_ptr() % 16):
+        return False
+    return True
 
 
 def _bnm_args(xyz, ctr, feat, count, lst, nsample, chans):
-    _lib.require_gpu(xyz, ctr, feat, count, lst)
+    _lib.require_gpu(xyz, ctr, count, lst)
     B = xyz.shape[0]
     N, sb, sc, sn = _pts(xyz, 2)
     S, cb, cc, cn = _pts(ctr, 2)
-    D = feat.shape[1]
-    return (B, N, S, D), (ptr(xyz), sb, sc, sn, N, ptr(ctr), cb, cc, cn, S, B, ptr(feat), feat.stride(0),
-                          feat.stride(2), D, ptr(count), ptr(lst), int(nsample), int(chans[1]), int(chans[2]))
+    if feat is not None:
+        D = feat.shape[1]
+        fb, fd, fn = feat.stride(0), feat.stride(1), feat.stride(2)
+    else:
+        D, fb, fd, fn = 0, 0, 0, 0
+    ch = torch.tensor(list(chans), dtype=torch.int32)
+    return (B, N, S, D), ch, (ptr(xyz), sb, sc, sn, N, ptr(ctr), cb, cc, cn, S, B, ptr(feat), fb, fd, fn, D,
+                              ptr(count), ptr(lst), int(nsample), len(chans) - 1, ptr(ch))
 
 
-def _bnm_ws(B, S, N, nsample, chans, backward, dev):
-    nb = int(_lib.load().dvcp_sa_bnm_workspace_bytes(B, S, N, int(nsample), int(chans[0]) - 3, int(chans[1]),
-                                                     int(chans[2]), int(backward)))
+def _bnm_ws(B, S, N, nsample, ch, backward, dev):
+    nb = int(_lib.load().dvcp_sa_bnm_workspace_bytes(B, S, N, int(nsample), ch.numel() - 1, ch.data_ptr(),
+                                                     int(backward)))
     if nb < 0:
         raise RuntimeError("dvcp_sa_bnm_workspace_bytes: size query failed")
     return torch.empty(max(1, (nb + 3) // 4), dtype=torch.float32, device=dev)
@@ -709,21 +720,22 @@ def _bnm_ws(B, S, N, nsample, chans, backward, dev):
 
 def sa_bnm_pre(feat, chans, pack):
     """U (B, N, C1) = W1[:, 3:] f_n + b1 for (B, D, N) point-major fp32 features: the per-point half
-    of layer 1 that every dvcp_sa_bnm pass starts from."""
+    of layer 1 that every dvcp_sa_bnm pass of a two-layer table starts from."""
     _lib.require_gpu(feat, pack)
     B, D, N = feat.shape
     C1 = int(chans[1])
+    ch = torch.tensor(list(chans), dtype=torch.int32)
     U = torch.empty(B, N, C1, dtype=torch.float32, device=feat.device)
-    call("dvcp_sa_bnm_pre", ptr(feat), feat.stride(0), feat.stride(2), N, B, D, C1, int(chans[2]), ptr(pack), ptr(U),
-         stream(), work=(2.0 * B * N * D * C1, 4.0 * B * N * (D + C1)))
+    call("dvcp_sa_bnm_pre", ptr(feat), feat.stride(0), feat.stride(2), N, B, len(chans) - 1, ch.data_ptr(), ptr(pack),
+         ptr(U), stream(), work=(2.0 * B * N * D * C1, 4.0 * B * N * (D + C1)))
     return U
 
 
 def sa_bnm_stats(xyz, ctr, feat, count, lst, nsample, chans, pack, U, layer):
-    """Training-mode BatchNorm statistics on the matrix cores (two-layer tables): (2, C_layer) fp64 =
-    sum z, sum z^2 of layer ``layer``'s conv output over all B * S * nsample grouped entries."""
-    (B, N, S, D), args = _bnm_args(xyz, ctr, feat, count, lst, nsample, chans)
-    ws = _bnm_ws(B, S, N, nsample, chans, False, xyz.device)
+    """Training-mode BatchNorm statistics on the matrix cores: (2, C_layer) fp64 = sum z, sum z^2 of
+    layer ``layer``'s conv output over all B * S * nsample grouped entries."""
+    (B, N, S, D), ch, args = _bnm_args(xyz, ctr, feat, count, lst, nsample, chans)
+    ws = _bnm_ws(B, S, N, nsample, ch, False, xyz.device)
     sums = torch.empty(2, int(chans[layer]), dtype=torch.float64, device=xyz.device)
     macs = sum(a * b for a, b in zip(chans[:layer], chans[1:layer + 1]))
     call("dvcp_sa_bnm_pass", int(layer), *args, ptr(pack), ptr(U), None, None, None, None, ptr(ws), ptr(sums), None,
@@ -732,41 +744,42 @@ def sa_bnm_stats(xyz, ctr, feat, count, lst, nsample, chans, pack, U, layer):
 
 
 def sa_bnm_forward(xyz, ctr, feat, count, lst, nsample, chans, pack, U):
-    """The training-mode forward output (B, S, C2) fp32 with batch statistics, plus each (centre,
-    channel)'s first arg-max slot (int32) and that slot's z2 (what routes the backward)."""
-    (B, N, S, D), args = _bnm_args(xyz, ctr, feat, count, lst, nsample, chans)
+    """The training-mode forward output (B, S, C_last) fp32 with batch statistics, plus each
+    (centre, channel)'s first arg-max slot (int32) and that slot's z (what routes the backward)."""
+    (B, N, S, D), ch, args = _bnm_args(xyz, ctr, feat, count, lst, nsample, chans)
     dev = xyz.device
-    C2 = int(chans[2])
-    out = torch.empty(B, S, C2, dtype=torch.float32, device=dev)
-    arg = torch.empty(B, S, C2, dtype=torch.int32, device=dev)
-    zb = torch.empty(B, S, C2, dtype=torch.float32, device=dev)
+    C = int(chans[-1])
+    out = torch.empty(B, S, C, dtype=torch.float32, device=dev)
+    arg = torch.empty(B, S, C, dtype=torch.int32, device=dev)
+    zb = torch.empty(B, S, C, dtype=torch.float32, device=dev)
     macs = sum(a * b for a, b in zip(chans[:-1], chans[1:]))
-    call("dvcp_sa_bnm_pass", 3, *args, ptr(pack), ptr(U), None, ptr(arg), ptr(out), ptr(zb), None, None, None, None,
-         stream(), work=(2.0 * macs * B * S * nsample, B * S * (4 * nsample + 12 * C2) + B * N * 4 * (3 + D)))
+    call("dvcp_sa_bnm_pass", 10, *args, ptr(pack), ptr(U), None, ptr(arg), ptr(out), ptr(zb), None, None, None, None,
+         stream(), work=(2.0 * macs * B * S * nsample, B * S * (4 * nsample + 12 * C) + B * N * 4 * (3 + D)))
     return out, arg, zb
 
 
 def sa_bnm_backward(xyz, ctr, feat, count, lst, nsample, chans, pack, U, fwd, grad_out, mode, want_feat_grad=False):
-    """Training-mode backward on the matrix cores.  mode 1: (2, C1) fp64 = A1, B1 (the pack holds
-    A2 / M, B2 / M); mode 0: (dW1 | db1 | dW2 | db2 fp32, dL/d feat (B, N, D) fp32 or None)."""
-    (B, N, S, D), args = _bnm_args(xyz, ctr, feat, count, lst, nsample, chans)
+    """Training-mode backward on the matrix cores.  mode k >= 1: (2, C_k) fp64 = A_k, B_k (the pack
+    holds A / M, B / M of the layers above); mode 0: (per layer dW | db fp32, dL/d feat (B, N, D)
+    fp32 or None -- two-layer tables only)."""
+    (B, N, S, D), ch, args = _bnm_args(xyz, ctr, feat, count, lst, nsample, chans)
     dev = xyz.device
     out, arg, _ = fwd
     g = grad_out.float().contiguous()
     macs = sum(a * b for a, b in zip(chans[:-1], chans[1:]))
     E = B * S * int(nsample)
-    if mode == 1:
-        ws = _bnm_ws(B, S, N, nsample, chans, False, dev)
-        sums = torch.empty(2, int(chans[1]), dtype=torch.float64, device=dev)
-        call("dvcp_sa_bnm_pass", 4, *args, ptr(pack), ptr(U), ptr(g), ptr(arg), ptr(out), None, ptr(ws), ptr(sums),
-             None, None, stream(), work=(2.0 * (macs + chans[1] * chans[2]) * E, E * 4 + B * N * 4 * (3 + D)))
+    if mode > 0:
+        ws = _bnm_ws(B, S, N, nsample, ch, False, dev)
+        sums = torch.empty(2, int(chans[mode]), dtype=torch.float64, device=dev)
+        call("dvcp_sa_bnm_pass", 20 + int(mode), *args, ptr(pack), ptr(U), ptr(g), ptr(arg), ptr(out), None, ptr(ws),
+             ptr(sums), None, None, stream(), work=(4.0 * macs * E, E * 4 + B * N * 4 * (3 + D)))
         return sums
-    ws = _bnm_ws(B, S, N, nsample, chans, True, dev)
-    C0, C1, C2 = (int(c) for c in chans)
-    grads = torch.empty(C1 * C0 + C1 + C2 * C1 + C2, dtype=torch.float32, device=dev)
-    gF = torch.empty(B, N, D, dtype=torch.float32, device=dev) if want_feat_grad else None
-    call("dvcp_sa_bnm_pass", 5, *args, ptr(pack), ptr(U), ptr(g), ptr(arg), ptr(out), None, ptr(ws), None,
-         ptr(grads), ptr(gF), stream(), work=(2.0 * (2 * macs + 2 * C1 * C2) * E, E * (8 + 4 * C1)))
+    ws = _bnm_ws(B, S, N, nsample, ch, True, dev)
+    ngrad = sum(a * b + b for a, b in zip(chans[:-1], chans[1:]))
+    grads = torch.empty(ngrad, dtype=torch.float32, device=dev)
+    gF = torch.empty(B, N, D, dtype=torch.float32, device=dev) if (want_feat_grad and D > 0) else None
+    call("dvcp_sa_bnm_pass", 30, *args, ptr(pack), ptr(U), ptr(g), ptr(arg), ptr(out), None, ptr(ws), None,
+         ptr(grads), ptr(gF), stream(), work=(6.0 * macs * E, E * (8 + 4 * int(chans[1]))))
     return grads, gF
 
 

@@ -328,35 +328,39 @@ int dvcp_sa_bn_backward(int dtype, const void* xyz, int64_t sb, int64_t sc, int6
                         const float* grad_out, float* grad_feat, void* workspace, double* sums,
                         float* rows, void* stream);
 
-/* The same training-mode forward / backward for the two-layer tables (sa2: D = 32, 32-64; sa3:
- * D = 64, 64-64) on the matrix cores (csrc/sa_bn_mfma.hip): nothing per entry is stored, every
- * pass recomputes the MLP per 32-entry tile.  fp32 points / centres; feat (B x N x D fp32 rows,
- * feat[b fb + n fn + d], 16-byte aligned); pack as dvcp_sa_bn_stats.  Replaces
- * pointnet2_utils.py:176-202 in train() for those tables (train.py:105-125).
- * dvcp_sa_bnm_supported(D, C1, C2): 1 for the two tables.
- * dvcp_sa_bnm_pre: U (B x N x C1 fp32) = W1[:, 3:] f_n + b1, the per-point half of layer 1.
+/* The same training-mode forward / backward on the matrix cores (csrc/sa_bn_mfma.hip) for the
+ * REF-R tables sa1 (3[+3]-16-16-32), sa2 (35-32-64) and sa3 (67-64-64): nothing per entry is
+ * stored, every pass recomputes the MLP per 32-entry tile.  fp32 points / centres / features
+ * (feat[b fb + d fd + n fn]; the two-layer tables need point-major rows, fd = 1, 16-byte
+ * aligned); pack and the grouping as dvcp_sa_bn_stats.  Replaces pointnet2_utils.py:176-202 in
+ * train() (train.py:105-125).
+ * dvcp_sa_bnm_supported(nlayer, chans): 1 for those tables.
+ * dvcp_sa_bnm_pre (two-layer tables): U (B x N x C1 fp32) = W1[:, 3:] f_n + b1, the per-point half
+ *   of layer 1 every pass of the call starts from (NULL for sa1).
  * dvcp_sa_bnm_pass(pass):
- *   1 / 2: sums (2 x C_pass fp64) = sum z, sum z^2 of layer `pass` over the M entries;
- *   3: the forward -- out (B S x C2) = max over slots of relu(y2), arg = its first arg-max slot,
- *      zbest = that slot's z2;
- *   4: sums (2 x C1 fp64) = A1, B1 (needs A2 / B2 in the pack: A2 = sum of grad_out where
- *      out > 0, B2 = the same weighted by xhat2(zbest), summed by the host);
- *   5: grads = dW1 | db1 | dW2 | db2 (fp32, C1 (3 + D) + C1 + C2 C1 + C2 floats) and, if
- *      grad_feat is given, dL/d feat (B x N x D fp32), all summed in a fixed order.
- *   grad_out: B S x C2 fp32; arg / out / zbest: pass 3's outputs (read by passes 4, 5).
- *   workspace: dvcp_sa_bnm_workspace_bytes(B, S, N, nsample, D, C1, C2, backward = pass 5).
+ *   1..nlayer: sums (2 x C_pass fp64) = sum z, sum z^2 of layer `pass` over the M entries;
+ *   10: the forward -- out (B S x C_last) = max over slots of relu(y_last), arg = its first
+ *       arg-max slot, zbest = that slot's z_last;
+ *   20 + k (k < nlayer): sums (2 x C_k fp64) = A_k, B_k (needs A, B of the layers above in the
+ *       pack; the last layer's: A = sum of grad_out where out > 0, B = the same weighted by
+ *       xhat(zbest), summed by the host);
+ *   30: grads = per layer dW | db (fp32, dvcp_sa_bn_pack order without the BN vectors) and, for
+ *       the two-layer tables if grad_feat is given, dL/d feat (B x N x D fp32); fixed-order sums.
+ *   grad_out: B S x C_last fp32; arg / out / zbest: pass 10's outputs (read by passes 20+, 30).
+ *   workspace: dvcp_sa_bnm_workspace_bytes(B, S, N, nsample, nlayer, chans, backward = pass 30).
  */
-int dvcp_sa_bnm_supported(int D, int C1, int C2);
-int64_t dvcp_sa_bnm_workspace_bytes(int B, int S, int N, int nsample, int D, int C1, int C2,
+int dvcp_sa_bnm_supported(int nlayer, const int* chans);
+int64_t dvcp_sa_bnm_workspace_bytes(int B, int S, int N, int nsample, int nlayer, const int* chans,
                                     int backward);
-int dvcp_sa_bnm_pre(const float* feat, int64_t fb, int64_t fn, int N, int B, int D, int C1, int C2,
-                    const float* pack, float* U, void* stream);
+int dvcp_sa_bnm_pre(const float* feat, int64_t fb, int64_t fn, int N, int B, int nlayer,
+                    const int* chans, const float* pack, float* U, void* stream);
 int dvcp_sa_bnm_pass(int pass, const float* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
                      const float* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
-                     const float* feat, int64_t fb, int64_t fn, int D, const int32_t* count,
-                     const int32_t* list, int nsample, int C1, int C2, const float* pack,
-                     const float* U, const float* grad_out, int32_t* arg, float* out, float* zbest,
-                     void* workspace, double* sums, float* grads, float* grad_feat, void* stream);
+                     const float* feat, int64_t fb, int64_t fd, int64_t fn, int D,
+                     const int32_t* count, const int32_t* list, int nsample, int nlayer,
+                     const int* chans, const float* pack, const float* U, const float* grad_out,
+                     int32_t* arg, float* out, float* zbest, void* workspace, double* sums,
+                     float* grads, float* grad_feat, void* stream);
 
 /* Backward of the feature extractor's fc (deep_feat_extraction.py:15, Linear 64 -> 32):
  * x: P x 64 fp32 (its input rows), params: fc.W (32 x 64) | fc.b (32), grad: P x 32;

@@ -292,8 +292,9 @@ def test_sa_backward_vs_oracle(cuda, table):
           "relative gradient errors:", {k: f"{v:.1e}" for k, v in errs.items()})
 
 
-@pytest.mark.parametrize("table", ["sa1", "sa1_normals", "sa1_normals_f64", "sa2", "sa3", "sa2_rows", "sa3_rows"])
-def test_sa_batch_stats_train_vs_oracle(cuda, table):
+@pytest.mark.parametrize("table", ["sa1", "sa1_normals", "sa1_normals_f64", "sa2", "sa3", "sa2_rows", "sa3_rows",
+                                   "sa1_valu", "sa1_normals_valu"])
+def test_sa_batch_stats_train_vs_oracle(cuda, table, monkeypatch):
     """pointnet2_utils.py:176-202 with the module in training mode (batch-statistics BatchNorm, as
     train.py's model.train()): the forward output, the running-statistics update and every conv /
     BN parameter gradient and the grouped-feature gradient against torch autograd through the
@@ -301,13 +302,17 @@ def test_sa_batch_stats_train_vs_oracle(cuda, table):
     pairs whose two best rows tie within 1e-5 (fp64, batch statistics) get a zero output gradient
     on both sides; the batch-norm mean terms still reach every entry.  ``*_rows``: the same case
     with point-major feature rows (as the extractor passes them), which the two-layer tables run
-    on the matrix cores (csrc/sa_bn_mfma.hip) -- channel-first features take the VALU passes."""
+    on the matrix cores (csrc/sa_bn_mfma.hip) -- channel-first features take the VALU passes; sa1
+    (fp32) runs on the matrix cores, ``*_valu`` forces its VALU passes."""
     import oracle as O
     import dvcp
     from dvcp import batchnorm, ops
     from tests_helpers import randomize_bn
-    rows = table.endswith("_rows")
-    table = table.replace("_rows", "")
+    rows, valu = table.endswith("_rows"), table.endswith("_valu")
+    table = table.replace("_rows", "").replace("_valu", "")
+    if valu:
+        monkeypatch.setattr(batchnorm, "USE_MFMA", False)
+    want_mfma = rows or (table in ("sa1", "sa1_normals") and not valu)
     g = torch.Generator().manual_seed(["sa1", "sa1_normals", "sa1_normals_f64", "sa2", "sa3"].index(table) + 400)
     cin, mlp, radius, ns, xyz, feat = _sa_case(table, g)
     B, _, N = xyz.shape
@@ -336,7 +341,7 @@ def test_sa_batch_stats_train_vs_oracle(cuda, table):
     _, ctr = ops.fps(x, S, start.to(cuda), pdim=2)
     count, lst, _ = ops.ball_query(x, ctr, radius, ns_, pdim=2, cdim_pts=2)
     out, st = batchnorm.train_forward(mine, x, ctr, f, count, lst, ns_)
-    assert bool(st.get("mfma")) == rows
+    assert bool(st.get("mfma")) == want_mfma
     torch.testing.assert_close(out.permute(0, 2, 1).cpu(), out_o.detach(), rtol=1e-4, atol=1e-4)
     for i, (bm, br) in enumerate(zip(mine.mlp_bns, ref.mlp_bns)):
         torch.testing.assert_close(bm.running_mean.cpu(), br.running_mean, rtol=1e-4, atol=1e-6)
@@ -697,12 +702,29 @@ def test_direct_module_calls_keep_or_refuse_gradients(cuda):
 
 
 def test_train_mode_forward_without_backward_keeps_no_zrows(cuda, monkeypatch):
-    """Batch-statistics forward with no backward to follow (under no_grad): no statistics pass is
-    asked for the per-entry z rows (several GB per layer at C3); with autograd the last pass of
-    every layer writes them for the backward."""
+    """Batch-statistics forward with no backward to follow (under no_grad): no statistics pass of
+    the VALU path is asked for the per-entry z rows (several GB per layer at C3); with autograd the
+    last pass of every layer writes them for the backward.  By default the extractor's
+    three tables run on the matrix cores, which keep nothing per entry."""
     import dvcp
-    from dvcp import ops
+    from dvcp import batchnorm, ops
     from dvcp.synthetic import make_pairs
+    n_mfma = []
+    real_m = ops.sa_bnm_stats
+
+    def spy_m(*a, **k):
+        n_mfma.append(1)
+        return real_m(*a, **k)
+
+    monkeypatch.setattr(ops, "sa_bnm_stats", spy_m)
+    src0, _, _, _ = make_pairs(2, 2048, seed=96)
+    torch.manual_seed(0)
+    fe0 = dvcp.feat_extraction_layer(use_normal=False, npoint=256).to(cuda).train()
+    _, feat0 = fe0(src0.to(cuda))
+    assert len(n_mfma) == 7         # 3 + 2 + 2 statistics passes, every layer on the matrix cores
+    feat0.sum().backward()
+
+    monkeypatch.setattr(batchnorm, "USE_MFMA", False)
     asked = []
     real = ops.sa_bn_stats
 
@@ -719,7 +741,5 @@ def test_train_mode_forward_without_backward_keeps_no_zrows(cuda, monkeypatch):
     assert asked and not any(asked)
     asked.clear()
     _, feat = fe(src.to(cuda))
-    # sa1's z-row pass; sa2 / sa3 run on the matrix cores (csrc/sa_bn_mfma.hip), which recompute
-    # the MLP in the backward and keep nothing per entry
-    assert sum(asked) == 1
+    assert sum(asked) == 3          # one z-row pass per set-abstraction layer
     feat.sum().backward()
