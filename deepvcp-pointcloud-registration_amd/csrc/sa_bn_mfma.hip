@@ -28,6 +28,9 @@
 // gz2 -> gh1 = gz2 W2 (N) -> gz1 (N) -> dW1 = gz1^T [x].  Products over 16+ channels run as the
 // three-way bf16 split of sa_mlp_mfma.hip (six v_mfma_f32_32x32x16_bf16, fp32-accurate).
 //
+// Statistics are summed per entry in fp64 (z^2 exact): the variance is E[z^2] - E[z]^2, a
+// difference of nearly equal sums wherever |mean| >> std (sa1's first layer sees local
+// coordinates of a few centimetres), and fp32 tile partials cost 5e-4 of the running variance there.
 // Passes: S1 / S2 = the statistics of layer 1 / 2 (fp64 per-wave partials), FWD = the output max
 // with its arg-max entry and that entry's z2 (what routes the backward), B1 = A1, B1 (layer 2's
 // sums come from the routed rows alone, host side), B0A = dW2, db2, B0B = dW1, db1 and the
@@ -321,12 +324,12 @@ __global__ __launch_bounds__(kBnmThreads) __attribute__((amdgpu_waves_per_eu(PAS
         z1_n(z1N, 0.0f);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-          float a1 = 0.0f, a2 = 0.0f;
+          double a1 = 0.0, a2 = 0.0;
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const float z = z1N[mt][r], w = wt(r);
-            a1 += w * z;
-            a2 += w * (z * z);
+            a1 += static_cast<double>(w) * z;
+            a2 += static_cast<double>(w) * (static_cast<double>(z) * z);
           }
           st1[mt] += a1;
           st2[mt] += a2;
@@ -380,12 +383,12 @@ __global__ __launch_bounds__(kBnmThreads) __attribute__((amdgpu_waves_per_eu(PAS
         if constexpr (PASS == kS2) {
 #pragma unroll
           for (int ct = 0; ct < CT; ++ct) {
-            float a1 = 0.0f, a2 = 0.0f;
+            double a1 = 0.0, a2 = 0.0;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const float z = z2N[ct][r], w = wt(r);
-              a1 += w * z;
-              a2 += w * (z * z);
+              a1 += static_cast<double>(w) * z;
+              a2 += static_cast<double>(w) * (static_cast<double>(z) * z);
             }
             st1[ct] += a1;
             st2[ct] += a2;
@@ -494,13 +497,13 @@ __global__ __launch_bounds__(kBnmThreads) __attribute__((amdgpu_waves_per_eu(PAS
         if constexpr (PASS == kB1) {
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
-            float a1 = 0.0f, a2 = 0.0f;
+            double a1 = 0.0, a2 = 0.0;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const float z = z1N[mt][r], w = wt(r);
               const float gy = z * s1n[mt] + t1n[mt] > 0.0f ? gh1[mt][r] : 0.0f;
-              a1 += w * gy;
-              a2 += w * (gy * ((z - mu1n[mt]) * is1n[mt]));
+              a1 += static_cast<double>(w) * gy;
+              a2 += static_cast<double>(w) * (gy * ((z - mu1n[mt]) * is1n[mt]));
             }
             st1[mt] += a1;
             st2[mt] += a2;
@@ -779,12 +782,12 @@ __global__ __launch_bounds__(kBnmThreads) __attribute__((amdgpu_waves_per_eu(PAS
         return z;
       };
       auto sums = [&](const f32x16& z) {
-        float a1 = 0.0f, a2 = 0.0f;
+        double a1 = 0.0, a2 = 0.0;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float w = wt(r);
-          a1 += w * z[r];
-          a2 += w * (z[r] * z[r]);
+          a1 += static_cast<double>(w) * z[r];
+          a2 += static_cast<double>(w) * (static_cast<double>(z[r]) * z[r]);
         }
         st1 += a1;
         st2 += a2;
@@ -865,13 +868,13 @@ __global__ __launch_bounds__(kBnmThreads) __attribute__((amdgpu_waves_per_eu(PAS
         for (int r = 0; r < 16; ++r) gh2N[r] = 0.0f;
         gh2N = bnm_mfma6(pg0, frag(L.w3t[0]), gh2N);
         gh2N = bnm_mfma6(pg1, frag(L.w3t[1]), gh2N);
-        float a1 = 0.0f, a2 = 0.0f;
+        double a1 = 0.0, a2 = 0.0;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float z = z2N[r], w = wt(r);
           const float gy = z * n2.s + n2.t > 0.0f ? gh2N[r] : 0.0f;
-          a1 += w * gy;
-          a2 += w * (gy * ((z - n2.mu) * n2.is));
+          a1 += static_cast<double>(w) * gy;
+          a2 += static_cast<double>(w) * (gy * ((z - n2.mu) * n2.is));
         }
         st1 += a1;
         st2 += a2;
@@ -896,13 +899,13 @@ __global__ __launch_bounds__(kBnmThreads) __attribute__((amdgpu_waves_per_eu(PAS
       gh1N = bnm_mfma6(piece(gz2T, 0), frag(L.w2t), gh1N);
       const f32x16 z1N = z1_n();
       if constexpr (PASS == kB1) {
-        float a1 = 0.0f, a2 = 0.0f;
+        double a1 = 0.0, a2 = 0.0;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float z = z1N[r], w = wt(r);
           const float gy = z * n1.s + n1.t > 0.0f ? gh1N[r] : 0.0f;
-          a1 += w * gy;
-          a2 += w * (gy * ((z - n1.mu) * n1.is));
+          a1 += static_cast<double>(w) * gy;
+          a2 += static_cast<double>(w) * (gy * ((z - n1.mu) * n1.is));
         }
         st1 += a1;
         st2 += a2;
@@ -1071,6 +1074,28 @@ __global__ __launch_bounds__(1024) void bnm_sum_kernel(const PT* __restrict__ pa
   }
 }
 
+// Slice sums of the partial rows: block (column group, slice s) sums rows [s per, (s + 1) per) in
+// a fixed order into tmp[s] (fp64); bnm_sum_kernel then adds the slices in order.  (One workgroup
+// per 64 columns over thousands of rows was latency-bound: 0.13 ms for a 128-column statistic.)
+template <typename PT>
+__global__ __launch_bounds__(1024) void bnm_slice_kernel(const PT* __restrict__ part, int nrows, int P, int per,
+                                                         double* __restrict__ tmp) {
+  __shared__ double sl[16][64];
+  const int tid = threadIdx.x, c = tid & 63, lane16 = tid >> 6;
+  const int e = blockIdx.x * 64 + c;
+  const int r0 = blockIdx.y * per, r1 = min(nrows, r0 + per);
+  double acc = 0.0;
+  if (e < P)
+    for (int k = r0 + lane16; k < r1; k += 16) acc += static_cast<double>(part[static_cast<int64_t>(k) * P + e]);
+  sl[lane16][c] = acc;
+  __syncthreads();
+  if (tid < 64 && e < P) {
+    double t = 0.0;
+    for (int k = 0; k < 16; ++k) t += sl[k][c];
+    tmp[static_cast<int64_t>(blockIdx.y) * P + e] = t;
+  }
+}
+
 // The feature columns of dW1 through the per-point sums: sum_e gz1[e] f[n(e)]^T = sum_n G[n] f[n]^T
 // (G = the segment sums of the gz1 rows, which the feature gradient needs anyway): a product over
 // the B N points instead of the B S nsample entries.  Block k sums points [k per, (k+1) per) into
@@ -1181,19 +1206,34 @@ int bnm_grads_floats(const BnmTable& t) {
   return n;
 }
 
-// Workspace: per-wave partials | (two layers) dW1's xyz / bias sums (C1 x 4) and feature columns
-// (C1 x D) | (backward) keys | gz1 rows | per-point sums G | segsum's own.
+// Workspace: per-wave partials | the reduction's slice sums | (two layers) dW1's xyz / bias sums
+// (C1 x 4) and feature columns (C1 x D) | (backward) keys | gz1 rows | per-point sums G | segsum's own.
 constexpr int kGtfBlocks = 512;
-int64_t bnm_part_bytes(int64_t centres, const BnmTable& t) {
+constexpr int kSumSlices = 64;
+struct BnmWs {
+  int64_t tmp, xb, fw, total;  // byte offsets; partials at 0
+};
+BnmWs bnm_ws_layout(int64_t centres, const BnmTable& t) {
   const int64_t nw = static_cast<int64_t>(bnm_grid(centres)) * kBnmWaves;
   const int64_t cmax = std::max(std::max(t.C1, t.C2), t.C3);
-  int64_t b = nw * 2 * 2 * cmax * 8;
-  if (t.nlayer == 3) return bnm_align(std::max<int64_t>(b, nw * bnm_grads_floats(t) * 4));
-  b = std::max<int64_t>(b, nw * (t.C2 * t.C1 + t.C2) * 4);
-  b = std::max<int64_t>(b, nw * 4 * t.C1 * 4);
-  b = std::max<int64_t>(b, static_cast<int64_t>(kGtfBlocks) * t.C1 * t.D * 4);
-  return bnm_align(b) + bnm_align(t.C1 * 4 * 4) + bnm_align(static_cast<int64_t>(t.C1) * t.D * 4);
+  int64_t b = nw * 2 * 2 * cmax * 8, pmax = 2 * cmax;
+  if (t.nlayer == 3) {
+    b = std::max<int64_t>(b, nw * bnm_grads_floats(t) * 4);
+    pmax = std::max<int64_t>(pmax, bnm_grads_floats(t));
+  } else {
+    b = std::max<int64_t>(b, nw * (t.C2 * t.C1 + t.C2) * 4);
+    b = std::max<int64_t>(b, nw * 4 * t.C1 * 4);
+    b = std::max<int64_t>(b, static_cast<int64_t>(kGtfBlocks) * t.C1 * t.D * 4);
+    pmax = std::max<int64_t>(std::max<int64_t>(pmax, t.C2 * t.C1 + t.C2), static_cast<int64_t>(t.C1) * t.D);
+  }
+  BnmWs w;
+  w.tmp = bnm_align(b);
+  w.xb = w.tmp + bnm_align(kSumSlices * pmax * 8);
+  w.fw = w.xb + bnm_align(t.C1 * 4 * 4);
+  w.total = w.fw + bnm_align(static_cast<int64_t>(t.C1) * t.D * 4);
+  return w;
 }
+int64_t bnm_part_bytes(int64_t centres, const BnmTable& t) { return bnm_ws_layout(centres, t).total; }
 int64_t bnm_feat_bytes(int64_t E, int64_t npts, int C1) {
   const int64_t seg = segment_sum_workspace_bytes(E, npts);
   return seg < 0 ? -1 : bnm_align(E * 4) + bnm_align(E * C1 * 4) + bnm_align(npts * C1 * 4) + seg;
@@ -1212,10 +1252,19 @@ int bnm3_launch(const BnmArgs& a, hipStream_t st) {
   return launch_status("dvcp_sa_bnm_pass");
 }
 
-int bnm_sums(const void* ws, int nw, int C, double* sums, hipStream_t st) {
-  hipLaunchKernelGGL((bnm_sum_kernel<double, double>), dim3(ceil_div(2 * C, 64)), dim3(1024), 0, st,
-                     static_cast<const double*>(ws), 2 * nw, 2 * C, sums);
+// out[e] = sum of the nrows partial rows (P columns) in a fixed order: slice sums into the
+// workspace's tmp area, then the slices in order.
+template <typename PT, typename OT>
+int bnm_reduce(const PT* part, int nrows, int P, OT* out, void* ws, int64_t tmp_off, hipStream_t st) {
+  double* tmp = reinterpret_cast<double*>(static_cast<char*>(ws) + tmp_off);
+  const int per = (nrows + kSumSlices - 1) / kSumSlices;
+  const int ns = (nrows + per - 1) / per;
+  hipLaunchKernelGGL((bnm_slice_kernel<PT>), dim3(ceil_div(P, 64), ns), dim3(1024), 0, st, part, nrows, P, per, tmp);
+  hipLaunchKernelGGL((bnm_sum_kernel<double, OT>), dim3(ceil_div(P, 64)), dim3(1024), 0, st, tmp, ns, P, out);
   return launch_status("dvcp_sa_bnm_pass(sum)");
+}
+int bnm_sums(void* ws, int nw, int C, double* sums, int64_t tmp_off, hipStream_t st) {
+  return bnm_reduce<double, double>(static_cast<const double*>(ws), 2 * nw, 2 * C, sums, ws, tmp_off, st);
 }
 
 // ABI pass codes: 1..3 statistics of layer l, 10 forward, 20 + l backward sums of layer l, 30 gradients
@@ -1223,11 +1272,12 @@ template <int D, int C1, int C2>
 int bnm_pass2(int pass, BnmArgs a, void* ws, double* sums, float* grads, float* gfeat, hipStream_t st) {
   const int64_t centres = static_cast<int64_t>(a.B) * a.S;
   const int nw = bnm_grid(centres) * kBnmWaves;
+  const BnmWs L = bnm_ws_layout(centres, BnmTable{2, D, C1, C2, 0});
   a.part = ws;
   if (pass == 1 || pass == 2 || pass == 21) {
     const int e = pass == 1 ? bnm_launch<D, C1, C2, kS1>(a, st)
                             : (pass == 2 ? bnm_launch<D, C1, C2, kS2>(a, st) : bnm_launch<D, C1, C2, kB1>(a, st));
-    return e ? e : bnm_sums(ws, nw, pass == 2 ? C2 : C1, sums, st);
+    return e ? e : bnm_sums(ws, nw, pass == 2 ? C2 : C1, sums, L.tmp, st);
   }
   if (pass == 10) return bnm_launch<D, C1, C2, kFwd>(a, st);
   if (pass != 30) {
@@ -1238,32 +1288,25 @@ int bnm_pass2(int pass, BnmArgs a, void* ws, double* sums, float* grads, float* 
   // their per-point segment sums G; dW1's feature columns G^T F; the feature gradient
   constexpr int C0 = 3 + D;
   constexpr int P1 = C1 * C0 + C1, P2 = C2 * C1 + C2;
-  const BnmTable tb{2, D, C1, C2, 0};
   if (int e = bnm_launch<D, C1, C2, kB0A>(a, st)) return e;
-  hipLaunchKernelGGL((bnm_sum_kernel<float, float>), dim3(ceil_div(P2, 64)), dim3(1024), 0, st,
-                     static_cast<const float*>(ws), nw, P2, grads + P1);
-  if (int e = launch_status("dvcp_sa_bnm_pass(dW2)")) return e;
+  if (int e = bnm_reduce<float, float>(static_cast<const float*>(ws), nw, P2, grads + P1, ws, L.tmp, st)) return e;
   const int64_t E = centres * a.nsample, npts = static_cast<int64_t>(a.B) * a.N;
-  const int64_t pb = bnm_part_bytes(centres, tb);
   char* w8 = static_cast<char*>(ws);
-  float* xb = reinterpret_cast<float*>(w8 + pb - bnm_align(C1 * 4 * 4) - bnm_align(static_cast<int64_t>(C1) * D * 4));
-  float* fw = reinterpret_cast<float*>(w8 + pb - bnm_align(static_cast<int64_t>(C1) * D * 4));
-  char* fws = w8 + pb;
+  float* xb = reinterpret_cast<float*>(w8 + L.xb);
+  float* fw = reinterpret_cast<float*>(w8 + L.fw);
+  char* fws = w8 + L.total;
   a.fkeys = reinterpret_cast<uint32_t*>(fws);
   a.frows = reinterpret_cast<float*>(fws + bnm_align(E * 4));
   float* G = reinterpret_cast<float*>(fws + bnm_align(E * 4) + bnm_align(E * C1 * 4));
   void* segws = fws + bnm_align(E * 4) + bnm_align(E * C1 * 4) + bnm_align(npts * C1 * 4);
   if (int e = bnm_launch<D, C1, C2, kB0B>(a, st)) return e;
-  hipLaunchKernelGGL((bnm_sum_kernel<float, float>), dim3(ceil_div(4 * C1, 64)), dim3(1024), 0, st,
-                     static_cast<const float*>(ws), nw, 4 * C1, xb);
-  if (int e = launch_status("dvcp_sa_bnm_pass(dW1 xyz)")) return e;
+  if (int e = bnm_reduce<float, float>(static_cast<const float*>(ws), nw, 4 * C1, xb, ws, L.tmp, st)) return e;
   if (int e = segment_sum(a.fkeys, a.frows, E, npts, C1, G, segws, st)) return e;
   const int64_t per = (npts + kGtfBlocks - 1) / kGtfBlocks;
   const int nblk = static_cast<int>((npts + per - 1) / per);
   hipLaunchKernelGGL((bnm_gtf_kernel<D, C1>), dim3(nblk), dim3(256), 0, st, G, a.feat, a.fb, a.fn, a.N, npts, per,
                      static_cast<float*>(ws));
-  hipLaunchKernelGGL((bnm_sum_kernel<float, float>), dim3(ceil_div(C1 * D, 64)), dim3(1024), 0, st,
-                     static_cast<const float*>(ws), nblk, C1 * D, fw);
+  if (int e = bnm_reduce<float, float>(static_cast<const float*>(ws), nblk, C1 * D, fw, ws, L.tmp, st)) return e;
   hipLaunchKernelGGL((bnm_dw1_kernel<D, C1>), dim3(1), dim3(256), 0, st, xb, fw, grads);
   if (int e = launch_status("dvcp_sa_bnm_pass(dW1)")) return e;
   if (gfeat) {
@@ -1276,7 +1319,9 @@ int bnm_pass2(int pass, BnmArgs a, void* ws, double* sums, float* grads, float* 
 
 template <int D>
 int bnm_pass3(int pass, BnmArgs a, void* ws, double* sums, float* grads, hipStream_t st) {
-  const int nw = bnm_grid(static_cast<int64_t>(a.B) * a.S) * kBnmWaves;
+  const int64_t centres = static_cast<int64_t>(a.B) * a.S;
+  const int nw = bnm_grid(centres) * kBnmWaves;
+  const BnmWs L = bnm_ws_layout(centres, BnmTable{3, D, 16, 16, 32});
   a.part = ws;
   int e = DVCP_OK, C = 16;
   switch (pass) {
@@ -1289,15 +1334,13 @@ int bnm_pass3(int pass, BnmArgs a, void* ws, double* sums, float* grads, hipStre
     case 30: {
       if (int e2 = bnm3_launch<D, kB0A>(a, st)) return e2;
       const int P = bnm_grads_floats(BnmTable{3, D, 16, 16, 32});
-      hipLaunchKernelGGL((bnm_sum_kernel<float, float>), dim3(ceil_div(P, 64)), dim3(1024), 0, st,
-                         static_cast<const float*>(ws), nw, P, grads);
-      return launch_status("dvcp_sa_bnm_pass(grads)");
+      return bnm_reduce<float, float>(static_cast<const float*>(ws), nw, P, grads, ws, L.tmp, st);
     }
     default:
       set_error("dvcp_sa_bnm_pass: pass %d is not one of 1, 2, 3, 10, 21, 22, 30 for a three-layer table", pass);
       return DVCP_EINVAL;
   }
-  return e ? e : bnm_sums(ws, nw, C, sums, st);
+  return e ? e : bnm_sums(ws, nw, C, sums, L.tmp, st);
 }
 
 }  // namespace
