@@ -29,6 +29,12 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef DVCP_DFE_SPLIT3
 #define DVCP_DFE_SPLIT3 1
 #endif
+// DVCP_DFE_ABL (timing experiments only, wrong results): 1 no gather, 2 no MFMA, 3 no weights.
+// Round 4 at C3 (0.68 ms): 0.51, 0.47, 0.67 ms -- neither the gathers nor the matrix cores alone
+// bound the kernel.  (Contiguous candidate runs per wave measured 0.71: not kept.)
+#ifndef DVCP_DFE_ABL
+#define DVCP_DFE_ABL 0
+#endif
 
 // x = x0 + x1 + x2 exactly in three bf16 pieces; a.b from the six significant piece products
 // (the fp32-accurate split of sa_mlp_mfma.hip, whose header gives the error bound)
@@ -340,7 +346,11 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
   auto gather = [&](const Cand& c, int nraw, Gathered& G) {
     const int bb = pair_of(c);
     const int gc = bb * Q + (c.li < total ? c.q : last.q);
+#if DVCP_DFE_ABL == 1  // (ablation builds only: every gather reads the lane's fixed row)
+    const int n = r32 + 0 * nraw;
+#else
     const int n = nraw < 0 ? 0 : (nraw >= M ? M - 1 : nraw);
+#endif
     if constexpr (sizeof(FT) == 4) {
       const float4* fr = reinterpret_cast<const float4*>(feat + (static_cast<int64_t>(bb) * M + n) * 32 + 16 * h);
 #pragma unroll
@@ -365,6 +375,10 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
   auto weights = [&](float dj, int buf) {
     // sum of the 32 distances: quad and row rotations by DPP (no LDS round trips), then the two
     // 16-lane row totals of the lower half read back and added (the upper half mirrors it)
+#if DVCP_DFE_ABL == 3  // (ablation builds only: no distance sum / division)
+    L.w[wave][buf][r32] = dj;
+    return;
+#endif
     double v = static_cast<double>(dj);
     v = dpp_add_f64<0xB1>(v);   // quad_perm [1,0,3,2]
     v = dpp_add_f64<0x4E>(v);   // quad_perm [2,3,0,1]
@@ -427,11 +441,15 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
     f32x16 a;
 #pragma unroll
     for (int r = 0; r < 16; ++r) a[r] = 0.0f;
+#if DVCP_DFE_ABL == 2  // (ablation builds only: no MFMA, the operands still consumed)
+    a[0] = X.x0 + X.x1 + static_cast<float>(X.s[0].p0[0]) + static_cast<float>(X.s[1].p2[7]) + L.ex[0][lane + zo];
+#else
     a = __builtin_amdgcn_mfma_f32_32x32x2f32(X.x0, L.ex[0][lane + zo], a, 0, 0, 0);
     a = __builtin_amdgcn_mfma_f32_32x32x2f32(X.x1, L.ex[1][lane + zo], a, 0, 0, 0);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
       a = dfe_mfma_split3(X.s[t], L.es[t][0][lane + zo], L.es[t][1][lane + zo], L.es[t][2][lane + zo], a);
+#endif
     return a;
   };
   auto finish = [&](const Cand& cg, const f32x16& a) {

@@ -540,6 +540,8 @@ constexpr int kSelBufN = 16;
 #ifndef DVCP_KNN_CHUNK
 #define DVCP_KNN_CHUNK 1
 #endif
+// (Round 4 also measured issuing the tile loads of 2 or 3 surviving positions together before
+// their visits: 0.77 / 0.83 against 0.76 ms -- the scan is not waiting on those loads.)
 // DVCP_KNN_SLOAD: an active tile's 16 points reach the wave as scalar loads (the tile index is
 // wave-uniform, the tile is read-only here) instead of one vector load and 48 readlanes; the
 // appends, which index the tile per lane, load their LDS copy from L2 when a lane needs one.
@@ -719,9 +721,9 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
   const float* P = reinterpret_cast<const float*>(sorted) + static_cast<int64_t>(b) * T * kTile * 4;
   // Visit the tile of sorted key `key` (its bound already known not to exceed wkth): the per-lane
   // test, then the distances, the filter and the appends.
-  auto visit = [&](uint32_t key) {
+  // (the tile's float for this lane, loaded by the caller once some lane is active)
+  auto visit_loaded = [&](uint32_t key, float lbq, float v_cur) {
     const int t = static_cast<int>(key & kTileIdBits);
-    const float lbq = hbox_lb2(hbox[t], qx, qy, qz, qx, qy, qz);
     const bool act = live & (lbq <= kth);
 #ifdef DVCP_KNN_DIAG
     ++dg_scanned;
@@ -744,7 +746,6 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
       }
     }
 #else
-    const float v_cur = P[static_cast<int64_t>(t) * (4 * kTile) + lane];
     auto bc = [&](int u) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v_cur), u)); };
 #pragma unroll
     for (int j = 0; j < kTile; ++j) {
@@ -798,6 +799,13 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
       }
       __builtin_amdgcn_wave_barrier();  // (the next active tile rewrites stile)
     }
+  };
+  auto visit = [&](uint32_t key) {
+    const int t = static_cast<int>(key & kTileIdBits);
+    const float lbq = hbox_lb2(hbox[t], qx, qy, qz, qx, qy, qz);
+    float v = 0.0f;
+    if (__ballot(live & (lbq <= kth)) != 0) v = P[static_cast<int64_t>(t) * (4 * kTile) + lane];
+    visit_loaded(key, lbq, v);
   };
 
 #if DVCP_KNN_CHUNK
