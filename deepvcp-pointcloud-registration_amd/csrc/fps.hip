@@ -905,7 +905,11 @@ void fps_select_kernel(PointsView<T> pts, int N, int npoint,
       }
       tl = wave_fmax_nn(tl);
       if (lane == 0) atomicMax(&tb_max, __float_as_uint(tl));
-      if (na < 4u * kSelTarget) f *= 0.85f;  // next round: keep a few hundred points above the floor
+      // next round: keep a few hundred points above the floor.  The decay sets how often a round
+      // lists more than kSelCap points and scans again: 0.85 rescanned in ~20 % of the C3 rounds
+      // (sa1: 74 of 367), 0.9 in ~2 % (6 of 367; sa2 / sa3 37 -> 4 of 302), with the same rounds
+      // (tools/fps_lab/fps_round_sim.py, a CPU model of this round logic; FPS lab: 81 of 382).
+      if (na < 4u * kSelTarget) f *= 0.9f;
       if (wave * kWave < kSelMax) srank[wave * kWave + lane] = 0u;  // (read last by the previous round)
       lds_barrier();
       const float Tb = __uint_as_float(tb_max);

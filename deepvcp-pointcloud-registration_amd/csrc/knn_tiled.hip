@@ -723,7 +723,7 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
   // test, then the distances, the filter and the appends.
   // (the tile's float for this lane, loaded by the caller once some lane is active)
   auto visit_loaded = [&](uint32_t key, float lbq, float v_cur) {
-    const int t = static_cast<int>(key & kTileIdBits);
+    [[maybe_unused]] const int t = static_cast<int>(key & kTileIdBits);  // (DVCP_KNN_SLOAD only)
     const bool act = live & (lbq <= kth);
 #ifdef DVCP_KNN_DIAG
     ++dg_scanned;

@@ -128,11 +128,24 @@ int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, c
                    const int32_t* list, int nsample, const float* params, float* U, int32_t* order, float* out,
                    const int64_t* rows, int Nf, hipStream_t st);
 
+// the three-layer table (sa1) on the matrix cores (sa_mlp_mfma.hip)
+template <typename T, typename FT, int D>
+int launch_sa3_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, const void* c, int64_t cb, int64_t cc,
+                    int64_t cn, int S, int B, const void* feat, int64_t fb, int64_t fd, int64_t fn, const int32_t* count,
+                    const int32_t* list, int nsample, const float* params, float* out, hipStream_t st);
+
+#ifndef DVCP_SA1_MFMA
+#define DVCP_SA1_MFMA 1
+#endif
+
 template <typename T, typename FT, int D, int C1, int C2, int C3>
 static int launch_sa(const void* xyz, int64_t sb, int64_t sc, int64_t sn, const void* c, int64_t cb, int64_t cc,
                      int64_t cn, int S, int B, const void* feat, int64_t fb, int64_t fd, int64_t fn,
                      const int32_t* count, const int32_t* list, int nsample, const float* params, float* out,
                      hipStream_t st) {
+  if constexpr (DVCP_SA1_MFMA && C1 == 16 && C2 == 16 && C3 == 32 && (D == 0 || D == 3))
+    return launch_sa3_mfma<T, FT, D>(xyz, sb, sc, sn, c, cb, cc, cn, S, B, feat, fb, fd, fn, count, list, nsample,
+                                     params, out, st);
   PointsView<T> pv{static_cast<const T*>(xyz), sb, sc, sn};
   PointsView<T> cv{static_cast<const T*>(c), cb, cc, cn};
   FeatView<FT> fv{static_cast<const FT*>(feat), fb, fd, fn};

@@ -1,5 +1,7 @@
 // sa_mlp_mfma.hip -- the two-layer set-abstraction MLPs (sa2: 35-32-64, sa3: 67-64-64;
-// pointnet2_utils.py:122-132 + :195-200 with REF-R R1) on fp32 MFMA (v_mfma_f32_32x32x2_f32).
+// pointnet2_utils.py:122-132 + :195-200 with REF-R R1) on fp32 MFMA (v_mfma_f32_32x32x2_f32), and
+// (sa3_mfma_kernel, further down) the three-layer sa1 table.  A centre without hits (count < 1)
+// gets zeros in every kernel, like the row-per-thread kernel of sa_mlp.hip; no list entry is read.
 //
 // Per centre the grouped rows form a dense batched GEMM chain, rows x C0 -> C1 -> C2 then a max
 // over rows, which is what the matrix cores are for.  One wave per centre; its rows go through in
@@ -39,6 +41,14 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 #ifndef DVCP_SA_SPLIT3
 #define DVCP_SA_SPLIT3 1
+#endif
+// DVCP_SA_PRE_MFMA: the per-point pass U = W1f f + b1 on the fp32 matrix cores (sa_pre_mfma_kernel)
+#ifndef DVCP_SA_PRE_MFMA
+#define DVCP_SA_PRE_MFMA 1
+#endif
+// DVCP_SA_PACK16: the pre-pass kernel packs each centre's rows in 16-row half tiles (see the kernel)
+#ifndef DVCP_SA_PACK16
+#define DVCP_SA_PACK16 1
 #endif
 
 // x = x0 + x1 + x2 exactly (bf16 pieces of eight fp32 values; see the header)
@@ -166,6 +176,84 @@ __global__ __launch_bounds__(256) void sa_pre_kernel(const float* __restrict__ f
   reinterpret_cast<float4*>(U + i * C1)[g] = acc;
 }
 
+// The same per-point pass as a plain GEMM on the fp32 matrix cores (U = F . W1f'^T + b1'): one
+// wave per 32 input points, v_mfma_f32_32x32x2_f32 with k-step s taking input channels s (lane
+// half 0) and s + D/2 (half 1), so each lane reads one contiguous half of its point's feature row;
+// the BN-folded weights are staged once per workgroup as B fragments.  The row-per-thread kernel
+// above read each point's whole row once per 4-channel group and the weights from LDS per FMA
+// (sa3's pass: 67 us per C3 batch for 1.3 GFLOP and 82 MB); the MFMA form is bound by the 82 MB.
+// The accumulation is a k-ordered fp32 chain like the VALU kernel's (the MFMA adds its two
+// k-products per step), within the fp32 tolerance of the SA tests.
+template <int D, int C1>
+__global__ __launch_bounds__(256) void sa_pre_mfma_kernel(const float* __restrict__ feat, int64_t fb, int64_t fn, int N,
+                                                          int B, const float* __restrict__ params,
+                                                          float* __restrict__ U, const int64_t* __restrict__ rows,
+                                                          int Nf) {
+  constexpr int C0 = 3 + D, MT = C1 / 32, KS = D / 2;
+  static_assert(D % 8 == 0 && C1 % 32 == 0, "MFMA tiling");
+  __shared__ float wf[MT][KS][64];  // B fragment: lane (o, h) of k-step s -> s1_o W1[o][3 + s + h D/2]
+  __shared__ float bias[C1];         // folded bias (the accumulators' channel is the lane)
+  const float* W1 = params;
+  const float* pb1 = W1 + C1 * C0;
+  const float* ps1 = pb1 + C1;
+  const float* pt1 = ps1 + C1;
+  for (int i = threadIdx.x; i < MT * KS * 64; i += blockDim.x) {
+    const int l = i % 64, s = (i / 64) % KS, mt = i / (64 * KS), o = 32 * mt + (l & 31);
+    wf[mt][s][l] = W1[o * C0 + 3 + s + (l >> 5) * (D / 2)] * ps1[o];
+  }
+  for (int c = threadIdx.x; c < C1; c += blockDim.x)
+    bias[c] = static_cast<float>(static_cast<double>(pb1[c]) * ps1[c] + static_cast<double>(pt1[c]));
+  __syncthreads();
+  const int lane = threadIdx.x & 63, h = lane >> 5, r32 = lane & 31;
+  const int64_t total = static_cast<int64_t>(B) * N;
+  const int64_t ntiles = (total + 31) / 32;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); t < ntiles;
+       t += static_cast<int64_t>(gridDim.x) * 4) {
+    // this lane's point (row r32 of the tile) and its half of the feature row
+    const int64_t i = t * 32 + r32;
+    const int64_t ic = i < total ? i : total - 1;
+    const int b = static_cast<int>(ic / N), n = static_cast<int>(ic % N);
+    int64_t src = n;
+    if (rows) {
+      const int64_t r = rows[ic];
+      src = r < 0 ? 0 : (r >= Nf ? Nf - 1 : r);
+    }
+    const float4* fr = reinterpret_cast<const float4*>(feat + b * fb + src * fn + h * (D / 2));
+    float x[KS];
+#pragma unroll
+    for (int v = 0; v < KS / 4; ++v) {
+      const float4 q = fr[v];
+      x[4 * v] = q.x;
+      x[4 * v + 1] = q.y;
+      x[4 * v + 2] = q.z;
+      x[4 * v + 3] = q.w;
+    }
+    int zo = 0;  // opaque zero: the fragments are read per tile, not hoisted into registers
+    asm volatile("" : "+v"(zo));
+    f32x16 acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const float bc = bias[32 * mt + r32 + zo];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mt][r] = bc;
+    }
+    // H (32 points x C1): A = the feature rows (lane = point), B = the weight fragments (lane = channel)
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(x[s], wf[mt][s][lane + zo], acc[mt], 0, 0, 0);
+    // D[point][channel]: lane = channel, register r = point acc_row(r, h)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t ip = t * 32 + acc_row(r, h);
+      if (ip < total)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) U[ip * C1 + 32 * mt + r32] = acc[mt][r];
+    }
+  }
+}
+
 // Centres of each cloud in 12-bit Hilbert-cell order (one workgroup per cloud), for the MFMA
 // kernel's visiting order.  The order changes only which wave computes which centre.
 template <typename T>
@@ -184,7 +272,7 @@ __global__ __launch_bounds__(kBuildThreads) void sa_order_kernel(PointsView<T> c
   morton_sort(S, get, [&](int pos, int i, const float (&)[3]) { o[pos] = i; }, lo, hi, bins, wsum);
 }
 
-template <typename T, int D, int C1, int C2, bool PRE>
+template <typename T, int D, int C1, int C2, bool PRE, bool PACK = false>
 __global__ __launch_bounds__(kMfmaWaves * kWave) __attribute__((amdgpu_waves_per_eu(3))) void sa_mlp_mfma_kernel(
     PointsView<T> pts, PointsView<T> ctr, int S, int B, const float* __restrict__ feat, int64_t fb, int64_t fn,
     const int32_t* __restrict__ count, const int32_t* __restrict__ list, int nsample,
@@ -287,7 +375,7 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) __attribute__((amdgpu_waves_per
   };
   for (int64_t qc = q0; qc < total; qc += 64 * qs) {
     const int64_t qm = qc + lane * qs;
-    int m_b = 0, m_rows = 1;
+    int m_b = 0, m_rows = 0;  // rows 0: no hit (the centre's output is 0)
     int64_t m_fc = 0;
     T m_cx = T(0), m_cy = T(0), m_cz = T(0);
     if (qm < total) {
@@ -298,7 +386,7 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) __attribute__((amdgpu_waves_per
       const int c = order ? order[q] : static_cast<int>(q % S);
       m_fc = static_cast<int64_t>(m_b) * S + c;
       const int r = count[m_fc];
-      m_rows = r < 1 ? 1 : (r > nsample ? nsample : r);
+      m_rows = r < 1 ? 0 : (r > nsample ? nsample : r);
       m_cx = ctr.at(m_b, 0, c);
       m_cy = ctr.at(m_b, 1, c);
       m_cz = ctr.at(m_b, 2, c);
@@ -309,8 +397,120 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) __attribute__((amdgpu_waves_per
       const int64_t fcj = lane_bcast(m_fc, j);
       const int rj = lane_bcast(m_rows, j);
       const int row = n0 + r32;
-      return list[fcj * nsample + (row < rj ? row : 0)];
+      return rj == 0 ? 0 : list[fcj * nsample + (row < rj ? row : 0)];
     };
+    constexpr bool BZ = PRE && DVCP_SA_SPLIT3;
+    if constexpr (PACK) {
+      static_assert(!PACK || (PRE && DVCP_SA_SPLIT3), "row packing runs on the split-3 pre-pass path");
+      // Rows in 16-row half tiles: a tile takes the next two half tiles of the wave's centres in
+      // order (rows 0-15 are accumulator registers 0..7 of both lane halves, rows 16-31 registers
+      // 8..15), so a centre wastes at most 15 padded rows instead of 31, and the two halves' maxima
+      // fold into running per-centre maxima in order.  Padded rows repeat the centre's first hit.
+      int js = 0, hs = 0;  // the next half tile: centre js, half hs
+      auto nh_of = [&](int jj) { return max(1, (lane_bcast(m_rows, jj) + 15) >> 4); };
+      int nhj = ncen > 0 ? nh_of(0) : 0;
+      int runj = -1;
+      float run[CT];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) run[ct] = 0.0f;
+      auto flush = [&]() {
+        const int64_t fcr = lane_bcast(m_fc, runj);
+        const bool empty = lane_bcast(m_rows, runj) == 0;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+          if (h == 0) out[fcr * C2 + 32 * ct + r32] = empty ? 0.0f : fmaxf(run[ct] + b2[ct], 0.0f);
+      };
+      auto fold = [&](int jj, const float (&m)[CT]) {
+        if (jj != runj) {
+          if (runj >= 0) flush();
+          runj = jj;
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct) run[ct] = m[ct];
+        } else {
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct) run[ct] = fmaxf(run[ct], m[ct]);
+        }
+      };
+      while (js < ncen) {
+        const int jA = js, hA = hs;
+        if (++hs >= nhj) {
+          hs = 0;
+          if (++js < ncen) nhj = nh_of(js);
+        }
+        const bool hasB = js < ncen;
+        const int jB = hasB ? js : jA, hB = hasB ? hs : hA;
+        if (hasB && ++hs >= nhj) {
+          hs = 0;
+          if (++js < ncen) nhj = nh_of(js);
+        }
+        int zo = 0;
+        asm volatile("" : "+v"(zo));
+        const bool sB = r32 >= 16;  // this lane's point: row r32 of the tile
+        const int b = sB ? lane_bcast(m_b, jB) : lane_bcast(m_b, jA);
+        const int64_t fc = sB ? lane_bcast(m_fc, jB) : lane_bcast(m_fc, jA);
+        const int rows = sB ? lane_bcast(m_rows, jB) : lane_bcast(m_rows, jA);
+        const T cx = sB ? lane_bcast(m_cx, jB) : lane_bcast(m_cx, jA);
+        const T cy = sB ? lane_bcast(m_cy, jB) : lane_bcast(m_cy, jA);
+        const T cz = sB ? lane_bcast(m_cz, jB) : lane_bcast(m_cz, jA);
+        const int row = 16 * (sB ? hB : hA) + (r32 & 15);
+        const int n = rows == 0 ? 0 : list[fc * nsample + (row < rows ? row : 0)];
+        f32x16 acc1[MT];
+        const float4* ur = reinterpret_cast<const float4*>(U + b * ub + static_cast<int64_t>(n) * C1 + 4 * h);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float4 u = ur[8 * mt + 2 * i];
+            acc1[mt][4 * i] = u.x;
+            acc1[mt][4 * i + 1] = u.y;
+            acc1[mt][4 * i + 2] = u.z;
+            acc1[mt][4 * i + 3] = u.w;
+          }
+        const float dx = static_cast<float>(pts.at(b, 0, n) - cx);
+        const float dy = static_cast<float>(pts.at(b, 1, n) - cy);
+        const float dz = static_cast<float>(pts.at(b, 2, n) - cz);
+        const float x0 = h == 0 ? dx : dy, x1 = h == 0 ? dz : 0.0f;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          acc1[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(L.wx[mt][0][lane + zo], x0, acc1[mt], 0, 0, 0);
+          acc1[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(L.wx[mt][1][lane + zo], x1, acc1[mt], 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc1[mt][r] = acc1[mt][r] > 0.0f ? acc1[mt][r] : 0.0f;
+        }
+        f32x16 acc2[CT];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc2[ct][r] = 0.0f;
+#pragma unroll
+        for (int st = 0; st < Sh::KB; ++st) {
+          float x[8];
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) x[jj] = acc1[st / 2][8 * (st % 2) + jj];
+          const Split3 a = split3(x);
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct)
+            acc2[ct] = mfma_split3(a, L.w2s[ct][st][0][lane + zo], L.w2s[ct][st][1][lane + zo],
+                                   L.w2s[ct][st][2][lane + zo], acc2[ct]);
+        }
+        float mA[CT], mB[CT];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          float a0 = acc2[ct][0], a1 = acc2[ct][8];
+#pragma unroll
+          for (int r = 1; r < 8; ++r) {
+            a0 = fmaxf(a0, acc2[ct][r]);
+            a1 = fmaxf(a1, acc2[ct][8 + r]);
+          }
+          mA[ct] = fmaxf(a0, __shfl_xor(a0, 32, kWave));
+          mB[ct] = fmaxf(a1, __shfl_xor(a1, 32, kWave));
+        }
+        fold(jA, mA);
+        if (hasB) fold(jB, mB);
+      }
+      if (runj >= 0) flush();
+      continue;
+    }
     int n_next = list_entry(0, 0);
   for (int j = 0; j < ncen; ++j) {
     const int b = lane_bcast(m_b, j);
@@ -320,7 +520,6 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) __attribute__((amdgpu_waves_per
     // PRE with the split layer 2 (BZ): the accumulators start from zero (an inline-constant C
     // operand, no 32 register moves per tile) and the bias is added once to the maximum:
     // max_i fl(a_i + b) = fl(max_i a_i + b) (rounding is monotone), then the ReLU.
-    constexpr bool BZ = PRE && DVCP_SA_SPLIT3;
     float mx[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) mx[ct] = BZ ? -__builtin_huge_valf() : 0.0f;  // else post-ReLU values are >= +0
@@ -449,6 +648,253 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) __attribute__((amdgpu_waves_per
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The three-layer table (sa1: 3-16-16-32 on xyz, 6-16-16-32 with normals; deep_feat_extraction.py:19,
+// pointnet2_utils.py:122-132 + :195-200) on the matrix cores.  The row-per-thread kernel
+// (sa_mlp.hip) spends ~816 fp32 FMAs and 32 LDS atomics per grouped row; here a wave takes 32 rows
+// (two 16-row half tiles, as the two-layer kernel's PACK path) through three chained MFMAs whose
+// accumulators feed the next layer in place:
+//   layer 1, fp32 32x32x2:       H1^T (32 ch x 32 rows) = W1 (32 x C0) . X^T, channels 16..31 zero
+//        (A: lane = output channel, one input channel per lane half and k-step; B: lane = row)
+//   layer 2, bf16 32x32x16 x 6:  H2^T = W2 (32 x 16) . H1^T -- the B operand (lane = row, k in
+//        registers) is layer 1's accumulator registers 0..7 as they stand: k-slot 8h + r of lane
+//        half h is channel acc_row(r, h); W2's A fragment is stored in that channel order
+//   layer 3, bf16 32x32x16 x 6:  H3 (32 rows x 32 ch) = H2 . W3^T -- the A operand (lane = row, k
+//        in registers) is again layer 2's registers 0..7, W3^T's B fragment in the same order
+// Layer 3's accumulator has channels on lanes and rows in registers: rows 0-15 (the first half
+// tile) are registers 0..7 of both lane halves, rows 16-31 registers 8..15, so each half tile's
+// maximum is a per-lane max plus one exchange between lane halves.  BN (eval) is folded into the
+// weights and biases, (W x + b) s + t = (s W) x + (s b + t); layer 3's bias and ReLU go after the
+// maximum (max_i fl(a_i + b) = fl(max_i a_i + b), rounding is monotone).  Layers 2 and 3 keep fp32
+// accuracy through the three-way bf16 split of the header.  A centre without hits (count < 1:
+// the reference would gather index N, :104) gets zeros, as the row-per-thread kernel gives it.
+struct Sa3Lds {
+  float w1[3][64];   // layer-1 A fragment per k-step: lane (o, kh) -> s1_o W1[o][2 s + kh]  (o < 16)
+  bf16x8 w2[3][64];  // layer-2 A fragment pieces: lane (o, kh), element r -> s2_o W2[o][acc_row(r, kh)]
+  bf16x8 w3[3][64];  // layer-3 B fragment pieces: lane (o, kh), element r -> s3_o W3[o][acc_row(r, kh)]
+  float b1[2][8];    // folded biases of layers 1, 2 by [lane half][accumulator register]
+  float b2[2][8];
+};
+
+template <typename T, typename FT, int D>
+__global__ __launch_bounds__(kMfmaWaves * kWave) void sa3_mfma_kernel(
+    PointsView<T> pts, PointsView<T> ctr, int S, int B, const FT* __restrict__ feat, int64_t fb, int64_t fd, int64_t fn,
+    const int32_t* __restrict__ count, const int32_t* __restrict__ list, int nsample, const float* __restrict__ params,
+    float* __restrict__ out, int xcd) {
+  constexpr int C0 = 3 + D, C1 = 16, C2 = 16, C3 = 32;
+  constexpr int KS = (C0 + 1) / 2;  // layer-1 k-steps: input channels (2 s, 2 s + 1) on lane halves (0, 1)
+  static_assert(D == 0 || D == 3, "sa1 tables");
+  __shared__ Sa3Lds L;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
+  const float* W1 = params;
+  const float* pb1 = W1 + C1 * C0;
+  const float* ps1 = pb1 + C1;
+  const float* pt1 = ps1 + C1;
+  const float* W2 = pt1 + C1;
+  const float* pb2 = W2 + C2 * C1;
+  const float* ps2 = pb2 + C2;
+  const float* pt2 = ps2 + C2;
+  const float* W3 = pt2 + C2;
+  const float* pb3 = W3 + C3 * C2;
+  const float* ps3 = pb3 + C3;
+  const float* pt3 = ps3 + C3;
+  auto fold_bias = [](float b, float s, float t) {
+    return static_cast<float>(static_cast<double>(b) * s + static_cast<double>(t));
+  };
+  for (int i = tid; i < KS * 64; i += blockDim.x) {
+    const int l = i % 64, s = i / 64, o = l & 31, c = 2 * s + (l >> 5);
+    L.w1[s][l] = (o < C1 && c < C0) ? W1[o * C0 + c] * ps1[o] : 0.0f;
+  }
+  if (tid < 64) {
+    const int o = tid & 31, kh = tid >> 5;
+    float a[8], w[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      a[r] = o < C2 ? W2[o * C1 + acc_row(r, kh)] * ps2[o] : 0.0f;
+      w[r] = W3[o * C2 + acc_row(r, kh)] * ps3[o];
+    }
+    const Split3 sa = split3(a), sw = split3(w);
+    L.w2[0][tid] = sa.p0;
+    L.w2[1][tid] = sa.p1;
+    L.w2[2][tid] = sa.p2;
+    L.w3[0][tid] = sw.p0;
+    L.w3[1][tid] = sw.p1;
+    L.w3[2][tid] = sw.p2;
+  } else if (tid < 80) {
+    const int kh = (tid - 64) >> 3, r = tid & 7, c = acc_row(r, kh);
+    L.b1[kh][r] = fold_bias(pb1[c], ps1[c], pt1[c]);
+    L.b2[kh][r] = fold_bias(pb2[c], ps2[c], pt2[c]);
+  }
+  const float b3 = fold_bias(pb3[r32], ps3[r32], pt3[r32]);
+  __syncthreads();
+
+  // centres grid-strided as in sa_mlp_mfma_kernel (xcd != 0: XCD x walks clouds x, x + 8, ...)
+  int64_t total, q0, qs;
+  int xo = 0;
+  if (xcd) {
+    xo = static_cast<int>(blockIdx.x) & 7;
+    total = static_cast<int64_t>((B - xo + 7) / 8) * S;
+    q0 = static_cast<int64_t>(blockIdx.x >> 3) * kMfmaWaves + wave;
+    qs = static_cast<int64_t>(gridDim.x >> 3) * kMfmaWaves;
+  } else {
+    total = static_cast<int64_t>(B) * S;
+    q0 = static_cast<int64_t>(blockIdx.x) * kMfmaWaves + wave;
+    qs = static_cast<int64_t>(gridDim.x) * kMfmaWaves;
+  }
+  auto lane_bcast = [](auto v, int j) {
+    if constexpr (sizeof(v) == 8) {
+      const int64_t u = __builtin_bit_cast(int64_t, v);
+      const int lo = __builtin_amdgcn_readlane(static_cast<int>(u & 0xFFFFFFFF), j);
+      const int hi = __builtin_amdgcn_readlane(static_cast<int>(u >> 32), j);
+      return __builtin_bit_cast(decltype(v), (static_cast<int64_t>(hi) << 32) | static_cast<uint32_t>(lo));
+    } else {
+      return __builtin_bit_cast(decltype(v), __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), j));
+    }
+  };
+  for (int64_t qc = q0; qc < total; qc += 64 * qs) {
+    // this lane's centre of the next 64: cloud, flat index, rows (0: no hit), coordinates
+    const int64_t qm = qc + lane * qs;
+    int m_b = 0, m_rows = 0;
+    int64_t m_fc = 0;
+    T m_cx = T(0), m_cy = T(0), m_cz = T(0);
+    if (qm < total) {
+      const int64_t q = xcd ? (xo + 8 * (qm / S)) * static_cast<int64_t>(S) + qm % S : qm;
+      m_b = static_cast<int>(q / S);
+      m_fc = q;
+      const int r = count[q];
+      m_rows = r < 0 ? 0 : (r > nsample ? nsample : r);
+      const int c = static_cast<int>(q % S);
+      m_cx = ctr.at(m_b, 0, c);
+      m_cy = ctr.at(m_b, 1, c);
+      m_cz = ctr.at(m_b, 2, c);
+    }
+    const int ncen = static_cast<int>(min<int64_t>(64, (total - qc + qs - 1) / qs));
+    int js = 0, hs = 0;  // the next half tile: centre js, half hs
+    auto nh_of = [&](int jj) { return max(1, (lane_bcast(m_rows, jj) + 15) >> 4); };
+    int nhj = ncen > 0 ? nh_of(0) : 0;
+    int runj = -1;
+    float run = 0.0f;
+    auto flush = [&]() {
+      const int64_t fcr = lane_bcast(m_fc, runj);
+      const bool empty = lane_bcast(m_rows, runj) == 0;
+      if (h == 0) out[fcr * C3 + r32] = empty ? 0.0f : fmaxf(run + b3, 0.0f);
+    };
+    auto fold = [&](int jj, float m) {
+      if (jj != runj) {
+        if (runj >= 0) flush();
+        runj = jj;
+        run = m;
+      } else {
+        run = fmaxf(run, m);
+      }
+    };
+    while (js < ncen) {
+      const int jA = js, hA = hs;
+      if (++hs >= nhj) {
+        hs = 0;
+        if (++js < ncen) nhj = nh_of(js);
+      }
+      const bool hasB = js < ncen;
+      const int jB = hasB ? js : jA, hB = hasB ? hs : hA;
+      if (hasB && ++hs >= nhj) {
+        hs = 0;
+        if (++js < ncen) nhj = nh_of(js);
+      }
+      // opaque zero on the LDS indices: fragments re-read per tile, not hoisted into registers
+      int zo = 0;
+      asm volatile("" : "+v"(zo));
+      const bool sB = r32 >= 16;  // this lane's row r32 of the tile: first or second half tile
+      const int b = sB ? lane_bcast(m_b, jB) : lane_bcast(m_b, jA);
+      const int64_t fc = sB ? lane_bcast(m_fc, jB) : lane_bcast(m_fc, jA);
+      const int rows = sB ? lane_bcast(m_rows, jB) : lane_bcast(m_rows, jA);
+      const T cx = sB ? lane_bcast(m_cx, jB) : lane_bcast(m_cx, jA);
+      const T cy = sB ? lane_bcast(m_cy, jB) : lane_bcast(m_cy, jA);
+      const T cz = sB ? lane_bcast(m_cz, jB) : lane_bcast(m_cz, jA);
+      const int row = 16 * (sB ? hB : hA) + (r32 & 15);
+      // padded rows repeat the first hit (:104-106); a centre without hits reads point 0 (discarded)
+      const int n = rows == 0 ? 0 : list[fc * nsample + (row < rows ? row : 0)];
+      const float dx = static_cast<float>(pts.at(b, 0, n) - cx);
+      const float dy = static_cast<float>(pts.at(b, 1, n) - cy);
+      const float dz = static_cast<float>(pts.at(b, 2, n) - cz);
+      float x[KS];
+      x[0] = h == 0 ? dx : dy;
+      if constexpr (D == 0) {
+        x[1] = h == 0 ? dz : 0.0f;
+      } else {
+        const FT* f = feat + b * fb + static_cast<int64_t>(n) * fn;
+        x[1] = h == 0 ? dz : static_cast<float>(f[0]);
+        x[2] = static_cast<float>(h == 0 ? f[fd] : f[2 * fd]);
+      }
+      f32x16 a1;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        a1[r] = L.b1[h][r + zo];
+        a1[8 + r] = 0.0f;
+      }
+#pragma unroll
+      for (int s = 0; s < KS; ++s) a1 = __builtin_amdgcn_mfma_f32_32x32x2f32(L.w1[s][lane + zo], x[s], a1, 0, 0, 0);
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = fmaxf(a1[r], 0.0f);
+      const Split3 p1 = split3(v);
+      f32x16 a2;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        a2[r] = L.b2[h][r + zo];
+        a2[8 + r] = 0.0f;
+      }
+      const Split3 w2{L.w2[0][lane + zo], L.w2[1][lane + zo], L.w2[2][lane + zo]};
+      a2 = mfma_split3(w2, p1.p0, p1.p1, p1.p2, a2);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = fmaxf(a2[r], 0.0f);
+      const Split3 p2 = split3(v);
+      f32x16 a3;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) a3[r] = 0.0f;
+      a3 = mfma_split3(p2, L.w3[0][lane + zo], L.w3[1][lane + zo], L.w3[2][lane + zo], a3);
+      float mA = a3[0], mB = a3[8];
+#pragma unroll
+      for (int r = 1; r < 8; ++r) {
+        mA = fmaxf(mA, a3[r]);
+        mB = fmaxf(mB, a3[8 + r]);
+      }
+      mA = fmaxf(mA, __shfl_xor(mA, 32, kWave));
+      mB = fmaxf(mB, __shfl_xor(mB, 32, kWave));
+      fold(jA, mA);
+      if (hasB) fold(jB, mB);
+    }
+    if (runj >= 0) flush();
+  }
+}
+
+template <typename T, typename FT, int D>
+int launch_sa3_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, const void* c, int64_t cb, int64_t cc,
+                    int64_t cn, int S, int B, const void* feat, int64_t fb, int64_t fd, int64_t fn, const int32_t* count,
+                    const int32_t* list, int nsample, const float* params, float* out, hipStream_t st) {
+  PointsView<T> pv{static_cast<const T*>(xyz), sb, sc, sn};
+  PointsView<T> cv{static_cast<const T*>(c), cb, cc, cn};
+  const int64_t centres = static_cast<int64_t>(B) * S;
+  const int grid = static_cast<int>(centres < 4096 * kMfmaWaves ? (centres + kMfmaWaves - 1) / kMfmaWaves : 4096);
+  const int xcd = B % 8 == 0 && grid % 8 == 0 ? 1 : 0;
+  hipLaunchKernelGGL((sa3_mfma_kernel<T, FT, D>), dim3(grid), dim3(kMfmaWaves * kWave), 0, st, pv, cv, S, B,
+                     static_cast<const FT*>(feat), fb, fd, fn, count, list, nsample, params, out, xcd);
+  return launch_status("dvcp_sa_group_mlp(mfma3)");
+}
+
+#define DVCP_SA3_MFMA_INST(T, FT, D)                                                                              \
+  template int launch_sa3_mfma<T, FT, D>(const void*, int64_t, int64_t, int64_t, const void*, int64_t, int64_t,  \
+                                         int64_t, int, int, const void*, int64_t, int64_t, int64_t, const int32_t*, \
+                                         const int32_t*, int, const float*, float*, hipStream_t);
+DVCP_SA3_MFMA_INST(float, float, 0)
+DVCP_SA3_MFMA_INST(float, double, 0)
+DVCP_SA3_MFMA_INST(double, float, 0)
+DVCP_SA3_MFMA_INST(double, double, 0)
+DVCP_SA3_MFMA_INST(float, float, 3)
+DVCP_SA3_MFMA_INST(float, double, 3)
+DVCP_SA3_MFMA_INST(double, float, 3)
+DVCP_SA3_MFMA_INST(double, double, 3)
+#undef DVCP_SA3_MFMA_INST
+
 template <typename T, int D, int C1, int C2>
 int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, const void* c, int64_t cb, int64_t cc,
                    int64_t cn, int S, int B, const float* feat, int64_t fb, int64_t fn, const int32_t* count,
@@ -463,10 +909,23 @@ int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, c
     hipLaunchKernelGGL((sa_order_kernel<T>), dim3(B), dim3(kBuildThreads), 0, st, cv, S, order);
   if (U) {
     const int64_t rows = static_cast<int64_t>(B) * N;
-    hipLaunchKernelGGL((sa_pre_kernel<D, C1>), dim3(ceil_div(rows, 256 / (C1 / 4))), dim3(256), 0, st, feat, fb, fn, N,
-                       B, params, U, frows, Nf);
-    hipLaunchKernelGGL((sa_mlp_mfma_kernel<T, D, C1, C2, true>), dim3(grid), dim3(kMfmaWaves * kWave), 0, st, pv, cv,
-                       S, B, feat, fb, fn, count, list, nsample, params, U, static_cast<int64_t>(N) * C1, order, out, xcd);
+    if constexpr (DVCP_SA_PRE_MFMA) {
+      const int64_t wgs = (rows + 127) / 128;  // four 32-point tiles per workgroup
+      hipLaunchKernelGGL((sa_pre_mfma_kernel<D, C1>), dim3(static_cast<unsigned>(wgs < 2048 ? wgs : 2048)), dim3(256), 0,
+                         st, feat, fb, fn, N, B, params, U, frows, Nf);
+    } else {
+      hipLaunchKernelGGL((sa_pre_kernel<D, C1>), dim3(ceil_div(rows, 256 / (C1 / 4))), dim3(256), 0, st, feat, fb, fn,
+                         N, B, params, U, frows, Nf);
+    }
+    // 16-row half tiles for sa2 only: A/B on one box (tools/sa_bench.py, r4q) sa2 0.312 -> 0.299 ms, sa3
+    // 0.626 -> 0.659 ms (its balls mostly fill whole 32-row tiles; the half-tile bookkeeping costs more)
+    if constexpr (DVCP_SA_PACK16 && DVCP_SA_SPLIT3 && D == 32)
+      hipLaunchKernelGGL((sa_mlp_mfma_kernel<T, D, C1, C2, true, DVCP_SA_PACK16 && DVCP_SA_SPLIT3>), dim3(grid),
+                         dim3(kMfmaWaves * kWave), 0, st, pv, cv, S, B, feat, fb, fn, count, list, nsample, params, U,
+                         static_cast<int64_t>(N) * C1, order, out, xcd);
+    else
+      hipLaunchKernelGGL((sa_mlp_mfma_kernel<T, D, C1, C2, true>), dim3(grid), dim3(kMfmaWaves * kWave), 0, st, pv, cv,
+                         S, B, feat, fb, fn, count, list, nsample, params, U, static_cast<int64_t>(N) * C1, order, out, xcd);
   } else {
     hipLaunchKernelGGL((sa_mlp_mfma_kernel<T, D, C1, C2, false>), dim3(grid), dim3(kMfmaWaves * kWave), 0, st, pv,
                        cv, S, B, feat, fb, fn, count, list, nsample, params, nullptr, 0, order, out, xcd);

@@ -141,16 +141,22 @@ MFMA_BF16_32X32X16_FLOPS = 2 * 32 * 32 * 16  # one v_mfma_f32_32x32x16_bf16
 def _sa_exec_flops(chans, B, N, S, nsample, count):
     """The flops the kernels execute on this launch, from the ball query's real hit counts
     (evaluated lazily -- after the timed region -- by bench.py: one device reduction of ``count``).
+    Rows run in 16-row half tiles, two per 32-row MFMA tile (csrc/sa_mlp_mfma.hip: a centre takes
+    ceil(clamp(count, 1, ns) / 16) half tiles; padded rows execute like real ones).
 
-    * two-layer MFMA tables (sa2 35-32-64, sa3 67-64-64; csrc/sa_mlp_mfma.hip): layer 1 is split
-      into the per-point pass sa_pre_kernel (VALU, 2 D C1 per input point) and, per 32-row tile of
-      a centre's distinct hits (ceil(clamp(count, 1, ns) / 32) tiles; padded lanes of a tile
-      execute like real ones), 2 MT v_mfma_f32_32x32x2_f32 (xyz k-steps) and layer 2 as MT 2 CT
-      16-deep k-steps of six v_mfma_f32_32x32x16_bf16 (the fp32-accurate three-way bf16 split);
-    * other tables (sa1, csrc/sa_mlp.hip, VALU): one row per distinct hit, clamp(count, 0, ns)
+    * two-layer MFMA tables (sa2 35-32-64, sa3 67-64-64): layer 1 is split into the per-point pass
+      sa_pre_kernel (VALU, 2 D C1 per input point) and, per tile, 2 MT v_mfma_f32_32x32x2_f32 (xyz
+      k-steps) and layer 2 as MT 2 CT 16-deep k-steps of six v_mfma_f32_32x32x16_bf16 (the
+      fp32-accurate three-way bf16 split);
+    * sa1 (3 / 6-16-16-32): per tile ceil(C0 / 2) v_mfma_f32_32x32x2_f32 (layer 1, 32 output
+      channels of which 16 are padding) and one 16-deep split k-step each for layers 2 (32 x 16
+      padded) and 3;
+    * other tables (csrc/sa_mlp.hip, VALU): one row per distinct hit, clamp(count, 0, ns)
       rows x 2 sum(C_l C_l+1).
     Returns a callable -> (executed fp32-equivalent flops, of which on the matrix cores, of which
     on the bf16 pipe as fp32-equivalent flops, the bf16 pipe's own flops (6 x those))."""
+    def tiles():
+        return float(((count.clamp(1, nsample).long() + 15) // 16).sum()) / 2.0
     if len(chans) == 3 and chans[0] - 3 in (32, 64):
         D, C1, C2 = chans[0] - 3, chans[1], chans[2]
         mt, ct = C1 // 32, C2 // 32
@@ -158,10 +164,18 @@ def _sa_exec_flops(chans, B, N, S, nsample, count):
         l2_tile = 2 * mt * ct * MFMA_BF16_32X32X16_FLOPS  # = 2 x 32 rows x C1 x C2
 
         def f():
-            tiles = float(((count.clamp(1, nsample).long() + 31) // 32).sum())
-            mfma = tiles * (xyz_tile + l2_tile)
-            return 2.0 * B * N * D * C1 + mfma, mfma, tiles * l2_tile, 6.0 * tiles * l2_tile
+            t = tiles()
+            mfma = t * (xyz_tile + l2_tile)
+            return 2.0 * B * N * D * C1 + mfma, mfma, t * l2_tile, 6.0 * t * l2_tile
         return f
+    if len(chans) == 4 and chans[0] in (3, 6) and list(chans[1:]) == [16, 16, 32]:
+        l1_tile = (chans[0] + 1) // 2 * MFMA_F32_32X32X2_FLOPS
+        bf_tile = 2 * MFMA_BF16_32X32X16_FLOPS
+
+        def h():
+            t = tiles()
+            return t * (l1_tile + bf_tile), t * (l1_tile + bf_tile), t * bf_tile, 6.0 * t * bf_tile
+        return h
     macs = sum(a * b for a, b in zip(chans[:-1], chans[1:]))
 
     def g():

@@ -384,12 +384,14 @@ def test_set_abstraction_vs_oracle(cuda, normals, layout, B):
         torch.testing.assert_close(G_f.cpu(), O_f, rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("table", [1, 2])
+@pytest.mark.parametrize("table", [0, 1, 2])
 def test_sa_split3_accuracy(cuda, table):
-    """The two-layer MFMA tables run layer 2 as a three-way bf16 split on the bf16 matrix cores
-    (csrc/sa_mlp_mfma.hip).  On the same groups (the GPU ball query's lists) its error against an
-    fp64 evaluation of pointnet2_utils.py:195-200 must be of the size of an fp32 evaluation's error
-    (torch fp32 on the CPU, the reference's own arithmetic), and within the fp32 tolerance of it."""
+    """The MFMA tables run their bf16 layers as a three-way bf16 split on the matrix cores
+    (csrc/sa_mlp_mfma.hip: layer 2 of sa2 / sa3, layers 2 and 3 of sa1).  On the same groups (the
+    GPU ball query's lists) the error against an fp64 evaluation of pointnet2_utils.py:195-200 must
+    be of the size of an fp32 evaluation's error (torch fp32 on the CPU, the reference's own
+    arithmetic), and within the fp32 tolerance of it.  sa1 (nsample 256) at ~3/4 of nsample hits per
+    ball runs up to 16 half tiles per centre."""
     import copy
     import oracle as O
     import dvcp.pointnet2_utils as P
@@ -409,14 +411,14 @@ def test_sa_split3_accuracy(cuda, table):
     ctr = gx[:, :, :S].contiguous()
     mine_g = copy.deepcopy(mine).to(cuda)
     count, lst, _ = ops.ball_query(gx, ctr, r, ns, pdim=2, cdim_pts=2)
-    out = ops.sa_group_mlp(gx, ctr, gf.transpose(1, 2), count, lst, ns, mine_g.chans, mine_g.packed_params(),
-                           xyz_pdim=2, feat_ddim=1, feat_pdim=2).cpu()           # (B, S, C2)
+    out = ops.sa_group_mlp(gx, ctr, gf.transpose(1, 2) if D else None, count, lst, ns, mine_g.chans,
+                           mine_g.packed_params(), xyz_pdim=2, feat_ddim=1, feat_pdim=2).cpu()  # (B, S, C_last)
     cnt = count.cpu().long().clamp(1, ns)
     idx = lst.cpu().long()
     idx = torch.where(torch.arange(ns).view(1, 1, ns) < cnt.unsqueeze(-1), idx, idx[:, :, :1])  # :104 padding
     bi = torch.arange(B).view(B, 1, 1)
     gxyz = xyz.transpose(1, 2)[bi, idx] - xyz.transpose(1, 2)[:, :S].unsqueeze(2)  # fp32 differences
-    rows = torch.cat([gxyz, feats[bi, idx]], dim=-1).permute(0, 3, 2, 1)             # (B, C0, ns, S)
+    rows = (torch.cat([gxyz, feats[bi, idx]], dim=-1) if D else gxyz).permute(0, 3, 2, 1)  # (B, C0, ns, S)
 
     def mlp(m, x):
         for conv, bn in zip(m.mlp_convs, m.mlp_bns):
@@ -431,6 +433,40 @@ def test_sa_split3_accuracy(cuda, table):
     print(f"sa table {table}: max |gpu - fp64| {err_gpu:.3e}, max |fp32 cpu - fp64| {err_f32:.3e}, |ref| {scale:.3f}")
     assert err_gpu <= 4.0 * err_f32 + 1e-7 * scale
     torch.testing.assert_close(out, ref32, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("table", [0, 1, 2])
+def test_sa_empty_ball_gives_zero(cuda, table):
+    """A centre whose ball holds no point (count 0; the reference would gather index N, :104) gets a
+    zero row from every table, and its list row is never read (filled here with an out-of-range
+    index); the other centres are unchanged."""
+    import dvcp.pointnet2_utils as P
+    import oracle as O
+    from dvcp import ops
+    from tests_helpers import randomize_bn
+    g = torch.Generator().manual_seed(231 + table)
+    cfg = O.fe_config(use_normal=False, npoint=600)[table]
+    B, N, S, ns, r = 2, 3000, 600, cfg["nsample"], cfg["radius"]
+    D = cfg["in_channel"] - 3
+    torch.manual_seed(13)
+    mine = P.PointNetSetAbstraction(**cfg).eval()
+    randomize_bn(mine)
+    mine = mine.to(cuda)
+    gx = ((torch.rand(B, 3, N, generator=g, dtype=torch.float64) - 0.5) * 4).float().to(cuda)
+    gf = torch.randn(B, N, D, generator=g).to(cuda) if D else None
+    ctr = gx[:, :, :S].contiguous()
+    count, lst, _ = ops.ball_query(gx, ctr, r, ns, pdim=2, cdim_pts=2)
+    args = dict(xyz_pdim=2, feat_ddim=1, feat_pdim=2)
+    feat = gf.transpose(1, 2) if D else None
+    full = ops.sa_group_mlp(gx, ctr, feat, count, lst, ns, mine.chans, mine.packed_params(), **args)
+    empty = torch.zeros(B, S, dtype=torch.bool, device=cuda)
+    empty[:, ::7] = True
+    count2 = torch.where(empty, torch.zeros_like(count), count)
+    lst2 = torch.where(empty.unsqueeze(-1), torch.full_like(lst, 1 << 30), lst)
+    got = ops.sa_group_mlp(gx, ctr, feat, count2, lst2, ns, mine.chans, mine.packed_params(), **args)
+    torch.cuda.synchronize()
+    assert torch.equal(got[empty], torch.zeros_like(got[empty]))
+    assert torch.equal(got[~empty], full[~empty])
 
 
 def _sa_oracle(ref, xyz, feats, start):
