@@ -545,7 +545,7 @@ constexpr int kSelBufN = 16;
 // DVCP_KNN_SLOAD: an active tile's 16 points reach the wave as scalar loads (the tile index is
 // wave-uniform, the tile is read-only here) instead of one vector load and 48 readlanes; the
 // appends, which index the tile per lane, load their LDS copy from L2 when a lane needs one.
-// Round 4, A/B on one box (tools/knn_bench.py --fast, profiles/round4/r4t_knn_sload_ab.log):
+// Round 4, A/B on one box (tools/knn_bench.py --fast, profiles/round4/r4t/r4t_knn_sload_ab.log):
 // 0.763 / 0.755 -> 0.751 / 0.742 ms per C3 call, identical results, although the 48 scalar values
 // push the kernel to 76 B of scratch at 168 VGPRs (filtering in two 8-point batches, or re-loading
 // the tile after a merge instead of holding it, spilled more: 80-624 B).
