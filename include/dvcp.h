@@ -110,7 +110,8 @@ int dvcp_square_distance(int dtype, const void* src, int64_t sb, int64_t sc, int
  * Layers: nlayer in {2,3}; chans = {C0=3+D, C1, ..., C_nlayer}; for layer l:
  * W_l (C_{l+1} x C_l), bias_l, bn_scale_l, bn_shift_l (all fp32) packed back-to-back in
  * `params` in that order, layer by layer.  y = relu((W x + bias) * scale + shift).
- * out: B x S x C_last fp32 (row-major per centre). */
+ * out: B x S x C_last fp32 (row-major per centre).  A centre with count 0 (no hit; the reference
+ * would gather the padding index N) gets a zero row, and its list row is not read. */
 int dvcp_sa_group_mlp(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N,
                       const void* ctr, int64_t cb, int64_t cc, int64_t cn, int S, int B,
                       int feat_dtype, const void* feat, int64_t fb, int64_t fd, int64_t fn, int D,
