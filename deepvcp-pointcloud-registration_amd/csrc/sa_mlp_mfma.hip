@@ -511,7 +511,18 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) __attribute__((amdgpu_waves_per
       if (runj >= 0) flush();
       continue;
     }
-    int n_next = list_entry(0, 0);
+    // The first list row of the next centre is fetched one tile ahead; a centre without hits runs
+    // no tile, so "next" is the next centre with hits (lane mask of the batch).
+    const uint64_t live_c = __ballot(lane < ncen && m_rows > 0);
+    auto next_live = [&](int j) {  // the first centre after j with hits, or 64
+      const uint64_t m = j >= 63 ? 0ull : (live_c & (~0ull << (j + 1)));
+      return m ? static_cast<int>(__builtin_ctzll(m)) : 64;
+    };
+    int n_next = 0;
+    {
+      const int j0 = (live_c & 1ull) ? 0 : next_live(0);
+      if (j0 < ncen) n_next = list_entry(j0, 0);
+    }
   for (int j = 0; j < ncen; ++j) {
     const int b = lane_bcast(m_b, j);
     const int64_t fc = lane_bcast(m_fc, j);
@@ -534,8 +545,8 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) __attribute__((amdgpu_waves_per
       const int n = n_next;
       if (n0 + 32 < rows)
         n_next = list_entry(j, n0 + 32);
-      else if (j + 1 < ncen)
-        n_next = list_entry(j + 1, 0);
+      else if (next_live(j) < ncen)
+        n_next = list_entry(next_live(j), 0);
       f32x16 acc1[MT];
       if constexpr (PRE) {
         // accumulators start from U[n] (channels (r&3) + 8(r>>2) + 4h of each 32-channel tile)
