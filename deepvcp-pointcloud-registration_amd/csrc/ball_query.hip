@@ -73,6 +73,7 @@ __global__ __launch_bounds__(kBqThreads) void ball_query_kernel(
   }
   if (!live) return;
   if (count) count[static_cast<int64_t>(b) * S + s] = cnt;
+  if (my_list && cnt == 0) my_list[0] = 0;  // (see bq_tiled_kernel)
   if (my_pad)
     for (int j = cnt; j < nsample; ++j) my_pad[j] = first;
 }
@@ -243,6 +244,7 @@ __global__ __launch_bounds__(256) void bq_wave_kernel(const float4* __restrict__
   }
   if (!live) return;
   if (count) count[static_cast<int64_t>(b) * S + s] = cnt;
+  if (list && cnt == 0) list[row] = 0;  // (see bq_tiled_kernel)
   if (padded)
     for (int j = cnt; j < nsample; ++j) padded[row + j] = first;
 }
@@ -491,6 +493,10 @@ __global__ __launch_bounds__(256) void bq_tiled_kernel(BqLayout L, int N, Points
   }
   if (!live) return;
   if (count) count[static_cast<int64_t>(b) * S + s] = cnt;
+  // A centre without hits (the reference pads it with index N, :104) gets a valid first list
+  // entry, point 0: consumers that clamp count to >= 1 (training passes) then read in bounds, and
+  // the forward MLP tables give such a centre a zero row without reading its list.
+  if (list && cnt == 0) list[row] = 0;
   if (padded)
     for (int j = cnt; j < nsample; ++j) padded[row + j] = first;
 }

@@ -159,6 +159,23 @@ def test_ball_query_no_hit_pads_with_N(cuda):
     assert (P.query_ball_point(0.5, 4, xyz, ctr) == 10).all()
 
 
+@pytest.mark.parametrize("dtype,N", [(torch.float32, 3000), (torch.float32, 70000), (torch.float64, 3000)])
+def test_ball_query_no_hit_compact_row(cuda, dtype, N):
+    """The compact output of a centre without hits: count 0 and a valid first list entry (point 0),
+    so consumers that clamp count to >= 1 read in bounds; every path (tiled, streaming above 65536
+    points, fp64)."""
+    from dvcp import ops
+    g = torch.Generator().manual_seed(109)
+    xyz = (torch.rand(2, 3, N, generator=g, dtype=torch.float64) * 2 - 1).to(dtype).to(cuda)
+    ctr = xyz[:, :, :40].clone()
+    ctr[:, :, ::3] = 50.0  # every third centre far from every point
+    count, lst, _ = ops.ball_query(xyz, ctr.contiguous(), 0.2, 16, pdim=2, cdim_pts=2)
+    far = torch.zeros(2, 40, dtype=torch.bool, device=cuda)
+    far[:, ::3] = True
+    assert (count[far] == 0).all() and (count[~far] >= 1).all()
+    assert (lst[far][:, 0] == 0).all()
+
+
 def _bq_case(case, g):
     """Inputs that stress the tiled ball query's pruning: far-from-origin coordinates (large
     |p|^2 rounding margin), dense clusters (early exit inside the candidate scan), ragged sizes,
