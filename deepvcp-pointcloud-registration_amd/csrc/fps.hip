@@ -1175,14 +1175,17 @@ __global__ __launch_bounds__(kFpsThreads) void fps_dense_kernel(PointsView<T> pt
 }
 
 // Split FPS for clouds above one CU's register budget (C5: 65536 points): S workgroups per cloud,
-// each holding a contiguous chunk of up to P * 512 points (coordinates and running minima in
-// VGPRs).  Every step each workgroup updates its minima with the current centre and publishes
-// its best (value, index) as one key -- float bits of the fp32 minimum (monotonic for values >= 0)
-// over the complemented index, so the maximum key is the largest minimum with the lowest index,
-// the dense kernel's and the reference's argmax rule -- then waits for the cloud's S keys of that
-// step (release/acquire atomics at agent scope, keys double-buffered by step parity: a workgroup
-// can only reach step + 2 after every peer has arrived at step + 1, i.e. after it read step's
-// keys).  Every workgroup reduces the same S keys, so all agree on the next centre.
+// each holding a contiguous chunk of P * NT points (coordinates and running minima in VGPRs, 512
+// threads, P = 16 points per lane, or 32 for fp32 clouds above 131072 points).  Every step each workgroup updates its
+// minima with the current centre and publishes its best point as one 64-bit key: the fp32 minimum's
+// bits (monotonic for values >= 0), then the complemented index (18 bits), then the step's 14-bit
+// tag -- so among one step's keys the maximum is the largest minimum with the lowest index, the
+// dense kernel's and the reference's argmax rule.  Wave 0 of every workgroup then polls the cloud's
+// S key slots, one lane per slot, until all carry this step's tag, and takes their maximum: one
+// L2 round trip per poll, no arrival counter (round 4: the counter's release/acquire round trip
+// plus a separate read of the keys made a step ~3.6 us).  Slots are double-buffered by step parity:
+// a workgroup can only publish step + 2 after every peer has published step + 1, i.e. after every
+// peer read step's keys; the slots start invalid (all ones: no minimum has those bits).
 //
 // Progress does not rest on the whole grid being co-resident.  A workgroup takes its (cloud,
 // chunk) from a ticket counter when it starts running, not from blockIdx, so the tickets handed
@@ -1194,18 +1197,29 @@ __global__ __launch_bounds__(kFpsThreads) void fps_dense_kernel(PointsView<T> pt
 // steps it could not finish, so nothing downstream reads out of bounds or a garbage centre.
 constexpr int kFpsSplitMax = 16;
 constexpr uint32_t kFpsSpinCap = 1u << 22;
+constexpr int kSplitTagBits = 14, kSplitIdxBits = 18;  // N <= 16 x 16384 points per cloud
+constexpr uint64_t kSplitTagMask = (1ull << kSplitTagBits) - 1;
+constexpr uint32_t kSplitIdxMask = (1u << kSplitIdxBits) - 1;
 
-template <typename T, int P>
-__global__ __launch_bounds__(kFpsThreads) void fps_split_kernel(PointsView<T> pts, int N, int npoint, int S,
-                                                                const int64_t* __restrict__ start,
-                                                                int64_t* __restrict__ out_idx,
-                                                                T* __restrict__ out_xyz,
-                                                                uint64_t* __restrict__ keys,
-                                                                uint32_t* __restrict__ arrived,
-                                                                uint32_t* __restrict__ ticket,
-                                                                int32_t* __restrict__ err, uint32_t spin_cap) {
-  constexpr int kW = kFpsThreads / kWave;
-  constexpr int chunk = P * kFpsThreads;
+constexpr int kFpsSplitThreads = 512;  // (1024 threads x 16 points spilled 840 B at 128 VGPRs)
+// Points per lane: 16 (chunks of 8192 points: twice the workgroups, half the per-step update)
+// while that needs at most kFpsSplitMax workgroups per cloud; fp32 clouds above 131072 points take
+// chunks of 16384.
+template <typename T>
+inline int fps_split_ppt(int N) {
+  return sizeof(T) == 4 && ceil_div(N, 16 * kFpsSplitThreads) > kFpsSplitMax ? 32 : 16;
+}
+template <typename T>
+constexpr int fps_split_max_chunk() { return (sizeof(T) == 4 ? 32 : 16) * kFpsSplitThreads; }
+
+template <typename T, int P, int NT>
+__global__ __launch_bounds__(NT) void fps_split_kernel(PointsView<T> pts, int N, int npoint, int S,
+                                                       const int64_t* __restrict__ start,
+                                                       int64_t* __restrict__ out_idx, T* __restrict__ out_xyz,
+                                                       uint64_t* __restrict__ keys, uint32_t* __restrict__ ticket,
+                                                       int32_t* __restrict__ err, uint32_t spin_cap) {
+  constexpr int kW = NT / kWave;
+  constexpr int chunk = P * NT;
   __shared__ uint64_t wbest[kW];
   __shared__ uint64_t gbest;
   __shared__ int timed_out;
@@ -1222,7 +1236,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_split_kernel(PointsView<T> pt
   float dm[P];
 #pragma unroll
   for (int p = 0; p < P; ++p) {
-    const int n = n0 + p * kFpsThreads + tid;
+    const int n = n0 + p * NT + tid;
     const bool ok = n < n1;
     px[p] = ok ? pts.at(b, 0, n) : static_cast<T>(0);
     py[p] = ok ? pts.at(b, 1, n) : static_cast<T>(0);
@@ -1234,7 +1248,6 @@ __global__ __launch_bounds__(kFpsThreads) void fps_split_kernel(PointsView<T> pt
   int64_t cur = first;
   T cx = pts.at(b, 0, cur), cy = pts.at(b, 1, cur), cz = pts.at(b, 2, cur);
   uint64_t* kb = keys + static_cast<int64_t>(b) * 2 * S;
-  uint32_t* cnt = arrived + b;
   int step = 0;
   for (; step < npoint; ++step) {
     if (s == 0 && tid == 0) {
@@ -1249,13 +1262,14 @@ __global__ __launch_bounds__(kFpsThreads) void fps_split_kernel(PointsView<T> pt
     uint64_t best = 0;
 #pragma unroll
     for (int p = 0; p < P; ++p) {
-      const int n = n0 + p * kFpsThreads + tid;
+      const int n = n0 + p * NT + tid;
       const T dx = px[p] - cx, dy = py[p] - cy, dz = pz[p] - cz;
       const T d = (dx * dx + dy * dy) + dz * dz;
       float m = dm[p];
       if (d < static_cast<T>(m)) m = static_cast<float>(d);
       dm[p] = m;
-      const uint64_t key = (static_cast<uint64_t>(__float_as_uint(m)) << 32) | (0xFFFFFFFFu - static_cast<uint32_t>(n));
+      const uint64_t key = (static_cast<uint64_t>(__float_as_uint(m)) << 32) |
+                           (static_cast<uint64_t>(kSplitIdxMask - static_cast<uint32_t>(n)) << kSplitTagBits);
       best = (n < n1 && key > best) ? key : best;
     }
     for (int off = 32; off > 0; off >>= 1) {
@@ -1264,31 +1278,36 @@ __global__ __launch_bounds__(kFpsThreads) void fps_split_kernel(PointsView<T> pt
     }
     if (lane == 0) wbest[wave] = best;
     __syncthreads();
-    if (tid == 0) {
-      uint64_t wb = wbest[0];
-      for (int w = 1; w < kW; ++w) wb = wbest[w] > wb ? wbest[w] : wb;
+    if (wave == 0) {
+      const uint64_t tag = static_cast<uint64_t>(step) & kSplitTagMask;
       uint64_t* slot = kb + (step & 1) * S;
-      __hip_atomic_store(slot + s, wb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t target = static_cast<uint32_t>(step + 1) * static_cast<uint32_t>(S);
+      if (lane == 0) {
+        uint64_t wb = wbest[0];
+        for (int w = 1; w < kW; ++w) wb = wbest[w] > wb ? wbest[w] : wb;
+        __hip_atomic_store(slot + s, wb | tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      uint64_t v = 0;
       uint32_t polls = 0;
-      while (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      for (;;) {
+        v = lane < S ? __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        const bool ok = lane >= S || ((v & kSplitTagMask) == tag && static_cast<uint32_t>(v >> 32) != 0xFFFFFFFFu);
+        if (__ballot(!ok) == 0) break;
         __builtin_amdgcn_s_sleep(1);
         if (++polls > spin_cap) {
-          timed_out = 1;
+          if (lane == 0) timed_out = 1;
           break;
         }
       }
-      uint64_t g = 0;
-      for (int k = 0; k < S; ++k) {
-        const uint64_t v = __hip_atomic_load(slot + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        g = v > g ? v : g;
+      uint64_t g = lane < S ? v : 0ull;
+      for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(g, off, kWave);
+        g = o > g ? o : g;
       }
-      gbest = g;
+      if (lane == 0) gbest = g;
     }
     __syncthreads();
     if (timed_out) break;
-    cur = static_cast<int64_t>(0xFFFFFFFFu - static_cast<uint32_t>(gbest & 0xFFFFFFFFull));
+    cur = static_cast<int64_t>(kSplitIdxMask - static_cast<uint32_t>((gbest >> kSplitTagBits) & kSplitIdxMask));
     cx = pts.at(b, 0, cur);
     cy = pts.at(b, 1, cur);
     cz = pts.at(b, 2, cur);
@@ -1301,7 +1320,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_split_kernel(PointsView<T> pt
       // ball query / MLP launched behind this one read real points before the host raises
       const T fx = pts.at(b, 0, first), fy = pts.at(b, 1, first), fz = pts.at(b, 2, first);
       T* ox = out_xyz ? out_xyz + static_cast<int64_t>(b) * 3 * npoint : nullptr;
-      for (int k = step + tid; k < npoint; k += kFpsThreads) {
+      for (int k = step + tid; k < npoint; k += NT) {
         out_idx[static_cast<int64_t>(b) * npoint + k] = first;
         if (ox) {
           ox[k] = fx;
@@ -1314,18 +1333,16 @@ __global__ __launch_bounds__(kFpsThreads) void fps_split_kernel(PointsView<T> pt
 }
 
 // Workspace of the split kernel, carved from the caller's B x N fp32 buffer (>= 64 KiB per cloud):
-// keys [B][2][S] u64 | arrived [B] u32 | ticket u32 | err i32 (err is the caller's when given).
+// keys [B][2][S] u64 | ticket u32 | err i32 (err is the caller's when given).
 struct FpsSplitWs {
   uint64_t* keys;
-  uint32_t* arrived;
   uint32_t* ticket;
   int32_t* err;
 };
 static FpsSplitWs fps_split_ws(float* ws, int B, int S) {
   FpsSplitWs w;
   w.keys = reinterpret_cast<uint64_t*>(ws);
-  w.arrived = reinterpret_cast<uint32_t*>(w.keys + static_cast<int64_t>(B) * 2 * S);
-  w.ticket = w.arrived + B;
+  w.ticket = reinterpret_cast<uint32_t*>(w.keys + static_cast<int64_t>(B) * 2 * S);
   w.err = reinterpret_cast<int32_t*>(w.ticket + 1);
   return w;
 }
@@ -1335,16 +1352,27 @@ static FpsSplitWs fps_split_ws(float* ws, int B, int S) {
 template <typename T>
 static int launch_fps_split(PointsView<T> v, int B, int N, int npoint, const int64_t* start, int64_t* out_idx,
                             T* out_xyz, float* ws, int32_t* err, uint32_t spin_cap, int withhold, hipStream_t st) {
-  constexpr int P = sizeof(T) == 4 ? 32 : 16;
-  const int S = ceil_div(N, P * kFpsThreads);
+  constexpr int NT = kFpsSplitThreads;
+  const int P = fps_split_ppt<T>(N);
+  const int S = ceil_div(N, P * NT);
+  if (N > S * P * NT || N - 1 > static_cast<int>(kSplitIdxMask)) {
+    set_error("dvcp_fps(split): N=%d too large", N);
+    return DVCP_EINVAL;
+  }
   FpsSplitWs w = fps_split_ws(ws, B, S);
-  hipError_t e = hipMemsetAsync(w.arrived, 0, sizeof(uint32_t) * (B + 2), st);
+  hipError_t e = hipMemsetAsync(w.keys, 0xFF, sizeof(uint64_t) * 2 * static_cast<size_t>(B) * S, st);  // invalid
+  if (e == hipSuccess) e = hipMemsetAsync(w.ticket, 0, sizeof(uint32_t) * 2, st);
   if (e != hipSuccess) return launch_status("dvcp_fps(split memset)");
   if (!err) err = w.err;
   const int grid = B * S - withhold;
-  if (grid > 0)
-    hipLaunchKernelGGL((fps_split_kernel<T, P>), dim3(grid), dim3(kFpsThreads), 0, st, v, N, npoint, S, start, out_idx,
-                       out_xyz, w.keys, w.arrived, w.ticket, err, spin_cap);
+  if (grid > 0) {
+    if (P == 16)
+      hipLaunchKernelGGL((fps_split_kernel<T, 16, NT>), dim3(grid), dim3(NT), 0, st, v, N, npoint, S, start, out_idx,
+                         out_xyz, w.keys, w.ticket, err, spin_cap);
+    else if constexpr (sizeof(T) == 4)
+      hipLaunchKernelGGL((fps_split_kernel<T, 32, NT>), dim3(grid), dim3(NT), 0, st, v, N, npoint, S, start, out_idx,
+                         out_xyz, w.keys, w.ticket, err, spin_cap);
+  }
   return launch_status("dvcp_fps(split)");
 }
 
@@ -1400,8 +1428,7 @@ static int launch_fps(const T* xyz, int64_t sb, int64_t sc, int64_t sn, int B, i
     set_error("dvcp_fps: N=%d needs the split/dense path and its B x N fp32 workspace (dvcp_fps_ws)", N);
     return DVCP_EINVAL;
   }
-  constexpr int P = sizeof(T) == 4 ? 32 : 16;
-  if (ceil_div(N, P * kFpsThreads) <= kFpsSplitMax)
+  if (ceil_div(N, fps_split_max_chunk<T>()) <= kFpsSplitMax)
     return launch_fps_split<T>(v, B, N, npoint, start, out_idx, out_xyz, ws, err, kFpsSpinCap, 0, st);
   hipLaunchKernelGGL((fps_dense_kernel<T>), grid, block, 0, st, v, N, npoint, start, out_idx, out_xyz, ws);
   return launch_status("dvcp_fps(dense)");
@@ -1447,8 +1474,8 @@ extern "C" int dvcp_fps_split_probe(int dtype, const void* xyz, int64_t sb, int6
                                     int32_t* err, uint32_t spin_cap, int withhold, void* stream) {
   DVCP_REQUIRE(xyz && start && out_idx && ws && err, "dvcp_fps_split_probe: null pointer");
   DVCP_REQUIRE(B > 0 && N > 0 && npoint > 0 && withhold >= 0, "dvcp_fps_split_probe: bad sizes");
-  const int P = dtype == DVCP_F32 ? 32 : 16;
-  const int S = dvcp::ceil_div(N, P * dvcp::kFpsThreads);
+  const int S = dvcp::ceil_div(N, (dtype == DVCP_F32 ? dvcp::fps_split_ppt<float>(N) : dvcp::fps_split_ppt<double>(N)) *
+                                     dvcp::kFpsSplitThreads);
   DVCP_REQUIRE(S >= 2 && S <= dvcp::kFpsSplitMax && withhold < S, "dvcp_fps_split_probe: N=%d is not a split size", N);
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (dtype == DVCP_F32)
