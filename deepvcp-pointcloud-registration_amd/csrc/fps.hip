@@ -1176,7 +1176,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_dense_kernel(PointsView<T> pt
 
 // Split FPS for clouds above one CU's register budget (C5: 65536 points): S workgroups per cloud,
 // each holding a contiguous chunk of P * NT points (coordinates and running minima in VGPRs, 512
-// threads, P = 8, 16 or 32 points per lane, see fps_split_ppt).  Every step each workgroup updates its
+// threads, P = 16 points per lane, or 32 for fp32 clouds above 131072 points).  Every step each workgroup updates its
 // minima with the current centre and publishes its best point as one 64-bit key: the fp32 minimum's
 // bits (monotonic for values >= 0), then the complemented index (18 bits), then the step's 14-bit
 // tag -- so among one step's keys the maximum is the largest minimum with the lowest index, the
@@ -1202,12 +1202,12 @@ constexpr uint64_t kSplitTagMask = (1ull << kSplitTagBits) - 1;
 constexpr uint32_t kSplitIdxMask = (1u << kSplitIdxBits) - 1;
 
 constexpr int kFpsSplitThreads = 512;  // (1024 threads x 16 points spilled 840 B at 128 VGPRs)
-// Points per lane: the smallest of 8, 16 (fp32: 32) whose chunks (4096, 8192, 16384 points) need
-// at most kFpsSplitMax workgroups per cloud -- more workgroups, shorter per-step update (C5:
-// 16384-point chunks 29.7 ms, 8192 22.3 ms, 4096 19.4 ms per launch).
+// Points per lane: 16 (chunks of 8192 points: twice the workgroups, half the per-step update)
+// while that needs at most kFpsSplitMax workgroups per cloud; fp32 clouds above 131072 points take
+// chunks of 16384.  (Chunks of 4096 ran one C5 launch in 19.4 instead of 22.3 ms, but with ten
+// batches in flight their spinning workgroups cost the C5 bench 367.7 -> 288.5 pairs/s.)
 template <typename T>
 inline int fps_split_ppt(int N) {
-  if (ceil_div(N, 8 * kFpsSplitThreads) <= kFpsSplitMax) return 8;
   return sizeof(T) == 4 && ceil_div(N, 16 * kFpsSplitThreads) > kFpsSplitMax ? 32 : 16;
 }
 template <typename T>
@@ -1367,10 +1367,7 @@ static int launch_fps_split(PointsView<T> v, int B, int N, int npoint, const int
   if (!err) err = w.err;
   const int grid = B * S - withhold;
   if (grid > 0) {
-    if (P == 8)
-      hipLaunchKernelGGL((fps_split_kernel<T, 8, NT>), dim3(grid), dim3(NT), 0, st, v, N, npoint, S, start, out_idx,
-                         out_xyz, w.keys, w.ticket, err, spin_cap);
-    else if (P == 16)
+    if (P == 16)
       hipLaunchKernelGGL((fps_split_kernel<T, 16, NT>), dim3(grid), dim3(NT), 0, st, v, N, npoint, S, start, out_idx,
                          out_xyz, w.keys, w.ticket, err, spin_cap);
     else if constexpr (sizeof(T) == 4)
