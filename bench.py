@@ -93,7 +93,15 @@ def parse():
                    help="diagnostic: no per-launch HIP events in the timed region")
     p.add_argument("--iso-steps", type=int, default=3,
                    help="steps timed per kernel with one batch in flight (stage roofline)")
-    p.add_argument("--cpu-pairs", type=int, default=3, help="C3 pairs timed for the CPU baseline (median)")
+    p.add_argument("--cpu-pairs", type=int, default=1,
+                   help="C3 pairs timed for the CPU baseline (median); one pair is ~20 s on 16 host threads")
+    p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                   help="process group for world > 1: nccl (= RCCL, one rank per GPU) or gloo (rehearsal: "
+                        "several ranks may share a GPU)")
+    p.add_argument("--rows-out", default=None,
+                   help="rank 0 writes the gathered per-pair rows (steps x global batch, 14 fp64: R, t, rotation "
+                        "and translation error) to this .pt file: a sharded run's rows equal a one-GPU run's of "
+                        "the same global batch (dvcp.dist.ShardPlan)")
     p.add_argument("--detail-json", default=None,
                    help="also write the full record (per-stage roofline, live launch times) to this file; it "
                         "always goes to stderr as one 'bench-detail' JSON line")
@@ -113,10 +121,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; --dist-backend gloo lets a rehearsal put several ranks on one GPU
+    # (device index LOCAL_RANK mod the visible count; device_count does not initialise HIP)
+    dev_idx = local % max(1, torch.cuda.device_count())
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+        else:
+            dist.init_process_group("gloo")
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
 
     import dvcp
     from dvcp import _lib
@@ -125,32 +139,31 @@ def main():
 
     B, N, K, r, s = args.batch, args.npoints, args.K, args.r, args.s
     P = max(1, args.inflight)
+    # rank-independent by construction (dvcp.dist.ShardPlan): every rank draws each lane's global
+    # batch and keeps its shard, builds the same model, and draws the global batch's FPS starts
+    plan = D.ShardPlan(B, world, rank)
     torch.manual_seed(0)
     model = dvcp.DeepVCP(use_normal=False, K=K, r=r, s=s,
                          feat_dtype=torch.float16 if args.feat_dtype == "f16" else torch.float32).eval().to(dev)
-    # one distinct synthetic global batch (B pairs per GPU x world) per in-flight lane; every rank
-    # takes its contiguous dvcp.dist.shard of it (weak scaling: B pairs per GPU)
-    lo, hi = D.shard(B * world, rank, world)
-    batches = []
-    for lane in range(P):
-        src, tgt, R_gt, t_gt = make_pairs(B * world, N, seed=1234 + 104729 * lane)
-        batches.append(tuple(x[lo:hi].contiguous().to(dev) for x in (src, tgt, R_gt, t_gt)))
+    batches = [tuple(x.to(dev) for x in plan.lane_pairs(lane, N, make_pairs)) for lane in range(P)]
     src, tgt, R_gt, t_gt = batches[0]
     # random init, conditioned so key-point scores are separated beyond fp32 noise (the default
-    # init's scores are 0.62 +- 1e-4): BN stats randomised, WL calibrated on this batch's features
+    # init's scores are 0.62 +- 1e-4): BN stats randomised, WL calibrated on global pair 0's
+    # features -- the same cloud on every rank and at every world size
     randomize_bn(model)
     with torch.no_grad():
-        _, calib, _ = model.FE1.run(src)
+        _, calib, _ = model.FE1.run(plan.calibration_src(N, make_pairs).to(dev))
     condition_weights(model, feats=calib)
     t_init = torch.zeros(1, 3)
-    torch.manual_seed(1 + rank)
+    torch.manual_seed(1)
     lanes = [torch.cuda.Stream(device=dev) for _ in range(P)]
 
     def step(lane=0):
         """One pass over one batch: DeepVCP.forward + deepVCP_loss, issued on the lane's stream."""
         b_src, b_tgt, b_R, b_t = batches[lane]
+        starts = plan.starts(model, N)   # this rank's columns of the global batch's draw
         with torch.no_grad(), torch.cuda.stream(lanes[lane]):
-            kp, vcp = model(b_src, b_tgt, b_R, t_init)
+            kp, vcp = model(b_src, b_tgt, b_R, t_init, starts=starts)
             loss, Rp, tp = dvcp.deepVCP_loss(kp, vcp, b_R, b_t, 0.5)
             rot, trans = dvcp.registration_errors(Rp, tp, b_R, b_t)  # train.py:112-120 harness
         return Rp, tp, rot, trans
@@ -181,13 +194,15 @@ def main():
     # per pair: R (9), t (3), rotation error (deg), translation error -> (steps*B, 14)
     res = torch.cat([torch.cat([o[0].reshape(B, 9), o[1].reshape(B, 3), o[2].reshape(B, 1), o[3].reshape(B, 1)], 1)
                      for o in outs])
+    if world > 1 and args.dist_backend == "gloo":
+        res = res.cpu()   # gloo gathers host tensors (rehearsal only; RCCL gathers in HBM)
     res = D.gather_results(res, world)      # the one collective: RCCL all_gather of the rows
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     log, _lib.EVENT_LOG = _lib.EVENT_LOG or [], None
     if world > 1:
         dist.barrier()
-    elapsed = D.max_over_ranks(elapsed, dev)
+    elapsed = D.max_over_ranks(elapsed, dev if args.dist_backend == "nccl" else torch.device("cpu"))
 
     # ---- per-kernel HIP-event timing (events on the stream each kernel is launched on) --------
     # (1) live over the timed region, 8 batches in flight: per-launch durations under contention
@@ -208,6 +223,11 @@ def main():
     roofline = dominant_roofline(live, iso, stages, pmc)
     fps_roof = fps_roofline(live, iso, floor_us, pmc)
     res_cpu = res.cpu()
+    if rank == 0 and args.rows_out:
+        # gathered in rank order (each rank: steps x B rows) -> (steps, global batch, 14)
+        by_step = res_cpu.reshape(world, args.steps, B, 14).permute(1, 0, 2, 3).reshape(args.steps, B * world, 14)
+        torch.save({"rows": by_step.contiguous(), "global_batch": B * world, "steps": args.steps, "world": world,
+                    "columns": "R (9), t (3), rotation error deg, translation error"}, args.rows_out)
     reg_err = {"rot_deg_mean": float(res_cpu[:, 12].mean()), "rot_deg_max": float(res_cpu[:, 12].max()),
                "trans_mean": float(res_cpu[:, 13].mean()), "trans_max": float(res_cpu[:, 13].max()),
                "pairs": int(res_cpu.shape[0]),

@@ -42,10 +42,6 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef DVCP_SA_SPLIT3
 #define DVCP_SA_SPLIT3 1
 #endif
-// DVCP_SA_PRE_MFMA: the per-point pass U = W1f f + b1 on the fp32 matrix cores (sa_pre_mfma_kernel)
-#ifndef DVCP_SA_PRE_MFMA
-#define DVCP_SA_PRE_MFMA 1
-#endif
 // DVCP_SA_PACK16: the pre-pass kernel packs each centre's rows in 16-row half tiles (see the kernel)
 #ifndef DVCP_SA_PACK16
 #define DVCP_SA_PACK16 1
@@ -121,69 +117,19 @@ __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >
 
 // Decomposed layer 1 (PRE = true).  Layer 1 is linear in its input row [p - c, f]:
 //   W1 [p - c; f] + b1 = W1x (p - c) + (W1f f + b1)
-// and the second term depends only on the neighbour point, not on the centre.  sa_pre_kernel
+// and the second term depends only on the neighbour point, not on the centre.  sa_pre_mfma_kernel
 // evaluates U[n] = W1f f_n + b1 once per input point (N rows instead of S x nsample), and the
 // grouped kernel starts each layer-1 accumulator from the gathered U row and adds the xyz part
 // with two MFMA k-steps.  Only the summation order changes (features first, then xyz); the local
 // coordinates are still formed per (centre, point) pair, so no cancellation is introduced.
-template <int D, int C1>
-// rows != nullptr: point n of cloud b takes feature row rows[b * N + n] (clamped to [0, Nf)) --
-// the previous layer's per-point rows gathered by its FPS order, folded into this load.
-__global__ __launch_bounds__(256) void sa_pre_kernel(const float* __restrict__ feat, int64_t fb, int64_t fn, int N,
-                                                     int B, const float* __restrict__ params,
-                                                     float* __restrict__ U, const int64_t* __restrict__ rows, int Nf) {
-  // Thread (point, 4-channel group): the C1/4 threads of a point write one contiguous U row
-  // (coalesced float4 stores), and read the BN-folded weights from LDS as [k][c] float4 rows.
-  constexpr int C0 = 3 + D, CG = C1 / 4, PPB = 256 / CG;  // channel groups, points per block
-  __shared__ float4 w[D][CG];
-  __shared__ float4 bias[CG];
-  const float* W1 = params;
-  const float* pb1 = W1 + C1 * C0;
-  const float* ps1 = pb1 + C1;
-  const float* pt1 = ps1 + C1;
-  for (int i = threadIdx.x; i < D * C1; i += 256) {  // BN folded in: (W x + b) s + t = (s W) x + (s b + t)
-    const int k = i / C1, c = i % C1;
-    reinterpret_cast<float*>(&w[k][0])[c] = W1[c * C0 + 3 + k] * ps1[c];
-  }
-  for (int c = threadIdx.x; c < C1; c += 256)
-    reinterpret_cast<float*>(&bias[0])[c] =
-        static_cast<float>(static_cast<double>(pb1[c]) * ps1[c] + static_cast<double>(pt1[c]));
-  __syncthreads();
-  const int g = threadIdx.x % CG;
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * PPB + threadIdx.x / CG;
-  if (i >= static_cast<int64_t>(B) * N) return;
-  const int b = static_cast<int>(i / N), n = static_cast<int>(i % N);
-  int64_t src = n;
-  if (rows) {
-    const int64_t r = rows[i];
-    src = r < 0 ? 0 : (r >= Nf ? Nf - 1 : r);
-  }
-  const float4* fr = reinterpret_cast<const float4*>(feat + b * fb + src * fn);
-  float4 acc = bias[g];
-#pragma unroll 4
-  for (int v = 0; v < D / 4; ++v) {
-    const float4 q = fr[v];
-    const float fq[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float4 wk = w[4 * v + e][g];
-      acc.x = __fmaf_rn(wk.x, fq[e], acc.x);
-      acc.y = __fmaf_rn(wk.y, fq[e], acc.y);
-      acc.z = __fmaf_rn(wk.z, fq[e], acc.z);
-      acc.w = __fmaf_rn(wk.w, fq[e], acc.w);
-    }
-  }
-  reinterpret_cast<float4*>(U + i * C1)[g] = acc;
-}
-
-// The same per-point pass as a plain GEMM on the fp32 matrix cores (U = F . W1f'^T + b1'): one
-// wave per 32 input points, v_mfma_f32_32x32x2_f32 with k-step s taking input channels s (lane
-// half 0) and s + D/2 (half 1), so each lane reads one contiguous half of its point's feature row;
-// the BN-folded weights are staged once per workgroup as B fragments.  The row-per-thread kernel
-// above read each point's whole row once per 4-channel group and the weights from LDS per FMA
-// (sa3's pass: 67 us per C3 batch for 1.3 GFLOP and 82 MB); the MFMA form is bound by the 82 MB.
-// The accumulation is a k-ordered fp32 chain like the VALU kernel's (the MFMA adds its two
-// k-products per step), within the fp32 tolerance of the SA tests.
+// The per-point pass is a plain GEMM on the fp32 matrix cores (U = F . W1f'^T + b1'): one wave
+// per 32 input points, v_mfma_f32_32x32x2_f32 with k-step s taking input channels s (lane half 0)
+// and s + D/2 (half 1), so each lane reads one contiguous half of its point's feature row; the
+// BN-folded weights are staged once per workgroup as B fragments; bound by its 82 MB (sa3, C3).
+// The accumulation is a k-ordered fp32 chain (the MFMA adds its two k-products per step).
+// (Round 4 had a row-per-thread VALU form of this pass, float4 FMA chains that hipcc packed into
+// v_pk_fma_f32.  With a second process on the GPU, single fp32 lanes of its accumulators came out
+// different -- the round-4 two-rank test failure, DESIGN.md section 5 -- so it was removed.)
 template <int D, int C1>
 __global__ __launch_bounds__(256) void sa_pre_mfma_kernel(const float* __restrict__ feat, int64_t fb, int64_t fn, int N,
                                                           int B, const float* __restrict__ params,
@@ -920,14 +866,9 @@ int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, c
     hipLaunchKernelGGL((sa_order_kernel<T>), dim3(B), dim3(kBuildThreads), 0, st, cv, S, order);
   if (U) {
     const int64_t rows = static_cast<int64_t>(B) * N;
-    if constexpr (DVCP_SA_PRE_MFMA) {
-      const int64_t wgs = (rows + 127) / 128;  // four 32-point tiles per workgroup
-      hipLaunchKernelGGL((sa_pre_mfma_kernel<D, C1>), dim3(static_cast<unsigned>(wgs < 2048 ? wgs : 2048)), dim3(256), 0,
-                         st, feat, fb, fn, N, B, params, U, frows, Nf);
-    } else {
-      hipLaunchKernelGGL((sa_pre_kernel<D, C1>), dim3(ceil_div(rows, 256 / (C1 / 4))), dim3(256), 0, st, feat, fb, fn,
-                         N, B, params, U, frows, Nf);
-    }
+    const int64_t wgs = (rows + 127) / 128;  // four 32-point tiles per workgroup
+    hipLaunchKernelGGL((sa_pre_mfma_kernel<D, C1>), dim3(static_cast<unsigned>(wgs < 2048 ? wgs : 2048)), dim3(256), 0,
+                       st, feat, fb, fn, N, B, params, U, frows, Nf);
     // 16-row half tiles for sa2 only: A/B on one box (tools/sa_bench.py, r4q) sa2 0.312 -> 0.299 ms, sa3
     // 0.626 -> 0.659 ms (its balls mostly fill whole 32-row tiles; the half-tile bookkeeping costs more)
     if constexpr (DVCP_SA_PACK16 && DVCP_SA_SPLIT3 && D == 32)

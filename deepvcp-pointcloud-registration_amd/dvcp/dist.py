@@ -8,6 +8,9 @@ latency-bound over xGMI (backend "nccl" = RCCL on ROCm), or gloo on CPU for test
 import torch
 import torch.distributed as dist
 
+# bench.py's synthetic data: lane L's global batch is make_pairs(P, N, seed=LANE_SEED0 + LANE_STRIDE * L)
+LANE_SEED0, LANE_STRIDE = 1234, 104729
+
 
 def shard(total, rank, world):
     """Contiguous [start, end) of `total` pairs for `rank` (sizes differ by at most one)."""
@@ -45,3 +48,44 @@ def max_over_ranks(seconds, device):
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+class ShardPlan:
+    """What every rank of a sharded run uses (bench.py), chosen so that rank r's rows equal rows
+    [lo, hi) of a single-process run of the same global batch, bit for bit:
+
+    * data: in-flight lane L's global batch of P = pairs_per_rank x world pairs is one
+      ``make_pairs(P, N, seed(L))`` draw on every rank; each rank takes its ``shard``;
+    * weights: the same seed on every rank, and the weighting layer's calibration
+      (``synthetic.condition_weights``) runs on ``calibration_src`` -- global pair 0 of lane 0, whose
+      points do not depend on P (make_pairs draws every source cloud before any pose) -- so the
+      model is the same whatever the world size and whichever rank holds pair 0;
+    * FPS starts: every rank draws the seven start vectors for the whole global batch from the
+      same CPU generator state (``starts``), in the reference's order, and keeps its columns.
+      Every rank makes the same draws in the same order, so step i's starts are the global
+      batch's whatever the world size.
+    (The round-4 bench calibrated on each rank's own shard and seeded the starts with 1 + rank,
+    so an N-GPU run used N different models and could not be checked against one GPU.)"""
+
+    def __init__(self, pairs_per_rank, world=1, rank=0):
+        self.pairs_per_rank, self.world, self.rank = int(pairs_per_rank), int(world), int(rank)
+        self.total = self.pairs_per_rank * self.world
+        self.lo, self.hi = shard(self.total, self.rank, self.world)
+
+    @staticmethod
+    def lane_seed(lane):
+        return LANE_SEED0 + LANE_STRIDE * int(lane)
+
+    def lane_pairs(self, lane, n_points, make_pairs):
+        """(src, tgt, R, t) of this rank's shard of lane ``lane``'s global batch (CPU tensors)."""
+        full = make_pairs(self.total, n_points, seed=self.lane_seed(lane))
+        return tuple(x[self.lo:self.hi].contiguous() for x in full)
+
+    def calibration_src(self, n_points, make_pairs):
+        """(1, C, N) source cloud of global pair 0 of lane 0: the same on every rank and world size."""
+        return make_pairs(1, n_points, seed=self.lane_seed(0))[0]
+
+    def starts(self, model, n_points):
+        """This rank's columns of the global batch's seven FPS start vectors (call on every rank
+        for every step, in the same order)."""
+        return model.draw_starts(self.total, n_points, n_points)[:, self.lo:self.hi].contiguous()
