@@ -1,7 +1,8 @@
-// sa_bn_mfma.hip -- batch-statistics BatchNorm training of the two-layer set-abstraction tables
-// (sa2 35-32-64, sa3 67-64-64; pointnet2_utils.py:195-200 with the module in train(), driven by
-// train.py:105-125) on the matrix cores.  The lane-per-entry VALU passes of sa_bn.hip remain for
-// sa1 (3-16-16-32) and for fp64 inputs.
+// sa_bn_mfma.hip -- batch-statistics BatchNorm training of the REF-R set-abstraction tables
+// (sa1 3[+3]-16-16-32, sa2 35-32-64, sa3 67-64-64; pointnet2_utils.py:195-200 with the module in
+// train(), driven by train.py:105-125) on the matrix cores (sa1: sa_bnm3_kernel, passes 1-3 / 10 /
+// 21 / 22 / 30; sa2 / sa3: sa_bnm_kernel).  The lane-per-entry VALU passes of sa_bn.hip remain only
+// for fp64 inputs and channel-first two-layer feature tables (and as batchnorm.USE_MFMA = False).
 //
 // Per grouped entry e = (centre, slot), x = [p - c, f_n]:
 //   z1 = W1 x + b1, h1 = relu(z1 s1 + t1), z2 = W2 h1 + b2, h2 = relu(z2 s2 + t2), out = max_slot h2

@@ -11,7 +11,9 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdvcp_hip.so")
+# DVCP_LIB_PATH: load another build of the library (the A/B scripts' variants) without touching
+# the in-tree one; it must report this package's ABI version like any other
+LIB_PATH = os.environ.get("DVCP_LIB_PATH") or os.path.join(_HERE, "libdvcp_hip.so")
 
 F32, F64 = 0, 1
 ABI_VERSION = 3   # include/dvcp.h DVCP_ABI_VERSION
@@ -97,10 +99,7 @@ def load():
     lib.dvcp_last_error.argtypes = []
     lib.dvcp_abi_version.restype = ctypes.c_int
     lib.dvcp_abi_version.argtypes = []
-    # DVCP_SKIP_ABI=1: the A/B harness (tools/gpu_ab_micro.sh) loading an older build for the entry
-    # points it times; entry points that build lacks are left undeclared
-    skip = os.environ.get("DVCP_SKIP_ABI") == "1"
-    if lib.dvcp_abi_version() != ABI_VERSION and not skip:
+    if lib.dvcp_abi_version() != ABI_VERSION:
         raise RuntimeError(f"dvcp: {LIB_PATH} has ABI version {lib.dvcp_abi_version()}, this package expects "
                            f"{ABI_VERSION}: rebuild it (make -j16 in deepvcp-pointcloud-registration_amd/)")
     lib.dvcp_knn_grid_workspace_bytes.restype = ctypes.c_int64
@@ -135,14 +134,11 @@ def load():
     lib.dvcp_cpg1d_nparams.argtypes = []
     lib.dvcp_sa_bn_pack_floats.restype = ctypes.c_int64
     lib.dvcp_sa_bn_pack_floats.argtypes = [ctypes.c_int, ctypes.c_void_p]
-    if hasattr(lib, "dvcp_sa_bnm_supported") or not skip:
-        lib.dvcp_sa_bnm_supported.restype = ctypes.c_int
-        lib.dvcp_sa_bnm_supported.argtypes = [ctypes.c_int, ctypes.c_void_p]
-        lib.dvcp_sa_bnm_workspace_bytes.restype = ctypes.c_int64
-        lib.dvcp_sa_bnm_workspace_bytes.argtypes = [ctypes.c_int] * 5 + [ctypes.c_void_p, ctypes.c_int]
+    lib.dvcp_sa_bnm_supported.restype = ctypes.c_int
+    lib.dvcp_sa_bnm_supported.argtypes = [ctypes.c_int, ctypes.c_void_p]
+    lib.dvcp_sa_bnm_workspace_bytes.restype = ctypes.c_int64
+    lib.dvcp_sa_bnm_workspace_bytes.argtypes = [ctypes.c_int] * 5 + [ctypes.c_void_p, ctypes.c_int]
     for name, args in SIGNATURES.items():
-        if skip and not hasattr(lib, name):
-            continue
         fn = getattr(lib, name)
         fn.restype = ctypes.c_int
         fn.argtypes = args

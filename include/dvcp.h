@@ -349,6 +349,11 @@ int dvcp_sa_bn_backward(int dtype, const void* xyz, int64_t sb, int64_t sc, int6
  *       the two-layer tables if grad_feat is given, dL/d feat (B x N x D fp32); fixed-order sums.
  *   grad_out: B S x C_last fp32; arg / out / zbest: pass 10's outputs (read by passes 20+, 30).
  *   workspace: dvcp_sa_bnm_workspace_bytes(B, S, N, nsample, nlayer, chans, backward = pass 30).
+ *   A centre without hits (count 0; FPS centres always hit themselves, so the reference never
+ *   has one) is treated here as the ball query's padded form describes it: count clamped to 1,
+ *   so its nsample slots are nsample copies of list entry 0 (point 0), counted in the batch
+ *   statistics, and its output row is the MLP of that entry.  (The eval tables,
+ *   dvcp_sa_group_mlp*, give such a centre a zero row instead.)
  */
 int dvcp_sa_bnm_supported(int nlayer, const int* chans);
 int64_t dvcp_sa_bnm_workspace_bytes(int B, int S, int N, int nsample, int nlayer, const int* chans,

@@ -374,6 +374,62 @@ def test_sa_batch_stats_train_vs_oracle(cuda, table, monkeypatch):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("table", ["sa1", "sa2_rows", "sa3_rows"])
+def test_sa_batch_stats_mfma_many_centres_per_wave(cuda, table, monkeypatch):
+    """The matrix-core batch-statistics passes (csrc/sa_bn_mfma.hip) with B x S = 8192 centres,
+    beyond the 4096 waves of their largest grid: every wave then takes several centres in turn,
+    carrying its statistics and gradient accumulators across them, as at C3 / C5 training size.
+    Against the VALU passes (batchnorm.USE_MFMA = False) on the same inputs: forward output,
+    running statistics, every conv / BN parameter gradient and the feature gradient."""
+    import dvcp
+    from dvcp import batchnorm, ops
+    from tests_helpers import randomize_bn
+    rows = table.endswith("_rows")
+    base = table.replace("_rows", "")
+    g = torch.Generator().manual_seed(["sa1", "sa2", "sa3"].index(base) + 500)
+    B, N = 4, 2048
+    S = N                                           # 8192 centres in all
+    cin, mlp, radius, ns = {"sa1": (3, [16, 16, 32], 0.1, 256), "sa2": (35, [32, 64], 0.2, 128),
+                            "sa3": (67, [64, 64], 0.4, 64)}[base]
+    span = {"sa1": 0.6, "sa2": 1.2, "sa3": 2.0}[base]
+    xyz = torch.rand(B, 3, N, generator=g) * span - span / 2
+    feat = None if base == "sa1" else torch.randn(B, cin - 3, N, generator=g)
+    torch.manual_seed(13)
+    mod = dvcp.pointnet2_utils.PointNetSetAbstraction(S, radius, ns, cin, mlp)
+    randomize_bn(mod)
+    x = xyz.to(cuda)
+    f = None if feat is None else (feat.permute(0, 2, 1).contiguous().to(cuda).permute(0, 2, 1) if rows
+                                   else feat.to(cuda))
+    start = torch.randint(0, N, (B,), generator=g).to(cuda)
+    _, ctr = ops.fps(x, S, start, pdim=2)
+    count, lst, _ = ops.ball_query(x, ctr, radius, ns, pdim=2, cdim_pts=2)
+    G = torch.randn(B, S, mlp[-1], generator=g).to(cuda)
+    res = {}
+    for use in (True, False):
+        monkeypatch.setattr(batchnorm, "USE_MFMA", use)
+        m = copy.deepcopy(mod).to(cuda).train()
+        out, st = batchnorm.train_forward(m, x, ctr, f, count, lst, ns)
+        assert bool(st.get("mfma")) == use
+        lay = dict(pts=x, ctr=ctr, feat=f, count=count, lst=lst, ns=ns, bn=st)
+        gp, gF = batchnorm.train_backward(m, lay, G, want_feat_grad=f is not None)
+        res[use] = (out, [(b.running_mean.clone(), b.running_var.clone()) for b in m.mlp_bns], gp, gF)
+    (om, sm, gm, fm), (ov, sv, gv, fv) = res[True], res[False]
+    torch.testing.assert_close(om, ov, rtol=1e-4, atol=1e-4)
+    for (a_mean, a_var), (b_mean, b_var) in zip(sm, sv):
+        torch.testing.assert_close(a_mean, b_mean, rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(a_var, b_var, rtol=1e-5, atol=1e-7)
+    o = 0
+    for i, conv in enumerate(mod.mlp_convs):
+        co, ci = conv.weight.shape[:2]
+        w_scale = float(gv[o:o + co * ci].abs().max())
+        for name, n, floor in (("conv.w", co * ci, None), ("conv.b", co, w_scale), ("bn.w", co, None), ("bn.b", co, None)):
+            _close(gm[o:o + n], gv[o:o + n], 1e-3 if name != "conv.b" else 5e-2, f"{table} layer {i} {name}",
+                   floor=floor or 1e-30)
+            o += n
+    if fv is not None:
+        _close(fm, fv, 1e-3, f"{table} feature gradient")
+
+
 def test_fe_head_backward_vs_torch(cuda):
     """deep_feat_extraction.py:15 fc backward: dW, db, dx against torch autograd."""
     from dvcp import ops
