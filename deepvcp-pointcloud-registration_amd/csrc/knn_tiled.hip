@@ -529,7 +529,16 @@ __global__ __launch_bounds__(kTiledThreads) void knn_tiled_query_kernel(const fl
 // Exactness is unchanged: the merged list is always the 32 smallest (d2, index) keys of every
 // point appended, and a point is only left out when its key is not below a k-th key that is at
 // least the true one (filters and pruning use the last merged, i.e. a stale-high, k-th key).
-constexpr int kSelBufN = 16;
+// DVCP_KNN_SORD: the sorted tile order in LDS (default); DVCP_KNN_STAGE_OUT: coalesced output rows
+#ifndef DVCP_KNN_SORD
+#define DVCP_KNN_SORD 1
+#endif
+#ifndef DVCP_KNN_STAGE_OUT
+#define DVCP_KNN_STAGE_OUT 2
+#endif
+constexpr int kSelBufN = 16;   // buffer capacity per lane (>= kTile: a merge makes room for a whole tile)
+constexpr int kSelSortN = 16;
+constexpr int kSordWords = (kMaxTiles + 2) / 3;  // a wave's sorted tile order, three 10-bit ids per word
 // A tile's 256 bytes are loaded once some lane is known to need it (prefetching one sorted position
 // ahead made every scanned tile wait for its successor's load at the loop latch, ~660 clk per
 // skipped tile under DVCP_KNN_DIAG; round 3).
@@ -581,7 +590,9 @@ __device__ __forceinline__ void key_ce(uint32_t& ah, uint32_t& al, uint32_t& bh,
   bl = sw ? tl : bl;
 }
 
-template <int R>
+// K32: k == 32 (the forward's), the k-th key is the last slot; otherwise a select loop over the
+// slots, whose 31 hoisted compare masks cost SGPRs the k = 32 kernel does not need.
+template <int R, bool K32>
 __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3))) void knn_sel_query_kernel(const float4* __restrict__ sorted,
                                                                       const float4* __restrict__ tbox,
                                                                       const int32_t* __restrict__ qperm, int M,
@@ -600,8 +611,13 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
     bx = slot % static_cast<int>(gridDim.x);
   }
   const int T = (M + kTile - 1) / kTile;
-  // 12 + 32 KB of LDS (half-precision boxes, candidate buffers): three workgroups per CU
+  // 12 + 32 + 5.3 KB of LDS (half-precision boxes, candidate buffers, sorted tile order): three
+  // workgroups per CU
   __shared__ uint3 hbox[kMaxTiles];
+  // each wave's tile order after the sort, three 10-bit tile ids per word (the chunked scan
+  // recomputes the keys from them): 16 key registers held across the scan spilled to scratch and
+  // were reloaded every chunk
+  __shared__ uint32_t sord[kTiledThreads / kWave][kSordWords];
   __shared__ double sbuf[kTiledThreads / kWave][kSelBufN][kWave];  // lane-private candidate buffers (packed keys)
   __shared__ float4 stile[kTiledThreads / kWave][kTile];            // the wave's current tile (appends)
   {
@@ -630,9 +646,9 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
   float wh[3] = {live ? qx : -__builtin_huge_valf(), live ? qy : -__builtin_huge_valf(),
                  live ? qz : -__builtin_huge_valf()};
 #pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    wl[a] = -wave_max_nonneg_signed(-wl[a]);
-    wh[a] = wave_max_nonneg_signed(wh[a]);
+  for (int a = 0; a < 3; ++a) {  // (wave-uniform: SGPRs)
+    wl[a] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(-wave_max_nonneg_signed(-wl[a]))));
+    wh[a] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wave_max_nonneg_signed(wh[a]))));
   }
   uint32_t keys[R];
 #pragma unroll
@@ -672,28 +688,28 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
     const uint64_t dg_m0 = __builtin_readcyclecounter();
     ++dg_merges;
 #endif
-    double bk[kSelBufN];
+    double bk[kSelSortN];
 #pragma unroll
-    for (int i = 0; i < kSelBufN; ++i) {
+    for (int i = 0; i < kSelSortN; ++i) {
       bk[i] = kKeyEmpty;
-      if (i < n) {
+      if (i < kSelBufN && i < n) {
         const double e = mybuf[i][lane];
         bk[i] = i < fill ? e : bk[i];
       }
     }
     // bitonic sort of the 16 buffered keys, ascending
 #pragma unroll
-    for (int kk = 2; kk <= kSelBufN; kk <<= 1)
+    for (int kk = 2; kk <= kSelSortN; kk <<= 1)
 #pragma unroll
       for (int j = kk >> 1; j > 0; j >>= 1)
 #pragma unroll
-        for (int i = 0; i < kSelBufN; ++i) {
+        for (int i = 0; i < kSelSortN; ++i) {
           const int l = i ^ j;
           if (l > i) key_ce_f64(bk[i], bk[l], (i & kk) == 0);
         }
     // C[i] = min(top[i], buf[31 - i]) (buf[16..31] = empty): bitonic, the 32 smallest keys
 #pragma unroll
-    for (int i = KT - kSelBufN; i < KT; ++i) tk[i] = __builtin_fmin(tk[i], bk[KT - 1 - i]);
+    for (int i = KT - kSelSortN; i < KT; ++i) tk[i] = __builtin_fmin(tk[i], bk[KT - 1 - i]);
     // bitonic merge, ascending
 #pragma unroll
     for (int j = KT >> 1; j > 0; j >>= 1)
@@ -704,7 +720,7 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
       }
     // the k-th key (a dynamically indexed double array would not stay in registers)
     double kk_ = tk[KT - 1];
-    if (kq != KT - 1) {  // wave-uniform; the forward's k = 32 never takes it
+    if (!K32) {  // k = 17..31
 #pragma unroll
       for (int t = 0; t < KT - 1; ++t) kk_ = t == kq ? tk[t] : kk_;
     }
@@ -847,12 +863,34 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
     sgbox[wave][lane / kSubLanes][0] = make_float4(gl[0], gl[1], gl[2], 0.0f);
     sgbox[wave][lane / kSubLanes][1] = make_float4(gh[0], gh[1], gh[2], 0.0f);
   }
+  // the sorted order to LDS; the keys are recomputed per chunk from the tile id (the same
+  // expression as above: the same bits)
+#if DVCP_KNN_SORD
+  for (int i = lane; i < kSordWords; i += kWave) sord[wave][i] = 0u;
   __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int p = r * 64 + lane;
+    if (p < T) atomicOr(&sord[wave][p / 3], (keys[r] & kTileIdBits) << (10 * (p % 3)));
+  }
+  __builtin_amdgcn_wave_barrier();
+#endif
   bool stop = false;
 #pragma unroll 1
   for (int base = 0; base < T && !stop; base += kWave) {
-    uint32_t mykey = keys[base >> 6];  // lane i: sorted position base + i (re-read below, not held)
     const bool inr = base + lane < T;
+#if DVCP_KNN_SORD
+    const int pos = base + lane;
+    const int tt = inr ? static_cast<int>((sord[wave][pos / 3] >> (10 * (pos % 3))) & kTileIdBits) : 0;
+    const uint3 hb = hbox[tt];
+    const uint32_t mykey = inr ? (__float_as_uint(hbox_lb2(hb, wl[0], wl[1], wl[2], wh[0], wh[1], wh[2])) &
+                                  ~kTileIdBits) | static_cast<uint32_t>(tt)
+                               : 0xFFFFFFFFu;  // lane i: sorted position base + i
+#else
+    const uint32_t mykey = keys[base >> 6];
+    const int tt = inr ? static_cast<int>(mykey & kTileIdBits) : 0;
+    const uint3 hb = hbox[tt < T ? tt : 0];
+#endif
     const float klb = __uint_as_float(mykey & ~kTileIdBits);
     const uint64_t over = __ballot(!inr || klb > wkth);
     const int lim = over ? __builtin_ctzll(over) : kWave;  // positions past lim are never needed
@@ -863,8 +901,6 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
     float gks[kKnnSub];
 #pragma unroll
     for (int g = 0; g < kKnnSub; ++g) gks[g] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gk), g * kSubLanes));
-    const int tt = inr ? static_cast<int>(mykey & kTileIdBits) : 0;
-    const uint3 hb = hbox[tt < T ? tt : 0];
     const float blx = half_lo(hb.x), bly = half_hi(hb.x), blz = half_lo(hb.y);
     const float bhx = half_hi(hb.y), bhy = half_lo(hb.z), bhz = half_hi(hb.z);
     bool pass = false;
@@ -878,7 +914,7 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
     while (cand) {
       const int i = __builtin_ctzll(cand);
       cand &= cand - 1ull;
-      const uint32_t key = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(keys[base >> 6]), i));
+      const uint32_t key = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(mykey), i));
       if (__uint_as_float(key & ~kTileIdBits) > wkth) {  // every later tile is farther
         stop = true;
         break;
@@ -913,8 +949,78 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
   uint32_t app_sum = static_cast<uint32_t>(dg_appends);
   for (int off = 32; off > 0; off >>= 1) app_sum += __shfl_xor(app_sum, off, kWave);
 #endif
+#ifndef DVCP_KNN_DIAG
+  if constexpr (K32 && DVCP_KNN_STAGE_OUT == 2) {
+    if (dist && idx && !idx64) {
+      // each lane writes its own 128-B rows as eight 16-byte stores (whole lines per lane)
+      if (!live) return;
+      const int qo = qperm[static_cast<int64_t>(b) * Q + sq];  // (re-read, not held)
+      float4* dr = reinterpret_cast<float4*>(dist + (static_cast<int64_t>(b) * Q + qo) * 32);
+      int4* ir = reinterpret_cast<int4*>(idx + (static_cast<int64_t>(b) * Q + qo) * 32);
+#pragma unroll
+      for (int v = 0; v < KT / 4; ++v) {
+        float dv[4];
+        int iv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const double kv = tk[4 * v + e];
+          const bool ok = kv != kKeyEmpty;
+          dv[e] = ok ? sqrt_rn(key_d2(kv)) : __builtin_huge_valf();
+          iv[e] = ok ? key_index(kv) : -1;
+        }
+        dr[v] = make_float4(dv[0], dv[1], dv[2], dv[3]);
+        ir[v] = make_int4(iv[0], iv[1], iv[2], iv[3]);
+      }
+      return;
+    }
+  }
+  if constexpr (K32 && DVCP_KNN_STAGE_OUT == 1) {
+    if (dist && idx && !idx64) {
+      // Coalesced output rows (the forward's case).  Each lane's query row is 128 B of distances
+      // and 128 B of indices at a scattered position (queries run in curve order); stored straight
+      // from the lanes, every store instruction touches 64 lines with 4 bytes each.  Instead the
+      // rows go through the wave's candidate buffer in LDS, 32 at a time, and eight lanes store a
+      // row as 16-byte pieces: each instruction writes eight whole lines.
+      const int qo = live ? qperm[static_cast<int64_t>(b) * Q + sq] : -1;  // (re-read, not held)
+      float* stage = reinterpret_cast<float*>(sbuf[wave]);             // 32 rows x 33 (4.2 KB of 8)
+#pragma unroll
+      for (int part = 0; part < 2; ++part) {      // 0: distances, 1: indices
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          if ((lane >> 5) == half) {
+#pragma unroll
+            for (int t = 0; t < KT; ++t) {
+              const bool ok = tk[t] != kKeyEmpty;  // fewer than k finite points
+              const float v = part == 0 ? (ok ? sqrt_rn(key_d2(tk[t])) : __builtin_huge_valf())
+                                        : __int_as_float(ok ? key_index(tk[t]) : -1);
+              stage[(lane & 31) * 33 + t] = v;     // (row stride 33: no bank conflicts)
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+          for (int it = 0; it < 4; ++it) {
+            const int row = it * 8 + (lane >> 3), piece = lane & 7;
+            const int rq = __shfl(qo, half * 32 + row, kWave);
+            const float* sr = stage + row * 33 + 4 * piece;
+            const float4 v = make_float4(sr[0], sr[1], sr[2], sr[3]);
+            if (rq >= 0) {
+              float* dst = part == 0 ? dist : reinterpret_cast<float*>(idx);
+              reinterpret_cast<float4*>(dst + (static_cast<int64_t>(b) * Q + rq) * 32)[piece] = v;
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        }
+      }
+      return;
+    }
+  }
+#endif
   if (!live) return;
-  const int64_t o = (static_cast<int64_t>(b) * Q + q) * k;
+  // the query's output row (its index re-read: held across the scan it was spilled)
+  const int qo = qperm[static_cast<int64_t>(b) * Q + sq];
+  const int64_t o = (static_cast<int64_t>(b) * Q + qo) * k;
 #ifdef DVCP_KNN_DIAG
   if (lane == 0 && dist && k == 32) {
     dist[o + 0] = static_cast<float>(dg_scanned);
@@ -991,8 +1097,12 @@ static int knn_tiled_impl(int dtype, const void* ref, int64_t rb, int64_t rc, in
   // k = 17..32 (the forward's 32): the buffered-selection kernel
 #define DVCP_KNNS(RR)                                                                                             \
   if (k > 16 && T <= 64 * RR) {                                                                                   \
-    hipLaunchKernelGGL((dvcp::knn_sel_query_kernel<RR>), grid, dim3(dvcp::kTiledThreads), 0, st, L.sorted, L.tbox, \
-                       L.qperm, M, qry, qb, qc, qn, qf64, Q, k, dist, idx, idx64, xcd);                           \
+    if (k == 32)                                                                                                  \
+      hipLaunchKernelGGL((dvcp::knn_sel_query_kernel<RR, true>), grid, dim3(dvcp::kTiledThreads), 0, st, L.sorted, \
+                         L.tbox, L.qperm, M, qry, qb, qc, qn, qf64, Q, k, dist, idx, idx64, xcd);                 \
+    else                                                                                                          \
+      hipLaunchKernelGGL((dvcp::knn_sel_query_kernel<RR, false>), grid, dim3(dvcp::kTiledThreads), 0, st,          \
+                         L.sorted, L.tbox, L.qperm, M, qry, qb, qc, qn, qf64, Q, k, dist, idx, idx64, xcd);       \
     return dvcp::launch_status("dvcp_knn_tiled(select)");                                                         \
   }
   if (!insertion) {

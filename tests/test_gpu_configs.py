@@ -174,6 +174,65 @@ def test_c5_fp16_features_vs_fp32(cuda):
     torch.testing.assert_close(t1, t0, rtol=0, atol=1e-3)
 
 
+def test_c5_feature_extractor_full_size_vs_oracle(cuda):
+    """C5's feature extractor at full size against the oracle, as test_e2e_c3_pair_vs_oracle does at C3:
+    one 65536-point pair, K = 256, the GPU's own outputs of one forward (extract_features + top-k):
+    * the FPS index sequences of all three layers of both clouds bit-exact (65536 -> 10000 -> 10000
+      -> 10000; pointnet2_utils.py:63-84);
+    * the six ball-query lists in the reference's padded form (pointnet2_utils.py:87-107; sa1
+      scans all 65536 points for each of its 10000 centres) exact, except rows whose differing
+      points sit within 4 ulp of r^2 (the oracle's BLAS-rounded square_distance; counted);
+    * FE geometry exact, FE features (deep_feat_extraction.py:18-32) within rtol 1e-4, scores
+      within 1e-3 relative (the conditioned WL's logit gain), and the K = 256 top-k rank by rank
+      (tests_helpers.topk_parity; weighting_layer.py:26-33)."""
+    import os
+
+    import oracle as O
+    from dvcp import ops
+    from dvcp.synthetic import make_pairs
+    from tests_helpers import ball_rows_mismatch_ok, padded_ball_rows, topk_parity
+    B, N, K, r, s = 1, 65536, 256, 2.0, 0.4
+    src, tgt, _, _ = make_pairs(B, N, seed=558)
+    ref, mine = _calibrated_pair(False, K, r, s, src)
+    mine = mine.to(cuda)
+    torch.manual_seed(2)
+    starts = mine.draw_starts(B, N, N)
+    tr = {}
+    with torch.no_grad():
+        f = mine.extract_features(src.to(cuda), tgt.to(cuda), starts, trace=tr)
+        top = ops.topk(f["score"], K)
+    torch.cuda.synchronize()
+    layers = tr["fe_layers"]
+    radii = [mine.FE1.sa1.radius, mine.FE1.sa2.radius, mine.FE1.sa3.radius]
+    n_boundary = 0
+    torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
+    for side, (cloud, o0, key_xyz, key_feat) in enumerate(((src, 0, "src_xyz", "src_feat"),
+                                                          (tgt, 4, "tgt_xyz", "tgt_feat"))):
+        with torch.no_grad(), O.fps_starts([starts[o0 + i] for i in range(3)]), O.tracing() as trace:
+            xyz_o, feat_o = ref.FE1(cloud)
+            if side == 0:
+                top_o = ref.WL(feat_o, K).view(B, K)
+        d = dict(trace)
+        fps_o = [v for n, v in trace if n == "fps_idx"]
+        ball_o = [v for n, v in trace if n == "ball_idx"]
+        pts = cloud[0].t().contiguous()
+        for lvl, layer in enumerate(layers):
+            fidx = fps_o[lvl][0]
+            assert torch.equal(layer["idx"][side].cpu(), fidx), (side, lvl)
+            ctr = pts[fidx]
+            got = padded_ball_rows(layer, side)
+            n_boundary += ball_rows_mismatch_ok(pts[None], ctr[None], got[None], ball_o[lvl], radii[lvl])
+            pts = ctr
+        assert torch.equal(f[key_xyz].transpose(1, 2).cpu(), xyz_o)
+        torch.testing.assert_close(f[key_feat].cpu(), feat_o, rtol=1e-4, atol=1e-5)
+        if side == 0:
+            want = d["wl_score"][..., 0]
+            torch.testing.assert_close(f["score"].cpu(), want, rtol=1e-3, atol=1e-5)
+            exact, n_amb = topk_parity(top, f["score"], top_o, want, K)
+    print(f"C5 FE: 6 FPS sequences exact, {n_boundary} ball rows differing only at r^2 rounding; GPU top-{K} == "
+          f"oracle top-{K}: {exact} ({n_amb} near-tie rank boundaries)")
+
+
 def test_c5_head_stage_decoupled_vs_oracle(cuda):
     """C5's head at full size, stage-decoupled: the GPU's feature extractor on
     a 65536-point pair, its K = 256 key points moved by R_init, then every head stage against the

@@ -6,3 +6,4 @@ timeout -k 10 700 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-me
   > gpurun_out/${tag}_pytest_gpu.log 2>&1 || exit $?
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.log 2>&1 || exit $?
 timeout -k 10 600 python bench.py --config c5 --no-cpu-baseline > gpurun_out/${tag}_bench_c5.log 2>&1
+timeout -k 10 300 python bench.py > gpurun_out/${tag}_bench.log 2>&1
