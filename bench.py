@@ -219,7 +219,7 @@ def main():
     S = model.FE1.sa1.npoint
     C = int((2 * r) / s + 1) ** 3
     stages, step_roof = stage_roofline(iso, args.iso_steps, ms_step)
-    pmc = _pmc() if args.config == "c3" else {}   # the PMC figures are measured at C3
+    pmc = _pmc(args.config)   # profiles/pmc_summary.json (C3) / pmc_summary_c5.json (C5)
     roofline = dominant_roofline(live, iso, stages, pmc)
     fps_roof = fps_roofline(live, iso, floor_us, pmc)
     res_cpu = res.cpu()
@@ -472,10 +472,12 @@ def fps_roofline(live, iso, floor_us, pmc):
                     "1; the fp32 fractions count the reference graph's 9 flop per point-update"}
 
 
-def _pmc():
-    """profiles/pmc_summary.json (measured at C3), {} if absent."""
+def _pmc(config="c3"):
+    """The PMC summary of this configuration (tools/gpu_pmc.sh, one batch in flight):
+    profiles/pmc_summary.json (C3) or profiles/pmc_summary_c5.json (C5); {} if absent."""
+    name = "pmc_summary.json" if config == "c3" else f"pmc_summary_{config}.json"
     try:
-        return json.load(open(os.path.join(ROOT, "profiles", "pmc_summary.json")))
+        return json.load(open(os.path.join(ROOT, "profiles", name)))
     except Exception:
         return {}
 

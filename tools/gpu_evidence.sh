@@ -17,4 +17,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT
   -- python3 "$ROOT/bench.py" --no-cpu-baseline --inflight 1 --steps 6 --warmup 2 > "$ROOT/gpurun_out/${tag}_iso.log" 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/${tag}_p10" -o run \
   -- python3 "$ROOT/bench.py" --no-cpu-baseline > "$ROOT/gpurun_out/${tag}_p10.log" 2>&1 || exit $?
-bash "$ROOT/tools/gpu_pmc.sh" "${tag}"
+bash "$ROOT/tools/gpu_pmc.sh" "${tag}" || exit $?
+CONFIG=c5 bash "$ROOT/tools/gpu_pmc.sh" "${tag}_c5" || exit $?
+cd "$ROOT" && timeout -k 10 400 python bench.py --config c5 > gpurun_out/${tag}_bench_c5.log 2>&1

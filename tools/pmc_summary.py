@@ -25,11 +25,12 @@ import sys
 # entry point (bench stage key) -> (kernels one call launches once each: the call count,
 #                                  helper kernels the same call also launches)
 ENTRY = {
-    "dvcp_fps_ws": (["fps_select_kernel", "fps_kernel"], []),
-    "dvcp_knn_tiled": (["knn_tiled_query_kernel", "knn_sel_query_kernel"], ["knn_tiled_build_kernel"]),
+    "dvcp_fps_ws": (["fps_select_kernel", "fps_kernel", "fps_split_kernel", "fps_dense_kernel"], []),
+    "dvcp_knn_tiled": (["knn_tiled_query_kernel", "knn_sel_query_kernel"],
+                       ["knn_tiled_build_kernel", "knn_qbox_kernel", "knn_qhist_kernel", "knn_qscan_kernel"]),
     "dvcp_sa_group_mlp_ws": (["sa3_mfma_kernel<", "sa_mlp_mfma_kernel<float, 32,"], ["sa_pre_mfma_kernel<32,", "sa_order_kernel"]),
     "dvcp_sa_group_mlp_rows_ws": (["sa_mlp_mfma_kernel<float, 64,"], ["sa_pre_mfma_kernel<64,"]),
-    "dvcp_ball_query_ws": (["bq_tiled_kernel", "bq_wave_kernel", "ball_query_kernel"], ["bq_build_kernel"]),
+    "dvcp_ball_query_ws": (["bq_tiled_kernel", "bq_wave_kernel", "ball_query_kernel"], ["bq_build_kernel", "bq_pack_kernel"]),
     "dvcp_dfe_tgt": (["dfe_tgt"], []),
     "dvcp_cpg": (["cpg_kernel"], []),
 }
