@@ -29,6 +29,16 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef DVCP_CPG_SPLIT3
 #define DVCP_CPG_SPLIT3 1
 #endif
+// DVCP_CPG_C2: conv2's loop.  2 (default): (ci, kd) planes of scalar weights loaded at once, the
+// second voxel chosen per wave; 1: the round-4 tap loop (a scalar load, a divergent branch and an
+// LDS + scalar-cache wait per tap).  C3 (8 x 64 key points), A/B on one box: 0.249 / 0.250 ->
+// 0.231 / 0.230 ms, conv2's phase 80.5k -> 52.5k clk and scratch 8 -> 0 B.  Measured and not kept:
+// the next plane's weights prefetched into a second SGPR set (spills to VGPR lanes), and W2
+// transposed into LDS read as broadcast float4 per tap (0.249 ms: the LDS pipe bounds it), the
+// same with a register prefetch 0.287 ms (profiles/round5/r5v_cpg_ab.log, r5x_cpg_ab.log).
+#ifndef DVCP_CPG_C2
+#define DVCP_CPG_C2 2
+#endif
 
 // x = x0 + x1 + x2 exactly (bf16 pieces, as sa_mlp_mfma.hip's split3)
 __device__ __forceinline__ void cpg_split3(float x, __bf16& p0, __bf16& p1, __bf16& p2) {
@@ -336,8 +346,7 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
   __syncthreads();
 
   // conv2 (16 -> 4) on VALU, one voxel per thread: a 16-column MFMA tile would leave 12 of its
-  // 16 output columns empty (4x the MFMA time of the useful work).  W2[co][ci][tap] comes through
-  // the scalar cache (wave-uniform), one tap plane (4 x 9 weights) at a time.
+  // 16 output columns empty (4x the MFMA time of the useful work).
   DVCP_CPG_TICK(15)
   int hv[kCpgV];
 #pragma unroll
@@ -347,6 +356,53 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
   for (int v = 0; v < kCpgV; ++v)
 #pragma unroll
     for (int co = 0; co < 4; ++co) o2[v][co] = 0.f;
+#if DVCP_CPG_C2 == 2
+  // The 48 (ci, kd) planes in turn; a plane's 36 weights W2[co][ci][kd][.][.] (9 contiguous floats
+  // per co) are loaded at once (four s_load_dwordx8 + four dwords), one scalar-cache wait per plane
+  // instead of one per tap.  A wave runs its second voxel (tid + 1024 < C: waves 0..4 at C = 1331)
+  // only when some lane has one -- a wave-uniform choice outside the loop, no branch per tap.
+  static_assert(kCpgV == 2, "conv2 plane loop: two voxels per thread at most");
+  {
+    const int hv0 = hv[0], hv1 = hv[1];
+    auto planes = [&](auto two) {
+      constexpr bool T2 = decltype(two)::value;
+      float w[4][9];
+      auto loadw = [&](int pl, float (&wt)[4][9]) {  // pl = 3 ci + kd
+#pragma unroll
+        for (int co = 0; co < 4; ++co)
+#pragma unroll
+          for (int t = 0; t < 9; ++t) wt[co][t] = P2[co * 16 * 27 + 9 * pl + t];
+      };
+      auto plane = [&](int pl, const float (&wt)[4][9]) {
+        const int ci = pl / 3, kd = pl - 3 * ci;
+        const float* xin = out1 + ci * PV + (kd - 1) * PGG;
+#pragma unroll
+        for (int t9 = 0; t9 < 9; ++t9) {
+          const int off = (t9 / 3 - 1) * PG + (t9 % 3 - 1);
+          const float xa = xin[hv0 + off];
+#pragma unroll
+          for (int co = 0; co < 4; ++co) o2[0][co] = __fmaf_rn(wt[co][t9], xa, o2[0][co]);
+          if constexpr (T2) {
+            const float xb = xin[hv1 + off];
+#pragma unroll
+            for (int co = 0; co < 4; ++co) o2[1][co] = __fmaf_rn(wt[co][t9], xb, o2[1][co]);
+          }
+        }
+      };
+#pragma unroll 1
+      for (int pl = 0; pl < 48; ++pl) {
+        loadw(pl, w);
+        plane(pl, w);
+      }
+    };
+    if (__builtin_amdgcn_readfirstlane(tid & ~63) + kCpgThreads < C)
+      planes(std::true_type{});
+    else
+      planes(std::false_type{});
+  }
+#else
+  // W2[co][ci][tap] comes through the scalar cache (wave-uniform), one tap plane (4 x 9 weights)
+  // at a time.
 #pragma unroll 1
   for (int ci = 0; ci < 16; ++ci) {
     const float* xin = out1 + ci * PV;
@@ -372,6 +428,7 @@ __global__ __launch_bounds__(kCpgThreads) void cpg_kernel(const float* __restric
       }
     }
   }
+#endif
   __syncthreads();  // every conv1 output read; out2 overwrites them
 #ifdef DVCP_CPG_DIAG
   uint64_t dg_c2 = __builtin_readcyclecounter();

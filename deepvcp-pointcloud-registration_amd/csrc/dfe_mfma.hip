@@ -35,6 +35,27 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef DVCP_DFE_ABL
 #define DVCP_DFE_ABL 0
 #endif
+// DVCP_DFE_WAHEAD: a candidate's w row is formed two steps before its MFMAs instead of one, so the
+// operands of candidate c + 1 need no w row of the same step (round 5 at C3, A/B on one box:
+// 0.659 / 0.651 -> 0.647 / 0.651 ms, profiles/round5/r5t_dfe_ab.log)
+#ifndef DVCP_DFE_WAHEAD
+#define DVCP_DFE_WAHEAD 1
+#endif
+// DVCP_DFE_SCAND: the candidate's coordinates as scalar loads (its index is wave-uniform; measured
+// equal to vector loads, 0.694 / 0.696 ms, profiles/round5/r5r_dfe_ab.log)
+#ifndef DVCP_DFE_SCAND
+#define DVCP_DFE_SCAND 1
+#endif
+// DVCP_DFE_PIN: the operands prepared for candidate c + 1 are pinned (an empty asm that reads
+// them) before step c's exit test.  Without it the compiler sinks their computation past the
+// loop's exit branch into step c + 1, in front of the MFMAs that read them, and the VALU work the
+// pipeline was built to overlap with step c's MFMA chain runs in series with its own chain.
+// Measured (round 5): the pinned schedule is slower, 0.647 / 0.651 -> 0.680 / 0.675 ms; three
+// waves per SIMD overlap one wave's chain with another's VALU better than one wave interleaves
+// both, so the default leaves the compiler's placement.
+#ifndef DVCP_DFE_PIN
+#define DVCP_DFE_PIN 0
+#endif
 
 // x = x0 + x1 + x2 exactly in three bf16 pieces; a.b from the six significant piece products
 // (the fp32-accurate split of sa_mlp_mfma.hip, whose header gives the error bound)
@@ -192,6 +213,13 @@ __global__ __launch_bounds__(kDfeMfmaWaves * kWave) void dfe_tgt_mfma_kernel(
 // mantissas, 5 bits of carry, 53-bit accumulator), so a butterfly sum equals the reference's
 // ordered sum; w_j = dist_j / dist_sum in fp64 is then bit-identical.
 constexpr int kDfe1Waves = 4;
+#ifndef DVCP_DFE_GRID
+#define DVCP_DFE_GRID 768
+#endif
+// workgroups (a multiple of 8): 768 = three per CU, every wave resident from the start (one fp64
+// prologue per workgroup, no tail of late workgroups); 2048 / 1536 / 1024 / 768 measured 0.703 /
+// 0.674 / 0.670 / 0.666 ms and 0.682 / 0.687 / 0.665 / 0.663 (profiles/round5/r5s_dfe_grid_ab.log)
+constexpr int kDfeGrid = DVCP_DFE_GRID;
 
 // v + (v moved by the DPP pattern CTRL), fp64 (the two halves moved separately)
 template <int CTRL>
@@ -214,7 +242,7 @@ struct Dfe1Lds {
   float e[kDfeKS][64];   // E as the B fragment: [k-step][lane]
 #endif
   float eb[32];          // e
-  float w[kDfe1Waves][2][32];  // per-wave w rows of two consecutive candidates (fp64 quotient rounded to fp32)
+  float w[kDfe1Waves][4][32];  // per-wave w rows of consecutive candidates (fp64 quotient rounded to fp32)
 };
 
 // FT: the feature table's element type -- float, or _Float16 (the C5 "fp16 features" storage:
@@ -363,9 +391,16 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
     G.px = ref.at(bb, 0, n);
     G.py = ref.at(bb, 1, n);
     G.pz = ref.at(bb, 2, n);
+#if DVCP_DFE_SCAND
+    const float* cq = cand + static_cast<int64_t>(__builtin_amdgcn_readfirstlane(gc)) * 3;
+    G.cx = cq[0];
+    G.cy = cq[1];
+    G.cz = cq[2];
+#else
     G.cx = cand[static_cast<int64_t>(gc) * 3];
     G.cy = cand[static_cast<int64_t>(gc) * 3 + 1];
     G.cz = cand[static_cast<int64_t>(gc) * 3 + 2];
+#endif
   };
   // get_cat_feat_tgt.py:57-58 (lanes 32..63 mirror lanes 0..31): the w row of a candidate, into
   // the wave's LDS row `buf` (two rows: a candidate's row is written while the previous one may
@@ -433,6 +468,14 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
       X.s[t] = dfe_split3(f8);
     }
   };
+#if DVCP_DFE_PIN
+  auto pin = [&](const Prepared& X) {
+    asm volatile("" ::"v"(X.x0), "v"(X.x1), "v"(X.s[0].p0), "v"(X.s[0].p1), "v"(X.s[0].p2), "v"(X.s[1].p0),
+                 "v"(X.s[1].p1), "v"(X.s[1].p2));
+  };
+#else
+  auto pin = [&](const Prepared&) {};
+#endif
   // H = X E^T on the matrix cores; zero-started accumulators, e added once to the row maximum:
   // max_j fl(h_j + e) = fl(max_j h_j + e) (rounding is monotone)
   auto mfma = [&](const Prepared& X) {
@@ -465,6 +508,7 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
   // the scheduler places between the MFMAs; kNN rows are loaded six candidates ahead (they come
   // from HBM / the infinity cache), gathered rows two ahead of their use.  Slots: rows U & 7,
   // gathered rows and operands U & 1 (unrolled by 8, so every slot index is a constant).
+  constexpr int WA = DVCP_DFE_WAHEAD;
   float dj[8];
   int nn[8];
   Gathered G[2];
@@ -482,15 +526,18 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
     gather(t0, nn[0], G[0]);
     gather(c1, nn[1], G[1]);
     weights(dj[0], 0);
+    if (WA) weights(dj[1], 1);
     prep(G[0], 0, X[0]);
   }
 #define DVCP_DFE_STEP(U)                                              \
   {                                                                   \
     const f32x16 acc = mfma(X[(U)&1]);                                \
-    weights(dj[((U) + 1) & 7], ((U) + 1) & 1);                        \
-    prep(G[((U) + 1) & 1], ((U) + 1) & 1, X[((U) + 1) & 1]);          \
+    if (!WA) weights(dj[((U) + 1) & 7], ((U) + 1) & 3);               \
+    prep(G[((U) + 1) & 1], ((U) + 1) & 3, X[((U) + 1) & 1]);          \
+    if (WA) weights(dj[((U) + 2) & 7], ((U) + 2) & 3);                \
     load_row(t6, dj[((U) + 6) & 7], nn[((U) + 6) & 7]);               \
     gather(t2, nn[((U) + 2) & 7], G[(U)&1]);                          \
+    pin(X[((U) + 1) & 1]);                                            \
     finish(t0, acc);                                                  \
     advance(t0);                                                      \
     advance(t2);                                                      \
@@ -526,8 +573,8 @@ int launch_dfe_tgt_mfma(PointsView<T> ref, const float* feat, int M, const float
                        dist, idx, Q, B, params, out);
   } else {
     // a few resident workgroups per CU amortise the fp64 prologue over many candidates
-    const int xcd = B % 8 == 0 && need >= 2048 ? 1 : 0;  // equal pairs per XCD
-    const int grid = static_cast<int>(need < 2048 ? need : 2048);
+    const int xcd = B % 8 == 0 && need >= kDfeGrid ? 1 : 0;  // equal pairs per XCD
+    const int grid = static_cast<int>(need < kDfeGrid ? need : kDfeGrid);
     hipLaunchKernelGGL((dfe_tgt_mfma1_kernel<T>), dim3(grid), dim3(kDfe1Waves * kWave), 0, st, ref, feat, M, cand,
                        dist, idx, Q, B, params, out, xcd);
   }
@@ -544,8 +591,8 @@ int launch_dfe_tgt_mfma_f16(PointsView<T> ref, const _Float16* feat, int M, cons
     return DVCP_EINVAL;
   }
   const int64_t need = (total + kDfeMfmaWaves - 1) / kDfeMfmaWaves;
-  const int xcd = B % 8 == 0 && need >= 2048 ? 1 : 0;
-  const int grid = static_cast<int>(need < 2048 ? need : 2048);
+  const int xcd = B % 8 == 0 && need >= kDfeGrid ? 1 : 0;
+  const int grid = static_cast<int>(need < kDfeGrid ? need : kDfeGrid);
   hipLaunchKernelGGL((dfe_tgt_mfma1_kernel<T, _Float16>), dim3(grid), dim3(kDfe1Waves * kWave), 0, st, ref, feat, M,
                      cand, dist, idx, Q, B, params, out, xcd);
   return launch_status("dvcp_dfe_tgt_f16");

@@ -824,6 +824,11 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa3_mfma_kernel(
   }
 }
 
+#ifndef DVCP_SA_GRID
+#define DVCP_SA_GRID 4096
+#endif
+constexpr int kSaGrid = DVCP_SA_GRID;  // workgroups of the grid-strided centre loops (a multiple of 8)
+
 template <typename T, typename FT, int D>
 int launch_sa3_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, const void* c, int64_t cb, int64_t cc,
                     int64_t cn, int S, int B, const void* feat, int64_t fb, int64_t fd, int64_t fn, const int32_t* count,
@@ -831,7 +836,7 @@ int launch_sa3_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, const v
   PointsView<T> pv{static_cast<const T*>(xyz), sb, sc, sn};
   PointsView<T> cv{static_cast<const T*>(c), cb, cc, cn};
   const int64_t centres = static_cast<int64_t>(B) * S;
-  const int grid = static_cast<int>(centres < 4096 * kMfmaWaves ? (centres + kMfmaWaves - 1) / kMfmaWaves : 4096);
+  const int grid = static_cast<int>(centres < kSaGrid * kMfmaWaves ? (centres + kMfmaWaves - 1) / kMfmaWaves : kSaGrid);
   const int xcd = B % 8 == 0 && grid % 8 == 0 ? 1 : 0;
   hipLaunchKernelGGL((sa3_mfma_kernel<T, FT, D>), dim3(grid), dim3(kMfmaWaves * kWave), 0, st, pv, cv, S, B,
                      static_cast<const FT*>(feat), fb, fd, fn, count, list, nsample, params, out, xcd);
@@ -860,7 +865,7 @@ int launch_sa_mfma(const void* xyz, int64_t sb, int64_t sc, int64_t sn, int N, c
   PointsView<T> pv{static_cast<const T*>(xyz), sb, sc, sn};
   PointsView<T> cv{static_cast<const T*>(c), cb, cc, cn};
   const int64_t centres = static_cast<int64_t>(B) * S;
-  const int grid = static_cast<int>(centres < 4096 * kMfmaWaves ? (centres + kMfmaWaves - 1) / kMfmaWaves : 4096);
+  const int grid = static_cast<int>(centres < kSaGrid * kMfmaWaves ? (centres + kMfmaWaves - 1) / kMfmaWaves : kSaGrid);
   const int xcd = B % 8 == 0 && grid % 8 == 0 ? 1 : 0;
   if (order)
     hipLaunchKernelGGL((sa_order_kernel<T>), dim3(B), dim3(kBuildThreads), 0, st, cv, S, order);
