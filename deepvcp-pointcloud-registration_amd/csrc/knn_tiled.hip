@@ -590,9 +590,11 @@ __device__ __forceinline__ void key_ce(uint32_t& ah, uint32_t& al, uint32_t& bh,
   bl = sw ? tl : bl;
 }
 
-// K32: k == 32 (the forward's), the k-th key is the last slot; otherwise a select loop over the
-// slots, whose 31 hoisted compare masks cost SGPRs the k = 32 kernel does not need.
-template <int R, bool K32>
+// Every k in 17..32 selects the 32 nearest keys (the pruning bound is the 32nd) and writes the
+// first k: ordered by (d^2, index), the first k of the 32 nearest are the k nearest.  (Round 5
+// had a k < 32 instantiation bounding by the k-th key: its select loop over the slots cost 272 B
+// of scratch per lane; k = 17..31 are test and API cases, the forward's k is 32.)
+template <int R>
 __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3))) void knn_sel_query_kernel(const float4* __restrict__ sorted,
                                                                       const float4* __restrict__ tbox,
                                                                       const int32_t* __restrict__ qperm, int M,
@@ -670,7 +672,6 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
   double tk[KT];
 #pragma unroll
   for (int t = 0; t < KT; ++t) tk[t] = kKeyEmpty;
-  const int kq = k - 1;  // wave-uniform
   float kth = live ? __builtin_huge_valf() : 0.0f;  // dead lanes never take a point
   float wkth = wave_max_nonneg(kth);
   int fill = 0;
@@ -718,13 +719,7 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
         const int l = i ^ j;
         if (l > i) key_ce_f64(tk[i], tk[l], true);
       }
-    // the k-th key (a dynamically indexed double array would not stay in registers)
-    double kk_ = tk[KT - 1];
-    if (!K32) {  // k = 17..31
-#pragma unroll
-      for (int t = 0; t < KT - 1; ++t) kk_ = t == kq ? tk[t] : kk_;
-    }
-    kth = live ? key_d2(kk_) : 0.0f;
+    kth = live ? key_d2(tk[KT - 1]) : 0.0f;
     wkth = wave_max_nonneg(kth);
     fill = 0;
 #ifdef DVCP_KNN_DIAG
@@ -950,8 +945,8 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
   for (int off = 32; off > 0; off >>= 1) app_sum += __shfl_xor(app_sum, off, kWave);
 #endif
 #ifndef DVCP_KNN_DIAG
-  if constexpr (K32 && DVCP_KNN_STAGE_OUT == 2) {
-    if (dist && idx && !idx64) {
+  if constexpr (DVCP_KNN_STAGE_OUT == 2) {
+    if (dist && idx && !idx64 && k == KT) {
       // each lane writes its own 128-B rows as eight 16-byte stores (whole lines per lane)
       if (!live) return;
       const int qo = qperm[static_cast<int64_t>(b) * Q + sq];  // (re-read, not held)
@@ -974,8 +969,8 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
       return;
     }
   }
-  if constexpr (K32 && DVCP_KNN_STAGE_OUT == 1) {
-    if (dist && idx && !idx64) {
+  if constexpr (DVCP_KNN_STAGE_OUT == 1) {
+    if (dist && idx && !idx64 && k == KT) {
       // Coalesced output rows (the forward's case).  Each lane's query row is 128 B of distances
       // and 128 B of indices at a scattered position (queries run in curve order); stored straight
       // from the lanes, every store instruction touches 64 lines with 4 bytes each.  Instead the
@@ -1097,12 +1092,8 @@ static int knn_tiled_impl(int dtype, const void* ref, int64_t rb, int64_t rc, in
   // k = 17..32 (the forward's 32): the buffered-selection kernel
 #define DVCP_KNNS(RR)                                                                                             \
   if (k > 16 && T <= 64 * RR) {                                                                                   \
-    if (k == 32)                                                                                                  \
-      hipLaunchKernelGGL((dvcp::knn_sel_query_kernel<RR, true>), grid, dim3(dvcp::kTiledThreads), 0, st, L.sorted, \
-                         L.tbox, L.qperm, M, qry, qb, qc, qn, qf64, Q, k, dist, idx, idx64, xcd);                 \
-    else                                                                                                          \
-      hipLaunchKernelGGL((dvcp::knn_sel_query_kernel<RR, false>), grid, dim3(dvcp::kTiledThreads), 0, st,          \
-                         L.sorted, L.tbox, L.qperm, M, qry, qb, qc, qn, qf64, Q, k, dist, idx, idx64, xcd);       \
+    hipLaunchKernelGGL((dvcp::knn_sel_query_kernel<RR>), grid, dim3(dvcp::kTiledThreads), 0, st, L.sorted,         \
+                       L.tbox, L.qperm, M, qry, qb, qc, qn, qf64, Q, k, dist, idx, idx64, xcd);                   \
     return dvcp::launch_status("dvcp_knn_tiled(select)");                                                         \
   }
   if (!insertion) {

@@ -322,15 +322,17 @@ def test_knn_tiled_xcd_clouds_equal_brute(cuda, B):
     assert torch.equal(i1, i2) and torch.equal(d1, d2)
 
 
-def test_knn_tiled_dyadic_ties_full(cuda):
-    """Coordinates on a 1/8 grid: nearly every distance is tied; order must be (d2, index)."""
+@pytest.mark.parametrize("k", [32, 20])
+def test_knn_tiled_dyadic_ties_full(cuda, k):
+    """Coordinates on a 1/8 grid: nearly every distance is tied; order must be (d2, index).  k = 20
+    runs the 32-key selection kernel and keeps the first k (ties at the k-th slot included)."""
     from dvcp import ops
     g = torch.Generator().manual_seed(7)
     ref = (torch.randint(-16, 17, (2, 12000, 3), generator=g).float() / 8).to(cuda)
     qry = (torch.randint(-20, 21, (2, 5000, 3), generator=g).float() / 8).to(cuda)
-    d1, i1, _ = ops.knn(ref, qry, 32, method="brute")
+    d1, i1, _ = ops.knn(ref, qry, k, method="brute")
     for method in ("tiled", "tiled_insert"):
-        d2, i2, _ = ops.knn(ref, qry, 32, method=method)
+        d2, i2, _ = ops.knn(ref, qry, k, method=method)
         assert torch.equal(i1, i2) and torch.equal(d1, d2), method
 
 
