@@ -25,6 +25,27 @@ struct PointsView {
   __device__ __forceinline__ T at(int b, int c, int64_t n) const {
     return p[b * sb + c * sc + n * sn];
   }
+  // fp32 points in (x, y, z, pad) rows (sc == 1, sn == 4, 16-byte aligned rows: dvcp_points_pack4)
+  __host__ __device__ __forceinline__ bool rows4() const {
+    return sizeof(T) == 4 && sc == 1 && sn == 4 && (sb & 3) == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+  }
+  // the three coordinates of point n: one 16-byte load from one line for rows4() views (a gathered
+  // point of the (B, 3, N) layout costs three 4-byte loads from three lines), else three loads.
+  // rows4() depends on kernel arguments only: the test is wave-uniform and hoisted.
+  __device__ __forceinline__ void load3(int b, int64_t n, T& x, T& y, T& z) const {
+    if constexpr (sizeof(T) == 4) {
+      if (rows4()) {
+        const float4 q = *reinterpret_cast<const float4*>(p + b * sb + 4 * n);
+        x = q.x;
+        y = q.y;
+        z = q.z;
+        return;
+      }
+    }
+    x = at(b, 0, n);
+    y = at(b, 1, n);
+    z = at(b, 2, n);
+  }
 };
 
 template <typename T>

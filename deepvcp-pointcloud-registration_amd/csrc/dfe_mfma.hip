@@ -29,7 +29,8 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef DVCP_DFE_SPLIT3
 #define DVCP_DFE_SPLIT3 1
 #endif
-// DVCP_DFE_ABL (timing experiments only, wrong results): 1 no gather, 2 no MFMA, 3 no weights.
+// DVCP_DFE_ABL (timing experiments only, wrong results): 1 no gather, 2 no MFMA, 3 no weights,
+// 4 no coordinate gather, 5 no feature-row gather.
 // Round 4 at C3 (0.68 ms): 0.51, 0.47, 0.67 ms -- neither the gathers nor the matrix cores alone
 // bound the kernel.  (Contiguous candidate runs per wave measured 0.71: not kept.)
 #ifndef DVCP_DFE_ABL
@@ -56,6 +57,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef DVCP_DFE_PIN
 #define DVCP_DFE_PIN 0
 #endif
+// (Round 5, measured without change: the E fragments held in 26 VGPRs instead of re-read per
+// candidate, 0.655 / 0.653 -> 0.664 / 0.654 ms, profiles/round5/r5aa_dfe_ereg_ab.log.  A build
+// without packed fp32 (target attribute) ran 11x slower with wrong results: not a usable switch.)
 
 // x = x0 + x1 + x2 exactly in three bf16 pieces; a.b from the six significant piece products
 // (the fp32-accurate split of sa_mlp_mfma.hip, whose header gives the error bound)
@@ -248,6 +252,11 @@ struct Dfe1Lds {
 // FT: the feature table's element type -- float, or _Float16 (the C5 "fp16 features" storage:
 // half the gathered bytes; each row is widened to fp32 before the weighting, which then runs in
 // fp32 exactly as for a float table holding the same values).
+// Target points in (x, y, z, pad) float4 rows (PointsView::rows4, dvcp_points_pack4) are gathered
+// as one 16-byte load per neighbour instead of three 4-byte loads from three lines of the
+// (B, 3, M) layout.  Round 5 ablation at C3: the three scattered coordinate loads alone cost
+// 0.664 -> 0.513 ms, the 128-byte feature rows 0.664 -> 0.62 (profiles/round5/r5ac_dfe_abl.log);
+// with packed rows the call (pack included) runs 0.54 ms (r5ad_p4.log).
 template <typename T, typename FT = float>
 __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per_eu(3))) void dfe_tgt_mfma1_kernel(
     PointsView<T> ref, const FT* __restrict__ feat, int M, const float* __restrict__ cand,
@@ -380,7 +389,11 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
     const int n = nraw < 0 ? 0 : (nraw >= M ? M - 1 : nraw);
 #endif
     if constexpr (sizeof(FT) == 4) {
+#if DVCP_DFE_ABL == 5  // (ablation builds only: the feature rows of the lane's fixed point)
+      const float4* fr = reinterpret_cast<const float4*>(feat + (static_cast<int64_t>(bb) * M + r32) * 32 + 16 * h);
+#else
       const float4* fr = reinterpret_cast<const float4*>(feat + (static_cast<int64_t>(bb) * M + n) * 32 + 16 * h);
+#endif
 #pragma unroll
       for (int v = 0; v < 4; ++v) G.f[v] = fr[v];
     } else {
@@ -388,9 +401,13 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
       G.hf[0] = fr[0];
       G.hf[1] = fr[1];
     }
-    G.px = ref.at(bb, 0, n);
-    G.py = ref.at(bb, 1, n);
-    G.pz = ref.at(bb, 2, n);
+#if DVCP_DFE_ABL == 4  // (ablation builds only: the coordinates of the lane's fixed point)
+    G.px = ref.at(bb, 0, r32);
+    G.py = ref.at(bb, 1, r32);
+    G.pz = ref.at(bb, 2, r32);
+#else
+    ref.load3(bb, n, G.px, G.py, G.pz);
+#endif
 #if DVCP_DFE_SCAND
     const float* cq = cand + static_cast<int64_t>(__builtin_amdgcn_readfirstlane(gc)) * 3;
     G.cx = cq[0];
@@ -557,6 +574,15 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
 #undef DVCP_DFE_STEP
 }
 
+// (x, y, z, 0) float4 rows of B clouds of M points (the layout dfe_tgt_mfma1_kernel's P4 reads)
+__global__ void points_pack4_kernel(PointsView<float> pts, int M, int B, float4* __restrict__ out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= static_cast<int64_t>(B) * M) return;
+  const int b = static_cast<int>(i / M);
+  const int64_t n = i - static_cast<int64_t>(b) * M;
+  out[i] = make_float4(pts.at(b, 0, n), pts.at(b, 1, n), pts.at(b, 2, n), 0.0f);
+}
+
 template <typename T>
 int launch_dfe_tgt_mfma(PointsView<T> ref, const float* feat, int M, const float* cand, const float* dist,
                         const int32_t* idx, int B, int Q, const float* params, float* out, bool literal,
@@ -622,4 +648,17 @@ extern "C" int dvcp_dfe_tgt_f16(int dtype, const void* ref_xyz, int64_t rb, int6
         out, st);
   dvcp::set_error("dvcp_dfe_tgt_f16: bad dtype %d", dtype);
   return DVCP_EINVAL;
+}
+
+extern "C" int dvcp_points_pack4(const float* xyz, int64_t sb, int64_t sc, int64_t sn, int M, int B, float* out,
+                                 void* stream) {
+  DVCP_REQUIRE(xyz && out, "dvcp_points_pack4: null pointer");
+  DVCP_REQUIRE(M >= 0 && B >= 0, "dvcp_points_pack4: bad sizes");
+  const int64_t total = static_cast<int64_t>(B) * M;
+  if (total == 0) return DVCP_OK;
+  DVCP_REQUIRE((reinterpret_cast<uintptr_t>(out) & 15) == 0, "dvcp_points_pack4: out must be 16-byte aligned");
+  hipLaunchKernelGGL(dvcp::points_pack4_kernel, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), dvcp::PointsView<float>{xyz, sb, sc, sn}, M, B,
+                     reinterpret_cast<float4*>(out));
+  return dvcp::launch_status("dvcp_points_pack4");
 }

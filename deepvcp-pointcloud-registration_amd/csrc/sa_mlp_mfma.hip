@@ -333,9 +333,7 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) __attribute__((amdgpu_waves_per
       m_fc = static_cast<int64_t>(m_b) * S + c;
       const int r = count[m_fc];
       m_rows = r < 1 ? 0 : (r > nsample ? nsample : r);
-      m_cx = ctr.at(m_b, 0, c);
-      m_cy = ctr.at(m_b, 1, c);
-      m_cz = ctr.at(m_b, 2, c);
+      ctr.load3(m_b, c, m_cx, m_cy, m_cz);
     }
     const int ncen = static_cast<int>(min<int64_t>(64, (total - qc + qs - 1) / qs));
     // list entry of this lane's point in the next tile to run (centre j, tile n0)
@@ -412,9 +410,14 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) __attribute__((amdgpu_waves_per
             acc1[mt][4 * i + 2] = u.z;
             acc1[mt][4 * i + 3] = u.w;
           }
-        const float dx = static_cast<float>(pts.at(b, 0, n) - cx);
-        const float dy = static_cast<float>(pts.at(b, 1, n) - cy);
-        const float dz = static_cast<float>(pts.at(b, 2, n) - cz);
+        // (points in packed (x, y, z, pad) rows measured no faster here -- sa2 0.298 -> 0.306, sa3
+        // 0.594 -> 0.597 ms, r5ae_sa_p4_bench.log: the U rows dominate the gather -- so the FE passes
+        // the (B, 3, N) layout; load3 takes either)
+        T px, py, pz;
+        pts.load3(b, n, px, py, pz);
+        const float dx = static_cast<float>(px - cx);
+        const float dy = static_cast<float>(py - cy);
+        const float dz = static_cast<float>(pz - cz);
         const float x0 = h == 0 ? dx : dy, x1 = h == 0 ? dz : 0.0f;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
@@ -507,9 +510,11 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) __attribute__((amdgpu_waves_per
             acc1[mt][4 * i + 2] = u.z;
             acc1[mt][4 * i + 3] = u.w;
           }
-        const float dx = static_cast<float>(pts.at(b, 0, n) - cx);
-        const float dy = static_cast<float>(pts.at(b, 1, n) - cy);
-        const float dz = static_cast<float>(pts.at(b, 2, n) - cz);
+        T px, py, pz;
+        pts.load3(b, n, px, py, pz);
+        const float dx = static_cast<float>(px - cx);
+        const float dy = static_cast<float>(py - cy);
+        const float dz = static_cast<float>(pz - cz);
         const float x0 = h == 0 ? dx : dy, x1 = h == 0 ? dz : 0.0f;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
@@ -721,9 +726,7 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa3_mfma_kernel(
       const int r = count[q];
       m_rows = r < 0 ? 0 : (r > nsample ? nsample : r);
       const int c = static_cast<int>(q % S);
-      m_cx = ctr.at(m_b, 0, c);
-      m_cy = ctr.at(m_b, 1, c);
-      m_cz = ctr.at(m_b, 2, c);
+      ctr.load3(m_b, c, m_cx, m_cy, m_cz);
     }
     const int ncen = static_cast<int>(min<int64_t>(64, (total - qc + qs - 1) / qs));
     int js = 0, hs = 0;  // the next half tile: centre js, half hs
@@ -770,9 +773,11 @@ __global__ __launch_bounds__(kMfmaWaves * kWave) void sa3_mfma_kernel(
       const int row = 16 * (sB ? hB : hA) + (r32 & 15);
       // padded rows repeat the first hit (:104-106); a centre without hits reads point 0 (discarded)
       const int n = rows == 0 ? 0 : list[fc * nsample + (row < rows ? row : 0)];
-      const float dx = static_cast<float>(pts.at(b, 0, n) - cx);
-      const float dy = static_cast<float>(pts.at(b, 1, n) - cy);
-      const float dz = static_cast<float>(pts.at(b, 2, n) - cz);
+      T px, py, pz;
+      pts.load3(b, n, px, py, pz);
+      const float dx = static_cast<float>(px - cx);
+      const float dy = static_cast<float>(py - cy);
+      const float dz = static_cast<float>(pz - cz);
       float x[KS];
       x[0] = h == 0 ? dx : dy;
       if constexpr (D == 0) {

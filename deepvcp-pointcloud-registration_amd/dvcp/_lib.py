@@ -49,6 +49,7 @@ SIGNATURES = {
     "dvcp_knn_tiled_insert": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P],
     "dvcp_dfe": [_I, _P, _L, _P, _P, _P],
     "dvcp_dfe_tgt": [_I, _P, _L, _L, _L, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P],
+    "dvcp_points_pack4": [_P, _L, _L, _L, _I, _I, _P, _P],
     "dvcp_dfe_tgt_f16": [_I, _P, _L, _L, _L, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P],
     "dvcp_dfe_tgt_literal": [_I, _P, _L, _L, _L, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P],
     "dvcp_cpg": [_P, _P, _L, _L, _L, _P, _I, _I, _P, _P, _P, _P],

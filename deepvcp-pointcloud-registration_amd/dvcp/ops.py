@@ -81,13 +81,15 @@ def square_distance(src, dst):
     return out
 
 
-def sa_group_mlp(xyz, ctr, feat, count, lst, nsample, chans, params, xyz_pdim=2, feat_ddim=1, feat_pdim=2):
+def sa_group_mlp(xyz, ctr, feat, count, lst, nsample, chans, params, xyz_pdim=2, feat_ddim=1, feat_pdim=2,
+                 ctr_pdim=2):
     """Grouping + [Conv1x1, BN, ReLU]* + max (pointnet2_utils.py:122-132, :195-200).
-    ``feat`` is None or a (B, D, N)-indexable strided view; output (B, S, C_last) fp32."""
+    ``feat`` is None or a (B, D, N)-indexable strided view; output (B, S, C_last) fp32.  Points
+    in (B, N, 4) rows (``points_pack4``, xyz_pdim=1) are gathered one 16-byte load per row."""
     _lib.require_gpu(xyz, ctr, count, lst, params)
     B = xyz.shape[0]
     N, sb, sc, sn = _pts(xyz, xyz_pdim)
-    S, cb, cc, cn = _pts(ctr, 2)
+    S, cb, cc, cn = _pts(ctr, ctr_pdim)
     if feat is not None:
         st = feat.stride()
         D = feat.shape[feat_ddim]
@@ -109,14 +111,14 @@ def sa_group_mlp(xyz, ctr, feat, count, lst, nsample, chans, params, xyz_pdim=2,
     return out
 
 
-def sa_group_mlp_rows(xyz, ctr, feat, rows, count, lst, nsample, chans, params, xyz_pdim=2):
+def sa_group_mlp_rows(xyz, ctr, feat, rows, count, lst, nsample, chans, params, xyz_pdim=2, ctr_pdim=2):
     """``sa_group_mlp`` for the two-layer tables with point n of cloud b taking feature row
     ``rows[b, n]`` of ``feat`` (B, Nf, D) fp32 point-major: the previous layer's per-point rows
     gathered by its FPS order (pointnet2_utils.py:59) without materialising the gathered table."""
     _lib.require_gpu(xyz, ctr, feat, rows, count, lst, params)
     B = xyz.shape[0]
     N, sb, sc, sn = _pts(xyz, xyz_pdim)
-    S, cb, cc, cn = _pts(ctr, 2)
+    S, cb, cc, cn = _pts(ctr, ctr_pdim)
     Nf, D = feat.shape[1], feat.shape[2]
     if feat.dtype != torch.float32 or feat.stride(2) != 1 or rows.dtype != torch.int64 or tuple(rows.shape) != (B, N):
         raise ValueError("sa_group_mlp_rows: feat must be (B, Nf, D) fp32 with contiguous rows, rows (B, N) int64")
@@ -338,10 +340,25 @@ def dfe_tgt(ref_xyz, ref_feat, cand, dist, idx, params, ref_pdim=2, literal=Fals
         raise TypeError(f"dfe_tgt: features must be float32 or float16, got {feat_c.dtype}")
     name = "dvcp_dfe_tgt_f16" if half else ("dvcp_dfe_tgt_literal" if literal else "dvcp_dfe_tgt")
     row = 64 if half else 128
+    if ref_xyz.dtype == torch.float32 and not literal and not (rc == 1 and rn == 4):
+        ref_xyz, rb, rc, rn = points_pack4(ref_xyz, ref_pdim), 4 * M, 1, 4
     call(name, dtype_code(ref_xyz), ptr(ref_xyz), rb, rc, rn, M, ptr(feat_c), ptr(cand_c), ptr(dist_c),
          ptr(idx_c), B, Q, ptr(params), ptr(out), stream(),
          work=(2.0 * 3168 * 32 * B * Q, B * (M * (12 + row) + Q * (12 + 32 * 8 + 128)),
                _dfe_tgt_exec(literal, float(B * Q))))
+    return out
+
+
+def points_pack4(xyz, pdim=2):
+    """(B, M, 4) fp32 rows (x, y, z, 0) of fp32 points (B, 3, M) (pdim=2) or (B, M, 3) (pdim=1):
+    the layout the target DFE gathers with one 16-byte load per neighbour (dvcp_points_pack4)."""
+    _lib.require_gpu(xyz)
+    if xyz.dtype != torch.float32:
+        raise TypeError(f"points_pack4: fp32 points only, got {xyz.dtype}")
+    B = xyz.shape[0]
+    M, rb, rc, rn = _pts(xyz, pdim)
+    out = torch.empty(B, M, 4, dtype=torch.float32, device=xyz.device)
+    call("dvcp_points_pack4", ptr(xyz), rb, rc, rn, M, B, ptr(out), stream(), work=(0.0, 28.0 * B * M, 0.0))
     return out
 
 

@@ -243,6 +243,14 @@ int dvcp_dfe_tgt(int dtype, const void* ref_xyz, int64_t rb, int64_t rc, int64_t
                  const float* ref_feat, const float* cand, const float* dist, const int32_t* idx,
                  int B, int Q, const float* params, float* out, void* stream);
 
+/* (x, y, z, 0) float4 rows of B clouds of M fp32 points (xyz strided like ref_xyz above) into out
+ * (B x M x 4 fp32, 16-byte aligned).  dvcp_dfe_tgt / dvcp_dfe_tgt_f16 given fp32 points in this
+ * layout (rb = 4 M, rc = 1, rn = 4) gather a neighbour's coordinates as one 16-byte load instead
+ * of three scattered 4-byte loads; the results are the same bits either way.  (Added in ABI 3
+ * without a version change: no existing entry point changed.) */
+int dvcp_points_pack4(const float* xyz, int64_t sb, int64_t sc, int64_t sn, int M, int B, float* out,
+                      void* stream);
+
 /* dvcp_dfe_tgt with the target feature table stored as fp16 (ref_feat: B x M x 32 IEEE halves) --
  * BASELINE C5's "fp16 features" storage, half the gathered feature bytes.  Each gathered row is
  * widened to fp32 and the rest is dvcp_dfe_tgt's fp32 arithmetic: the output equals dvcp_dfe_tgt

@@ -796,6 +796,29 @@ def test_paper_pose_vs_checker(cuda, fix):
     assert torch.equal(R2, R) and torch.equal(t2, t)
 
 
+def test_dfe_tgt_packed_point_rows_bit_identical(cuda):
+    """ops.dfe_tgt hands fp32 points to the kernel as (x, y, z, 0) rows (dvcp_points_pack4, one
+    16-byte gather per neighbour); the kernel on the strided (B, 3, M) layout gives the same bits.
+    The pack itself copies the coordinates exactly (pad 0).  Both XCD mappings (B = 2 and 8)."""
+    import dvcp
+    from dvcp import _lib, ops
+    from dvcp.ops import ptr, stream
+    g = torch.Generator().manual_seed(113)
+    mine = dvcp.feat_embedding_layer().eval().to(cuda)
+    for B, Q, M in ((2, 700, 900), (8, 3000, 2000)):
+        xyz = (torch.rand(B, 3, M, generator=g) * 2 - 1).to(cuda)          # (B, 3, M): the FE's layout
+        feat = torch.randn(B, M, 32, generator=g).to(cuda)
+        qry = (torch.rand(B, Q, 3, generator=g) * 2 - 1).to(cuda)
+        dist, idx, _ = ops.knn(xyz, qry, 32, ref_pdim=2, qry_pdim=1)
+        pk = ops.points_pack4(xyz, 2)
+        assert torch.equal(pk[..., :3], xyz.permute(0, 2, 1)) and torch.equal(pk[..., 3], torch.zeros_like(pk[..., 3]))
+        got = ops.dfe_tgt(xyz, feat, qry, dist, idx, mine.packed_params(), ref_pdim=2)
+        raw = torch.empty_like(got)
+        _lib.call("dvcp_dfe_tgt", _lib.F32, ptr(xyz), xyz.stride(0), xyz.stride(1), xyz.stride(2), M, ptr(feat),
+                  ptr(qry), ptr(dist), ptr(idx), B, Q, ptr(mine.packed_params()), ptr(raw), stream())
+        assert torch.equal(got, raw)
+
+
 @pytest.mark.parametrize("f64", [False, True])
 def test_dfe_tgt_fp16_features(cuda, f64):
     """BASELINE C5's fp16 feature storage (dvcp_dfe_tgt_f16): the gathered rows are widened to fp32

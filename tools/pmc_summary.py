@@ -31,7 +31,7 @@ ENTRY = {
     "dvcp_sa_group_mlp_ws": (["sa3_mfma_kernel<", "sa_mlp_mfma_kernel<float, 32,"], ["sa_pre_mfma_kernel<32,", "sa_order_kernel"]),
     "dvcp_sa_group_mlp_rows_ws": (["sa_mlp_mfma_kernel<float, 64,"], ["sa_pre_mfma_kernel<64,"]),
     "dvcp_ball_query_ws": (["bq_tiled_kernel", "bq_wave_kernel", "ball_query_kernel"], ["bq_build_kernel", "bq_pack_kernel"]),
-    "dvcp_dfe_tgt": (["dfe_tgt"], []),
+    "dvcp_dfe_tgt": (["dfe_tgt"], ["points_pack4_kernel"]),
     "dvcp_cpg": (["cpg_kernel"], []),
 }
 READ_CORRECTION = 2.0
