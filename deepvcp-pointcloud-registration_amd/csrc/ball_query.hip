@@ -98,6 +98,10 @@ __global__ __launch_bounds__(kBqThreads) void ball_query_kernel(
 __host__ __device__ constexpr int bq_padded_n(int N) { return (N + 15) & ~15; }
 
 constexpr int kBqTile = 64;
+// DVCP_BQ_ABL (timing experiments only, wrong results): 1 the list stores of the tiled scan skipped
+#ifndef DVCP_BQ_ABL
+#define DVCP_BQ_ABL 0
+#endif
 constexpr int kBqMaxTiles = 1024;             // tiled path: N <= 65536
 constexpr int kBqSmallTiles = 256;            // N <= 16384: the small-bitmap instantiation (occupancy)
 constexpr int kBqCap = 256;                   // candidate points staged in LDS per round
@@ -477,7 +481,9 @@ __global__ __launch_bounds__(256) void bq_tiled_kernel(BqLayout L, int N, Points
               if (act & (j1 + u < je) & !(d2 > r2) & (cnt < nsample)) {
                 const int n = myid[j1 + u];
                 first = cnt == 0 ? n : first;
+#if DVCP_BQ_ABL != 1
                 if (list) list[row + cnt] = n;
+#endif
                 if (padded) padded[row + cnt] = n;
                 ++cnt;
               }
