@@ -57,6 +57,11 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef DVCP_DFE_PIN
 #define DVCP_DFE_PIN 0
 #endif
+// DVCP_DFE_WPE: waves per SIMD the kernel is compiled for (3: 136 VGPRs, no spills; 4: 128 VGPRs
+// and 48 B of spills)
+#ifndef DVCP_DFE_WPE
+#define DVCP_DFE_WPE 3
+#endif
 // (Round 5, measured without change: the E fragments held in 26 VGPRs instead of re-read per
 // candidate, 0.655 / 0.653 -> 0.664 / 0.654 ms, profiles/round5/r5aa_dfe_ereg_ab.log.  A build
 // without packed fp32 (target attribute) ran 11x slower with wrong results: not a usable switch.)
@@ -258,7 +263,7 @@ struct Dfe1Lds {
 // 0.664 -> 0.513 ms, the 128-byte feature rows 0.664 -> 0.62 (profiles/round5/r5ac_dfe_abl.log);
 // with packed rows the call (pack included) runs 0.54 ms (r5ad_p4.log).
 template <typename T, typename FT = float>
-__global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per_eu(3))) void dfe_tgt_mfma1_kernel(
+__global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per_eu(DVCP_DFE_WPE))) void dfe_tgt_mfma1_kernel(
     PointsView<T> ref, const FT* __restrict__ feat, int M, const float* __restrict__ cand,
     const float* __restrict__ dist, const int32_t* __restrict__ idx, int Q, int B, const float* __restrict__ params,
     float* __restrict__ out, int xcd) {

@@ -6,7 +6,8 @@ Same constructor, submodule names (FE1, WL, DFE, cpg) and state_dict keys as the
     forward(src_pts (B, C_in, N), tgt_pts (B, C_in, N), R_init (B|1, 3, 3) fp64, t_init)
         -> (src_keypts (B, K, 3), tgt_vcp (B, K, 3) fp32)
 
-Pipeline (every stage a gfx950 HIP kernel, all on torch's current stream):
+Pipeline (every stage a gfx950 HIP kernel; the set abstractions' ball queries and tables and the
+source rows' DFE run on a side stream beside the FPS chain / the target side of the head):
     FE(src) [fps, ball query, grouped MLP x3, fc + weighting] -> top-K
     -> key-point stage [gather, FPS among key points, ball query, Get_Cat_Feat_Src, R_init]
     -> DFE(src) -> FE(tgt) -> candidate grid -> kNN(k=32) -> fused gather + DFE(tgt) -> CPG.
@@ -182,7 +183,17 @@ class DeepVCP(nn.Module):
         else:
             keypts, src_cat, moved = ops.src_keypoints(src_xyz, src_feat, top, starts[3], R_init, radius=1.0,
                                                        nsample=32)
-        src_dfe = autograd.dfe_rows(src_cat, self.DFE) if train_head else ops.dfe(src_cat, self.DFE.packed_params())
+        if train_head:
+            src_dfe, side = autograd.dfe_rows(src_cat, self.DFE), None
+        else:
+            # the source rows' DFE (a small launch) runs on the side stream beside the candidate
+            # grid, kNN and target DFE, which do not read it; the CPG waits for it
+            cur, side = torch.cuda.current_stream(dev), self._side_stream(dev)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                src_dfe = ops.dfe(src_cat, self.DFE.packed_params())
+            src_cat.record_stream(side)
+            src_dfe.record_stream(cur)
 
         G = int((2 * r) / s + 1)                    # cpg.py:29
         if grid_side(r, s) != G:
@@ -203,6 +214,7 @@ class DeepVCP(nn.Module):
             feat_t = tgt_feat if self.feat_dtype == torch.float32 else tgt_feat.to(self.feat_dtype)
             tgt_dfe = ops.dfe_tgt(tgt_xyz, feat_t, qry, dist, idx, self.DFE.packed_params(), ref_pdim=2)
             tgt_dfe = tgt_dfe.view(B, K, C, 32)
+            torch.cuda.current_stream(dev).wait_stream(side)
             vcp = ops.cpg(src_dfe, tgt_dfe.permute(0, 1, 3, 2), cand, G, self.cpg.packed_params())
         if trace is not None:
             trace.update(src_xyz=src_xyz, src_feat=src_feat, score=score, topk=top, keypts=keypts,
