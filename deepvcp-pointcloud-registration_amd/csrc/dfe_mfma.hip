@@ -63,7 +63,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #define DVCP_DFE_WPE 3
 #endif
 // (Round 5, measured without change: the E fragments held in 26 VGPRs instead of re-read per
-// candidate, 0.655 / 0.653 -> 0.664 / 0.654 ms, profiles/round5/r5aa_dfe_ereg_ab.log.  A build
+// candidate, 0.655 / 0.653 -> 0.664 / 0.654 ms, profiles/round5/r5aa_dfe_ereg_ab.log; the
+// gathered rows three candidates ahead instead of two, 0.597 / 0.587 -> 0.599 / 0.595 ms,
+// r5an_dfe_ga.log.  A build
 // without packed fp32 (target attribute) ran 11x slower with wrong results: not a usable switch.)
 
 // x = x0 + x1 + x2 exactly in three bf16 pieces; a.b from the six significant piece products
