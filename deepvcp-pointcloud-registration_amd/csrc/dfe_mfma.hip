@@ -354,28 +354,35 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
   // Local candidate index li = pl * Q + q -> pair b = xo + P * pl and global candidate b * Q + q,
   // tracked incrementally per pipeline slot (wave-uniform, no integer division per candidate);
   // indices past the end clamp to the last candidate (loads stay in bounds, results unused).
+  // A tracker holds its pair bb and global candidate gc = bb Q + q as well, advanced by constant
+  // steps, so a use is one select against the last candidate instead of a multiply-add chain.
   struct Cand {
-    int li, pl, q;
+    int li, q, bb, gc;
   };
   auto cand_at = [&](int li) {
     Cand c;
     c.li = li;
-    c.pl = li / Q;  // once per slot at the start
-    c.q = li - c.pl * Q;
+    const int pl = li / Q;  // once per slot at the start
+    c.q = li - pl * Q;
+    c.bb = xo + P * pl;
+    c.gc = c.bb * Q + c.q;
     return c;
   };
   const int st_pl = stride / Q, st_q = stride - st_pl * Q;
+  const int st_bb = P * st_pl, st_gc = P * st_pl * Q + st_q, wrap_gc = (P - 1) * Q;
   auto advance = [&](Cand& c) {  // branch-free (scalar selects): li += stride
     c.li += stride;
     c.q += st_q;
-    c.pl += st_pl;
+    c.bb += st_bb;
+    c.gc += st_gc;
     const bool wrap = c.q >= Q;
     c.q = wrap ? c.q - Q : c.q;
-    c.pl = wrap ? c.pl + 1 : c.pl;
+    c.bb = wrap ? c.bb + P : c.bb;
+    c.gc = wrap ? c.gc + wrap_gc : c.gc;
   };
   const Cand last = cand_at(total - 1);
-  auto pair_of = [&](const Cand& c) { return xo + P * (c.li < total ? c.pl : last.pl); };
-  auto glob_of = [&](const Cand& c) { return pair_of(c) * Q + (c.li < total ? c.q : last.q); };
+  auto pair_of = [&](const Cand& c) { return c.li < total ? c.bb : last.bb; };
+  auto glob_of = [&](const Cand& c) { return c.li < total ? c.gc : last.gc; };
   auto load_row = [&](const Cand& c, float& dj, int& n) {
     const int gc = glob_of(c);
     dj = dist[static_cast<int64_t>(gc) * 32 + r32];
@@ -389,7 +396,7 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
   };
   auto gather = [&](const Cand& c, int nraw, Gathered& G) {
     const int bb = pair_of(c);
-    const int gc = bb * Q + (c.li < total ? c.q : last.q);
+    const int gc = glob_of(c);
 #if DVCP_DFE_ABL == 1  // (ablation builds only: every gather reads the lane's fixed row)
     const int n = r32 + 0 * nraw;
 #else
