@@ -539,13 +539,48 @@ __device__ __forceinline__ float wave_fmax_nn(float v) { return float_unorder_fp
 template <int PPT, int THREADS>
 constexpr int fps_select_waves_per_eu() { return PPT <= 10 && THREADS == 1024 ? 5 : 1; }
 
-template <typename T, int PPT, bool TIMING = false, int THREADS = kFpsThreads>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(fps_select_waves_per_eu<PPT, THREADS>())))
-void fps_select_kernel(PointsView<T> pts, int N, int npoint,
-                                                                 const int64_t* __restrict__ start,
-                                                                 int64_t* __restrict__ out_idx,
-                                                                 T* __restrict__ out_xyz,
-                                                                 unsigned long long* __restrict__ prof) {
+// Paired FPS of two full-permutation layers (FE layers 2 and 3 of C3: 10000 -> 10000 -> 10000).
+// Layer 3's FPS runs over layer 2's centres, which are layer 2's points in FPS order: the same
+// point set.  FPS over a set is a function of the set and the start point except where an argmax
+// ties (ties go to the lowest index, which depends on the order), so layer 3 can run on layer 2's
+// points in their own order, from the start point layer 2 picks at step start3, beside layer 2:
+//   * fps_pair_kernel, 2B workgroups: the first B tickets run layer 2 (cloud t) and publish the
+//     index of their pick number start3[t] in slot[t]; the next B run layer 3 over the same cloud
+//     in the same order, waiting only for that slot.  A workgroup's role comes from a ticket taken
+//     when it starts, so a waiting workgroup's producer is always already running.  Layer 2 also
+//     publishes each point's pick number (inv2), by which layer 3 resolves the ties of its argmax
+//     (see the round's tie notes).  flag[t] is raised where neither applies (the one-argmax
+//     fallback of either layer, or a wait that gave up); layer 3's indices are into layer 2's points;
+//   * fps_pair_remap_kernel maps them into layer 2's FPS order (idx3 = layer 2's pick number of
+//     each point) for the clouds without a flag, and orders tie groups (see the round's tie notes);
+//   * the gated select kernel recomputes layer 3 in the reference's order for the flagged clouds.
+// The results are those of the two serial launches, bit for bit (tests/test_gpu_kernels.py).
+template <typename T>
+struct FpsPairArgs {
+  uint32_t* ticket;       // 0 before the launch
+  uint32_t* slot;         // B, 0 before the launch; bit 31 | the point layer 2 picks at step start3
+  int32_t* flag;          // B, 0 before the launch: the cloud needs the gated recomputation
+  uint32_t* inv2;         // B x N, 0 before the launch; bit 31 | layer 2's pick number of each point
+  const int64_t* start3;  // B
+  int64_t* out3_idx;      // B x npoint (indices into layer 2's points until the remap)
+  T* out3_xyz;            // B x 3 x npoint
+};
+constexpr uint32_t kFpsPairSpinCap = 1u << 22;
+// DVCP_FPS_PAIR_DIAG (timing experiments only, wrong results for 1 and 2): 1 layer 3 stops after
+// its start; 2 no tie re-ranking; 3 layer 3 leaves its re-ranked round count in slot[b]
+#ifndef DVCP_FPS_PAIR_DIAG
+#define DVCP_FPS_PAIR_DIAG 0
+#endif
+
+// MODE 0: one cloud per workgroup; 1: the paired launch (role from a ticket); 2: only the clouds
+// whose pair flag is set (the paired launch's fallback).
+template <typename T, int PPT, bool TIMING, int THREADS, int MODE>
+__device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int npoint,
+                                                const int64_t* __restrict__ start,
+                                                int64_t* __restrict__ out_idx,
+                                                T* __restrict__ out_xyz,
+                                                unsigned long long* __restrict__ prof,
+                                                const FpsPairArgs<T>& pa) {
   constexpr int W = THREADS / kWave;
   static_assert(PPT <= 32 && kSelMax == 128 && (THREADS == 512 || THREADS == 1024), "layout");
   // group lanes: lane l holds the box and exact maximum of the wave's group p = l % GP, replicated
@@ -575,11 +610,47 @@ void fps_select_kernel(PointsView<T> pts, int N, int npoint,
   __shared__ T acx[kSelAccept], acy[kSelAccept], acz[kSelAccept];  // the round's accepted centres, rank order
   __shared__ T gbox[W][6][GP];  // group boxes, read back per round by the update (not held in VGPRs)
   __shared__ uint32_t na_cnt, cand_fill;
+  __shared__ int ckey[MODE == 1 ? kSelMax : 1];  // MODE 1: candidates' point indices in a re-ranked round
+  __shared__ int s_gaveup;
   float* lv = reinterpret_cast<float*>(bins);
   uint32_t* lpos = bins + kSelCap;
 
-  const int b = blockIdx.x, tid = threadIdx.x, lane_outer = tid & 63, lane = lane_outer;
+  const int tid = threadIdx.x, lane_outer = tid & 63, lane = lane_outer;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: its LDS addresses stay in SGPRs
+  int b = blockIdx.x;
+  bool consumer = false;  // MODE 1: this workgroup runs layer 3
+  int s3 = -1;            // MODE 1, layer 2: the pick number whose index layer 3 waits for
+  if constexpr (MODE == 1) {
+    __shared__ uint32_t s_ticket;
+    if (tid == 0) s_gaveup = 0;
+    if (tid == 0) s_ticket = __hip_atomic_fetch_add(pa.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int t = __builtin_amdgcn_readfirstlane(static_cast<int>(s_ticket));
+    const int B = static_cast<int>(gridDim.x) / 2;
+    consumer = t >= B;
+    b = consumer ? t - B : t;
+    if (!consumer) {
+      const int64_t s = pa.start3[b];
+      s3 = (s < 0 || s >= npoint) ? 0 : static_cast<int>(s);  // (the layer-3 launch clamps the same way)
+    }
+  }
+  if constexpr (MODE == 2) {
+    if (pa.flag[b] == 0) return;
+  }
+  auto publish = [&](int pick, int64_t idx) {  // layer 2: pick number s3 -> layer 3's start; inverse order
+    if constexpr (MODE == 1) {
+      if (!consumer) {
+        __hip_atomic_store(pa.inv2 + static_cast<int64_t>(b) * N + idx, 0x80000000u | static_cast<uint32_t>(pick),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (pick == s3)
+          __hip_atomic_store(pa.slot + b, 0x80000000u | static_cast<uint32_t>(idx), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  };
+  bool tied = false;  // MODE 1: this cloud needs the gated recomputation (see the fallback below)
+  [[maybe_unused]] int n_repair = 0;
+  [[maybe_unused]] uint64_t rep_clk = 0;
   fps_morton_sort<T, THREADS>(pts, b, N, bins, perm, red, wsum);
 
   T px[PPT], py[PPT], pz[PPT];
@@ -621,15 +692,50 @@ void fps_select_kernel(PointsView<T> pts, int N, int npoint,
     for (int a = 0; a < 6; ++a) gbox[wave][a][lane] = gb[a];
   }
 
-  int64_t* oi = out_idx + static_cast<int64_t>(b) * npoint;
-  T* ox = out_xyz ? out_xyz + static_cast<int64_t>(b) * 3 * npoint : nullptr;
-  int64_t cur = start[b];
+  int64_t* const oidx = MODE == 1 && consumer ? pa.out3_idx : out_idx;
+  T* const oxyz = MODE == 1 && consumer ? pa.out3_xyz : out_xyz;
+  int64_t* oi = oidx + static_cast<int64_t>(b) * npoint;
+  T* ox = oxyz ? oxyz + static_cast<int64_t>(b) * 3 * npoint : nullptr;
+  int64_t cur;
+  if constexpr (MODE == 1) {
+    if (consumer) {  // wait for layer 2's pick number start3 (the setup above ran meanwhile)
+      __shared__ uint32_t s_start;
+      if (tid == 0) {
+        uint32_t v = 0, polls = 0;
+        for (;;) {
+          v = __hip_atomic_load(pa.slot + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (v & 0x80000000u) break;
+          __builtin_amdgcn_s_sleep(8);
+          if (++polls > kFpsPairSpinCap) {
+            v = 0u;
+            break;
+          }
+        }
+        s_start = v;
+      }
+      __syncthreads();
+      const uint32_t v = s_start;
+      if (!(v & 0x80000000u)) {  // gave up waiting: the gated launch recomputes this cloud
+        if (tid == 0) __hip_atomic_fetch_or(pa.flag + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+      cur = static_cast<int64_t>(v & 0x7FFFFFFFu);
+#if DVCP_FPS_PAIR_DIAG == 1
+      return;
+#endif
+    } else {
+      cur = start[b];
+    }
+  } else {
+    cur = start[b];
+  }
   if (cur < 0 || cur >= N) cur = 0;  // host validates; keep the kernel in bounds regardless
   float gub, vmax;
   {
     const T cx = pts.at(b, 0, cur), cy = pts.at(b, 1, cur), cz = pts.at(b, 2, cur);
     if (tid == 0) {
       oi[0] = cur;
+      publish(0, cur);
       if (ox) {
         ox[0] = cx;
         ox[npoint] = cy;
@@ -866,6 +972,7 @@ void fps_select_kernel(PointsView<T> pts, int N, int npoint,
           acy[0] = gy;
           acz[0] = gz;
           oi[step] = static_cast<int64_t>(gp);
+          publish(step, static_cast<int64_t>(gp));
           if (ox) {
             ox[step] = gx;
             ox[npoint + step] = gy;
@@ -875,6 +982,10 @@ void fps_select_kernel(PointsView<T> pts, int N, int npoint,
         lds_barrier();
         kstar = 1;
         vmax = gmax;  // every value is <= gmax; the new centre's drops to 0
+        // MODE 1: layer 3 does not resolve this argmax's ties, and a layer-2 pick at value 0 means
+        // layer 2 may repeat points (its centres are then not layer 2's points as a set): the gated
+        // launch recomputes such a cloud
+        if (consumer || !(gmax > 0.0f)) tied = true;
         break;
       }
       // ---- 3. list: entries in bins >= bsel are the candidates; T over the rest ---------------
@@ -925,9 +1036,17 @@ void fps_select_kernel(PointsView<T> pts, int N, int npoint,
       // is "touched" if some c_i preceding it lowers its running minimum (d(c_i, c_j) < v_j, the
       // point update's formula).  Wave w covers i in [16w, 16w + 16) for j = lane and lane + 64:
       // every wave takes part, and each wave-uniform (broadcast) LDS read of four c_i serves both j.
+      // MODE 1, layer 3: a round whose steps meet a tie is ranked again with the candidates' layer-2
+      // pick numbers as the index (the reference's order for layer 3); cpid then holds those and
+      // ckey the point indices.
+      bool repaired = false;
+      int rk[2];
+      bool eqp[2] = {false, false};
+      auto rank_decide = [&]() {  // phases 4 and 5's decision (twice in a re-ranked round)
       {
         const int i_lo = wave * (kSelMax / W);
         int r0 = 0, r1 = 0, t0 = 0, t1 = 0;
+        int e0 = 0, e1 = 0;  // MODE 1: c_j has an equal-valued predecessor (bits 24+ of srank)
         if (i_lo < cnt) {  // wave-uniform
           const int j0 = lane, j1 = lane + kWave;
           const float v0 = cvv[j0], v1 = cvv[j1];
@@ -964,12 +1083,16 @@ void fps_select_kernel(PointsView<T> pts, int N, int npoint,
               r1 += b1 ? 1 : 0;
               t0 |= (b0 & (d0 < static_cast<T>(v0))) ? 1 : 0;
               t1 |= (b1 & (d1 < static_cast<T>(v1))) ? 1 : 0;
+              if constexpr (MODE == 1) {
+                e0 |= (in & (vv[k] == v0) & (pp[k] < p0)) ? 1 : 0;
+                e1 |= (in & (vv[k] == v1) & (pp[k] < p1)) ? 1 : 0;
+              }
             }
           }
         }
         if (i_lo < cnt) {  // wave-uniform
-          if (r0 | t0) atomicAdd(&srank[lane], static_cast<uint32_t>(r0 | (t0 << 16)));
-          if (r1 | t1) atomicAdd(&srank[lane + kWave], static_cast<uint32_t>(r1 | (t1 << 16)));
+          if (r0 | t0 | e0) atomicAdd(&srank[lane], static_cast<uint32_t>(r0 | (t0 << 16) | (e0 << 24)));
+          if (r1 | t1 | e1) atomicAdd(&srank[lane + kWave], static_cast<uint32_t>(r1 | (t1 << 16) | (e1 << 24)));
         }
       }
       lds_barrier();
@@ -977,7 +1100,7 @@ void fps_select_kernel(PointsView<T> pts, int N, int npoint,
       // ---- 5. k = the smallest rank that fails; accepted = ranks < k (every wave, redundantly) ----
       if (tid == 0) tb_max = 0u;  // every wave read T before the phase-4 barrier
       const int left = npoint - step;
-      int rk[2];
+      eqp[0] = eqp[1] = false;
       uint32_t failr = 0xFFFFFFFFu;
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
@@ -986,7 +1109,8 @@ void fps_select_kernel(PointsView<T> pts, int N, int npoint,
         if (jj < cnt) {
           const uint32_t e = srank[jj];
           const int r = static_cast<int>(e & 0xFFFFu);
-          const bool touched = (e >> 16) != 0u;
+          const bool touched = MODE == 1 ? ((e >> 16) & 0xFFu) != 0u : (e >> 16) != 0u;
+          if constexpr (MODE == 1) eqp[hh] = (e >> 24) != 0u;
           rk[hh] = r;
           const bool fail = r >= left || (r > 0 && (touched || !(cvv[jj] > Tb)));
           failr = fail ? min(failr, static_cast<uint32_t>(r)) : failr;
@@ -994,6 +1118,60 @@ void fps_select_kernel(PointsView<T> pts, int N, int npoint,
       }
       kstar = static_cast<int>(min(min(wave_umin(failr), static_cast<uint32_t>(cnt)),
                                    static_cast<uint32_t>(kSelAccept)));
+      };
+      rank_decide();
+      if constexpr (MODE == 1) {
+        // Ties (layer 3).  Values only drop and unlisted ones stay below every listed one, so a
+        // step's argmax can only tie with listed candidates of the same round-start value, and
+        // equal values are adjacent in rank order.  A tie group inside the accepted prefix (no
+        // member lowers another's minimum) leaves the same state after it in any order: its
+        // members are marked in the output and reordered by layer 2's pick numbers once layer 2
+        // is done (fps_pair_remap_kernel).  A group that reaches the first rejected candidate
+        // is left to the next round; one that starts at rank 0 is ranked now by those pick
+        // numbers, waiting for them.  (Every wave reads the same srank: uniform decisions.)
+        const bool cut = __ballot((eqp[0] && rk[0] == kstar) || (eqp[1] && rk[1] == kstar)) != 0ull;
+        int g0 = 0;  // the group's first rank: the last rank <= k without an equal-valued predecessor
+        if (consumer && cut && !repaired) {
+          int m = -1;
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) m = (rk[hh] <= kstar && !eqp[hh]) ? max(m, rk[hh]) : m;
+          g0 = static_cast<int>(wave_umax(static_cast<uint32_t>(m + 1))) - 1;
+          if (g0 > 0) kstar = g0;
+        }
+        if (consumer && cut && !repaired && g0 == 0 && DVCP_FPS_PAIR_DIAG != 2) {
+#if DVCP_FPS_PAIR_DIAG == 3
+          const uint64_t t_rep = fps_clock();
+#endif
+          lds_barrier();  // every wave has read srank and cpid
+          if (tid < cnt) {
+            const int n = cpid[tid];
+            ckey[tid] = n;
+            uint32_t v = 0, polls = 0;
+            for (;;) {  // layer 2 picks every point (else it flags the cloud): wait for this one
+              v = __hip_atomic_load(pa.inv2 + static_cast<int64_t>(b) * N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if (v & 0x80000000u) break;
+              __builtin_amdgcn_s_sleep(2);
+              if (++polls > kFpsPairSpinCap) {
+                s_gaveup = 1;
+                break;
+              }
+            }
+            cpid[tid] = static_cast<int>(v & 0x7FFFFFFFu);
+          }
+          if (tid < kSelMax) srank[tid] = 0u;
+          lds_barrier();
+          if (s_gaveup) {  // the gated launch recomputes this cloud
+            if (tid == 0) __hip_atomic_fetch_or(pa.flag + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+          }
+          repaired = true;
+          ++n_repair;
+          rank_decide();
+#if DVCP_FPS_PAIR_DIAG == 3
+          rep_clk += fps_clock() - t_rep;
+#endif
+        }
+      }
       // the accepted centres in rank order, for the update: every wave writes the same values
       // (its own reads below follow its own writes in LDS order)
 #pragma unroll
@@ -1017,7 +1195,11 @@ void fps_select_kernel(PointsView<T> pts, int N, int npoint,
         for (int hh = 0; hh < 2; ++hh) {
           const int jj = hh * 64 + lane;
           if (rk[hh] < kstar) {
-            oi[step + rk[hh]] = cpid[jj];
+            const int n = MODE == 1 && repaired ? ckey[jj] : cpid[jj];
+            // MODE 1, layer 3: bit 62 marks a member of a tie group after its first
+            const bool mk = MODE == 1 && consumer && !repaired && eqp[hh];
+            oi[step + rk[hh]] = static_cast<int64_t>(n) | (mk ? (int64_t(1) << 62) : int64_t(0));
+            publish(step + rk[hh], n);
             if (ox) {
               ox[step + rk[hh]] = cxx[jj];
               ox[npoint + step + rk[hh]] = cyy[jj];
@@ -1068,6 +1250,12 @@ void fps_select_kernel(PointsView<T> pts, int N, int npoint,
     tick(4);
     step += kstar;
   }
+  if constexpr (MODE == 1) {
+    if (tied && tid == 0) __hip_atomic_fetch_or(pa.flag + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if DVCP_FPS_PAIR_DIAG == 3
+    if (consumer && tid == 0) pa.slot[b] = static_cast<uint32_t>(n_repair) | (static_cast<uint32_t>(min(rep_clk >> 10, uint64_t(0xFFFFFF))) << 8);
+#endif
+  }
   if constexpr (TIMING) {
     if (prof && lane == 0) {  // per wave: [rounds, scans, fallbacks, clk: scan, decide+list, rank, prefix, update]
       unsigned long long* o = prof + (static_cast<int64_t>(b) * W + wave) * kFpsProf;
@@ -1076,6 +1264,89 @@ void fps_select_kernel(PointsView<T> pts, int N, int npoint,
       o[2] = n_fallback;
       for (int k = 0; k < 5; ++k) o[3 + k] = ph[k];
       for (int k = 0; k < 4; ++k) o[8 + k] = why[k];
+    }
+  }
+}
+
+template <typename T, int PPT, bool TIMING = false, int THREADS = kFpsThreads>
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(fps_select_waves_per_eu<PPT, THREADS>())))
+void fps_select_kernel(PointsView<T> pts, int N, int npoint, const int64_t* __restrict__ start,
+                       int64_t* __restrict__ out_idx, T* __restrict__ out_xyz,
+                       unsigned long long* __restrict__ prof) {
+  fps_select_body<T, PPT, TIMING, THREADS, 0>(pts, N, npoint, start, out_idx, out_xyz, prof, FpsPairArgs<T>{});
+}
+
+// grid 2B: layer 2 (out_idx / out_xyz, start) and layer 3 (pa) of B clouds, see FpsPairArgs.
+// (Up to 128 VGPRs: at the select kernel's 96 the tie re-ranking loop spilled 72 B.)
+template <typename T, int PPT>
+__global__ __launch_bounds__(kFpsSel1024) __attribute__((amdgpu_waves_per_eu(4)))
+void fps_pair_kernel(PointsView<T> pts, int N, const int64_t* __restrict__ start, int64_t* __restrict__ out_idx,
+                     T* __restrict__ out_xyz, FpsPairArgs<T> pa) {
+  fps_select_body<T, PPT, false, kFpsSel1024, 1>(pts, N, N, start, out_idx, out_xyz, nullptr, pa);
+}
+
+// grid B: layer 3 in the reference's order for the clouds whose pair flag is set
+template <typename T, int PPT>
+__global__ __launch_bounds__(kFpsSel1024) __attribute__((amdgpu_waves_per_eu(fps_select_waves_per_eu<PPT, kFpsSel1024>())))
+void fps_select_gated_kernel(PointsView<T> pts, int N, const int64_t* __restrict__ start, int64_t* __restrict__ out_idx,
+                             T* __restrict__ out_xyz, FpsPairArgs<T> pa) {
+  fps_select_body<T, PPT, false, kFpsSel1024, 2>(pts, N, N, start, out_idx, out_xyz, nullptr, pa);
+}
+
+// grid B: layer 3's indices (into layer 2's points) -> layer 2's pick numbers (its FPS order), for
+// the clouds without a flag (layer 2 then picked every point once).  A tie group (a run of entries
+// marked by bit 62 after its first) is put in ascending pick-number order -- the reference's
+// lowest-index-first argmax among equal values -- with its centres' coordinates.
+constexpr int kFpsRemapThreads = 1024;
+__global__ __launch_bounds__(kFpsRemapThreads) void fps_pair_remap_kernel(const uint32_t* __restrict__ inv2,
+                                                                          int64_t* __restrict__ idx3,
+                                                                          float* __restrict__ xyz3,
+                                                                          const int32_t* __restrict__ flag, int N) {
+  const int b = blockIdx.x;
+  if (flag[b] != 0) return;
+  constexpr int64_t kMark = int64_t(1) << 62;
+  const uint32_t* inv = inv2 + static_cast<int64_t>(b) * N;
+  int64_t* i3 = idx3 + static_cast<int64_t>(b) * N;
+  float* x3 = xyz3 + static_cast<int64_t>(b) * 3 * N;
+  auto key_of = [&](int64_t v) -> int64_t {
+    const int64_t n = v & ~kMark;
+    return (n >= 0 && n < N) ? static_cast<int64_t>(inv[n] & 0x7FFFFFFFu) : 0;
+  };
+  __shared__ uint32_t marks[16384 / 32];  // the marks as written, before any entry is rewritten
+  for (int w = threadIdx.x; w < (N + 31) / 32; w += kFpsRemapThreads) marks[w] = 0u;
+  __syncthreads();
+  for (int j = threadIdx.x; j < N; j += kFpsRemapThreads)
+    if (i3[j] & kMark) atomicOr(&marks[j >> 5], 1u << (j & 31));
+  __syncthreads();
+  auto marked = [&](int j) { return (marks[j >> 5] >> (j & 31)) & 1u; };
+  for (int j = threadIdx.x; j < N; j += kFpsRemapThreads) {
+    if (marked(j)) continue;  // written by its group's first entry
+    const int64_t v = i3[j];
+    int e = j;
+    while (e + 1 < N && marked(e + 1)) ++e;
+    if (e == j) {
+      i3[j] = key_of(v);
+      continue;
+    }
+    // group j..e (at most kSelAccept entries): selection sort by pick number, in place
+    for (int p = j; p <= e; ++p) {
+      int best = p;
+      int64_t kb = key_of(i3[p]);
+      for (int q = p + 1; q <= e; ++q) {
+        const int64_t kq = key_of(i3[q]);
+        if (kq < kb) {
+          kb = kq;
+          best = q;
+        }
+      }
+      const int64_t vp = i3[p];
+      i3[best] = vp;  // (an unresolved member: its raw index)
+      i3[p] = kb;     // resolved
+      for (int a = 0; a < 3; ++a) {
+        const float t = x3[a * N + best];
+        x3[a * N + best] = x3[a * N + p];
+        x3[a * N + p] = t;
+      }
     }
   }
 }
@@ -1435,7 +1706,62 @@ static int launch_fps(const T* xyz, int64_t sb, int64_t sc, int64_t sn, int B, i
   return launch_status("dvcp_fps(dense)");
 }
 
+// Paired launch of two full-permutation fp32 layers (see FpsPairArgs); N in the select kernel's
+// 1024-thread range.
+static int launch_fps_pair(PointsView<float> v, int B, int N, const int64_t* start2, const int64_t* start3,
+                           int64_t* idx2, float* xyz2, int64_t* idx3, float* xyz3, uint32_t* ws, hipStream_t st) {
+  // ws: ticket | slot[B] | flag[B] | inv2[B x N], all zero before the launch
+  FpsPairArgs<float> pa{ws, ws + 1, reinterpret_cast<int32_t*>(ws + 1 + B), ws + 1 + 2 * static_cast<int64_t>(B),
+                        start3, idx3, xyz3};
+  if (hipMemsetAsync(ws, 0, sizeof(uint32_t) * (1 + 2 * static_cast<size_t>(B) + static_cast<size_t>(B) * N), st) !=
+      hipSuccess)
+    return launch_status("dvcp_fps_pair(memset)");
+  const PointsView<float> v2{xyz2, 3 * static_cast<int64_t>(N), N, 1};
+  const int p16 = ceil_div(N, kFpsSel1024);
+#define DVCP_FPS_PAIR(P)                                                                                        \
+  if (p16 <= P) {                                                                                               \
+    hipLaunchKernelGGL((fps_pair_kernel<float, P>), dim3(2 * B), dim3(kFpsSel1024), 0, st, v, N, start2, idx2,   \
+                       xyz2, pa);                                                                               \
+    if (int e = launch_status("dvcp_fps_pair")) return e;                                                       \
+    hipLaunchKernelGGL(fps_pair_remap_kernel, dim3(B), dim3(kFpsRemapThreads), 0, st, pa.inv2, idx3, xyz3, pa.flag, \
+                       N);                                                                                      \
+    if (int e = launch_status("dvcp_fps_pair(remap)")) return e;                                                \
+    hipLaunchKernelGGL((fps_select_gated_kernel<float, P>), dim3(B), dim3(kFpsSel1024), 0, st, v2, N, start3,    \
+                       idx3, xyz3, pa);                                                                         \
+    return launch_status("dvcp_fps_pair(gated)");                                                               \
+  }
+  DVCP_FPS_PAIR(2)
+  DVCP_FPS_PAIR(4)
+  DVCP_FPS_PAIR(8)
+  DVCP_FPS_PAIR(10)
+  DVCP_FPS_PAIR(16)
+#undef DVCP_FPS_PAIR
+  set_error("dvcp_fps_pair: N=%d out of range", N);
+  return DVCP_EINVAL;
+}
+
 }  // namespace dvcp
+
+// Two chained full-permutation FPS layers in one launch (FE layers 2 and 3): bit-identical to
+//   dvcp_fps(xyz, N, start2) -> (idx2, xyz2);  dvcp_fps(xyz2, N, start3) -> (idx3, xyz3).
+// fp32, 2048 <= N <= 16384; ws: dvcp_fps_pair_workspace_bytes(B, N) bytes, 4-byte aligned.
+extern "C" int64_t dvcp_fps_pair_workspace_bytes(int B, int N) {
+  return B < 0 || N < 0 ? -1 : 4 * (1 + 2 * static_cast<int64_t>(B) + static_cast<int64_t>(B) * N);
+}
+
+extern "C" int dvcp_fps_pair(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N,
+                             const int64_t* start2, const int64_t* start3, int64_t* idx2, void* xyz2, int64_t* idx3,
+                             void* xyz3, void* ws, void* stream) {
+  DVCP_REQUIRE(xyz && start2 && start3 && idx2 && xyz2 && idx3 && xyz3 && ws, "dvcp_fps_pair: null pointer");
+  DVCP_REQUIRE(dtype == DVCP_F32, "dvcp_fps_pair: fp32 only (dtype %d)", dtype);
+  DVCP_REQUIRE(B >= 0 && B <= 32767 && N >= dvcp::kFpsBatchedMinN && N <= 16 * dvcp::kFpsSel1024,
+               "dvcp_fps_pair: bad sizes B=%d N=%d", B, N);
+  DVCP_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 3) == 0, "dvcp_fps_pair: workspace not 4-byte aligned");
+  if (B == 0) return DVCP_OK;
+  return dvcp::launch_fps_pair(dvcp::PointsView<float>{static_cast<const float*>(xyz), sb, sc, sn}, B, N, start2,
+                               start3, idx2, static_cast<float*>(xyz2), idx3, static_cast<float*>(xyz3),
+                               static_cast<uint32_t*>(ws), static_cast<hipStream_t>(stream));
+}
 
 extern "C" int dvcp_fps_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N, int npoint,
                            const int64_t* start, int64_t* out_idx, void* out_xyz, float* ws, int32_t* err,

@@ -27,6 +27,7 @@ SIGNATURES = {
     "dvcp_fps": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P],
     "dvcp_fps_ws": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P, _P],
     "dvcp_fps_step_floor": [_I, _I, _P, _P],
+    "dvcp_fps_pair": [_I, _P, _L, _L, _L, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P],
     "dvcp_fps_split_probe": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P, ctypes.c_uint32, _I, _P],
     "dvcp_ball_query": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _D, _I, _P, _P, _P, _P],
     "dvcp_ball_query_ws": [_I, _P, _L, _L, _L, _I, _P, _L, _L, _L, _I, _I, _D, _I, _P, _P, _P, _P, _P],
@@ -107,6 +108,8 @@ def load():
     lib.dvcp_knn_grid_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
     lib.dvcp_knn_tiled_workspace_bytes.restype = ctypes.c_int64
     lib.dvcp_knn_tiled_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.dvcp_fps_pair_workspace_bytes.restype = ctypes.c_int64
+    lib.dvcp_fps_pair_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
     lib.dvcp_ball_query_workspace_bytes.restype = ctypes.c_int64
     lib.dvcp_ball_query_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
     lib.dvcp_sa_group_mlp_workspace_bytes.restype = ctypes.c_int64
@@ -155,7 +158,8 @@ def exported_symbols():
             "dvcp_cpg_backward_workspace_bytes", "dvcp_sa_group_mlp_backward_workspace_bytes",
             "dvcp_fe_head_backward_workspace_bytes", "dvcp_sa_bn_workspace_bytes",
             "dvcp_sa_bn_pack_floats", "dvcp_sa_bn_rows_floats", "dvcp_sa_bn_feat_workspace_bytes", "dvcp_sa_bn_zrows_floats",
-            "dvcp_cpg1d_nparams", "dvcp_sa_bnm_supported", "dvcp_sa_bnm_workspace_bytes"] + list(SIGNATURES)
+            "dvcp_cpg1d_nparams", "dvcp_sa_bnm_supported", "dvcp_sa_bnm_workspace_bytes",
+            "dvcp_fps_pair_workspace_bytes"] + list(SIGNATURES)
 
 
 # When a list, every entry-point call appends (name, start_event, end_event, work) recorded on

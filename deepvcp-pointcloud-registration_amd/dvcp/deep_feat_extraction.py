@@ -45,18 +45,37 @@ class feat_extraction_layer(nn.Module):
         chain while the first one's layers run (extract_features in training mode).  ->
         (indices, centres, events recorded on ``stream``)."""
         xyz = pts[:, :3, :] if self.use_normal else pts
-        idxs, centres, events = [], [], []
         stream.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(stream):
-            prev = xyz
-            for sa, st in zip((self.sa1, self.sa2, self.sa3), starts):
-                i, c = ops.fps(prev, sa.npoint, st.to(prev.device), pdim=2)
-                idxs.append(i)
-                centres.append(c)
+            return self._fps_chain(xyz, starts, stream)
+
+    def _fps_chain(self, xyz, starts, stream):
+        """The three FPS launches on ``stream`` (the current stream): -> (indices, centres, an
+        event per layer recorded after its centres exist).  Layers 2 and 3 pick every point of
+        their input (npoint = its point count, C3): one paired launch (ops.fps_pair) runs layer 3
+        beside layer 2, and both layers' events are the pair's."""
+        layers = (self.sa1, self.sa2, self.sa3)
+        idxs, centres, events = [], [], []
+        prev = xyz
+        li = 0
+        while li < 3:
+            sa, st = layers[li], starts[li]
+            if li == 1 and ops.fps_pair_ok(prev, sa.npoint, layers[2].npoint, pdim=2):
+                i2, c2, i3, c3 = ops.fps_pair(prev, st.to(prev.device), starts[2].to(prev.device), pdim=2)
                 ev = torch.cuda.Event()
                 ev.record(stream)
-                events.append(ev)
-                prev = c
+                idxs += [i2, i3]
+                centres += [c2, c3]
+                events += [ev, ev]
+                break
+            i, c = ops.fps(prev, sa.npoint, st.to(prev.device), pdim=2)
+            idxs.append(i)
+            centres.append(c)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            events.append(ev)
+            prev = c
+            li += 1
         return idxs, centres, events
 
     def run(self, pts, starts=None, wl=None, side_stream=None, saved=None, fps=None, layer_trace=None):
@@ -67,7 +86,8 @@ class feat_extraction_layer(nn.Module):
         fc input rows.
 
         FPS of layer l+1 depends only on layer l's sampled centres, not on its features, so the
-        three FPS launches (the serial critical path) run back to back on the current stream
+        FPS launches (the serial critical path; layers 2 and 3 as one paired launch where both
+        pick every point, see ``_fps_chain``) run back to back on the current stream
         while each layer's ball query + grouped MLP runs on ``side_stream``.  A layer whose FPS
         picks every point (npoint >= its point count, layers 2 and 3 of the reference) is
         evaluated per point before its FPS finishes and gathered by the FPS order.
@@ -98,16 +118,7 @@ class feat_extraction_layer(nn.Module):
                     t.record_stream(main)
                     t.record_stream(side)
         else:
-            idxs, centres, events = [], [], []
-            prev = xyz
-            for sa, st in zip(layers, starts):
-                i, c = ops.fps(prev, sa.npoint, st.to(prev.device), pdim=2)
-                idxs.append(i)
-                centres.append(c)
-                ev = torch.cuda.Event()
-                ev.record(main)
-                events.append(ev)
-                prev = c
+            idxs, centres, events = self._fps_chain(xyz, starts, main)
         # Inference folds the gathers of per-point layers into their consumers: the next layer's
         # MLP reads its features through the FPS indices (dvcp_sa_group_mlp_rows_ws) and the head
         # reads sa3's rows the same way (dvcp_fe_head_rows).  Training (``saved``) keeps the

@@ -4,6 +4,8 @@ Every function takes GPU tensors, allocates its outputs with torch's caching all
 launches on torch's current stream.  Point tensors are passed as strided views: ``pdim`` is
 the dimension that indexes points (1 for (B, N, 3), 2 for the reference's (B, 3, N)).
 """
+import os
+
 import torch
 
 from . import _lib
@@ -42,6 +44,44 @@ def fps(xyz, npoint, start, pdim=1):
     if split:
         _lib.defer_flag_check(f"dvcp_fps: split FPS workgroups gave up waiting for their peers (N={N})", err)
     return idx, ctr
+
+
+FPS_PAIR_RANGE = (2048, 16384)
+
+
+def fps_pair_ok(xyz, npoint2, npoint3, pdim=1):
+    """Whether the FE chain takes ``fps_pair`` (opt-in: ``DVCP_FPS_PAIR=1``): fp32, both layers
+    pick every point (npoint equal to the cloud's point count, FE layers 2 and 3) and the select
+    kernel's cloud size.  Off by default: a launch ends with its slowest cloud, and with 16 clouds
+    (C3) the largest of their random start3 draws sits near the end of layer 2's chain, where the
+    pair takes as long as the serial launches (tools/fps_bench.py, profiles/round5/r5aw_pair_ab.log)
+    while layer 3's per-point tables lose their overlap with layer 3's FPS.  It pays with one or
+    two clouds per launch."""
+    N = xyz.shape[pdim]
+    return (os.environ.get("DVCP_FPS_PAIR", "0") == "1" and xyz.dtype == torch.float32
+            and npoint2 == N and npoint3 == N and FPS_PAIR_RANGE[0] <= N <= FPS_PAIR_RANGE[1])
+
+
+def fps_pair(xyz, start2, start3, pdim=1):
+    """Two chained full-permutation FPS layers in one launch (dvcp_fps_pair): equal, bit for bit,
+    to ``i2, c2 = fps(xyz, N, start2); i3, c3 = fps(c2, N, start3, pdim=2)``.  Returns
+    (i2, c2, i3, c3)."""
+    _lib.require_gpu(xyz, start2, start3)
+    B = xyz.shape[0]
+    N, sb, sc, sn = _pts(xyz, pdim)
+    dev = xyz.device
+    s2 = start2.to(device=dev, dtype=torch.int64).contiguous()
+    s3 = start3.to(device=dev, dtype=torch.int64).contiguous()
+    i2 = torch.empty(B, N, dtype=torch.int64, device=dev)
+    i3 = torch.empty(B, N, dtype=torch.int64, device=dev)
+    c2 = torch.empty(B, 3, N, dtype=xyz.dtype, device=dev)
+    c3 = torch.empty(B, 3, N, dtype=xyz.dtype, device=dev)
+    ws = torch.empty(int(_lib.load().dvcp_fps_pair_workspace_bytes(B, N)) // 4, dtype=torch.int32, device=dev)
+    es = xyz.element_size()
+    call("dvcp_fps_pair", dtype_code(xyz), ptr(xyz), sb, sc, sn, B, N, ptr(s2), ptr(s3), ptr(i2), ptr(c2), ptr(i3),
+         ptr(c3), ptr(ws), stream(),
+         work=(2 * 9.0 * B * N * N, 2 * B * (3 * N * es + N * (8 + 3 * es)), None, 2 * B, N))
+    return i2, c2, i3, c3
 
 
 def ball_query(xyz, ctr, radius, nsample, pdim=1, cdim_pts=1, compact=True, padded=False):

@@ -59,6 +59,18 @@ int dvcp_fps_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, 
                 int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz, float* ws,
                 int32_t* err, void* stream);
 
+/* Two chained full-permutation FPS layers in one launch (the FE's layers 2 and 3 at C3:
+ * pointnet2_utils.py:63-84 called by deep_feat_extraction.py:28 and :29 with npoint equal to the
+ * layer's point count).  Bit-identical to dvcp_fps(xyz, N, start2) -> (idx2, xyz2) followed by
+ * dvcp_fps(xyz2, N, start3) -> (idx3, xyz3); the second layer runs beside the first from the
+ * point the first picks at step start3 (clouds whose second-layer argmax meets a tie are
+ * recomputed in the serial order).  fp32, 2048 <= N <= 16384; xyz2 / xyz3 B x 3 x N contiguous;
+ * ws: dvcp_fps_pair_workspace_bytes(B, N) bytes, 4-byte aligned, reserved for this call. */
+int64_t dvcp_fps_pair_workspace_bytes(int B, int N);
+int dvcp_fps_pair(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N,
+                  const int64_t* start2, const int64_t* start3, int64_t* idx2, void* xyz2,
+                  int64_t* idx3, void* xyz3, void* ws, void* stream);
+
 /* Measurement probe (no reference counterpart): `blocks` workgroups each run `steps` steps of
  * the FPS chain's per-step synchronisation with no point work (wave DPP argmax, LDS slot, one
  * barrier, slot reduction); out: blocks floats.  bench.py times it as the latency floor. */

@@ -119,6 +119,83 @@ def test_fps_full_size_property(cuda):
         assert (prev[1:] <= prev[:-1] * (1 + 1e-6) + 1e-12).all()
 
 
+def _fps_pair_vs_serial(cuda, xyz_cf, s2, s3):
+    """ops.fps_pair against the two serial launches it replaces (bit-exact indices and centres)."""
+    from dvcp import ops
+    N = xyz_cf.shape[2]
+    i2, c2, i3, c3 = ops.fps_pair(xyz_cf, s2, s3, pdim=2)
+    w2, d2 = ops.fps(xyz_cf, N, s2, pdim=2)
+    w3, d3 = ops.fps(d2, N, s3, pdim=2)
+    assert torch.equal(i2, w2) and torch.equal(c2, d2)
+    assert torch.equal(i3, w3), int((i3 != w3).nonzero()[0, 1])
+    assert torch.equal(c3, d3)
+
+
+@pytest.mark.parametrize("N", [10000, 4096, 2048, 16384])
+def test_fps_pair_matches_serial(cuda, N):
+    """The paired layer-2/3 launch (layer 3 beside layer 2, from layer 2's pick number start3) on
+    generic clouds, with start3 at both ends of the chain and in between."""
+    g = torch.Generator().manual_seed(400 + N % 97)
+    B = 6
+    xyz = (torch.rand(B, 3, N, generator=g) * 2 - 1).to(cuda)
+    s2 = torch.randint(0, N, (B,), generator=g)
+    s3 = torch.tensor([0, N - 1, 1, N // 2, 37, N - 2])
+    _fps_pair_vs_serial(cuda, xyz, s2.to(cuda), s3.to(cuda))
+
+
+@pytest.mark.parametrize("case", ["dyadic", "duplicates", "mixed", "symmetric"])
+def test_fps_pair_ties(cuda, case):
+    """Layer-3 argmax ties.  "symmetric": a point-symmetric cloud (p and -p, plus the origin) with
+    both layers started at the origin (start3 = 0 picks layer 2's start), so nearly every step
+    ties a mirrored pair: the tie groups are reordered by layer 2's pick numbers, or ranked by
+    them in the round.  Equal minima everywhere (dyadic grid) and duplicate points (minima
+    reaching 0) take the gated serial recomputation; "mixed" puts such clouds beside generic ones
+    in one launch.  Every case: the serial launches' result."""
+    g = torch.Generator().manual_seed({"dyadic": 410, "duplicates": 411, "mixed": 412, "symmetric": 413}[case])
+    B, N = 4, 4096
+    if case == "symmetric":
+        half = torch.rand(B, 3, 2048, generator=g) * 2 - 1
+        xyz = torch.cat([torch.zeros(B, 3, 1), half, -half], 2)[:, :, torch.randperm(4097, generator=g)]
+        s2 = torch.stack([int((xyz[b] == 0).all(0).nonzero()[0]) * torch.ones((), dtype=torch.long)
+                          for b in range(B)])
+        _fps_pair_vs_serial(cuda, xyz.to(cuda), s2.to(cuda), torch.zeros(B, dtype=torch.long).to(cuda))
+        return
+    if case == "dyadic":
+        xyz = torch.randint(-8, 9, (B, 3, N), generator=g).float() / 8
+    elif case == "duplicates":
+        xyz = (torch.rand(B, 3, N // 4, generator=g) * 2 - 1).repeat_interleave(4, dim=2)
+    else:
+        xyz = torch.rand(B, 3, N, generator=g) * 2 - 1
+        xyz[1] = torch.randint(-8, 9, (3, N), generator=g).float() / 8
+        xyz[3, :, N // 2:] = xyz[3, :, :N // 2]
+    s2 = torch.randint(0, N, (B,), generator=g)
+    s3 = torch.randint(0, N, (B,), generator=g)
+    _fps_pair_vs_serial(cuda, xyz.to(cuda), s2.to(cuda), s3.to(cuda))
+
+
+def test_fps_pair_many_clouds_in_flight(cuda):
+    """A C3-sized paired launch (2 x 16 clouds of 10000 points) next to independent work on other
+    streams: every layer-3 workgroup waits only for its own cloud's layer-2 workgroup."""
+    from dvcp import ops
+    g = torch.Generator().manual_seed(420)
+    B, N = 16, 10000
+    xyz = (torch.rand(B, 3, N, generator=g) * 2 - 1).to(cuda)
+    s2 = torch.randint(0, N, (B,), generator=g).to(cuda)
+    s3 = torch.randint(0, N, (B,), generator=g).to(cuda)
+    other = [torch.cuda.Stream() for _ in range(3)]
+    outs = []
+    for k, st in enumerate(other):
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            outs.append(ops.fps_pair(xyz, s2, torch.roll(s3, k), pdim=2))
+    for st in other:
+        torch.cuda.current_stream().wait_stream(st)
+    for k, (i2, c2, i3, c3) in enumerate(outs):
+        w2, d2 = ops.fps(xyz, N, s2, pdim=2)
+        w3, d3 = ops.fps(d2, N, torch.roll(s3, k), pdim=2)
+        assert torch.equal(i2, w2) and torch.equal(i3, w3) and torch.equal(c3, d3)
+
+
 # --------------------------------------------------------------------------------- ball query
 @pytest.mark.parametrize("name,radii", [("ball_f32", [(0.1, 256), (0.2, 128), (0.4, 64)]),
                                          ("ball_dyadic", [(0.25, 32), (0.25, 200)]),
@@ -848,3 +925,23 @@ def test_dfe_tgt_fp16_features(cuda, f64):
     with pytest.raises(ValueError):
         ops.dfe_tgt(ref_xyz, half, qry, dist, idx, mine.packed_params(), ref_pdim=1, literal=True)
 
+
+
+def test_fe_chain_with_fps_pair_equals_serial(cuda, monkeypatch):
+    """The feature extractor with the opt-in paired layer-2/3 FPS (DVCP_FPS_PAIR=1) against the
+    default serial chain: same centres, features and scores, bit for bit."""
+    from dvcp.deep_feat_extraction import feat_extraction_layer
+    g = torch.Generator().manual_seed(430)
+    torch.manual_seed(430)
+    fe = feat_extraction_layer(use_normal=False, npoint=4096).to(cuda).eval()
+    pts = (torch.rand(2, 3, 6000, generator=g) * 2 - 1).to(cuda)
+    starts = [torch.randint(0, n, (2,), generator=g) for n in (6000, 4096, 4096)]
+    outs = {}
+    with torch.no_grad():
+        for mode in ("0", "1"):
+            monkeypatch.setenv("DVCP_FPS_PAIR", mode)
+            xyz, feat, _ = fe.run(pts, starts)
+            torch.cuda.synchronize()
+            outs[mode] = (xyz.clone(), feat.clone())
+    assert torch.equal(outs["0"][0], outs["1"][0])
+    assert torch.equal(outs["0"][1], outs["1"][1])

@@ -26,6 +26,7 @@ import sys
 #                                  helper kernels the same call also launches)
 ENTRY = {
     "dvcp_fps_ws": (["fps_select_kernel", "fps_kernel", "fps_split_kernel", "fps_dense_kernel"], []),
+    "dvcp_fps_pair": (["fps_pair_kernel"], ["fps_pair_remap_kernel", "fps_select_gated_kernel"]),
     "dvcp_knn_tiled": (["knn_tiled_query_kernel", "knn_sel_query_kernel"],
                        ["knn_tiled_build_kernel", "knn_qbox_kernel", "knn_qhist_kernel", "knn_qscan_kernel"]),
     "dvcp_sa_group_mlp_ws": (["sa3_mfma_kernel<", "sa_mlp_mfma_kernel<float, 32,"], ["sa_pre_mfma_kernel<32,", "sa_order_kernel"]),
