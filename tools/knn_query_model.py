@@ -49,3 +49,35 @@ for bits in (4, 5, 6, 8, 10):
     order = np.argsort(code, kind='stable')  # (within-cell order: the generation order)
     print(f"morton {3*bits}-bit: mean points in expanded wave box per query {evals(order):.0f}")
 print("mean 32nd-NN distance", rk.mean(), "queries", len(Q))
+
+
+# ---- tile-level union: 64-point Morton tiles of the target points with boxes; a wave scans a tile
+# when some lane's box distance to it is within that lane's 32nd-neighbour distance
+def tile_union(order, tiles_lo, tiles_hi):
+    tot = 0
+    for w in range(0, len(order), 64):
+        idx = order[w:w + 64]
+        q = Q[idx][:, None, :]
+        gap = np.maximum(np.maximum(tiles_lo[None] - q, q - tiles_hi[None]), 0.0)
+        need = (gap * gap).sum(-1) <= (rk[idx] ** 2)[:, None]
+        tot += np.count_nonzero(need.any(0)) * 64 * len(idx)
+    return tot / len(Q)
+
+
+plo, phi = P.min(0), P.max(0)
+pc = np.clip(((P - plo) / (phi - plo) * 16).astype(np.int64), 0, 15)
+pcode = spread(pc[:, 0], 4) | (spread(pc[:, 1], 4) << 1) | (spread(pc[:, 2], 4) << 2)
+Ps = P[np.argsort(pcode, kind='stable')]
+T = (len(Ps) + 63) // 64
+Ps = np.concatenate([Ps, np.repeat(Ps[-1:], T * 64 - len(Ps), 0)])
+tl, th = Ps.reshape(T, 64, 3).min(1), Ps.reshape(T, 64, 3).max(1)
+o_q = np.argsort(morton(Q, 4), kind='stable')
+print(f"tile union, queries by own 12-bit Morton cell: {tile_union(o_q, tl, th):.0f} points per query")
+Qc = np.clip(Q, plo, phi)   # each query's nearest point of the cloud's bounding box
+lo_s, hi_s = lo, hi
+lo, hi = plo, phi
+for bits in (4, 6):
+    o_c = np.lexsort((np.linalg.norm(Q - Qc, axis=1), morton(Qc, bits)))
+    print(f"tile union, queries by the {3*bits}-bit Morton cell of their clamp to the cloud box: "
+          f"{tile_union(o_c, tl, th):.0f} points per query")
+lo, hi = lo_s, hi_s
