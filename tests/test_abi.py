@@ -100,3 +100,20 @@ def test_product_never_imports_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(dirpath, f)).read()
                 assert "import oracle" not in src and "from oracle" not in src, f
+
+
+def test_fps_pair_gating(monkeypatch):
+    """The FE chain takes the paired layer-2/3 FPS launch only when asked (DVCP_FPS_PAIR=1) and
+    only where it is defined: fp32, both layers picking every point, 2048..16384 points."""
+    from dvcp import _lib, ops
+    x = torch.zeros(2, 3, 10000)
+    monkeypatch.delenv("DVCP_FPS_PAIR", raising=False)
+    assert not ops.fps_pair_ok(x, 10000, 10000, pdim=2)
+    monkeypatch.setenv("DVCP_FPS_PAIR", "1")
+    assert ops.fps_pair_ok(x, 10000, 10000, pdim=2)
+    assert not ops.fps_pair_ok(x, 9999, 10000, pdim=2)
+    assert not ops.fps_pair_ok(x, 10000, 4096, pdim=2)
+    assert not ops.fps_pair_ok(x.double(), 10000, 10000, pdim=2)
+    assert not ops.fps_pair_ok(torch.zeros(2, 3, 1000), 1000, 1000, pdim=2)
+    assert not ops.fps_pair_ok(torch.zeros(2, 3, 20000), 20000, 20000, pdim=2)
+    assert _lib.load().dvcp_fps_pair_workspace_bytes(16, 10000) == 4 * (1 + 32 + 160000)
