@@ -1227,6 +1227,9 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
       const int ci = cq < kstar ? cq : kstar - 1;
       const T cx = acx[ci], cy = acy[ci], cz = acz[ci];
       uint64_t m = __ballot(cq < kstar && grp && !(box_lb2(cx, cy, cz, gbl) >= static_cast<T>(gub)));
+      // (Round 5, tools/fps_lab A/B, profiles/round5/r5bb_fps_updgrp.log: taking each slot's pairs of
+      // the batch together -- one indexed read and write of the slot for all its centres -- ran
+      // 5.23 -> 5.45 ms (16384 -> 10000) and 3.25 -> 3.32 ms (10000): few pairs share a slot.)
       while (m) {  // touched (centre, slot) pairs; p is wave-uniform -> indexed register access
         const int k = __ffsll(static_cast<long long>(m)) - 1;
         m &= m - 1;
