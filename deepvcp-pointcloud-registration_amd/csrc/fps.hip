@@ -509,6 +509,15 @@ __device__ __forceinline__ float fps_update(float m, T px, T py, T pz, T cx, T c
 // Ties beyond kSelMax points at one value (dyadic grids, npoint > N tails) fall back to one exact
 // block argmax per round.  On uniform C3 clouds a round accepts ~27 centres (~370 rounds for
 // 10000; tools/fps_lab), against ~9 for the batched walker.
+// DVCP_FPS_ACC4 (default): the round's accepted centres as one LDS row (x, y, z, 0) each; a touched
+// (centre, slot) pair of the update reads its centre as one broadcast LDS load instead of three
+// v_readlane from the batch's lanes, moving that work off the VALU, which the update is issue-bound
+// on (four waves per SIMD hide the load).  Round 5, tools/fps_lab A/B on one box
+// (profiles/round5/r5bc_fps_acc4.log): 16384 -> 10000 5.20 -> 4.81 ms, 10000 -> 10000 (1024 x 10)
+// 3.25 -> 3.09 ms, 16 clouds, identical indices.
+#ifndef DVCP_FPS_ACC4
+#define DVCP_FPS_ACC4 1
+#endif
 constexpr int kSelCap = 1024;    // list capacity
 constexpr int kSelBins = 256;
 constexpr int kSelTarget = 64;
@@ -607,7 +616,14 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
   // reads one word instead of W
   __shared__ uint32_t tf_max, tb_max;
   __shared__ uint32_t wpid[W];
+#if DVCP_FPS_ACC4
+  struct alignas(4 * sizeof(T)) AccC {
+    T x, y, z, w;
+  };
+  __shared__ AccC acc4[kSelAccept];  // the round's accepted centres, rank order, one row each
+#else
   __shared__ T acx[kSelAccept], acy[kSelAccept], acz[kSelAccept];  // the round's accepted centres, rank order
+#endif
   __shared__ T gbox[W][6][GP];  // group boxes, read back per round by the update (not held in VGPRs)
   __shared__ uint32_t na_cnt, cand_fill;
   __shared__ int ckey[MODE == 1 ? kSelMax : 1];  // MODE 1: candidates' point indices in a re-ranked round
@@ -968,9 +984,13 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
         for (int w = 1; w < W; ++w) gp = min(gp, wpid[w]);
         if (tid == 0) {
           const T gx = pts.at(b, 0, gp), gy = pts.at(b, 1, gp), gz = pts.at(b, 2, gp);
+#if DVCP_FPS_ACC4
+          acc4[0] = AccC{gx, gy, gz, static_cast<T>(0)};
+#else
           acx[0] = gx;
           acy[0] = gy;
           acz[0] = gz;
+#endif
           oi[step] = static_cast<int64_t>(gp);
           publish(step, static_cast<int64_t>(gp));
           if (ox) {
@@ -1178,9 +1198,13 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
       for (int hh = 0; hh < 2; ++hh) {
         const int jj = hh * 64 + lane;
         if (rk[hh] < kstar) {
+#if DVCP_FPS_ACC4
+          acc4[rk[hh]] = AccC{cxx[jj], cyy[jj], czz[jj], static_cast<T>(0)};
+#else
           acx[rk[hh]] = cxx[jj];
           acy[rk[hh]] = cyy[jj];
           acz[rk[hh]] = czz[jj];
+#endif
         }
       }
       // upper bound of every running minimum after this round: T, and the listed not accepted
@@ -1225,7 +1249,12 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
     for (int c0 = 0; c0 < kstar; c0 += QC) {
       const int cq = c0 + static_cast<int>(static_cast<unsigned>(lane) / GP);
       const int ci = cq < kstar ? cq : kstar - 1;
+#if DVCP_FPS_ACC4
+      const AccC cc = acc4[ci];
+      const T cx = cc.x, cy = cc.y, cz = cc.z;
+#else
       const T cx = acx[ci], cy = acy[ci], cz = acz[ci];
+#endif
       uint64_t m = __ballot(cq < kstar && grp && !(box_lb2(cx, cy, cz, gbl) >= static_cast<T>(gub)));
       // (Round 5, tools/fps_lab A/B, profiles/round5/r5bb_fps_updgrp.log: taking each slot's pairs of
       // the batch together -- one indexed read and write of the slot for all its centres -- ran
@@ -1235,8 +1264,13 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
         m &= m - 1;
         const int p = k & (GP - 1);
         dirty |= 1u << p;
+#if DVCP_FPS_ACC4
+        const AccC sc = acc4[c0 + k / GP];  // (a broadcast LDS read: the LDS pipe instead of three readlanes)
+        dmin[p] = fps_update<T>(dmin[p], px[p], py[p], pz[p], sc.x, sc.y, sc.z);
+#else
         const T sx = readlane_t(cx, k), sy = readlane_t(cy, k), sz = readlane_t(cz, k);
         dmin[p] = fps_update<T>(dmin[p], px[p], py[p], pz[p], sx, sy, sz);
+#endif
       }
     }
     // re-reduce the touched groups whose maximum point dropped (values only drop: a group keeps
