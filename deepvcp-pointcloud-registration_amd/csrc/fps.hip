@@ -469,13 +469,25 @@ __device__ __forceinline__ T box_ub2(T cx, T cy, T cz, const T (&bx)[6]) {
   return (ex * ex + ey * ey) + ez * ez;
 }
 
+// DVCP_FPS_IMIN: the running-minimum update as an integer min of the bit patterns (see fps_update)
+#ifndef DVCP_FPS_IMIN
+#define DVCP_FPS_IMIN 1
+#endif
+
 // The reference's running-minimum update (:80-82): d in the coordinate dtype, strict '<', stored fp32.
 template <typename T>
 __device__ __forceinline__ float fps_update(float m, T px, T py, T pz, T cx, T cy, T cz) {
   const T dx = px - cx, dy = py - cy, dz = pz - cz;
   const T d = (dx * dx + dy * dy) + dz * dz;
   if constexpr (sizeof(T) == 4) {
+#if DVCP_FPS_IMIN
+    // = (d < m ? d : m) as one signed-integer min of the bit patterns: d >= +0 (a sum of squares;
+    // a NaN d has a larger pattern than any m and keeps m) and m is 1e10, a kept d, or -1 on a
+    // padding lane -- all ordered like their patterns.  (fminf adds a canonicalizing v_max.)
+    return __int_as_float(min(__float_as_int(d), __float_as_int(m)));
+#else
     return d < m ? d : m;
+#endif
   } else {
     return d < static_cast<T>(m) ? static_cast<float>(d) : m;
   }
@@ -538,8 +550,11 @@ __device__ __forceinline__ int sel_shift(uint32_t range) {  // smallest s with (
 __device__ __forceinline__ float prev_float(float v) {  // largest float below v (v > 0)
   return __uint_as_float(__float_as_uint(v) - 1u);
 }
-// wave-wide max / min of non-negative floats (as ordered bits)
-__device__ __forceinline__ float wave_fmax_nn(float v) { return float_unorder_fps(wave_umax(float_order(v))); }
+// wave-wide max of max(v, +0) for v not NaN: the clamp and the max on the bit patterns, which order
+// non-negative floats like their values (no order transform, no canonicalizing v_max)
+__device__ __forceinline__ float wave_fmax_clamp0(float v) {
+  return __uint_as_float(wave_umax(static_cast<uint32_t>(max(__float_as_int(v), 0))));
+}
 
 // Up to 10 points per lane at 1024 threads (sa2 / sa3 of C3: 10000 points) the kernel fits in 96
 // VGPRs (5 waves per SIMD worth), so a fifth wave of up to 128 VGPRs -- a set-abstraction MFMA
@@ -768,11 +783,11 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
     gub = -1.0f;
 #pragma unroll 1
     for (int p = 0; p < PPT; ++p) {
-      const float gm = wave_fmax_nn(fmaxf(dmin[p], 0.f));
+      const float gm = wave_fmax_clamp0(dmin[p]);
       gub = gl == p ? gm : gub;
     }
     gub = grp ? gub : -1.0f;
-    m = wave_fmax_nn(fmaxf(m, 0.f));
+    m = wave_fmax_clamp0(m);
     if (lane == 0) wtf[wave] = m;
   }
   for (int i = tid; i < kSelBins; i += THREADS) hist[i] = 0u;
@@ -854,7 +869,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
           }
         }
       }
-      tf = wave_fmax_nn(tf);
+      tf = wave_fmax_clamp0(tf);
       if (lane == 0) atomicMax(&tf_max, __float_as_uint(tf));
       lds_barrier();
       tick(0);
@@ -956,7 +971,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
         asm volatile("" : "+v"(bv));
 #pragma unroll
         for (int p = 0; p < PPT; ++p) bv = fmaxf(bv, dmin[p]);
-        bv = wave_fmax_nn(fmaxf(bv, 0.f));
+        bv = wave_fmax_clamp0(bv);
         lds_barrier();  // (wtf / hist reads above are done)
         if (lane == 0) wtf[wave] = bv;
         for (int i = tid; i < kSelBins; i += THREADS) hist[i] = 0u;
@@ -1034,7 +1049,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
           }
         }
       }
-      tl = wave_fmax_nn(tl);
+      tl = wave_fmax_clamp0(tl);
       if (lane == 0) atomicMax(&tb_max, __float_as_uint(tl));
       // next round: keep a few hundred points above the floor.  The decay sets how often a round
       // lists more than kSelCap points and scans again: 0.85 rescanned in ~20 % of the C3 rounds
@@ -1232,7 +1247,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
           }
         }
       }
-      vmax = wave_fmax_nn(fmaxf(vm, 0.f));
+      vmax = wave_fmax_clamp0(vm);
       tick(3);
       break;
     }
@@ -1280,7 +1295,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
       dirty &= dirty - 1;
       const float gp = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gub), p));
       if (!__ballot(dmin[p] == gp)) {
-        const float gm = wave_fmax_nn(fmaxf(dmin[p], 0.f));
+        const float gm = wave_fmax_clamp0(dmin[p]);
         gub = (lane & (GP - 1)) == p ? gm : gub;
       }
     }
