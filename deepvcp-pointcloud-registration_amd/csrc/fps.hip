@@ -469,6 +469,9 @@ __device__ __forceinline__ T box_ub2(T cx, T cy, T cz, const T (&bx)[6]) {
   return (ex * ex + ey * ey) + ez * ez;
 }
 
+// (Round 5, measured and not kept: the update's x / y differences and squares as packed fp32 pairs,
+// v_pk_add_f32 / v_pk_mul_f32, 13 instead of 15 VALU per pair -- 2.99 -> 3.02 ms at 10000,
+// profiles/round5/r5bh_fps_pk.log.)
 // DVCP_FPS_IMIN: the running-minimum update as an integer min of the bit patterns (see fps_update)
 #ifndef DVCP_FPS_IMIN
 #define DVCP_FPS_IMIN 1
