@@ -593,6 +593,44 @@ struct FpsPairArgs {
   T* out3_xyz;            // B x 3 x npoint
 };
 constexpr uint32_t kFpsPairSpinCap = 1u << 22;
+
+// Split select (MODE 3, round 6): S workgroups per cloud run the select rounds together.  Every
+// workgroup sorts the whole cloud (the same Morton order), keeps the 64-point groups g with
+// g % S == part (then dealt round robin over its waves, as above) and, per round:
+//   1. scans, decides and lists its OWN points exactly as the one-workgroup kernel does, with a
+//      per-workgroup candidate cap of 128 / S: its candidates and T_w, the largest of its running
+//      minima it did not list;
+//   2. publishes them as 8-byte {data, round} granules (agent-scope, L2-served stores; each
+//      granule carries its own tag, so no fence or flag orders them) into its slot of the round's
+//      parity, and polls the other workgroups' granules until every one carries the round;
+//   3. every workgroup now holds the same merged list (128 slots, part q's at [q cap, (q+1) cap),
+//      unused slots v = -1) and the same T = max_w T_w, a bound on every unlisted running
+//      minimum of the cloud, and ranks and certifies the same prefix as the one-workgroup kernel
+//      would on that list: identical decisions in every workgroup, so they stay in lockstep;
+//   4. updates its own points with the accepted centres.
+// A workgroup that falls back (ties beyond its cap) or whose points are all at 0 ("empty", after
+// every one of its points was picked) publishes no candidates but its best (value, index) key;
+// such a round, or one without any candidate, accepts the single global argmax (value desc,
+// index asc) -- the reference's step.  Slots are double-buffered by round parity (a workgroup
+// can publish round r + 2 only after every peer published r + 1, i.e. finished reading r).
+// Roles: block b -> cloud (b / 8 / S) * 8 + b % 8, part (b / 8) % S, so a cloud's workgroups share
+// b % 8 -- one XCD (one L2) under the observed round-robin placement, for speed only -- and,
+// blocks being dispatched in order, a waiting workgroup waits for blocks at most 8 (S - 1)
+// behind it.  The wait is bounded (spin_cap polls) as a guard: a workgroup that gives up raises
+// err and the cloud's remaining outputs repeat the start point (in range, finite).
+struct FpsPartArgs {
+  uint64_t* slots;  // [B][2][S][kPartHdr + 5 * (128 / S)] granules, all ones before the launch
+  int32_t* err;
+  int S;            // workgroups per cloud: 2, 4 or 8
+  int B;            // clouds (the grid is ceil(B / 8) * 8 * S blocks)
+  uint32_t spin_cap;
+};
+constexpr int kPartHdr = 8;            // granules: T_w, count | flags << 16, best v, idx, x, y, z, (spare)
+constexpr int kPartMaxN = 16384;       // the whole cloud's Morton order is kept in LDS
+constexpr uint32_t kPartFlagFb = 1u, kPartFlagEmpty = 2u;
+__device__ __forceinline__ void granule_put(uint64_t* g, uint32_t data, uint32_t tag) {
+  __hip_atomic_store(g, (static_cast<uint64_t>(tag) << 32) | data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // DVCP_FPS_PAIR_DIAG (timing experiments only, wrong results for 1 and 2): 1 layer 3 stops after
 // its start; 2 no tie re-ranking; 3 layer 3 leaves its re-ranked round count in slot[b]
 #ifndef DVCP_FPS_PAIR_DIAG
@@ -600,22 +638,23 @@ constexpr uint32_t kFpsPairSpinCap = 1u << 22;
 #endif
 
 // MODE 0: one cloud per workgroup; 1: the paired launch (role from a ticket); 2: only the clouds
-// whose pair flag is set (the paired launch's fallback).
+// whose pair flag is set (the paired launch's fallback); 3: S workgroups per cloud (FpsPartArgs).
 template <typename T, int PPT, bool TIMING, int THREADS, int MODE>
 __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int npoint,
                                                 const int64_t* __restrict__ start,
                                                 int64_t* __restrict__ out_idx,
                                                 T* __restrict__ out_xyz,
                                                 unsigned long long* __restrict__ prof,
-                                                const FpsPairArgs<T>& pa) {
+                                                const FpsPairArgs<T>& pa, const FpsPartArgs& qa = FpsPartArgs{}) {
   constexpr int W = THREADS / kWave;
-  static_assert(PPT <= 32 && kSelMax == 128 && (THREADS == 512 || THREADS == 1024), "layout");
+  static_assert(PPT <= 32 && kSelMax == 128 && (THREADS == 256 || THREADS == 512 || THREADS == 1024), "layout");
+  static_assert(MODE != 3 || (sizeof(T) == 4 && DVCP_FPS_ACC4), "split select: fp32, centres as LDS rows");
   // group lanes: lane l holds the box and exact maximum of the wave's group p = l % GP, replicated
   // over the QC = 64 / GP lane blocks, so one update test covers QC (centre, group) pairs per group
   constexpr int GP = PPT <= 2 ? 2 : PPT <= 4 ? 4 : PPT <= 8 ? 8 : PPT <= 16 ? 16 : 32;
   constexpr int QC = kWave / GP;
   __shared__ uint32_t bins[kMortonBins];  // setup; then the list's values [0, kSelCap) and positions
-  __shared__ uint16_t perm[THREADS * PPT];
+  __shared__ uint16_t perm[MODE == 3 ? kPartMaxN : THREADS * PPT];
   __shared__ T red[2][3][W];
   __shared__ uint32_t wsum[W];
   __shared__ T lx[kSelCap], ly[kSelCap], lz[kSelCap];
@@ -646,12 +685,35 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
   __shared__ uint32_t na_cnt, cand_fill;
   __shared__ int ckey[MODE == 1 ? kSelMax : 1];  // MODE 1: candidates' point indices in a re-ranked round
   __shared__ int s_gaveup;
+  // MODE 3: the round's headers of every part (kPartHdr words each) and this part's empty-key
+  __shared__ uint32_t phdr[MODE == 3 ? 8 : 1][kPartHdr];
+  __shared__ uint32_t s_minidx;
   float* lv = reinterpret_cast<float*>(bins);
   uint32_t* lpos = bins + kSelCap;
 
   const int tid = threadIdx.x, lane_outer = tid & 63, lane = lane_outer;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: its LDS addresses stay in SGPRs
   int b = blockIdx.x;
+  // MODE 3: this workgroup's part of the cloud (see FpsPartArgs); S = 1, part = 0 otherwise
+  int S = 1, part = 0;
+  int capw = kSelMax;         // candidates this workgroup may list per round
+  int seltarget = kSelTarget;
+  uint64_t* qslot = nullptr;  // MODE 3: [2][S][slot] granules of this cloud
+  int slotsz = 0;
+  if constexpr (MODE == 3) {
+    S = qa.S;
+    const int x = static_cast<int>(blockIdx.x) & 7, q = static_cast<int>(blockIdx.x) >> 3;
+    b = (q / S) * 8 + x;
+    part = q % S;
+    if (b >= qa.B) return;  // grid padding: no partner waits for it (its whole cloud is padding)
+    capw = kSelMax / S;
+    seltarget = max(kSelMin, kSelTarget / S);
+    slotsz = kPartHdr + 5 * capw;
+    qslot = qa.slots + static_cast<int64_t>(b) * 2 * S * slotsz;
+    if (tid == 0) s_gaveup = 0;
+  }
+  // sorted position of point slot p of `wv`'s lane `ln` (groups dealt to the parts, then the waves)
+  auto posof = [&](int p, int wv, int ln) { return ((p * W + wv) * S + part) * kWave + ln; };
   bool consumer = false;  // MODE 1: this workgroup runs layer 3
   int s3 = -1;            // MODE 1, layer 2: the pick number whose index layer 3 waits for
   if constexpr (MODE == 1) {
@@ -698,7 +760,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
   }
 #pragma unroll 1
   for (int p = 0; p < PPT; ++p) {
-    const int pos = (p * W + wave) * kWave + lane;  // groups interleaved over the waves
+    const int pos = posof(p, wave, lane);  // groups interleaved over the (parts and) waves
     const bool real = pos < N;
     const uint32_t n = perm[real ? pos : 0];
     const T x = pts.at(b, 0, n), y = pts.at(b, 1, n), z = pts.at(b, 2, n);
@@ -720,10 +782,24 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
       gb[3 + a] = gl == p ? h[a] : gb[3 + a];
     }
   }
-  const bool grp = gl < PPT && (gl * W + wave) * kWave < N;  // lane l: a non-empty group
+  const bool grp = gl < PPT && posof(gl, wave, 0) < N;  // lane l: a non-empty group
   if (lane < GP) {
 #pragma unroll
     for (int a = 0; a < 6; ++a) gbox[wave][a][lane] = gb[a];
+  }
+  if constexpr (MODE == 3) {
+    // the key this part publishes once all its points are at 0: the lowest original index it holds
+    // (every point of an empty part has running minimum 0, the argmax's value)
+    if (tid == 0) s_minidx = 0xFFFFFFFFu;
+    lds_barrier();
+    uint32_t mi = 0xFFFFFFFFu;
+#pragma unroll 1
+    for (int p = 0; p < PPT; ++p) {
+      const int pos = posof(p, wave, lane);
+      if (pos < N) mi = min(mi, static_cast<uint32_t>(perm[pos]));
+    }
+    mi = wave_umin(mi);
+    if (lane == 0 && mi != 0xFFFFFFFFu) atomicMin(&s_minidx, mi);
   }
 
   int64_t* const oidx = MODE == 1 && consumer ? pa.out3_idx : out_idx;
@@ -767,7 +843,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
   float gub, vmax;
   {
     const T cx = pts.at(b, 0, cur), cy = pts.at(b, 1, cur), cz = pts.at(b, 2, cur);
-    if (tid == 0) {
+    if (tid == 0 && part == 0) {
       oi[0] = cur;
       publish(0, cur);
       if (ox) {
@@ -809,7 +885,8 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
   float f = 0.0f;  // floor: the first scan lists every positive value and re-derives f
   int step = 1;
   unsigned long long n_round = 0, n_scan = 0, n_fallback = 0;
-  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};  // TIMING: scan, decide+list, rank, prefix+k, update, outputs
+  [[maybe_unused]] bool part_quit = false;  // MODE 3: gave up waiting for a peer (guard)
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};  // TIMING: scan, decide+list(+exchange), rank, prefix+k, update
   unsigned long long why[4] = {0, 0, 0, 0};       // TIMING: rescans for none above f, > cap, < kSelMin, crowded bin
   uint64_t tp = 0;
   auto tick = [&](int k) {
@@ -818,6 +895,91 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
       if (k >= 0) ph[k] += t - tp;
       tp = t;
     }
+  };
+  // MODE 3, step 2 of a round: publish this part's header (and the unused candidate slots; its
+  // candidates went out from the list pass) and read every other part's granules of the round
+  // into the merged list / phdr.  Called by every thread after the barrier that completed this
+  // part's list; ends with a barrier.  best_i / best_v: this part's argmax key (flags != 0 only).
+  auto part_exchange = [&](uint32_t flags, uint32_t tw_bits, uint32_t bv_bits, uint32_t best_i, int cntw) {
+    if constexpr (MODE == 3) {
+      const uint32_t tag = static_cast<uint32_t>(n_round);
+      uint64_t* const round_slots = qslot + static_cast<int64_t>(n_round & 1) * S * slotsz;
+      uint64_t* const mine = round_slots + part * slotsz;
+      if (wave == 0) {
+        if (lane < kPartHdr) {
+          uint32_t d = lane == 0 ? tw_bits : lane == 1 ? (static_cast<uint32_t>(cntw) | (flags << 16))
+                                           : lane == 2 ? bv_bits : lane == 3 ? best_i : 0u;
+          if (lane >= 4 && lane < 7 && flags != 0u && best_i < static_cast<uint32_t>(N))
+            d = __float_as_uint(pts.at(b, lane - 4, static_cast<int>(best_i)));
+          phdr[part][lane] = d;
+          granule_put(mine + lane, d, tag);
+        }
+        for (int o = cntw + lane; o < capw; o += kWave) {  // unused slots: v = -1 never ranks or wins
+          const int j = part * capw + o;
+          cvv[j] = -1.0f;
+          cpid[j] = 0x7FFFFFFF;
+          cxx[j] = 0.0f;
+          cyy[j] = 0.0f;
+          czz[j] = 0.0f;
+          uint64_t* g = mine + kPartHdr + o;
+          granule_put(g, __float_as_uint(-1.0f), tag);
+          granule_put(g + capw, 0x7FFFFFFFu, tag);
+          granule_put(g + 2 * capw, 0u, tag);
+          granule_put(g + 3 * capw, 0u, tag);
+          granule_put(g + 4 * capw, 0u, tag);
+        }
+      }
+      const int others = (S - 1) * slotsz;
+      for (int t = tid; t < others; t += THREADS) {
+        const int qq = t / slotsz, k = t - qq * slotsz;
+        const int q = qq + (qq >= part ? 1 : 0);
+        const uint64_t* g = round_slots + q * slotsz + k;
+        uint64_t v = 0;
+        uint32_t polls = 0;
+        for (;;) {
+          v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (static_cast<uint32_t>(v >> 32) == tag) break;
+          if (++polls > qa.spin_cap) {
+            s_gaveup = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        const uint32_t d = static_cast<uint32_t>(v);
+        if (k < kPartHdr) {
+          phdr[q][k] = d;
+        } else {
+          const int c = (k - kPartHdr) / capw, o = (k - kPartHdr) - c * capw, j = q * capw + o;
+          if (c == 0) cvv[j] = __uint_as_float(d);
+          else if (c == 1) cpid[j] = static_cast<int>(d);
+          else if (c == 2) cxx[j] = __uint_as_float(d);
+          else if (c == 3) cyy[j] = __uint_as_float(d);
+          else czz[j] = __uint_as_float(d);
+        }
+      }
+      lds_barrier();
+    }
+  };
+  // MODE 3: a round without certification (some part fell back, or no part listed a candidate)
+  // accepts the single global argmax over the listed candidates and the fallen-back / empty parts'
+  // keys: value desc, original index asc (:83).  Every wave computes the same key; returns it.
+  auto part_argmax = [&]() -> uint32_t {
+    uint64_t key = 0;
+    if constexpr (MODE != 3) return 0u;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int jj = hh * kWave + lane;
+      const float v = cvv[jj];
+      if (v >= 0.0f)
+        key = max(key, (static_cast<uint64_t>(__float_as_uint(v)) << 32) | (0xFFFFFFFFu - static_cast<uint32_t>(cpid[jj])));
+    }
+    if (lane < S && (phdr[lane][1] >> 16) != 0u)
+      key = max(key, (static_cast<uint64_t>(phdr[lane][2]) << 32) | (0xFFFFFFFFu - phdr[lane][3]));
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint64_t o = __shfl_xor(key, off, kWave);
+      key = o > key ? o : key;
+    }
+    return 0xFFFFFFFFu - static_cast<uint32_t>(key);
   };
   while (step < npoint) {
     // The lane index is re-materialised (v_mbcnt in a volatile asm, fresh_lane) at the start of
@@ -863,7 +1025,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
             atomicAdd(&hist[bin], 1u);
             if (li < kSelCap) {
               lv[li] = v;
-              lpos[li] = static_cast<uint32_t>((p * W + wave) * kWave + lane);
+              lpos[li] = static_cast<uint32_t>(posof(p, wave, lane));
               lx[li] = px[p];
               ly[li] = py[p];
               lz[li] = pz[p];
@@ -904,7 +1066,9 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
         const uint32_t mine = (k == 0 ? hs[0] : k == 1 ? hs[1] : k == 2 ? hs[2] : hs[3]) + above;
         return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(mine), L));
       };
-      int mode = 0;  // 0: select, 1: rescan with the new f, 2: fallback (one exact argmax)
+      // 0: select, 1: rescan with the new f, 2: fallback (one exact argmax), 3 (MODE 3): every point
+      // of this part is at 0 (empty)
+      int mode = 0;
       int bsel = 0;
       if (scan >= kSelMaxScans) {
         mode = 2;
@@ -914,7 +1078,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
           mode = 1;
           ++why[0];
         } else {
-          mode = 2;
+          mode = MODE == 3 ? 3 : 2;
         }
       } else {
         // highest non-empty bin: values lie below its upper edge, a tighter vmax for a rescan
@@ -926,7 +1090,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
           return __uint_as_float(kf + (static_cast<uint32_t>(bin) << shift) - 1u);
         };
         if (na > static_cast<uint32_t>(kSelCap)) {
-          int bb = max(0, last_bin_at_least(4 * kSelTarget));
+          int bb = max(0, last_bin_at_least(4 * seltarget));
           while (bb + 1 < kSelBins && suf_of(bb) > static_cast<uint32_t>(kSelCap) && suf_of(bb + 1) > 0u) ++bb;
           if (shift == 0 && suf_of(bb) > static_cast<uint32_t>(kSelCap)) {
             mode = 2;  // more than kSelCap points share one value
@@ -942,9 +1106,9 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
           mode = 1;
           ++why[2];
         } else {
-          bsel = max(0, last_bin_at_least(min(static_cast<uint32_t>(kSelTarget), na)));
-          while (bsel + 1 < kSelBins && suf_of(bsel) > static_cast<uint32_t>(kSelMax) && suf_of(bsel + 1) > 0u) ++bsel;
-          if (suf_of(bsel) > static_cast<uint32_t>(kSelMax)) {  // a crowded top bin
+          bsel = max(0, last_bin_at_least(min(static_cast<uint32_t>(seltarget), na)));
+          while (bsel + 1 < kSelBins && suf_of(bsel) > static_cast<uint32_t>(capw) && suf_of(bsel + 1) > 0u) ++bsel;
+          if (suf_of(bsel) > static_cast<uint32_t>(capw)) {  // a crowded top bin
             if (shift == 0) {
               mode = 2;
             } else {
@@ -989,7 +1153,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
         uint32_t mp = 0xFFFFFFFFu;
 #pragma unroll
         for (int p = 0; p < PPT; ++p) {
-          const int pos = (p * W + wave) * kWave + lane;
+          const int pos = posof(p, wave, lane);
           if (__ballot(dmin[p] == gmax)) {
             if (dmin[p] == gmax) mp = min(mp, static_cast<uint32_t>(perm[pos]));
           }
@@ -1000,6 +1164,14 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
         uint32_t gp = wpid[0];
 #pragma unroll
         for (int w = 1; w < W; ++w) gp = min(gp, wpid[w]);
+        if constexpr (MODE == 3) {  // this part's key goes to the others; the round takes the global one
+          part_exchange(kPartFlagFb, __float_as_uint(gmax), __float_as_uint(gmax), gp, 0);
+          if (s_gaveup) {
+            part_quit = true;
+            break;
+          }
+          gp = part_argmax();
+        }
         if (tid == 0) {
           const T gx = pts.at(b, 0, gp), gy = pts.at(b, 1, gp), gz = pts.at(b, 2, gp);
 #if DVCP_FPS_ACC4
@@ -1009,12 +1181,14 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
           acy[0] = gy;
           acz[0] = gz;
 #endif
-          oi[step] = static_cast<int64_t>(gp);
-          publish(step, static_cast<int64_t>(gp));
-          if (ox) {
-            ox[step] = gx;
-            ox[npoint + step] = gy;
-            ox[2 * npoint + step] = gz;
+          if (part == 0) {
+            oi[step] = static_cast<int64_t>(gp);
+            publish(step, static_cast<int64_t>(gp));
+            if (ox) {
+              ox[step] = gx;
+              ox[npoint + step] = gy;
+              ox[2 * npoint + step] = gz;
+            }
           }
         }
         lds_barrier();
@@ -1027,7 +1201,12 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
         break;
       }
       // ---- 3. list: entries in bins >= bsel are the candidates; T over the rest ---------------
-      const int cnt = static_cast<int>(suf_of(bsel));
+      // (MODE 3: this part's candidates go to its own range of the merged list and out as
+      // granules; an empty part lists nothing: na = 0)
+      int cnt = static_cast<int>(suf_of(bsel));
+      const int cbase = part * capw;
+      uint64_t* const cgran = MODE == 3 ? qslot + (static_cast<int64_t>(n_round & 1) * S + part) * slotsz + kPartHdr
+                                        : nullptr;
       float tl = Tf;
       for (int i = wave * (kSelCap / W) + lane; i < (wave + 1) * (kSelCap / W); i += kWave) {
         const bool live = i < static_cast<int>(na);
@@ -1044,11 +1223,22 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
           const uint32_t o = base + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
                                                               __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0));
           if (in) {
-            cvv[o] = v;
-            cpid[o] = static_cast<int>(perm[lpos[i]]);
-            cxx[o] = lx[i];
-            cyy[o] = ly[i];
-            czz[o] = lz[i];
+            const int j = cbase + static_cast<int>(o);
+            const int pid = static_cast<int>(perm[lpos[i]]);
+            cvv[j] = v;
+            cpid[j] = pid;
+            cxx[j] = lx[i];
+            cyy[j] = ly[i];
+            czz[j] = lz[i];
+            if constexpr (MODE == 3) {
+              const uint32_t tag = static_cast<uint32_t>(n_round);
+              uint64_t* g = cgran + o;
+              granule_put(g, __float_as_uint(v), tag);
+              granule_put(g + capw, static_cast<uint32_t>(pid), tag);
+              granule_put(g + 2 * capw, __float_as_uint(lx[i]), tag);
+              granule_put(g + 3 * capw, __float_as_uint(ly[i]), tag);
+              granule_put(g + 4 * capw, __float_as_uint(lz[i]), tag);
+            }
           }
         }
       }
@@ -1058,16 +1248,61 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
       // lists more than kSelCap points and scans again: 0.85 rescanned in ~20 % of the C3 rounds
       // (sa1: 74 of 367), 0.9 in ~2 % (6 of 367; sa2 / sa3 37 -> 4 of 302), with the same rounds
       // (tools/fps_lab/fps_round_sim.py, a CPU model of this round logic; FPS lab: 81 of 382).
-      if (na < 4u * kSelTarget) f *= 0.9f;
+      if (na < 4u * static_cast<uint32_t>(seltarget)) f *= 0.9f;
       if (wave * kWave < kSelMax) srank[wave * kWave + lane] = 0u;  // (read last by the previous round)
       lds_barrier();
-      const float Tb = __uint_as_float(tb_max);
+      float Tb = __uint_as_float(tb_max);
       if (tid == 0) {  // (T_f was read by every wave before this barrier)
         na_cnt = 0u;
         tf_max = 0u;
       }
       if (tid == kWave) cand_fill = 0u;
       for (int i = tid; i < kSelBins; i += THREADS) hist[i] = 0u;
+      [[maybe_unused]] const float Tw = Tb;  // MODE 3: this part's own T (its next vmax bound)
+      if constexpr (MODE == 3) {
+        // ---- MODE 3, step 2: exchange; then the merged list and T = max_w T_w --------------------
+        part_exchange(mode == 3 ? kPartFlagEmpty : 0u, tb_max, 0u, mode == 3 ? s_minidx : 0u, cnt);
+        if (s_gaveup) {
+          part_quit = true;
+          break;
+        }
+        if (tid == 0) tb_max = 0u;  // (every wave read it before the exchange's barrier)
+        uint32_t tg = 0u, total = 0u, fb = 0u;
+        for (int q = 0; q < S; ++q) {
+          tg = max(tg, phdr[q][0]);
+          total += phdr[q][1] & 0xFFFFu;
+          fb |= (phdr[q][1] >> 16) & kPartFlagFb;
+        }
+        if (fb != 0u || total == 0u) {  // one exact argmax for the round
+          ++n_fallback;
+          const uint32_t gp = part_argmax();
+          if (tid == 0) {
+            const T gx = pts.at(b, 0, gp), gy = pts.at(b, 1, gp), gz = pts.at(b, 2, gp);
+            acc4[0] = AccC{gx, gy, gz, static_cast<T>(0)};
+            if (part == 0) {
+              oi[step] = static_cast<int64_t>(gp);
+              if (ox) {
+                ox[step] = gx;
+                ox[npoint + step] = gy;
+                ox[2 * npoint + step] = gz;
+              }
+            }
+          }
+          // this part's values are at most its T and its listed values
+          float vm = Tw;
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const int jj = hh * kWave + lane;
+            vm = (jj >= cbase && jj < cbase + capw) ? fmaxf(vm, cvv[jj]) : vm;
+          }
+          vmax = wave_fmax_clamp0(vm);
+          lds_barrier();
+          kstar = 1;
+          break;
+        }
+        cnt = S * capw;  // the merged list (unused slots: v = -1)
+        Tb = __uint_as_float(tg);
+      }
       tick(1);
       // ---- 4. rank and prefix test in one pass over candidate pairs ----------------------------
       // c_i precedes c_j (value desc, index asc) iff beats(i, j); rank_j = #{i : beats(i, j)}; c_j
@@ -1226,13 +1461,15 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
         }
       }
       // upper bound of every running minimum after this round: T, and the listed not accepted
-      float vm = Tb;
+      // (MODE 3: this part's own -- its T_w and its own listed values -- for a tighter histogram)
+      float vm = MODE == 3 ? Tw : Tb;
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const int jj = hh * 64 + lane;
-        vm = (jj < cnt && rk[hh] >= kstar) ? fmaxf(vm, cvv[jj]) : vm;
+        const bool mine = MODE != 3 || (jj >= cbase && jj < cbase + capw);
+        vm = (mine && jj < cnt && rk[hh] >= kstar) ? fmaxf(vm, cvv[jj]) : vm;
       }
-      if (wave == 0) {  // outputs in rank order
+      if (wave == 0 && part == 0) {  // outputs in rank order
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
           const int jj = hh * 64 + lane;
@@ -1253,6 +1490,9 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
       vmax = wave_fmax_clamp0(vm);
       tick(3);
       break;
+    }
+    if constexpr (MODE == 3) {
+      if (part_quit) break;
     }
     // ---- the update: apply the accepted centres ----------------------------------------------
     tick(-1);
@@ -1305,6 +1545,24 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
     tick(4);
     step += kstar;
   }
+  if constexpr (MODE == 3) {
+    if (part_quit) {  // gave up waiting for a peer: raise err; the remaining outputs repeat the start point
+      if (tid == 0) __hip_atomic_fetch_or(qa.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (part == 0) {
+        int64_t first = start[b];
+        if (first < 0 || first >= N) first = 0;
+        const T fx = pts.at(b, 0, first), fy = pts.at(b, 1, first), fz = pts.at(b, 2, first);
+        for (int k = step + tid; k < npoint; k += THREADS) {
+          oi[k] = first;
+          if (ox) {
+            ox[k] = fx;
+            ox[npoint + k] = fy;
+            ox[2 * npoint + k] = fz;
+          }
+        }
+      }
+    }
+  }
   if constexpr (MODE == 1) {
     if (tied && tid == 0) __hip_atomic_fetch_or(pa.flag + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #if DVCP_FPS_PAIR_DIAG == 3
@@ -1313,7 +1571,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
   }
   if constexpr (TIMING) {
     if (prof && lane == 0) {  // per wave: [rounds, scans, fallbacks, clk: scan, decide+list, rank, prefix, update]
-      unsigned long long* o = prof + (static_cast<int64_t>(b) * W + wave) * kFpsProf;
+      unsigned long long* o = prof + ((static_cast<int64_t>(b) * S + part) * W + wave) * kFpsProf;
       o[0] = n_round;
       o[1] = n_scan;
       o[2] = n_fallback;
@@ -1329,6 +1587,16 @@ void fps_select_kernel(PointsView<T> pts, int N, int npoint, const int64_t* __re
                        int64_t* __restrict__ out_idx, T* __restrict__ out_xyz,
                        unsigned long long* __restrict__ prof) {
   fps_select_body<T, PPT, TIMING, THREADS, 0>(pts, N, npoint, start, out_idx, out_xyz, prof, FpsPairArgs<T>{});
+}
+
+// Split select (FpsPartArgs): grid ceil(B / 8) * 8 * S, THREADS threads, PPT groups per lane
+// slot of a part's share of the cloud.
+template <int PPT, int THREADS>
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(THREADS / 256)))
+void fps_part_kernel(PointsView<float> pts, int N, int npoint, const int64_t* __restrict__ start,
+                     int64_t* __restrict__ out_idx, float* __restrict__ out_xyz, FpsPartArgs qa) {
+  fps_select_body<float, PPT, false, THREADS, 3>(pts, N, npoint, start, out_idx, out_xyz, nullptr, FpsPairArgs<float>{},
+                                                 qa);
 }
 
 // grid 2B: layer 2 (out_idx / out_xyz, start) and layer 3 (pa) of B clouds, see FpsPairArgs.
@@ -1703,12 +1971,67 @@ static int launch_fps_split(PointsView<T> v, int B, int N, int npoint, const int
   return launch_status("dvcp_fps(split)");
 }
 
+// Workgroups per cloud of the split select (FpsPartArgs) for an fp32 cloud of N points; 1 = the
+// one-workgroup select kernel.  DVCP_FPS_PARTS overrides (1, 2, 4 or 8; A/B runs), as does
+// DVCP_FPS_PART_THREADS the workgroup size (256, 512 or 1024).
+static int fps_env_int(const char* name, int dflt) {
+  const char* s = getenv(name);
+  return s && *s ? atoi(s) : dflt;
+}
+static int fps_parts(int N) {
+  static const int forced = fps_env_int("DVCP_FPS_PARTS", 0);
+  if (forced == 1 || forced == 2 || forced == 4 || forced == 8) return forced;
+  return N > 8192 ? 4 : N >= 4096 ? 2 : 1;
+}
+
+// Launch the split select over B fp32 clouds with S workgroups each; returns 1 (nothing launched)
+// when the workspace or the instantiated point slots do not cover this (N, S).
+static int launch_fps_part(PointsView<float> v, int B, int N, int npoint, const int64_t* start, int64_t* out_idx,
+                           float* out_xyz, float* ws, int32_t* err, int S, hipStream_t st) {
+  static const int threads = fps_env_int("DVCP_FPS_PART_THREADS", 1024);
+  const int capw = kSelMax / S, slotsz = kPartHdr + 5 * capw;
+  const int64_t slot_bytes = static_cast<int64_t>(B) * 2 * S * slotsz * 8;
+  if (slot_bytes + 8 > static_cast<int64_t>(B) * N * 4 || N > kPartMaxN) return 1;
+  uint64_t* slots = reinterpret_cast<uint64_t*>(ws);
+  if (!err) err = reinterpret_cast<int32_t*>(slots + static_cast<int64_t>(B) * 2 * S * slotsz);
+  if (hipMemsetAsync(slots, 0xFF, static_cast<size_t>(slot_bytes), st) != hipSuccess)
+    return launch_status("dvcp_fps(part memset)");
+  const FpsPartArgs qa{slots, err, S, B, kFpsSpinCap};
+  const dim3 grid(ceil_div(B, 8) * 8 * S);
+  const int groups = ceil_div(ceil_div(N, kWave), S);  // 64-point groups per part (at most)
+#define DVCP_FPS_PART(P, NT)                                                                                  \
+  if (threads == NT && groups <= P * (NT / kWave)) {                                                          \
+    hipLaunchKernelGGL((fps_part_kernel<P, NT>), grid, dim3(NT), 0, st, v, N, npoint, start, out_idx, out_xyz, qa); \
+    return launch_status("dvcp_fps(part)");                                                                   \
+  }
+  DVCP_FPS_PART(2, 1024)
+  DVCP_FPS_PART(4, 1024)
+  DVCP_FPS_PART(8, 1024)
+  DVCP_FPS_PART(4, 512)
+  DVCP_FPS_PART(8, 512)
+  DVCP_FPS_PART(8, 256)
+  DVCP_FPS_PART(16, 256)
+#undef DVCP_FPS_PART
+  return 1;
+}
+
 template <typename T>
 static int launch_fps(const T* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N, int npoint,
-                      const int64_t* start, int64_t* out_idx, T* out_xyz, float* ws, int32_t* err, hipStream_t st) {
+                      const int64_t* start, int64_t* out_idx, T* out_xyz, float* ws, int32_t* err, hipStream_t st,
+                      int parts = 0) {
   PointsView<T> v{xyz, sb, sc, sn};
   const int ppt = ceil_div(N, kFpsThreads);
   dim3 grid(B), block(kFpsThreads);
+  // fp32 clouds of 2048..16384 points with a workspace: the split select, S workgroups per cloud
+  if constexpr (sizeof(T) == 4) {
+    if (ws && N >= kFpsBatchedMinN && N <= kPartMaxN && npoint > 1) {
+      const int S = parts > 0 ? parts : fps_parts(N);
+      if (S > 1) {
+        const int e = launch_fps_part(v, B, N, npoint, start, out_idx, out_xyz, ws, err, S, st);
+        if (e != 1) return e;
+      }
+    }
+  }
   // fp32 clouds of 2048..16384 points: the select kernel with 1024 threads (16 waves, 4 per SIMD,
   // up to 16 points per lane): per-wave scan and update halve while the per-round decisions stay
   // (tools/fps_lab: 16384 -> 10000 5.52 -> 5.07 ms, 10000 -> 10000 4.13 -> 3.30 ms on 16 clouds)
@@ -1833,6 +2156,29 @@ extern "C" int dvcp_fps_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, i
     return dvcp::launch_fps<double>(static_cast<const double*>(xyz), sb, sc, sn, B, N, npoint, start, out_idx,
                                     static_cast<double*>(out_xyz), ws, err, st);
   dvcp::set_error("dvcp_fps: bad dtype %d", dtype);
+  return DVCP_EINVAL;
+}
+
+// dvcp_fps_ws with the split select's workgroups per cloud chosen by the caller (tests, A/B runs):
+// parts 1 = the one-workgroup select kernel, 2 / 4 / 8 = the split select (fp32, 2048 <= N <= 16384,
+// ws of B x N fp32 holding its exchange slots); other sizes take dvcp_fps_ws's path.
+extern "C" int dvcp_fps_parts(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N,
+                              int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz, float* ws,
+                              int32_t* err, int parts, void* stream) {
+  DVCP_REQUIRE(xyz && start && out_idx, "dvcp_fps_parts: null pointer");
+  DVCP_REQUIRE(B >= 0 && N > 0 && npoint >= 0, "dvcp_fps_parts: bad sizes B=%d N=%d npoint=%d", B, N, npoint);
+  DVCP_REQUIRE(parts == 1 || parts == 2 || parts == 4 || parts == 8, "dvcp_fps_parts: parts=%d not 1, 2, 4 or 8", parts);
+  DVCP_REQUIRE(N <= 65535 || ws, "dvcp_fps_parts: N=%d needs a workspace", N);
+  if (B == 0 || npoint == 0) return DVCP_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (dtype == DVCP_F32)
+    return dvcp::launch_fps<float>(static_cast<const float*>(xyz), sb, sc, sn, B, N, npoint, start, out_idx,
+                                   static_cast<float*>(out_xyz), parts == 1 && N <= 16384 ? nullptr : ws, err, st,
+                                   parts);
+  if (dtype == DVCP_F64)
+    return dvcp::launch_fps<double>(static_cast<const double*>(xyz), sb, sc, sn, B, N, npoint, start, out_idx,
+                                    static_cast<double*>(out_xyz), ws, err, st, parts);
+  dvcp::set_error("dvcp_fps_parts: bad dtype %d", dtype);
   return DVCP_EINVAL;
 }
 

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DVCP_LIB_PATH") or os.path.join(_HERE, "libdvcp_hip.so")
 
 F32, F64 = 0, 1
-ABI_VERSION = 3   # include/dvcp.h DVCP_ABI_VERSION
+ABI_VERSION = 4   # include/dvcp.h DVCP_ABI_VERSION
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _L = ctypes.c_int64
@@ -26,6 +26,7 @@ _D = ctypes.c_double
 SIGNATURES = {
     "dvcp_fps": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P],
     "dvcp_fps_ws": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P, _P],
+    "dvcp_fps_parts": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P],
     "dvcp_fps_step_floor": [_I, _I, _P, _P],
     "dvcp_fps_pair": [_I, _P, _L, _L, _L, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P],
     "dvcp_fps_split_probe": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P, ctypes.c_uint32, _I, _P],
@@ -143,7 +144,11 @@ def load():
     lib.dvcp_sa_bnm_workspace_bytes.restype = ctypes.c_int64
     lib.dvcp_sa_bnm_workspace_bytes.argtypes = [ctypes.c_int] * 5 + [ctypes.c_void_p, ctypes.c_int]
     for name, args in SIGNATURES.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            raise RuntimeError(f"dvcp: {LIB_PATH} does not export {name} (a stale build of ABI {ABI_VERSION}): "
+                               "rebuild it (make -j16 in deepvcp-pointcloud-registration_amd/)") from None
         fn.restype = ctypes.c_int
         fn.argtypes = args
     _lib = lib

@@ -184,15 +184,20 @@ class DeepVCP(nn.Module):
             keypts, src_cat, moved = ops.src_keypoints(src_xyz, src_feat, top, starts[3], R_init, radius=1.0,
                                                        nsample=32)
         if train_head:
-            src_dfe, side = autograd.dfe_rows(src_cat, self.DFE), None
+            src_dfe, side, dfe_pack = autograd.dfe_rows(src_cat, self.DFE), None, None
         else:
             # the source rows' DFE (a small launch) runs on the side stream beside the candidate
-            # grid, kNN and target DFE, which do not read it; the CPG waits for it
+            # grid, kNN and target DFE, which do not read it; the CPG waits for it.  The packed
+            # DFE parameters are formed (or fetched from the cache) on the current stream BEFORE
+            # the side stream forks, so both DFE launches read one buffer that the current
+            # stream owns and whose (re)build both streams are ordered after.
             cur, side = torch.cuda.current_stream(dev), self._side_stream(dev)
+            dfe_pack = self.DFE.packed_params()
             side.wait_stream(cur)
             with torch.cuda.stream(side):
-                src_dfe = ops.dfe(src_cat, self.DFE.packed_params())
+                src_dfe = ops.dfe(src_cat, dfe_pack)
             src_cat.record_stream(side)
+            dfe_pack.record_stream(side)
             src_dfe.record_stream(cur)
 
         G = int((2 * r) / s + 1)                    # cpg.py:29
@@ -212,7 +217,7 @@ class DeepVCP(nn.Module):
             vcp = autograd.cpg(src_dfe, tgt_dfe.permute(0, 1, 3, 2), cand, G, self.cpg)
         else:
             feat_t = tgt_feat if self.feat_dtype == torch.float32 else tgt_feat.to(self.feat_dtype)
-            tgt_dfe = ops.dfe_tgt(tgt_xyz, feat_t, qry, dist, idx, self.DFE.packed_params(), ref_pdim=2)
+            tgt_dfe = ops.dfe_tgt(tgt_xyz, feat_t, qry, dist, idx, dfe_pack, ref_pdim=2)
             tgt_dfe = tgt_dfe.view(B, K, C, 32)
             torch.cuda.current_stream(dev).wait_stream(side)
             vcp = ops.cpg(src_dfe, tgt_dfe.permute(0, 1, 3, 2), cand, G, self.cpg.packed_params())

@@ -24,8 +24,26 @@ def _pts(t, pdim):
 FPS_REG_LIMIT = {torch.float32: 16384, torch.float64: 8192}
 
 
-def fps(xyz, npoint, start, pdim=1):
-    """pointnet2_utils.py:63-84.  Returns (idx (B, npoint) int64, centres (B, 3, npoint))."""
+# fp32 clouds the split select takes (several workgroups per cloud, one exchange per round;
+# csrc/fps.hip FpsPartArgs), given a workspace
+FPS_PART_RANGE = (2048, 16384)
+
+
+def fps_parts(N, dtype=torch.float32):
+    """Workgroups per cloud of the select kernel for an N-point cloud (csrc/fps.hip fps_parts;
+    DVCP_FPS_PARTS overrides both): 4 above 8192 points, 2 from 4096, else 1."""
+    if dtype != torch.float32 or not FPS_PART_RANGE[0] <= N <= FPS_PART_RANGE[1]:
+        return 1
+    forced = int(os.environ.get("DVCP_FPS_PARTS", "0") or 0)
+    if forced in (1, 2, 4, 8):
+        return forced
+    return 4 if N > 8192 else 2 if N >= 4096 else 1
+
+
+def fps(xyz, npoint, start, pdim=1, parts=None):
+    """pointnet2_utils.py:63-84.  Returns (idx (B, npoint) int64, centres (B, 3, npoint)).
+    ``parts`` (tests, A/B): workgroups per cloud of the select kernel (1, 2, 4 or 8; fp32 clouds of
+    2048..16384 points), else ``fps_parts``; the indices are the same for every choice."""
     _lib.require_gpu(xyz, start)
     B = xyz.shape[0]
     N, sb, sc, sn = _pts(xyz, pdim)
@@ -35,14 +53,21 @@ def fps(xyz, npoint, start, pdim=1):
     limit = FPS_REG_LIMIT[xyz.dtype]
     _lib.check_device_flags()   # earlier launches' guards (non-blocking)
     split = N > limit
-    ws = torch.empty(B, N, dtype=torch.float32, device=xyz.device) if split else None
-    err = torch.zeros(1, dtype=torch.int32, device=xyz.device) if split else None
+    S = parts if parts is not None else fps_parts(N, xyz.dtype)
+    multi = split or (S > 1 and xyz.dtype == torch.float32 and FPS_PART_RANGE[0] <= N <= FPS_PART_RANGE[1])
+    ws = torch.empty(B, N, dtype=torch.float32, device=xyz.device) if multi else None
+    err = torch.zeros(1, dtype=torch.int32, device=xyz.device) if multi else None
     es = xyz.element_size()
-    call("dvcp_fps_ws", dtype_code(xyz), ptr(xyz), sb, sc, sn, B, N, npoint, ptr(start), ptr(idx), ptr(ctr), ptr(ws),
-         ptr(err), stream(), work=(9.0 * B * npoint * N, B * (3 * N * es + npoint * (8 + 3 * es)), None,
-                                   B * (-(-N // 16384) if split else 1), npoint))
-    if split:
-        _lib.defer_flag_check(f"dvcp_fps: split FPS workgroups gave up waiting for their peers (N={N})", err)
+    wgs = B * (-(-N // 16384) if split else S if multi else 1)
+    work = (9.0 * B * npoint * N, B * (3 * N * es + npoint * (8 + 3 * es)), None, wgs, npoint)
+    if parts is None:
+        call("dvcp_fps_ws", dtype_code(xyz), ptr(xyz), sb, sc, sn, B, N, npoint, ptr(start), ptr(idx), ptr(ctr),
+             ptr(ws), ptr(err), stream(), work=work)
+    else:
+        call("dvcp_fps_parts", dtype_code(xyz), ptr(xyz), sb, sc, sn, B, N, npoint, ptr(start), ptr(idx), ptr(ctr),
+             ptr(ws), ptr(err), int(parts), stream(), work=work)
+    if multi:
+        _lib.defer_flag_check(f"dvcp_fps: FPS workgroups gave up waiting for their peers (N={N})", err)
     return idx, ctr
 
 

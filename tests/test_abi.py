@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared() if n not in exported]
     assert not missing, missing
     assert sorted(_lib.exported_symbols()) == declared()
-    assert lib.dvcp_abi_version() == 3
+    assert lib.dvcp_abi_version() == 4
 
 
 def test_ctypes_prototypes_match_header_arity():

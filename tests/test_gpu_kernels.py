@@ -97,6 +97,93 @@ def test_fps_select_vs_oracle(cuda, case):
     assert torch.equal(got, want), (case, int((got != want).nonzero()[0, 1]) if (got != want).any() else -1)
 
 
+def _split_cloud(case, g, B=2):
+    N, npoint = 4096, 1500
+    if case == "dyadic":
+        xyz = torch.randint(-8, 9, (B, N, 3), generator=g).float() / 8
+    elif case == "duplicates":
+        xyz = (torch.rand(B, N // 4, 3, generator=g) * 2 - 1).repeat_interleave(4, dim=1)
+    elif case == "surface":
+        v = torch.randn(B, N, 3, generator=g)
+        xyz = v / v.norm(dim=2, keepdim=True)
+    elif case == "npoint_gt_n":
+        N, npoint = 3000, 3600
+        xyz = torch.rand(B, N, 3, generator=g) * 2 - 1
+    elif case == "full_perm":  # sa2 / sa3 of C3: every point picked, parts run empty near the end
+        N, npoint = 10000, 10000
+        xyz = torch.rand(B, N, 3, generator=g) * 2 - 1
+    elif case == "clustered":  # one dense blob and a sparse halo: the parts' maxima differ widely
+        xyz = torch.cat([torch.randn(B, N // 2, 3, generator=g) * 0.02,
+                         torch.rand(B, N - N // 2, 3, generator=g) * 2 - 1], 1)
+        xyz = xyz[:, torch.randperm(N, generator=g)]
+    else:
+        xyz = torch.rand(B, N, 3, generator=g) * 2 - 1
+    return xyz, npoint
+
+
+@pytest.mark.parametrize("parts", [2, 4, 8])
+@pytest.mark.parametrize("case", ["generic", "dyadic", "duplicates", "surface", "npoint_gt_n", "full_perm",
+                                  "clustered"])
+def test_fps_split_select_vs_oracle(cuda, parts, case):
+    """The split select (round 6: S workgroups per cloud, one candidate-list exchange per round)
+    against the oracle, bit for bit, on the inputs that stress the select kernel's exactness
+    argument -- equal minima everywhere (the per-part fallback and the global argmax round),
+    duplicates (minima reaching 0), npoint > N and a full permutation (parts whose points are all
+    at 0: "empty"), a surface, and a clustered cloud whose parts' values differ widely."""
+    import oracle as O
+    from dvcp import ops
+    g = torch.Generator().manual_seed(500 + 7 * parts + ["generic", "dyadic", "duplicates", "surface", "npoint_gt_n",
+                                                         "full_perm", "clustered"].index(case))
+    xyz, npoint = _split_cloud(case, g)
+    N = xyz.shape[1]
+    start = torch.randint(0, N, (xyz.shape[0],), generator=g)
+    want = O.farthest_point_sample(xyz, npoint, start)
+    got, ctr = ops.fps(xyz.to(cuda), npoint, start.to(cuda), pdim=1, parts=parts)
+    got = got.cpu()
+    assert torch.equal(got, want), (case, parts, int((got != want).nonzero()[0, 1]) if (got != want).any() else -1)
+    gathered = torch.stack([xyz[b, want[b]] for b in range(xyz.shape[0])]).transpose(1, 2)
+    assert torch.equal(ctr.cpu(), gathered)
+
+
+@pytest.mark.parametrize("N", [16384, 10000])
+def test_fps_split_select_c3_equals_one_workgroup(cuda, N):
+    """C3's FE chain sizes, 16 clouds as one launch (the bench's batch): the split select at 2, 4
+    and 8 workgroups per cloud returns the one-workgroup kernel's indices (itself bit-exact
+    against the oracle: test_fps_live_vs_oracle, test_e2e_c3_pair_vs_oracle)."""
+    from dvcp import ops
+    g = torch.Generator().manual_seed(520 + N % 13)
+    xyz = (torch.rand(16, 3, N, generator=g) * 2 - 1).to(cuda)
+    start = torch.randint(0, N, (16,), generator=g).to(cuda)
+    want, cw = ops.fps(xyz, 10000, start, pdim=2, parts=1)
+    for parts in (2, 4, 8):
+        got, cg = ops.fps(xyz, 10000, start, pdim=2, parts=parts)
+        assert torch.equal(got, want), (parts, int((got != want).nonzero()[0, 1]))
+        assert torch.equal(cg, cw)
+
+
+def test_fps_split_select_many_launches_in_flight(cuda):
+    """Ten split-select launches of 16 clouds on ten streams at once (more workgroups than the
+    chip holds beside each other): every cloud's workgroups find their peers, the guard word stays
+    clear, and each launch equals the one-workgroup kernel."""
+    from dvcp import _lib, ops
+    g = torch.Generator().manual_seed(530)
+    xyz = (torch.rand(16, 3, 16384, generator=g) * 2 - 1).to(cuda)
+    starts = [torch.randint(0, 16384, (16,), generator=g).to(cuda) for _ in range(10)]
+    streams = [torch.cuda.Stream() for _ in starts]
+    outs = []
+    for st, s in zip(streams, starts):
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            outs.append(ops.fps(xyz, 4000, s, pdim=2, parts=4)[0])
+    for st in streams:
+        torch.cuda.current_stream().wait_stream(st)
+    torch.cuda.synchronize()
+    _lib.check_device_flags(block=True)
+    for s, got in zip(starts, outs):
+        want, _ = ops.fps(xyz, 4000, s, pdim=2, parts=1)
+        assert torch.equal(got, want)
+
+
 def test_fps_full_size_property(cuda):
     """C3 scale: 16384 -> 10000; the min-distance of each newly picked point to the already
     picked set never increases (the defining FPS invariant), and no index repeats."""
