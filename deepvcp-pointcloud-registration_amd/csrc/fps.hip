@@ -618,11 +618,18 @@ constexpr uint32_t kFpsPairSpinCap = 1u << 22;
 // blocks being dispatched in order, a waiting workgroup waits for blocks at most 8 (S - 1)
 // behind it.  The wait is bounded (spin_cap polls) as a guard: a workgroup that gives up raises
 // err and the cloud's remaining outputs repeat the start point (in range, finite).
+// The Morton order is computed once per cloud, by part 0: its within-cell order comes from LDS
+// atomics and differs between workgroups, so independent sorts would deal some points to two parts
+// and others to none.  Part 0 hands its permutation to the other parts through `perm` (write-through
+// stores, then the cloud's flag), once per launch.
 struct FpsPartArgs {
-  uint64_t* slots;  // [B][2][S][kPartHdr + 5 * (128 / S)] granules, all ones before the launch
+  uint64_t* slots;   // [B][2][S][kPartHdr + 5 * (128 / S)] granules, all ones before the launch
+  uint32_t* flag;    // [B], all ones before the launch; 1 once part 0 has published the permutation
+  uint32_t* perm;    // [B][perm_words]: the cloud's Morton permutation, two u16 per word
   int32_t* err;
-  int S;            // workgroups per cloud: 2, 4 or 8
-  int B;            // clouds (the grid is ceil(B / 8) * 8 * S blocks)
+  int S;             // workgroups per cloud: 2, 4 or 8
+  int B;             // clouds (the grid is ceil(B / 8) * 8 * S blocks)
+  int perm_words;    // ceil(N / 2)
   uint32_t spin_cap;
 };
 constexpr int kPartHdr = 8;            // granules: T_w, count | flags << 16, best v, idx, x, y, z, (spare)
@@ -747,7 +754,39 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
   bool tied = false;  // MODE 1: this cloud needs the gated recomputation (see the fallback below)
   [[maybe_unused]] int n_repair = 0;
   [[maybe_unused]] uint64_t rep_clk = 0;
-  fps_morton_sort<T, THREADS>(pts, b, N, bins, perm, red, wsum);
+  if constexpr (MODE == 3) {
+    uint32_t* const gperm = qa.perm + static_cast<int64_t>(b) * qa.perm_words;
+    uint32_t* const lperm = reinterpret_cast<uint32_t*>(perm);
+    if (part == 0) {  // sort, publish: write-through stores, drained, then the flag (one lane)
+      fps_morton_sort<T, THREADS>(pts, b, N, bins, perm, red, wsum);
+      for (int w = tid; w < qa.perm_words; w += THREADS)
+        __hip_atomic_store(gperm + w, lperm[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(qa.flag + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {          // wait for part 0's flag (one lane), then read the permutation write-through
+      if (tid == 0) {
+        uint32_t polls = 0;
+        while (__hip_atomic_load(qa.flag + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1u) {
+          if (++polls > qa.spin_cap) {
+            s_gaveup = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      __syncthreads();
+      if (s_gaveup) {  // guard: raise err; part 0 (which never waits here) fills the outputs
+        if (tid == 0) __hip_atomic_fetch_or(qa.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+      for (int w = tid; w < qa.perm_words; w += THREADS)
+        lperm[w] = __hip_atomic_load(gperm + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+    }
+  } else {
+    fps_morton_sort<T, THREADS>(pts, b, N, bins, perm, red, wsum);
+  }
 
   T px[PPT], py[PPT], pz[PPT];
   float dmin[PPT];
@@ -1986,17 +2025,41 @@ static int fps_parts(int N) {
 
 // Launch the split select over B fp32 clouds with S workgroups each; returns 1 (nothing launched)
 // when the workspace or the instantiated point slots do not cover this (N, S).
+// Workspace of the split select, carved from the caller's buffer: slots [B][2][S][slot] u64 |
+// flags [B] u32 (padded to 8 bytes) | perm [B][ceil(N / 2)] u32 | err i32.  The slots and flags are
+// set to all ones per launch.
+struct FpsPartWs {
+  int64_t slot_bytes, flag_bytes, total;
+};
+static FpsPartWs fps_part_ws(int B, int N, int S) {
+  const int64_t slotsz = kPartHdr + 5 * (kSelMax / S);
+  FpsPartWs w;
+  w.slot_bytes = static_cast<int64_t>(B) * 2 * S * slotsz * 8;
+  w.flag_bytes = (static_cast<int64_t>(B) * 4 + 7) / 8 * 8;
+  w.total = w.slot_bytes + w.flag_bytes + static_cast<int64_t>(B) * ((N + 1) / 2) * 4 + 8;
+  return w;
+}
+static int64_t fps_workspace_bytes(int B, int N) {  // the split path's B x N fp32, or the split select's
+  int64_t need = static_cast<int64_t>(B) * N * 4;
+  for (int S = 2; S <= 8; S *= 2) {
+    const int64_t t = fps_part_ws(B, N, S).total;
+    need = t > need ? t : need;
+  }
+  return need;
+}
+
 static int launch_fps_part(PointsView<float> v, int B, int N, int npoint, const int64_t* start, int64_t* out_idx,
-                           float* out_xyz, float* ws, int32_t* err, int S, hipStream_t st) {
+                           float* out_xyz, float* ws, int64_t ws_bytes, int32_t* err, int S, hipStream_t st) {
   static const int threads = fps_env_int("DVCP_FPS_PART_THREADS", 1024);
-  const int capw = kSelMax / S, slotsz = kPartHdr + 5 * capw;
-  const int64_t slot_bytes = static_cast<int64_t>(B) * 2 * S * slotsz * 8;
-  if (slot_bytes + 8 > static_cast<int64_t>(B) * N * 4 || N > kPartMaxN) return 1;
+  const FpsPartWs w = fps_part_ws(B, N, S);
+  if (w.total > ws_bytes || N > kPartMaxN) return 1;
   uint64_t* slots = reinterpret_cast<uint64_t*>(ws);
-  if (!err) err = reinterpret_cast<int32_t*>(slots + static_cast<int64_t>(B) * 2 * S * slotsz);
-  if (hipMemsetAsync(slots, 0xFF, static_cast<size_t>(slot_bytes), st) != hipSuccess)
+  uint32_t* flags = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + w.slot_bytes);
+  uint32_t* permw = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + w.slot_bytes + w.flag_bytes);
+  if (!err) err = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(ws) + w.total - 8);
+  if (hipMemsetAsync(slots, 0xFF, static_cast<size_t>(w.slot_bytes + w.flag_bytes), st) != hipSuccess)
     return launch_status("dvcp_fps(part memset)");
-  const FpsPartArgs qa{slots, err, S, B, kFpsSpinCap};
+  const FpsPartArgs qa{slots, flags, permw, err, S, B, (N + 1) / 2, kFpsSpinCap};
   const dim3 grid(ceil_div(B, 8) * 8 * S);
   const int groups = ceil_div(ceil_div(N, kWave), S);  // 64-point groups per part (at most)
 #define DVCP_FPS_PART(P, NT)                                                                                  \
@@ -2018,16 +2081,17 @@ static int launch_fps_part(PointsView<float> v, int B, int N, int npoint, const 
 template <typename T>
 static int launch_fps(const T* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N, int npoint,
                       const int64_t* start, int64_t* out_idx, T* out_xyz, float* ws, int32_t* err, hipStream_t st,
-                      int parts = 0) {
+                      int parts = 0, int64_t ws_bytes = -1) {
+  if (ws_bytes < 0) ws_bytes = ws ? static_cast<int64_t>(B) * N * 4 : 0;  // dvcp_fps_ws's B x N fp32
   PointsView<T> v{xyz, sb, sc, sn};
   const int ppt = ceil_div(N, kFpsThreads);
   dim3 grid(B), block(kFpsThreads);
   // fp32 clouds of 2048..16384 points with a workspace: the split select, S workgroups per cloud
   if constexpr (sizeof(T) == 4) {
     if (ws && N >= kFpsBatchedMinN && N <= kPartMaxN && npoint > 1) {
-      const int S = parts > 0 ? parts : fps_parts(N);
+      const int S = parts > 0 ? parts : fps_parts(N);  // (parts 1: the one-workgroup kernel below)
       if (S > 1) {
-        const int e = launch_fps_part(v, B, N, npoint, start, out_idx, out_xyz, ws, err, S, st);
+        const int e = launch_fps_part(v, B, N, npoint, start, out_idx, out_xyz, ws, ws_bytes, err, S, st);
         if (e != 1) return e;
       }
     }
@@ -2159,25 +2223,33 @@ extern "C" int dvcp_fps_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, i
   return DVCP_EINVAL;
 }
 
-// dvcp_fps_ws with the split select's workgroups per cloud chosen by the caller (tests, A/B runs):
-// parts 1 = the one-workgroup select kernel, 2 / 4 / 8 = the split select (fp32, 2048 <= N <= 16384,
-// ws of B x N fp32 holding its exchange slots); other sizes take dvcp_fps_ws's path.
+// Workspace bytes dvcp_fps_parts needs for B clouds of N points (any parts).
+extern "C" int64_t dvcp_fps_workspace_bytes(int B, int N) {
+  return B < 0 || N < 0 ? -1 : dvcp::fps_workspace_bytes(B, N);
+}
+
+// dvcp_fps_ws with a sized workspace and the split select's workgroups per cloud: parts 0 = the
+// library's choice (dvcp_fps_ws's), 1 = the one-workgroup select kernel, 2 / 4 / 8 = the split select
+// (fp32, 2048 <= N <= 16384).  ws: ws_bytes >= dvcp_fps_workspace_bytes(B, N) bytes (8-aligned).
 extern "C" int dvcp_fps_parts(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N,
-                              int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz, float* ws,
-                              int32_t* err, int parts, void* stream) {
-  DVCP_REQUIRE(xyz && start && out_idx, "dvcp_fps_parts: null pointer");
+                              int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz, void* ws,
+                              int64_t ws_bytes, int32_t* err, int parts, void* stream) {
+  DVCP_REQUIRE(xyz && start && out_idx && ws, "dvcp_fps_parts: null pointer");
   DVCP_REQUIRE(B >= 0 && N > 0 && npoint >= 0, "dvcp_fps_parts: bad sizes B=%d N=%d npoint=%d", B, N, npoint);
-  DVCP_REQUIRE(parts == 1 || parts == 2 || parts == 4 || parts == 8, "dvcp_fps_parts: parts=%d not 1, 2, 4 or 8", parts);
-  DVCP_REQUIRE(N <= 65535 || ws, "dvcp_fps_parts: N=%d needs a workspace", N);
+  DVCP_REQUIRE(parts == 0 || parts == 1 || parts == 2 || parts == 4 || parts == 8,
+               "dvcp_fps_parts: parts=%d not 0, 1, 2, 4 or 8", parts);
+  DVCP_REQUIRE(ws_bytes >= dvcp::fps_workspace_bytes(B, N) && (reinterpret_cast<uintptr_t>(ws) & 7) == 0,
+               "dvcp_fps_parts: workspace of %lld bytes (need %lld, 8-aligned)", static_cast<long long>(ws_bytes),
+               static_cast<long long>(dvcp::fps_workspace_bytes(B, N)));
   if (B == 0 || npoint == 0) return DVCP_OK;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  float* w = static_cast<float*>(ws);
   if (dtype == DVCP_F32)
     return dvcp::launch_fps<float>(static_cast<const float*>(xyz), sb, sc, sn, B, N, npoint, start, out_idx,
-                                   static_cast<float*>(out_xyz), parts == 1 && N <= 16384 ? nullptr : ws, err, st,
-                                   parts);
+                                   static_cast<float*>(out_xyz), w, err, st, parts, ws_bytes);
   if (dtype == DVCP_F64)
     return dvcp::launch_fps<double>(static_cast<const double*>(xyz), sb, sc, sn, B, N, npoint, start, out_idx,
-                                    static_cast<double*>(out_xyz), ws, err, st, parts);
+                                    static_cast<double*>(out_xyz), w, err, st, parts, ws_bytes);
   dvcp::set_error("dvcp_fps_parts: bad dtype %d", dtype);
   return DVCP_EINVAL;
 }

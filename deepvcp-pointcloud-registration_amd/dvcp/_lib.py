@@ -26,7 +26,7 @@ _D = ctypes.c_double
 SIGNATURES = {
     "dvcp_fps": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P],
     "dvcp_fps_ws": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P, _P],
-    "dvcp_fps_parts": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P],
+    "dvcp_fps_parts": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _L, _P, _I, _P],
     "dvcp_fps_step_floor": [_I, _I, _P, _P],
     "dvcp_fps_pair": [_I, _P, _L, _L, _L, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P],
     "dvcp_fps_split_probe": [_I, _P, _L, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P, ctypes.c_uint32, _I, _P],
@@ -109,6 +109,8 @@ def load():
     lib.dvcp_knn_grid_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
     lib.dvcp_knn_tiled_workspace_bytes.restype = ctypes.c_int64
     lib.dvcp_knn_tiled_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.dvcp_fps_workspace_bytes.restype = ctypes.c_int64
+    lib.dvcp_fps_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
     lib.dvcp_fps_pair_workspace_bytes.restype = ctypes.c_int64
     lib.dvcp_fps_pair_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
     lib.dvcp_ball_query_workspace_bytes.restype = ctypes.c_int64
@@ -164,7 +166,7 @@ def exported_symbols():
             "dvcp_fe_head_backward_workspace_bytes", "dvcp_sa_bn_workspace_bytes",
             "dvcp_sa_bn_pack_floats", "dvcp_sa_bn_rows_floats", "dvcp_sa_bn_feat_workspace_bytes", "dvcp_sa_bn_zrows_floats",
             "dvcp_cpg1d_nparams", "dvcp_sa_bnm_supported", "dvcp_sa_bnm_workspace_bytes",
-            "dvcp_fps_pair_workspace_bytes"] + list(SIGNATURES)
+            "dvcp_fps_pair_workspace_bytes", "dvcp_fps_workspace_bytes"] + list(SIGNATURES)
 
 
 # When a list, every entry-point call appends (name, start_event, end_event, work) recorded on

@@ -55,17 +55,14 @@ def fps(xyz, npoint, start, pdim=1, parts=None):
     split = N > limit
     S = parts if parts is not None else fps_parts(N, xyz.dtype)
     multi = split or (S > 1 and xyz.dtype == torch.float32 and FPS_PART_RANGE[0] <= N <= FPS_PART_RANGE[1])
-    ws = torch.empty(B, N, dtype=torch.float32, device=xyz.device) if multi else None
+    nbytes = int(_lib.load().dvcp_fps_workspace_bytes(B, N))
+    ws = torch.empty((nbytes + 7) // 8, dtype=torch.int64, device=xyz.device)
     err = torch.zeros(1, dtype=torch.int32, device=xyz.device) if multi else None
     es = xyz.element_size()
     wgs = B * (-(-N // 16384) if split else S if multi else 1)
     work = (9.0 * B * npoint * N, B * (3 * N * es + npoint * (8 + 3 * es)), None, wgs, npoint)
-    if parts is None:
-        call("dvcp_fps_ws", dtype_code(xyz), ptr(xyz), sb, sc, sn, B, N, npoint, ptr(start), ptr(idx), ptr(ctr),
-             ptr(ws), ptr(err), stream(), work=work)
-    else:
-        call("dvcp_fps_parts", dtype_code(xyz), ptr(xyz), sb, sc, sn, B, N, npoint, ptr(start), ptr(idx), ptr(ctr),
-             ptr(ws), ptr(err), int(parts), stream(), work=work)
+    call("dvcp_fps_parts", dtype_code(xyz), ptr(xyz), sb, sc, sn, B, N, npoint, ptr(start), ptr(idx), ptr(ctr),
+         ptr(ws), ws.numel() * 8, ptr(err), int(parts or 0), stream(), work=work)
     if multi:
         _lib.defer_flag_check(f"dvcp_fps: FPS workgroups gave up waiting for their peers (N={N})", err)
     return idx, ctr

@@ -53,21 +53,25 @@ int dvcp_fps(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int
 /* dvcp_fps with a B x N fp32 workspace, required when N exceeds the register-resident limit
  * (16384 fp32 / 8192 fp64 points per cloud).  Such clouds are split over ceil(N / 16384)
  * workgroups (8192 fp64) that exchange one argmax key per step through device-scope atomics.
- * fp32 clouds of 4096..16384 points use it too (ABI 4): their select rounds run on 2 or 4
- * workgroups per cloud that exchange one candidate list per round (the split select,
- * csrc/fps.hip FpsPartArgs); without a workspace they take the one-workgroup kernel.  Same
- * indices either way.  err (optional int32, zeroed by the caller): set to 1 if a workgroup
+ * fp32 clouds of 4096..16384 points use it too (ABI 4) where B x N x 4 bytes hold the exchange
+ * slots: their select rounds run on 2 or 4 workgroups per cloud that exchange one candidate
+ * list per round (the split select, csrc/fps.hip FpsPartArgs); without a workspace they take
+ * the one-workgroup kernel.  Same indices either way.  err (optional int32, zeroed by the caller): set to 1 if a workgroup
  * gave up waiting for its peers (a guard; the indices then stay in range but are not FPS). */
 int dvcp_fps_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N,
                 int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz, float* ws,
                 int32_t* err, void* stream);
 
-/* dvcp_fps_ws with the split select's workgroups per cloud chosen by the caller (tests, A/B):
- * parts = 1 (the one-workgroup select kernel), 2, 4 or 8 (fp32, 2048 <= N <= 16384; ws as for
- * dvcp_fps_ws).  Same contract and results as dvcp_fps. */
+/* Bytes of workspace dvcp_fps_parts needs for B clouds of N points (>= B x N x 4). */
+int64_t dvcp_fps_workspace_bytes(int B, int N);
+
+/* dvcp_fps_ws with a sized workspace (ws_bytes >= dvcp_fps_workspace_bytes(B, N), 8-byte aligned)
+ * and the split select's workgroups per cloud: parts = 0 (the library's choice, as dvcp_fps_ws),
+ * 1 (the one-workgroup select kernel), 2, 4 or 8 (fp32, 2048 <= N <= 16384).  Same contract and
+ * results as dvcp_fps; err as for dvcp_fps_ws.  The product path (dvcp/ops.py fps) calls this. */
 int dvcp_fps_parts(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N,
-                   int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz, float* ws,
-                   int32_t* err, int parts, void* stream);
+                   int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz, void* ws,
+                   int64_t ws_bytes, int32_t* err, int parts, void* stream);
 
 /* Two chained full-permutation FPS layers in one launch (the FE's layers 2 and 3 at C3:
  * pointnet2_utils.py:63-84 called by deep_feat_extraction.py:28 and :29 with npoint equal to the
