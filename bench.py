@@ -93,8 +93,11 @@ def parse():
                    help="diagnostic: no per-launch HIP events in the timed region")
     p.add_argument("--iso-steps", type=int, default=3,
                    help="steps timed per kernel with one batch in flight (stage roofline)")
-    p.add_argument("--cpu-pairs", type=int, default=1,
-                   help="C3 pairs timed for the CPU baseline (median); one pair is ~20 s on 16 host threads")
+    p.add_argument("--cpu-pairs", type=int, default=3,
+                   help="C3 pairs timed for the CPU baseline (median, SURVEY 8(d)); one pair is ~20 s on 16 host threads")
+    p.add_argument("--dfe", choices=["collapsed", "literal"], default="collapsed",
+                   help="target DFE: fc3.fc2.fc1 collapsed into one 32x35 map (dvcp_dfe_tgt, default) or the three "
+                        "layers chained as written (dvcp_dfe_tgt_literal, SURVEY App. A.3 Q14)")
     p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                    help="process group for world > 1: nccl (= RCCL, one rank per GPU) or gloo (rehearsal: "
                         "several ranks may share a GPU)")
@@ -144,7 +147,8 @@ def main():
     plan = D.ShardPlan(B, world, rank)
     torch.manual_seed(0)
     model = dvcp.DeepVCP(use_normal=False, K=K, r=r, s=s,
-                         feat_dtype=torch.float16 if args.feat_dtype == "f16" else torch.float32).eval().to(dev)
+                         feat_dtype=torch.float16 if args.feat_dtype == "f16" else torch.float32,
+                         dfe_literal=args.dfe == "literal").eval().to(dev)
     batches = [tuple(x.to(dev) for x in plan.lane_pairs(lane, N, make_pairs)) for lane in range(P)]
     src, tgt, R_gt, t_gt = batches[0]
     # random init, conditioned so key-point scores are separated beyond fp32 noise (the default
@@ -222,6 +226,7 @@ def main():
     pmc = _pmc(args.config)   # profiles/pmc_summary.json (C3) / pmc_summary_c5.json (C5)
     roofline = dominant_roofline(live, iso, stages, pmc)
     fps_roof = fps_roofline(live, iso, floor_us, pmc)
+    roofline["by_kernel_time"] = kernel_time_dominant(iso, stages, fps_roof)
     res_cpu = res.cpu()
     if rank == 0 and args.rows_out:
         # gathered in rank order (each rank: steps x B rows) -> (steps, global batch, 14)
@@ -246,7 +251,15 @@ def main():
                                 "C3: KITTI-like synthetic pairs, DeepVCP.forward + deepVCP_loss (eval)"),
                    "pairs_per_gpu": B, "global_batch": B * world, "n_points": N, "K": K, "r": r, "s": s,
                    "candidates": C, "fe_npoint": S, "parallelism": f"pairs sharded x{world}, all_gather(R,t)",
-                   "inflight_batches": P, "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
+                   "inflight_batches": P, "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
+                   # what the headline runs where it regroups the reference's arithmetic
+                   "dfe": ("literal: fc1, fc2, fc3 chained as written (dvcp_dfe_tgt_literal)" if args.dfe == "literal" else
+                           "collapsed: fc3.fc2.fc1 as one 32x35 map formed in fp64, rounded once (SURVEY App. A.3 "
+                           "Q14 deviation; --dfe literal runs the chain)") if args.feat_dtype == "f32" else
+                          "collapsed, fp16 feature table (dvcp_dfe_tgt_f16)",
+                   "sa_layer1": "per-point split: W1f.f + b1 once per point, W1x.(p - c) per grouped row (exact in "
+                                "real arithmetic; held to the fp32 bars)",
+                   "fps": f"select rounds on {_fps_parts_label(N)} workgroup(s) per cloud"},
         "latency_ms_single_batch": round(latency_ms, 3),
         "host_issue_ms_per_step": round(t_issue / args.steps * 1e3, 3),
         "registration_error_vs_gt": reg_err,
@@ -283,6 +296,11 @@ def main():
 HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
                  "vs_baseline", "dtype", "data", "config", "latency_ms_single_batch", "roofline", "cpu_baseline",
                  "parity", "registration_error_vs_gt")
+
+
+def _fps_parts_label(N):
+    from dvcp import ops
+    return ops.fps_parts(N)
 
 
 def headline(out):
@@ -432,7 +450,9 @@ def dominant_roofline(live, iso, stages, pmc):
                           "equals the fp32 MFMA rate, 157.3 TF/s) or hbm",
             "flop_convention": FLOP_CONVENTION.get(name, "executed flops as counted by dvcp/ops.py"),
             "kernel": name, "achieved": round(achieved, 3), "peak": round(peak, 3), "unit": unit,
-            "frac": round(achieved / peak, 4), "traffic": p.get("hbm_bytes_per_launch"),
+            "frac": round(achieved / peak, 4),
+            "frac_survey_8flop": round(achieved / peak * 8 / 9, 4) if name in FLOP_CONVENTION else None,
+            "traffic": p.get("hbm_bytes_per_launch"),
             "work_basis": st["work_basis"], "flops_per_launch": flops / v["n"],
             "algorithmic_bytes_per_launch": v["bytes"] / v["n"],
             "avg_launch_ms_isolated": round(launch_ms, 4),
@@ -446,13 +466,41 @@ def dominant_roofline(live, iso, stages, pmc):
                     "or 8 TB/s; traffic = PMC HBM bytes per launch"}
 
 
+FPS_ENTRIES = ("dvcp_fps_parts", "dvcp_fps_ws")   # ops.fps's entry point (ABI 4), and its predecessor
+
+
+def kernel_time_dominant(iso, stages, fps_roof):
+    """The entry point with the largest kernel time per step (rocprof's ranking: the FPS chain at C3,
+    16 clouds on a fraction of the chip), beside ``roofline``'s device-share-dominant one: its
+    reference-graph rate against the fp32 peak of the whole chip and of the CUs its grid occupies,
+    and, for the FPS, its time per centre against the measured step floor."""
+    name = max(iso, key=lambda k: iso[k]["ms"])
+    v, st = iso[name], stages[name]
+    tot = sum(x["ms"] for x in iso.values())
+    rec = {"kernel": name, "share_of_kernel_time": round(v["ms"] / tot, 4),
+           "avg_launch_ms_isolated": round(v["ms"] / v["n"], 4)}
+    if fps_roof and name == fps_roof["kernel"]:
+        rec.update({"bound": "latency (serial chain)", "unit": "TFLOP/s", "achieved": fps_roof["tflops_ref_graph"],
+                    "peak": PEAK_FP32_TFLOPS, "frac": fps_roof["frac_of_fp32_peak_chip"],
+                    "frac_own_cus": fps_roof["frac_of_fp32_peak_own_cus"], "cu_share": st["cu_share"],
+                    "traffic": fps_roof["traffic"], "us_per_centre": fps_roof["us_per_centre"],
+                    "step_floor_us": fps_roof["step_floor_us"], "frac_of_step_floor": fps_roof["frac_of_step_floor"],
+                    "flop_convention": "9 flop per point-update of the reference graph (npoint x N per cloud); "
+                                       "SURVEY 8(d)'s 8 flop: x 8/9"})
+    else:
+        tf = v["flops"] / (v["ms"] * 1e-3) / 1e12
+        rec.update({"bound": st["bound"], "unit": "TFLOP/s", "achieved": round(tf, 3), "peak": PEAK_FP32_TFLOPS,
+                    "frac": round(tf / PEAK_FP32_TFLOPS, 4), "cu_share": st["cu_share"]})
+    return rec
+
+
 def fps_roofline(live, iso, floor_us, pmc):
     """FPS is a serial chain of npoint dependent argmax steps per cloud, one workgroup per cloud:
     reported against the measured step floor of its synchronisation (dvcp_fps_step_floor, us per
     centre) AND against the fp32 VALU peak, both of the whole chip and of the 16 CUs a C3 batch's
     16 clouds occupy (reference-graph flops: 9 per point-update, npoint x N per cloud)."""
-    name = "dvcp_fps_ws"
-    if name not in iso:
+    name = next((n for n in FPS_ENTRIES if n in iso), None)
+    if name is None:
         return None
     v, w = iso[name], live.get(name)
     us_iso = v["ms"] * 1e3 / v["steps"]

@@ -87,7 +87,7 @@ struct alignas(16) FpsSlot {
 constexpr int kFpsThreads = 512;  // 8 waves: 2 per SIMD, up to 256 VGPRs each
 constexpr int kFpsSel1024 = 1024;  // the fp32 select kernel's workgroup: 16 waves, 4 per SIMD
 constexpr int kMortonBins = 4096;
-constexpr int kFpsProf = 12;      // timing probe words per wave (fps_kernel<..., TIMING=true>)
+constexpr int kFpsProf = 13;      // timing probe words per wave (fps_kernel<..., TIMING=true>)
 
 __device__ __forceinline__ uint32_t spread4(uint32_t v) {  // 4 bits -> every third bit
   v &= 0xF;
@@ -623,7 +623,7 @@ constexpr uint32_t kFpsPairSpinCap = 1u << 22;
 // and others to none.  Part 0 hands its permutation to the other parts through `perm` (write-through
 // stores, then the cloud's flag), once per launch.
 struct FpsPartArgs {
-  uint64_t* slots;   // [B][2][S][kPartHdr + 5 * (128 / S)] granules, all ones before the launch
+  uint64_t* slots;   // [B][2][S][kPartHdr + W + 5 * (128 / S)] granules, all ones before the launch
   uint32_t* flag;    // [B], all ones before the launch; 1 once part 0 has published the permutation
   uint32_t* perm;    // [B][perm_words]: the cloud's Morton permutation, two u16 per word
   int32_t* err;
@@ -632,7 +632,10 @@ struct FpsPartArgs {
   int perm_words;    // ceil(N / 2)
   uint32_t spin_cap;
 };
-constexpr int kPartHdr = 8;            // granules: T_w, count | flags << 16, best v, idx, x, y, z, (spare)
+// a part's slot: kPartHdr header granules (count | flags << 16, best v, best idx, its x, y, z, two
+// spare), then one T granule per wave (the largest running minimum it did not list), then the
+// candidates' v, idx, x, y, z (capw each)
+constexpr int kPartHdr = 8;
 constexpr int kPartMaxN = 16384;       // the whole cloud's Morton order is kept in LDS
 constexpr uint32_t kPartFlagFb = 1u, kPartFlagEmpty = 2u;
 __device__ __forceinline__ void granule_put(uint64_t* g, uint32_t data, uint32_t tag) {
@@ -692,8 +695,10 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
   __shared__ uint32_t na_cnt, cand_fill;
   __shared__ int ckey[MODE == 1 ? kSelMax : 1];  // MODE 1: candidates' point indices in a re-ranked round
   __shared__ int s_gaveup;
-  // MODE 3: the round's headers of every part (kPartHdr words each) and this part's empty-key
+  // MODE 3: the round's headers of every part (kPartHdr words each), every part's per-wave T, and
+  // this part's empty-key
   __shared__ uint32_t phdr[MODE == 3 ? 8 : 1][kPartHdr];
+  __shared__ uint32_t phdrT[MODE == 3 ? 8 * W : 1];
   __shared__ uint32_t s_minidx;
   float* lv = reinterpret_cast<float*>(bins);
   uint32_t* lpos = bins + kSelCap;
@@ -715,7 +720,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
     if (b >= qa.B) return;  // grid padding: no partner waits for it (its whole cloud is padding)
     capw = kSelMax / S;
     seltarget = max(kSelMin, kSelTarget / S);
-    slotsz = kPartHdr + 5 * capw;
+    slotsz = kPartHdr + W + 5 * capw;
     qslot = qa.slots + static_cast<int64_t>(b) * 2 * S * slotsz;
     if (tid == 0) s_gaveup = 0;
   }
@@ -935,44 +940,54 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
       tp = t;
     }
   };
-  // MODE 3, step 2 of a round: publish this part's header (and the unused candidate slots; its
-  // candidates went out from the list pass) and read every other part's granules of the round
-  // into the merged list / phdr.  Called by every thread after the barrier that completed this
-  // part's list; ends with a barrier.  best_i / best_v: this part's argmax key (flags != 0 only).
-  auto part_exchange = [&](uint32_t flags, uint32_t tw_bits, uint32_t bv_bits, uint32_t best_i, int cntw) {
+  // MODE 3, step 2 of a round.  The granules of the round: wave 0 publishes the header and the
+  // unused candidate slots once the round's decision is final (part_publish); every wave its T
+  // (part_publish_t, from the list pass); the list pass the candidates.  part_gather then reads
+  // every other part's granules of the round into the merged list, phdr and phdrT (the caller's
+  // next barrier completes it).
+  auto round_slot = [&](int q) { return qslot + (static_cast<int64_t>(n_round & 1) * S + q) * slotsz; };
+  auto part_publish = [&](uint32_t flags, int cntw, uint32_t bv_bits, uint32_t best_i) {  // wave 0
     if constexpr (MODE == 3) {
       const uint32_t tag = static_cast<uint32_t>(n_round);
-      uint64_t* const round_slots = qslot + static_cast<int64_t>(n_round & 1) * S * slotsz;
-      uint64_t* const mine = round_slots + part * slotsz;
-      if (wave == 0) {
-        if (lane < kPartHdr) {
-          uint32_t d = lane == 0 ? tw_bits : lane == 1 ? (static_cast<uint32_t>(cntw) | (flags << 16))
-                                           : lane == 2 ? bv_bits : lane == 3 ? best_i : 0u;
-          if (lane >= 4 && lane < 7 && flags != 0u && best_i < static_cast<uint32_t>(N))
-            d = __float_as_uint(pts.at(b, lane - 4, static_cast<int>(best_i)));
-          phdr[part][lane] = d;
-          granule_put(mine + lane, d, tag);
-        }
-        for (int o = cntw + lane; o < capw; o += kWave) {  // unused slots: v = -1 never ranks or wins
-          const int j = part * capw + o;
-          cvv[j] = -1.0f;
-          cpid[j] = 0x7FFFFFFF;
-          cxx[j] = 0.0f;
-          cyy[j] = 0.0f;
-          czz[j] = 0.0f;
-          uint64_t* g = mine + kPartHdr + o;
-          granule_put(g, __float_as_uint(-1.0f), tag);
-          granule_put(g + capw, 0x7FFFFFFFu, tag);
-          granule_put(g + 2 * capw, 0u, tag);
-          granule_put(g + 3 * capw, 0u, tag);
-          granule_put(g + 4 * capw, 0u, tag);
-        }
+      uint64_t* const mine = round_slot(part);
+      if (lane < kPartHdr) {
+        uint32_t d = lane == 0 ? (static_cast<uint32_t>(cntw) | (flags << 16)) : lane == 1 ? bv_bits
+                                                                               : lane == 2 ? best_i : 0u;
+        if (lane >= 3 && lane < 6 && flags != 0u && best_i < static_cast<uint32_t>(N))
+          d = __float_as_uint(pts.at(b, lane - 3, static_cast<int>(best_i)));
+        phdr[part][lane] = d;
+        granule_put(mine + lane, d, tag);
       }
+      for (int o = cntw + lane; o < capw; o += kWave) {  // unused slots: v = -1 never ranks or wins
+        const int j = part * capw + o;
+        cvv[j] = -1.0f;
+        cpid[j] = 0x7FFFFFFF;
+        cxx[j] = 0.0f;
+        cyy[j] = 0.0f;
+        czz[j] = 0.0f;
+        uint64_t* g = mine + kPartHdr + W + o;
+        granule_put(g, __float_as_uint(-1.0f), tag);
+        granule_put(g + capw, 0x7FFFFFFFu, tag);
+        granule_put(g + 2 * capw, 0u, tag);
+        granule_put(g + 3 * capw, 0u, tag);
+        granule_put(g + 4 * capw, 0u, tag);
+      }
+    }
+  };
+  auto part_publish_t = [&](uint32_t t_bits) {  // lane 0 of every wave: this wave's T
+    if constexpr (MODE == 3) {
+      phdrT[part * W + wave] = t_bits;
+      granule_put(round_slot(part) + kPartHdr + wave, t_bits, static_cast<uint32_t>(n_round));
+    }
+  };
+  auto part_gather = [&]() {
+    if constexpr (MODE == 3) {
+      const uint32_t tag = static_cast<uint32_t>(n_round);
       const int others = (S - 1) * slotsz;
       for (int t = tid; t < others; t += THREADS) {
         const int qq = t / slotsz, k = t - qq * slotsz;
         const int q = qq + (qq >= part ? 1 : 0);
-        const uint64_t* g = round_slots + q * slotsz + k;
+        const uint64_t* g = round_slot(q) + k;
         uint64_t v = 0;
         uint32_t polls = 0;
         for (;;) {
@@ -987,8 +1002,10 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
         const uint32_t d = static_cast<uint32_t>(v);
         if (k < kPartHdr) {
           phdr[q][k] = d;
+        } else if (k < kPartHdr + W) {
+          phdrT[q * W + (k - kPartHdr)] = d;
         } else {
-          const int c = (k - kPartHdr) / capw, o = (k - kPartHdr) - c * capw, j = q * capw + o;
+          const int c = (k - kPartHdr - W) / capw, o = (k - kPartHdr - W) - c * capw, j = q * capw + o;
           if (c == 0) cvv[j] = __uint_as_float(d);
           else if (c == 1) cpid[j] = static_cast<int>(d);
           else if (c == 2) cxx[j] = __uint_as_float(d);
@@ -996,8 +1013,32 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
           else czz[j] = __uint_as_float(d);
         }
       }
-      lds_barrier();
     }
+  };
+  // MODE 3, after the gather's barrier: T = max over every part's waves, the candidate total, whether
+  // some part fell back, and this part's own T (lane-parallel reads, wave reductions; every wave)
+  auto part_merge = [&](uint32_t& tg, uint32_t& total, uint32_t& fb, uint32_t& tw) {
+    uint32_t t = 0u, tt = 0u, c = 0u, f = 0u;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int i = hh * kWave + lane;
+      if (i < S * W) {
+        const uint32_t x = phdrT[i];
+        t = max(t, x);
+        if (i / W == part) tt = max(tt, x);
+      }
+    }
+    if (lane < S) {
+      const uint32_t h = phdr[lane][0];
+      c = h & 0xFFFFu;
+      f = (h >> 16) & kPartFlagFb;
+    }
+    uint32_t ma, mb;
+    wave_umax2(t, tt, ma, mb);
+    tg = ma;
+    tw = mb;
+    fb = wave_umax(f);
+    total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wave_incl_scan(c)), 63));
   };
   // MODE 3: a round without certification (some part fell back, or no part listed a candidate)
   // accepts the single global argmax over the listed candidates and the fallen-back / empty parts'
@@ -1012,8 +1053,8 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
       if (v >= 0.0f)
         key = max(key, (static_cast<uint64_t>(__float_as_uint(v)) << 32) | (0xFFFFFFFFu - static_cast<uint32_t>(cpid[jj])));
     }
-    if (lane < S && (phdr[lane][1] >> 16) != 0u)
-      key = max(key, (static_cast<uint64_t>(phdr[lane][2]) << 32) | (0xFFFFFFFFu - phdr[lane][3]));
+    if (lane < S && (phdr[lane][0] >> 16) != 0u)
+      key = max(key, (static_cast<uint64_t>(phdr[lane][1]) << 32) | (0xFFFFFFFFu - phdr[lane][2]));
     for (int off = 32; off > 0; off >>= 1) {
       const uint64_t o = __shfl_xor(key, off, kWave);
       key = o > key ? o : key;
@@ -1204,7 +1245,10 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
 #pragma unroll
         for (int w = 1; w < W; ++w) gp = min(gp, wpid[w]);
         if constexpr (MODE == 3) {  // this part's key goes to the others; the round takes the global one
-          part_exchange(kPartFlagFb, __float_as_uint(gmax), __float_as_uint(gmax), gp, 0);
+          if (wave == 0) part_publish(kPartFlagFb, 0, __float_as_uint(gmax), gp);
+          if (lane == 0) part_publish_t(__float_as_uint(gmax));
+          part_gather();
+          lds_barrier();
           if (s_gaveup) {
             part_quit = true;
             break;
@@ -1243,9 +1287,12 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
       // (MODE 3: this part's candidates go to its own range of the merged list and out as
       // granules; an empty part lists nothing: na = 0)
       int cnt = static_cast<int>(suf_of(bsel));
+      int nreal = cnt;  // candidates in the list (MODE 3: the merged list's, without its unused slots)
       const int cbase = part * capw;
-      uint64_t* const cgran = MODE == 3 ? qslot + (static_cast<int64_t>(n_round & 1) * S + part) * slotsz + kPartHdr
-                                        : nullptr;
+      uint64_t* const cgran = MODE == 3 ? round_slot(part) + kPartHdr + W : nullptr;
+      if constexpr (MODE == 3) {  // the decision is final: header and unused slots go out now
+        if (wave == 0) part_publish(mode == 3 ? kPartFlagEmpty : 0u, cnt, 0u, mode == 3 ? s_minidx : 0u);
+      }
       float tl = Tf;
       for (int i = wave * (kSelCap / W) + lane; i < (wave + 1) * (kSelCap / W); i += kWave) {
         const bool live = i < static_cast<int>(na);
@@ -1283,12 +1330,19 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
       }
       tl = wave_fmax_clamp0(tl);
       if (lane == 0) atomicMax(&tb_max, __float_as_uint(tl));
+      if constexpr (MODE == 3) {
+        if (lane == 0) part_publish_t(__float_as_uint(tl));
+      }
       // next round: keep a few hundred points above the floor.  The decay sets how often a round
       // lists more than kSelCap points and scans again: 0.85 rescanned in ~20 % of the C3 rounds
       // (sa1: 74 of 367), 0.9 in ~2 % (6 of 367; sa2 / sa3 37 -> 4 of 302), with the same rounds
       // (tools/fps_lab/fps_round_sim.py, a CPU model of this round logic; FPS lab: 81 of 382).
       if (na < 4u * static_cast<uint32_t>(seltarget)) f *= 0.9f;
       if (wave * kWave < kSelMax) srank[wave * kWave + lane] = 0u;  // (read last by the previous round)
+      if constexpr (MODE == 3) {  // ---- MODE 3, step 2: the other parts' granules of the round ------
+        tick(1);
+        part_gather();
+      }
       lds_barrier();
       float Tb = __uint_as_float(tb_max);
       if (tid == 0) {  // (T_f was read by every wave before this barrier)
@@ -1299,19 +1353,14 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
       for (int i = tid; i < kSelBins; i += THREADS) hist[i] = 0u;
       [[maybe_unused]] const float Tw = Tb;  // MODE 3: this part's own T (its next vmax bound)
       if constexpr (MODE == 3) {
-        // ---- MODE 3, step 2: exchange; then the merged list and T = max_w T_w --------------------
-        part_exchange(mode == 3 ? kPartFlagEmpty : 0u, tb_max, 0u, mode == 3 ? s_minidx : 0u, cnt);
+        // ---- the merged list: T = max over every part's T, the candidate total, fallbacks --------
+        tick(5);
         if (s_gaveup) {
           part_quit = true;
           break;
         }
-        if (tid == 0) tb_max = 0u;  // (every wave read it before the exchange's barrier)
-        uint32_t tg = 0u, total = 0u, fb = 0u;
-        for (int q = 0; q < S; ++q) {
-          tg = max(tg, phdr[q][0]);
-          total += phdr[q][1] & 0xFFFFu;
-          fb |= (phdr[q][1] >> 16) & kPartFlagFb;
-        }
+        uint32_t tg, total, fb, twb;
+        part_merge(tg, total, fb, twb);
         if (fb != 0u || total == 0u) {  // one exact argmax for the round
           ++n_fallback;
           const uint32_t gp = part_argmax();
@@ -1336,10 +1385,12 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
           }
           vmax = wave_fmax_clamp0(vm);
           lds_barrier();
+          if (tid == 0) tb_max = 0u;  // (every wave read it before this barrier)
           kstar = 1;
           break;
         }
         cnt = S * capw;  // the merged list (unused slots: v = -1)
+        nreal = static_cast<int>(total);
         Tb = __uint_as_float(tg);
       }
       tick(1);
@@ -1372,6 +1423,8 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
             const int i0 = i_lo + 4 * c4;
             if (i0 >= cnt) break;  // wave-uniform
             const float4 v4 = *reinterpret_cast<const float4*>(&cvv[i0]);
+            // MODE 3: a part's unused slots (v = -1) follow its candidates; skip all-unused batches
+            if (MODE == 3 && v4.x < 0.0f) continue;  // (wave-uniform)
             const int4 p4 = *reinterpret_cast<const int4*>(&cpid[i0]);
             const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
             const int pp[4] = {p4.x, p4.y, p4.z, p4.w};
@@ -1384,7 +1437,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-              const bool in = i0 + k < cnt;
+              const bool in = MODE == 3 ? vv[k] >= 0.0f : i0 + k < cnt;
               const bool b0 = in & ((vv[k] > v0) | ((vv[k] == v0) & (pp[k] < p0)));
               const bool b1 = in & ((vv[k] > v1) | ((vv[k] == v1) & (pp[k] < p1)));
               const T ax = x0 - xx[k], ay = y0 - yy[k], az = z0 - zz[k];
@@ -1403,6 +1456,12 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
           }
         }
         if (i_lo < cnt) {  // wave-uniform
+          if (MODE == 3) {  // (unused slots take no rank)
+            r0 = cvv[lane] >= 0.0f ? r0 : 0;
+            t0 = cvv[lane] >= 0.0f ? t0 : 0;
+            r1 = cvv[lane + kWave] >= 0.0f ? r1 : 0;
+            t1 = cvv[lane + kWave] >= 0.0f ? t1 : 0;
+          }
           if (r0 | t0 | e0) atomicAdd(&srank[lane], static_cast<uint32_t>(r0 | (t0 << 16) | (e0 << 24)));
           if (r1 | t1 | e1) atomicAdd(&srank[lane + kWave], static_cast<uint32_t>(r1 | (t1 << 16) | (e1 << 24)));
         }
@@ -1418,7 +1477,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
       for (int hh = 0; hh < 2; ++hh) {
         const int jj = hh * 64 + lane;
         rk[hh] = 0x7FFFFFFF;
-        if (jj < cnt) {
+        if (jj < cnt && (MODE != 3 || cvv[jj] >= 0.0f)) {  // (MODE 3: unused slots are no candidates)
           const uint32_t e = srank[jj];
           const int r = static_cast<int>(e & 0xFFFFu);
           const bool touched = MODE == 1 ? ((e >> 16) & 0xFFu) != 0u : (e >> 16) != 0u;
@@ -1428,7 +1487,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
           failr = fail ? min(failr, static_cast<uint32_t>(r)) : failr;
         }
       }
-      kstar = static_cast<int>(min(min(wave_umin(failr), static_cast<uint32_t>(cnt)),
+      kstar = static_cast<int>(min(min(wave_umin(failr), static_cast<uint32_t>(nreal)),
                                    static_cast<uint32_t>(kSelAccept)));
       };
       rank_decide();
@@ -1616,6 +1675,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
       o[2] = n_fallback;
       for (int k = 0; k < 5; ++k) o[3 + k] = ph[k];
       for (int k = 0; k < 4; ++k) o[8 + k] = why[k];
+      o[12] = ph[5];
     }
   }
 }
@@ -1630,12 +1690,14 @@ void fps_select_kernel(PointsView<T> pts, int N, int npoint, const int64_t* __re
 
 // Split select (FpsPartArgs): grid ceil(B / 8) * 8 * S, THREADS threads, PPT groups per lane
 // slot of a part's share of the cloud.
-template <int PPT, int THREADS>
+// TIMING (tools/fps_lab): per-wave round clocks of every part, prof[((b S + part) W + wave) kFpsProf].
+template <int PPT, int THREADS, bool TIMING = false>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(THREADS / 256)))
 void fps_part_kernel(PointsView<float> pts, int N, int npoint, const int64_t* __restrict__ start,
-                     int64_t* __restrict__ out_idx, float* __restrict__ out_xyz, FpsPartArgs qa) {
-  fps_select_body<float, PPT, false, THREADS, 3>(pts, N, npoint, start, out_idx, out_xyz, nullptr, FpsPairArgs<float>{},
-                                                 qa);
+                     int64_t* __restrict__ out_idx, float* __restrict__ out_xyz, FpsPartArgs qa,
+                     unsigned long long* __restrict__ prof) {
+  fps_select_body<float, PPT, TIMING, THREADS, 3>(pts, N, npoint, start, out_idx, out_xyz, prof,
+                                                  FpsPairArgs<float>{}, qa);
 }
 
 // grid 2B: layer 2 (out_idx / out_xyz, start) and layer 3 (pa) of B clouds, see FpsPairArgs.
@@ -2064,7 +2126,8 @@ static int launch_fps_part(PointsView<float> v, int B, int N, int npoint, const 
   const int groups = ceil_div(ceil_div(N, kWave), S);  // 64-point groups per part (at most)
 #define DVCP_FPS_PART(P, NT)                                                                                  \
   if (threads == NT && groups <= P * (NT / kWave)) {                                                          \
-    hipLaunchKernelGGL((fps_part_kernel<P, NT>), grid, dim3(NT), 0, st, v, N, npoint, start, out_idx, out_xyz, qa); \
+    hipLaunchKernelGGL((fps_part_kernel<P, NT>), grid, dim3(NT), 0, st, v, N, npoint, start, out_idx, out_xyz, qa, \
+                       nullptr);                                                                              \
     return launch_status("dvcp_fps(part)");                                                                   \
   }
   DVCP_FPS_PART(2, 1024)

@@ -44,11 +44,15 @@ def _warn_f16_autograd():
 
 
 class DeepVCP(nn.Module):
-    def __init__(self, use_normal, K=64, r=1.0, s=0.4, fe_npoint=10000, feat_dtype=torch.float32):
+    def __init__(self, use_normal, K=64, r=1.0, s=0.4, fe_npoint=10000, feat_dtype=torch.float32, dfe_literal=False):
         """``feat_dtype``: storage of the target feature table the fused target stage gathers
         (torch.float16: BASELINE C5's "fp16 features", dvcp_dfe_tgt_f16; inference only -- the
-        reference keeps fp32 features, so float16 is not reference precision)."""
+        reference keeps fp32 features, so float16 is not reference precision).
+        ``dfe_literal``: the fused target DFE chains fc1, fc2, fc3 as written (dvcp_dfe_tgt_literal,
+        SURVEY App. A.3 Q14) instead of the collapsed 32x35 map (dvcp_dfe_tgt, the default: fc3.fc2.fc1
+        formed in fp64 and rounded once; the same within 1e-7 on the tests)."""
         super().__init__()
+        self.dfe_literal = bool(dfe_literal)
         if feat_dtype not in (torch.float32, torch.float16):
             raise ValueError(f"feat_dtype must be torch.float32 or torch.float16, got {feat_dtype}")
         self.feat_dtype = feat_dtype
@@ -217,7 +221,8 @@ class DeepVCP(nn.Module):
             vcp = autograd.cpg(src_dfe, tgt_dfe.permute(0, 1, 3, 2), cand, G, self.cpg)
         else:
             feat_t = tgt_feat if self.feat_dtype == torch.float32 else tgt_feat.to(self.feat_dtype)
-            tgt_dfe = ops.dfe_tgt(tgt_xyz, feat_t, qry, dist, idx, dfe_pack, ref_pdim=2)
+            tgt_dfe = ops.dfe_tgt(tgt_xyz, feat_t, qry, dist, idx, dfe_pack, ref_pdim=2,
+                                  literal=self.dfe_literal and self.feat_dtype == torch.float32)
             tgt_dfe = tgt_dfe.view(B, K, C, 32)
             torch.cuda.current_stream(dev).wait_stream(side)
             vcp = ops.cpg(src_dfe, tgt_dfe.permute(0, 1, 3, 2), cand, G, self.cpg.packed_params())

@@ -117,6 +117,74 @@ int main(int argc, char** argv) {
   };
   std::vector<int64_t> got(static_cast<size_t>(B) * npoint);
   const std::vector<unsigned long long> pr_dummy(1);
+  // split select (round 6): S workgroups per cloud; `fps_lab B N npoint parts` runs only these
+  if (argc > 4) {
+    struct PartCfg {
+      const char* name;
+      void (*fn)(PointsView<float>, int, int, const int64_t*, int64_t*, float*, dvcp::FpsPartArgs, unsigned long long*);
+      int threads, ppt, S;
+      bool timing;
+    };
+#define PART(P, NT, S, TM, NAME) PartCfg{NAME, dvcp::fps_part_kernel<P, NT, TM>, NT, P, S, TM}
+    const std::vector<PartCfg> pcs = {
+        PART(8, 1024, 2, false, "part 2 x 1024x8"),      PART(8, 1024, 2, true, "part 2 x 1024x8 +stats"),
+        PART(4, 1024, 4, false, "part 4 x 1024x4"),      PART(4, 1024, 4, true, "part 4 x 1024x4 +stats"),
+        PART(2, 1024, 8, false, "part 8 x 1024x2"),      PART(2, 1024, 8, true, "part 8 x 1024x2 +stats"),
+        PART(8, 512, 4, false, "part 4 x 512x8"),        PART(8, 512, 4, true, "part 4 x 512x8 +stats"),
+    };
+#undef PART
+    uint64_t* dws;
+    const size_t ws_bytes = static_cast<size_t>(dvcp::fps_workspace_bytes(B, N));
+    CK(hipMalloc(&dws, ws_bytes));
+    const size_t pprof_words = static_cast<size_t>(B) * 8 * 16 * dvcp::kFpsProf;
+    unsigned long long* dpp;
+    CK(hipMalloc(&dpp, pprof_words * 8));
+    for (const auto& c : pcs) {
+      const int groups = (N + 63) / 64, gpart = (groups + c.S - 1) / c.S;
+      if (gpart > c.ppt * (c.threads / 64)) continue;
+      const dvcp::FpsPartWs w = dvcp::fps_part_ws(B, N, c.S);
+      const int capw = dvcp::kSelMax / c.S;
+      char* base = reinterpret_cast<char*>(dws);
+      const dvcp::FpsPartArgs qa{dws, reinterpret_cast<uint32_t*>(base + w.slot_bytes),
+                                 reinterpret_cast<uint32_t*>(base + w.slot_bytes + w.flag_bytes),
+                                 reinterpret_cast<int32_t*>(base + w.total - 8), c.S, B, (N + 1) / 2, dvcp::kFpsSpinCap};
+      (void)capw;
+      CK(hipMemset(dpp, 0, pprof_words * 8));
+      float best = 1e30f;
+      for (int rep = 0; rep < 3; ++rep) {
+        CK(hipMemset(dws, 0xFF, w.slot_bytes + w.flag_bytes));
+        CK(hipEventRecord(e0));
+        hipLaunchKernelGGL(c.fn, dim3((B + 7) / 8 * 8 * c.S), dim3(c.threads), 0, 0, view, N, npoint, ds, dout, dox, qa,
+                           dpp);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        best = ms < best ? ms : best;
+      }
+      CK(hipMemcpy(got.data(), dout, got.size() * 8, hipMemcpyDeviceToHost));
+      int bad = 0;
+      for (int b = 0; b < ncheck; ++b)
+        for (int s = 0; s < npoint; ++s) bad += got[static_cast<size_t>(b) * npoint + s] != want[b][s];
+      printf("%-28s B %3d N %6d npoint %6d  %8.3f ms  %6.3f us/step  mismatches %d\n", c.name, B, N, npoint, best,
+             1e3f * best / npoint, bad);
+      if (c.timing) {
+        std::vector<unsigned long long> pr(pprof_words);
+        CK(hipMemcpy(pr.data(), dpp, pr.size() * 8, hipMemcpyDeviceToHost));
+        const int W = c.threads / 64;
+        printf("   cloud 0: rounds %llu  scans %llu  fallbacks %llu  centres/round %.1f\n", pr[0], pr[1], pr[2],
+               pr[0] ? double(npoint - 1) / pr[0] : 0.0);
+        for (int part = 0; part < c.S; ++part)
+          for (int wv = 0; wv < W; wv += (W > 4 ? W / 4 : 1)) {
+            const unsigned long long* q = &pr[(static_cast<size_t>(part) * W + wv) * dvcp::kFpsProf];
+            const double r = q[0] ? double(q[0]) : 1.0;
+            printf("   part %d wave %2d clk/round: scan %.0f  decide+list %.0f  exchange %.0f  rank %.0f  prefix %.0f  "
+                   "update %.0f\n", part, wv, q[3] / r, q[4] / r, q[12] / r, q[5] / r, q[6] / r, q[7] / r);
+          }
+      }
+    }
+    return 0;
+  }
   for (const auto& c : cfgs) {
     if (N > c.threads * c.ppt) continue;
     CK(hipMemset(dprof, 0, prof_words * 8));

@@ -26,6 +26,8 @@ import sys
 #                                  helper kernels the same call also launches)
 ENTRY = {
     "dvcp_fps_ws": (["fps_select_kernel", "fps_kernel", "fps_split_kernel", "fps_dense_kernel"], []),
+    "dvcp_fps_parts": (["fps_part_kernel", "fps_select_kernel", "fps_kernel", "fps_split_kernel", "fps_dense_kernel"],
+                       []),
     "dvcp_fps_pair": (["fps_pair_kernel"], ["fps_pair_remap_kernel", "fps_select_gated_kernel"]),
     "dvcp_knn_tiled": (["knn_tiled_query_kernel", "knn_sel_query_kernel"],
                        ["knn_tiled_build_kernel", "knn_qbox_kernel", "knn_qhist_kernel", "knn_qscan_kernel"]),
