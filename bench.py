@@ -95,6 +95,9 @@ def parse():
                    help="steps timed per kernel with one batch in flight (stage roofline)")
     p.add_argument("--cpu-pairs", type=int, default=3,
                    help="C3 pairs timed for the CPU baseline (median, SURVEY 8(d)); one pair is ~20 s on 16 host threads")
+    p.add_argument("--fps-parts-latency", type=int, default=8, choices=[0, 2, 4, 8],
+                   help="also time the single-batch latency with the FPS select rounds split over this many "
+                        "workgroups per cloud (DeepVCP(fps_parts=...); 0: skip)")
     p.add_argument("--dfe", choices=["collapsed", "literal"], default="collapsed",
                    help="target DFE: fc3.fc2.fc1 collapsed into one 32x35 map (dvcp_dfe_tgt, default) or the three "
                         "layers chained as written (dvcp_dfe_tgt_literal, SURVEY App. A.3 Q14)")
@@ -219,6 +222,20 @@ def main():
         torch.cuda.synchronize()
     iso, _lib.EVENT_LOG = _per_kernel(_lib.EVENT_LOG), None
     floor_us = fps_step_floor_us(dev)
+    # the single-batch latency with the split-select FPS (opt-in: it shortens a lone batch's chain;
+    # with batches in flight its workgroups' waits can starve), same batch and model
+    lat_split = None
+    if args.fps_parts_latency and args.config == "c3":
+        model.FE1.fps_parts = args.fps_parts_latency
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+        t_ls = time.perf_counter()
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+        lat_split = {"parts": args.fps_parts_latency, "ms": round((time.perf_counter() - t_ls) / 2 * 1e3, 3)}
+        model.FE1.fps_parts = None
     ms_step = elapsed / args.steps * 1e3
     S = model.FE1.sa1.npoint
     C = int((2 * r) / s + 1) ** 3
@@ -259,8 +276,9 @@ def main():
                           "collapsed, fp16 feature table (dvcp_dfe_tgt_f16)",
                    "sa_layer1": "per-point split: W1f.f + b1 once per point, W1x.(p - c) per grouped row (exact in "
                                 "real arithmetic; held to the fp32 bars)",
-                   "fps": f"select rounds on {_fps_parts_label(N)} workgroup(s) per cloud"},
+                   "fps": f"select rounds on {model.FE1.fps_parts or _fps_parts_label(N)} workgroup(s) per cloud"},
         "latency_ms_single_batch": round(latency_ms, 3),
+        "latency_ms_single_batch_split_fps": lat_split,
         "host_issue_ms_per_step": round(t_issue / args.steps * 1e3, 3),
         "registration_error_vs_gt": reg_err,
         "roofline": roofline,
@@ -294,8 +312,8 @@ def main():
 
 
 HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
-                 "vs_baseline", "dtype", "data", "config", "latency_ms_single_batch", "roofline", "cpu_baseline",
-                 "parity", "registration_error_vs_gt")
+                 "vs_baseline", "dtype", "data", "config", "latency_ms_single_batch",
+                 "latency_ms_single_batch_split_fps", "roofline", "cpu_baseline", "parity", "registration_error_vs_gt")
 
 
 def _fps_parts_label(N):

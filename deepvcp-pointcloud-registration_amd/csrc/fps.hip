@@ -631,6 +631,7 @@ struct FpsPartArgs {
   int B;             // clouds (the grid is ceil(B / 8) * 8 * S blocks)
   int perm_words;    // ceil(N / 2)
   uint32_t spin_cap;
+  int target;        // candidates a part aims to list per round (0: max(kSelMin, kSelTarget / S))
 };
 // a part's slot: kPartHdr header granules (count | flags << 16, best v, best idx, its x, y, z, two
 // spare), then one T granule per wave (the largest running minimum it did not list), then the
@@ -719,7 +720,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
     part = q % S;
     if (b >= qa.B) return;  // grid padding: no partner waits for it (its whole cloud is padding)
     capw = kSelMax / S;
-    seltarget = max(kSelMin, kSelTarget / S);
+    seltarget = qa.target > 0 ? min(qa.target, capw) : max(kSelMin, kSelTarget / S);
     slotsz = kPartHdr + W + 5 * capw;
     qslot = qa.slots + static_cast<int64_t>(b) * 2 * S * slotsz;
     if (tid == 0) s_gaveup = 0;
@@ -2072,17 +2073,20 @@ static int launch_fps_split(PointsView<T> v, int B, int N, int npoint, const int
   return launch_status("dvcp_fps(split)");
 }
 
-// Workgroups per cloud of the split select (FpsPartArgs) for an fp32 cloud of N points; 1 = the
-// one-workgroup select kernel.  DVCP_FPS_PARTS overrides (1, 2, 4 or 8; A/B runs), as does
-// DVCP_FPS_PART_THREADS the workgroup size (256, 512 or 1024).
+// Workgroups per cloud of the select rounds when the caller does not choose (dvcp_fps_ws, parts 0):
+// one, unless DVCP_FPS_PARTS asks for the split select (2, 4 or 8).  The split select shortens a
+// lone batch's chain, but its workgroups wait for each other: with many batches in flight (the
+// bench's ten) a waiting full-CU workgroup's peer can starve behind other kernels' smaller
+// workgroups, which take every CU that frees (round 6: the guard fired at four parts).
+// DVCP_FPS_PART_THREADS sets its workgroup size (256, 512 or 1024; A/B runs).
 static int fps_env_int(const char* name, int dflt) {
   const char* s = getenv(name);
   return s && *s ? atoi(s) : dflt;
 }
 static int fps_parts(int N) {
   static const int forced = fps_env_int("DVCP_FPS_PARTS", 0);
-  if (forced == 1 || forced == 2 || forced == 4 || forced == 8) return forced;
-  return N > 8192 ? 4 : N >= 4096 ? 2 : 1;
+  (void)N;
+  return forced == 2 || forced == 4 || forced == 8 ? forced : 1;
 }
 
 // Launch the split select over B fp32 clouds with S workgroups each; returns 1 (nothing launched)
@@ -2121,7 +2125,8 @@ static int launch_fps_part(PointsView<float> v, int B, int N, int npoint, const 
   if (!err) err = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(ws) + w.total - 8);
   if (hipMemsetAsync(slots, 0xFF, static_cast<size_t>(w.slot_bytes + w.flag_bytes), st) != hipSuccess)
     return launch_status("dvcp_fps(part memset)");
-  const FpsPartArgs qa{slots, flags, permw, err, S, B, (N + 1) / 2, kFpsSpinCap};
+  static const int target = fps_env_int("DVCP_FPS_PART_TARGET", 0);
+  const FpsPartArgs qa{slots, flags, permw, err, S, B, (N + 1) / 2, kFpsSpinCap, target};
   const dim3 grid(ceil_div(B, 8) * 8 * S);
   const int groups = ceil_div(ceil_div(N, kWave), S);  // 64-point groups per part (at most)
 #define DVCP_FPS_PART(P, NT)                                                                                  \

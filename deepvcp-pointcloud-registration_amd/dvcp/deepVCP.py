@@ -44,19 +44,26 @@ def _warn_f16_autograd():
 
 
 class DeepVCP(nn.Module):
-    def __init__(self, use_normal, K=64, r=1.0, s=0.4, fe_npoint=10000, feat_dtype=torch.float32, dfe_literal=False):
+    def __init__(self, use_normal, K=64, r=1.0, s=0.4, fe_npoint=10000, feat_dtype=torch.float32, dfe_literal=False,
+                 fps_parts=None):
         """``feat_dtype``: storage of the target feature table the fused target stage gathers
         (torch.float16: BASELINE C5's "fp16 features", dvcp_dfe_tgt_f16; inference only -- the
         reference keeps fp32 features, so float16 is not reference precision).
         ``dfe_literal``: the fused target DFE chains fc1, fc2, fc3 as written (dvcp_dfe_tgt_literal,
         SURVEY App. A.3 Q14) instead of the collapsed 32x35 map (dvcp_dfe_tgt, the default: fc3.fc2.fc1
-        formed in fp64 and rounded once; the same within 1e-7 on the tests)."""
+        formed in fp64 and rounded once; the same within 1e-7 on the tests).
+        ``fps_parts``: workgroups per cloud of the feature extractor's FPS select rounds (1, 2, 4 or 8;
+        None: one, or DVCP_FPS_PARTS).  More workgroups shorten a lone batch's FPS chain (the split
+        select, csrc/fps.hip FpsPartArgs: the same indices); with many batches in flight they cost
+        CU time and their waits for each other's workgroups can starve, so one is the default
+        (DESIGN.md section 4.1, round 6)."""
         super().__init__()
         self.dfe_literal = bool(dfe_literal)
         if feat_dtype not in (torch.float32, torch.float16):
             raise ValueError(f"feat_dtype must be torch.float32 or torch.float16, got {feat_dtype}")
         self.feat_dtype = feat_dtype
         self.FE1 = feat_extraction_layer(use_normal=use_normal, npoint=fe_npoint)
+        self.FE1.fps_parts = fps_parts
         self.WL = weighting_layer()
         self.DFE = feat_embedding_layer()
         self.cpg = cpg()

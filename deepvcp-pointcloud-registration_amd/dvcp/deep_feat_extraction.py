@@ -33,6 +33,9 @@ class feat_extraction_layer(nn.Module):
         self.sa2 = PointNetSetAbstraction(**cfg[1])
         self.sa3 = PointNetSetAbstraction(**cfg[2])
         self.fc = nn.Linear(64, 32)
+        # workgroups per cloud of the FPS select rounds (None: ops.fps_parts, one unless
+        # DVCP_FPS_PARTS says otherwise); see DeepVCP(fps_parts=...)
+        self.fps_parts = None
 
     def fc_params(self, wl=None):
         lins = [self.fc] + ([wl.fc1[0], wl.fc2[0], wl.fc3[0]] if wl is not None else [])
@@ -68,7 +71,7 @@ class feat_extraction_layer(nn.Module):
                 centres += [c2, c3]
                 events += [ev, ev]
                 break
-            i, c = ops.fps(prev, sa.npoint, st.to(prev.device), pdim=2)
+            i, c = ops.fps(prev, sa.npoint, st.to(prev.device), pdim=2, parts=self.fps_parts)
             idxs.append(i)
             centres.append(c)
             ev = torch.cuda.Event()

@@ -30,14 +30,12 @@ FPS_PART_RANGE = (2048, 16384)
 
 
 def fps_parts(N, dtype=torch.float32):
-    """Workgroups per cloud of the select kernel for an N-point cloud (csrc/fps.hip fps_parts;
-    DVCP_FPS_PARTS overrides both): 4 above 8192 points, 2 from 4096, else 1."""
+    """Workgroups per cloud of the select kernel for an N-point cloud when the caller does not say
+    (csrc/fps.hip fps_parts): one, unless DVCP_FPS_PARTS (2, 4 or 8) asks for the split select."""
     if dtype != torch.float32 or not FPS_PART_RANGE[0] <= N <= FPS_PART_RANGE[1]:
         return 1
     forced = int(os.environ.get("DVCP_FPS_PARTS", "0") or 0)
-    if forced in (1, 2, 4, 8):
-        return forced
-    return 4 if N > 8192 else 2 if N >= 4096 else 1
+    return forced if forced in (1, 2, 4, 8) else 1
 
 
 def fps(xyz, npoint, start, pdim=1, parts=None):

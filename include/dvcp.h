@@ -53,10 +53,10 @@ int dvcp_fps(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int
 /* dvcp_fps with a B x N fp32 workspace, required when N exceeds the register-resident limit
  * (16384 fp32 / 8192 fp64 points per cloud).  Such clouds are split over ceil(N / 16384)
  * workgroups (8192 fp64) that exchange one argmax key per step through device-scope atomics.
- * fp32 clouds of 4096..16384 points use it too (ABI 4) where B x N x 4 bytes hold the exchange
- * slots: their select rounds run on 2 or 4 workgroups per cloud that exchange one candidate
- * list per round (the split select, csrc/fps.hip FpsPartArgs); without a workspace they take
- * the one-workgroup kernel.  Same indices either way.  err (optional int32, zeroed by the caller): set to 1 if a workgroup
+ * With DVCP_FPS_PARTS=2|4|8 in the environment, fp32 clouds of 2048..16384 points whose
+ * exchange slots fit in B x N x 4 bytes run their select rounds on that many workgroups per
+ * cloud, exchanging one candidate list per round (the split select, csrc/fps.hip FpsPartArgs;
+ * dvcp_fps_parts chooses per call).  Same indices either way.  err (optional int32, zeroed by the caller): set to 1 if a workgroup
  * gave up waiting for its peers (a guard; the indices then stay in range but are not FPS). */
 int dvcp_fps_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N,
                 int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz, float* ws,

@@ -147,7 +147,8 @@ int main(int argc, char** argv) {
       char* base = reinterpret_cast<char*>(dws);
       const dvcp::FpsPartArgs qa{dws, reinterpret_cast<uint32_t*>(base + w.slot_bytes),
                                  reinterpret_cast<uint32_t*>(base + w.slot_bytes + w.flag_bytes),
-                                 reinterpret_cast<int32_t*>(base + w.total - 8), c.S, B, (N + 1) / 2, dvcp::kFpsSpinCap};
+                                 reinterpret_cast<int32_t*>(base + w.total - 8), c.S, B, (N + 1) / 2, dvcp::kFpsSpinCap,
+                                 argc > 5 ? atoi(argv[5]) : 0};
       (void)capw;
       CK(hipMemset(dpp, 0, pprof_words * 8));
       float best = 1e30f;
