@@ -472,7 +472,11 @@ __device__ __forceinline__ T box_ub2(T cx, T cy, T cz, const T (&bx)[6]) {
 // (Round 5, measured and not kept: the update's x / y differences and squares as packed fp32 pairs,
 // v_pk_add_f32 / v_pk_mul_f32, 13 instead of 15 VALU per pair -- 2.99 -> 3.02 ms at 10000,
 // profiles/round5/r5bh_fps_pk.log.)
-// DVCP_FPS_IMIN: the running-minimum update as an integer min of the bit patterns (see fps_update)
+// DVCP_FPS_IMIN: the running-minimum update as an integer min of the bit patterns (see fps_update).
+// Non-finite coordinates are outside the parity contract: a NaN point keeps 1e10 in the reference
+// (NaN < m is false), which then picks it at every later step (its own distance never drops); the
+// select kernels certify prefixes on d(c, c) = 0 and diverge there, as does the integer min on a
+// NaN with the sign bit set (it is stored; the reference keeps m).  Callers pass finite clouds.
 #ifndef DVCP_FPS_IMIN
 #define DVCP_FPS_IMIN 1
 #endif
@@ -1282,6 +1286,12 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
         // layer 2 may repeat points (its centres are then not layer 2's points as a set): the gated
         // launch recomputes such a cloud
         if (consumer || !(gmax > 0.0f)) tied = true;
+        if constexpr (MODE == 1) {
+          // layer 2 repeating points: raise the cloud's flag now, not at the end, so a layer-3
+          // workgroup waiting for a pick number that will never come stops at its next poll
+          if (!consumer && !(gmax > 0.0f) && tid == 0)
+            __hip_atomic_fetch_or(pa.flag + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         break;
       }
       // ---- 3. list: entries in bins >= bsel are the candidates; T over the rest ---------------
@@ -1522,11 +1532,13 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
             for (;;) {  // layer 2 picks every point (else it flags the cloud): wait for this one
               v = __hip_atomic_load(pa.inv2 + static_cast<int64_t>(b) * N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               if (v & 0x80000000u) break;
-              __builtin_amdgcn_s_sleep(2);
-              if (++polls > kFpsPairSpinCap) {
+              // layer 2 flagged the cloud (it repeats points: this one may never be picked)
+              if (__hip_atomic_load(pa.flag + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+                  ++polls > kFpsPairSpinCap) {
                 s_gaveup = 1;
                 break;
               }
+              __builtin_amdgcn_s_sleep(2);
             }
             cpid[tid] = static_cast<int>(v & 0x7FFFFFFFu);
           }

@@ -265,3 +265,24 @@ def test_return_weights_and_paper_loss(cuda):
     assert torch.equal(w, torch.gather(tr["score"], 1, tr["topk"]))
     assert (w[:, 1:] <= w[:, :-1]).all() and (w > 0).all()
     assert torch.isfinite(loss) and (torch.linalg.det(Rp) > 0).all()
+
+
+def test_dfe_weight_change_between_eval_forwards(cuda):
+    """The packed DFE parameters are formed on the calling stream before the source-row DFE forks
+    to the side stream, and both DFE launches read that one buffer: after a DFE weight
+    changes between two eval forwards, the second forward equals a fresh model's with the new
+    weights, bit for bit (a stale or half-rebuilt pack would differ)."""
+    z = golden("e2e_c1")
+    model = _load_model(cuda, z)
+    _forward(cuda, model, z)  # builds and caches the pack
+    with torch.no_grad():
+        model.DFE.fc2.weight.mul_(1.5)
+        model.DFE.fc3.bias.add_(0.25)
+    _, kp1, vcp1, _, R1, t1 = _forward(cuda, model, z)
+    fresh = _load_model(cuda, z)
+    fresh.load_state_dict(model.state_dict())
+    _, kp2, vcp2, _, R2, t2 = _forward(cuda, fresh, z)
+    assert torch.equal(kp1, kp2) and torch.equal(vcp1, vcp2) and torch.equal(R1, R2) and torch.equal(t1, t2)
+    # and the change did reach the kernels: the pose moved against the fixture's weights
+    _, _, vcp0, _, _, _ = _forward(cuda, _load_model(cuda, z), z)
+    assert not torch.equal(vcp0, vcp1)
