@@ -87,6 +87,8 @@ def parse():
     p.add_argument("--inflight", type=int, default=10,
                    help="independent batches in flight (one stream each); 1 = strictly serial steps")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--lane-priority", choices=["default", "high"], default="default",
+                   help="stream priority of the in-flight batches' lanes (FPS chain + head)")
     p.add_argument("--hw-queues", type=int, default=24, help="GPU_MAX_HW_QUEUES for this process (<= 32)")
     p.add_argument("--stage-report", action="store_true", help="print the per-kernel table to stderr")
     p.add_argument("--no-kernel-events", action="store_true",
@@ -163,7 +165,9 @@ def main():
     condition_weights(model, feats=calib)
     t_init = torch.zeros(1, 3)
     torch.manual_seed(1)
-    lanes = [torch.cuda.Stream(device=dev) for _ in range(P)]
+    # lane streams (each batch's FPS chain and head); --lane-priority high puts them above the
+    # extractor's side streams (the set-abstraction tables), which keep the default priority
+    lanes = [torch.cuda.Stream(device=dev, priority=-1 if args.lane_priority == "high" else 0) for _ in range(P)]
 
     def step(lane=0):
         """One pass over one batch: DeepVCP.forward + deepVCP_loss, issued on the lane's stream."""

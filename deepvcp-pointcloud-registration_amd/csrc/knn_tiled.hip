@@ -28,7 +28,7 @@ constexpr int kBoxBatch = 1;          // tiles whose boxes are read (LDS) and te
 struct TiledLayout {
   float4* sorted;  // B x T*64: x, y, z, original index bits (padding: NaN, index 0x7FFFFFFF)
   float4* tbox;    // B x T x 2: {lo.xyz, _}, {hi.xyz, _}
-  int32_t* qperm;  // B x Q: query index by curve position
+  float4* qsorted;  // B x Q: the queries in curve order as (x, y, z, original index bits), fp32
   uint32_t* qbins;  // B x kSortBins: the queries' cell counts, then their running positions
   uint32_t* qbox;   // B x 8: ~float_order(lo.xyz), float_order(hi.xyz) of the queries (atomicMax)
 };
@@ -43,8 +43,8 @@ inline TiledLayout tiled_layout(void* ws, int B, int M, int Q) {
   p += align256(16 * int64_t(B) * T * kTile);
   L.tbox = reinterpret_cast<float4*>(p);
   p += align256(32 * int64_t(B) * T);
-  L.qperm = reinterpret_cast<int32_t*>(p);
-  p += align256(4 * int64_t(B) * Q);
+  L.qsorted = reinterpret_cast<float4*>(p);
+  p += align256(16 * int64_t(B) * Q);
   L.qbins = reinterpret_cast<uint32_t*>(p);  // qbins and qbox are one zeroed range
   L.qbox = L.qbins + int64_t(B) * kSortBins;
   return L;
@@ -154,16 +154,27 @@ __global__ __launch_bounds__(kBuildThreads) void knn_tiled_build_kernel(PointsVi
   __shared__ uint32_t boxk[kMaxTiles][6];  // order-preserving float keys: lo.xyz (min), hi.xyz (max)
   __shared__ uint32_t wsum[16];
   __shared__ float red[2][3][16];
-  const int b = blockIdx.y, tid = threadIdx.x;
-  if (blockIdx.x > 0) {  // the queries' scatter into curve order (the scanned bins are running positions)
-    const int i0 = (blockIdx.x - 1) * kQSortItems, i1 = min(Q, i0 + kQSortItems);
+  const int tid = threadIdx.x;
+  // With B % 8 == 0 the linear block id is re-mapped so that every block of cloud b runs on XCD
+  // b % 8 (blocks reach the XCDs round robin, speed only): the scatter's 16-byte rows of a cloud
+  // then meet in one L2 and leave it as whole lines (round 5's 4-byte index scatter from all eight
+  // XCDs wrote 34 MB per C3 launch for 2.7 MB of permutation).
+  int b = blockIdx.y, bx = blockIdx.x;
+  if ((gridDim.y & 7) == 0) {
+    const int lin = static_cast<int>(blockIdx.y * gridDim.x + blockIdx.x);
+    const int xo = lin & 7, slot = lin >> 3;
+    b = xo + 8 * (slot / static_cast<int>(gridDim.x));
+    bx = slot % static_cast<int>(gridDim.x);
+  }
+  if (bx > 0) {  // the queries' scatter into curve order (the scanned bins are running positions)
+    const int i0 = (bx - 1) * kQSortItems, i1 = min(Q, i0 + kQSortItems);
     const CurveGrid g = qry_grid(L.qbox, b);
     uint32_t* gb = L.qbins + static_cast<int64_t>(b) * kSortBins;
-    int32_t* qp = L.qperm + static_cast<int64_t>(b) * Q;
+    float4* qs = L.qsorted + static_cast<int64_t>(b) * Q;
     for (int i = i0 + tid; i < i1; i += kBuildThreads) {
       float v[3];
       qry_point(qry, b, i, v);
-      qp[atomicAdd(&gb[curve_cell(g, v)], 1u)] = i;
+      qs[atomicAdd(&gb[curve_cell(g, v)], 1u)] = make_float4(v[0], v[1], v[2], __int_as_float(i));
     }
     return;
   }
@@ -291,6 +302,14 @@ __device__ __forceinline__ uint32_t wave_umax_i(uint32_t v) {
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
 }
 
+// This lane's index, formed where it is used (an opaque v_mbcnt pair the compiler cannot hoist):
+// a lane-dependent value held across the select kernel's scan was its last scratch spill.
+__device__ __forceinline__ int knn_fresh_lane() {
+  int r;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(r));
+  return r;
+}
+
 // Bitonic sort (ascending) of 64*R keys held as keys[r] at position r*64 + lane.
 template <int R>
 __device__ __forceinline__ void wave_bitonic(uint32_t (&keys)[R]) {
@@ -330,9 +349,7 @@ __device__ __forceinline__ void wave_bitonic(uint32_t (&keys)[R]) {
 template <int KT, int R>
 __global__ __launch_bounds__(kTiledThreads) void knn_tiled_query_kernel(const float4* __restrict__ sorted,
                                                                         const float4* __restrict__ tbox,
-                                                                        const int32_t* __restrict__ qperm, int M,
-                                                                        const void* __restrict__ qry_raw,
-                                                                        int64_t qb, int64_t qc, int64_t qn, int qf64,
+                                                                        const float4* __restrict__ qsorted, int M,
                                                                         int Q, int k, float* __restrict__ dist,
                                                                         int32_t* __restrict__ idx,
                                                                         int64_t* __restrict__ idx64, int B8) {
@@ -359,19 +376,11 @@ __global__ __launch_bounds__(kTiledThreads) void knn_tiled_query_kernel(const fl
   const int sq = (bx * (kTiledThreads / kWave) + wave) * kWave + lane;
   if ((bx * (kTiledThreads / kWave) + wave) * kWave >= Q) return;  // whole wave past the end
   const bool live = sq < Q;
-  const int q = live ? qperm[static_cast<int64_t>(b) * Q + sq] : 0;
-  float qx, qy, qz;
-  if (qf64) {
-    const double* p = static_cast<const double*>(qry_raw);
-    qx = static_cast<float>(p[b * qb + 0 * qc + q * qn]);
-    qy = static_cast<float>(p[b * qb + 1 * qc + q * qn]);
-    qz = static_cast<float>(p[b * qb + 2 * qc + q * qn]);
-  } else {
-    const float* p = static_cast<const float*>(qry_raw);
-    qx = p[b * qb + 0 * qc + q * qn];
-    qy = p[b * qb + 1 * qc + q * qn];
-    qz = p[b * qb + 2 * qc + q * qn];
-  }
+  // this lane's query in curve order: one coalesced 16-byte row (converted to fp32 by the scatter,
+  // knn_cuda's .float())
+  const float4 qrow = live ? qsorted[static_cast<int64_t>(b) * Q + sq] : make_float4(0.f, 0.f, 0.f, 0.f);
+  [[maybe_unused]] const int q = __float_as_int(qrow.w);
+  const float qx = qrow.x, qy = qrow.y, qz = qrow.z;
   // the wave's query box (live lanes only)
   float wl[3] = {live ? qx : __builtin_huge_valf(), live ? qy : __builtin_huge_valf(),
                  live ? qz : __builtin_huge_valf()};
@@ -597,9 +606,8 @@ __device__ __forceinline__ void key_ce(uint32_t& ah, uint32_t& al, uint32_t& bh,
 template <int R>
 __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3))) void knn_sel_query_kernel(const float4* __restrict__ sorted,
                                                                       const float4* __restrict__ tbox,
-                                                                      const int32_t* __restrict__ qperm, int M,
-                                                                      const void* __restrict__ qry_raw, int64_t qb,
-                                                                      int64_t qc, int64_t qn, int qf64, int Q, int k,
+                                                                      const float4* __restrict__ qsorted, int M,
+                                                                      int Q, int k,
                                                                       float* __restrict__ dist,
                                                                       int32_t* __restrict__ idx,
                                                                       int64_t* __restrict__ idx64, int B8) {
@@ -627,22 +635,21 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
     for (int i = threadIdx.x; i < T; i += kTiledThreads) hbox[i] = pack_hbox(tbg[2 * i], tbg[2 * i + 1]);
     __syncthreads();
   }
-  const int sq = (bx * (kTiledThreads / kWave) + wave) * kWave + lane;
-  if ((bx * (kTiledThreads / kWave) + wave) * kWave >= Q) return;  // whole wave past the end
+  // the wave's first curve position (wave-uniform) and this lane's
+  const int sq0 = __builtin_amdgcn_readfirstlane((bx * (kTiledThreads / kWave) + wave) * kWave);
+  const int sq = sq0 + lane;
+  if (sq0 >= Q) return;  // whole wave past the end
   const bool live = sq < Q;
-  const int q = live ? qperm[static_cast<int64_t>(b) * Q + sq] : 0;
-  float qx, qy, qz;
-  if (qf64) {
-    const double* p = static_cast<const double*>(qry_raw);
-    qx = static_cast<float>(p[b * qb + 0 * qc + q * qn]);
-    qy = static_cast<float>(p[b * qb + 1 * qc + q * qn]);
-    qz = static_cast<float>(p[b * qb + 2 * qc + q * qn]);
-  } else {
-    const float* p = static_cast<const float*>(qry_raw);
-    qx = p[b * qb + 0 * qc + q * qn];
-    qy = p[b * qb + 1 * qc + q * qn];
-    qz = p[b * qb + 2 * qc + q * qn];
-  }
+  // this lane's query in curve order: one coalesced 16-byte row (converted to fp32 by the scatter,
+  // knn_cuda's .float())
+  const float4 qrow = live ? qsorted[static_cast<int64_t>(b) * Q + sq] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float qx = qrow.x, qy = qrow.y, qz = qrow.z;
+  // the query's output row index, re-read from its curve row where the rows are written (held
+  // across the scan, it and the position were spilled)
+  auto out_row = [&]() {
+    const int sqn = sq0 + knn_fresh_lane();
+    return __float_as_int(qsorted[static_cast<int64_t>(b) * Q + sqn].w);
+  };
   float wl[3] = {live ? qx : __builtin_huge_valf(), live ? qy : __builtin_huge_valf(),
                  live ? qz : __builtin_huge_valf()};
   float wh[3] = {live ? qx : -__builtin_huge_valf(), live ? qy : -__builtin_huge_valf(),
@@ -949,7 +956,7 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
     if (dist && idx && !idx64 && k == KT) {
       // each lane writes its own 128-B rows as eight 16-byte stores (whole lines per lane)
       if (!live) return;
-      const int qo = qperm[static_cast<int64_t>(b) * Q + sq];  // (re-read, not held)
+      const int qo = out_row();
       float4* dr = reinterpret_cast<float4*>(dist + (static_cast<int64_t>(b) * Q + qo) * 32);
       int4* ir = reinterpret_cast<int4*>(idx + (static_cast<int64_t>(b) * Q + qo) * 32);
 #pragma unroll
@@ -976,7 +983,7 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
       // from the lanes, every store instruction touches 64 lines with 4 bytes each.  Instead the
       // rows go through the wave's candidate buffer in LDS, 32 at a time, and eight lanes store a
       // row as 16-byte pieces: each instruction writes eight whole lines.
-      const int qo = live ? qperm[static_cast<int64_t>(b) * Q + sq] : -1;  // (re-read, not held)
+      const int qo = live ? out_row() : -1;
       float* stage = reinterpret_cast<float*>(sbuf[wave]);             // 32 rows x 33 (4.2 KB of 8)
 #pragma unroll
       for (int part = 0; part < 2; ++part) {      // 0: distances, 1: indices
@@ -1014,7 +1021,7 @@ __global__ __launch_bounds__(kTiledThreads) __attribute__((amdgpu_waves_per_eu(3
 #endif
   if (!live) return;
   // the query's output row (its index re-read: held across the scan it was spilled)
-  const int qo = qperm[static_cast<int64_t>(b) * Q + sq];
+  const int qo = out_row();
   const int64_t o = (static_cast<int64_t>(b) * Q + qo) * k;
 #ifdef DVCP_KNN_DIAG
   if (lane == 0 && dist && k == 32) {
@@ -1048,7 +1055,7 @@ extern "C" int64_t dvcp_knn_tiled_workspace_bytes(int B, int M, int Q) {
   if (B < 0 || M < 0 || Q < 0) return -1;
   const int64_t T = dvcp::ceil_div(M, dvcp::kTile);
   return dvcp::align256(16 * int64_t(B) * T * dvcp::kTile) + dvcp::align256(32 * int64_t(B) * T) +
-         dvcp::align256(4 * int64_t(B) * Q) + dvcp::align256(dvcp::tiled_zeroed_bytes(B));
+         dvcp::align256(16 * int64_t(B) * Q) + dvcp::align256(dvcp::tiled_zeroed_bytes(B));
 }
 
 static int knn_tiled_impl(int dtype, const void* ref, int64_t rb, int64_t rc, int64_t rn, int M, const void* qry,
@@ -1086,14 +1093,13 @@ static int knn_tiled_impl(int dtype, const void* ref, int64_t rb, int64_t rc, in
   }
   if (int e = dvcp::launch_status("dvcp_knn_tiled(build)")) return e;
   const int T = dvcp::ceil_div(M, dvcp::kTile);
-  const int qf64 = dtype == DVCP_F64;
   dim3 grid(dvcp::ceil_div(Q, dvcp::kTiledThreads), B);
   const int xcd = B % 8 == 0 ? 1 : 0;  // XCD-aware cloud mapping (equal clouds per XCD)
   // k = 17..32 (the forward's 32): the buffered-selection kernel
 #define DVCP_KNNS(RR)                                                                                             \
   if (k > 16 && T <= 64 * RR) {                                                                                   \
     hipLaunchKernelGGL((dvcp::knn_sel_query_kernel<RR>), grid, dim3(dvcp::kTiledThreads), 0, st, L.sorted,         \
-                       L.tbox, L.qperm, M, qry, qb, qc, qn, qf64, Q, k, dist, idx, idx64, xcd);                   \
+                       L.tbox, L.qsorted, M, Q, k, dist, idx, idx64, xcd);                                         \
     return dvcp::launch_status("dvcp_knn_tiled(select)");                                                         \
   }
   if (!insertion) {
@@ -1107,7 +1113,7 @@ static int knn_tiled_impl(int dtype, const void* ref, int64_t rb, int64_t rc, in
 #define DVCP_KNNT(KK, RR)                                                                                          \
   if (k <= KK && T <= 64 * RR) {                                                                                   \
     hipLaunchKernelGGL((dvcp::knn_tiled_query_kernel<KK, RR>), grid, dim3(dvcp::kTiledThreads), 0, st, L.sorted,   \
-                       L.tbox, L.qperm, M, qry, qb, qc, qn, qf64, Q, k, dist, idx, idx64, xcd);                                                                                \
+                       L.tbox, L.qsorted, M, Q, k, dist, idx, idx64, xcd);                                          \
     return dvcp::launch_status("dvcp_knn_tiled(query)");                                                           \
   }
   DVCP_KNNT(1, 1)
