@@ -87,6 +87,9 @@ def parse():
     p.add_argument("--inflight", type=int, default=10,
                    help="independent batches in flight (one stream each); 1 = strictly serial steps")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--graphs", choices=["on", "off"], default="on",
+                   help="replay each lane's step as a captured HIP graph (dvcp.graphs.CapturedStep) or issue it "
+                        "eagerly, one Python + ctypes call per kernel")
     p.add_argument("--lane-priority", choices=["default", "high"], default="default",
                    help="stream priority of the in-flight batches' lanes (FPS chain + head)")
     p.add_argument("--hw-queues", type=int, default=24, help="GPU_MAX_HW_QUEUES for this process (<= 32)")
@@ -169,7 +172,11 @@ def main():
     # extractor's side streams (the set-abstraction tables), which keep the default priority
     lanes = [torch.cuda.Stream(device=dev, priority=-1 if args.lane_priority == "high" else 0) for _ in range(P)]
 
-    def step(lane=0):
+    def rows(Rp, tp, rot, trans):
+        # per pair: R (9), t (3), rotation error (deg), translation error -> (B, 14)
+        return torch.cat([Rp.reshape(B, 9), tp.reshape(B, 3), rot.reshape(B, 1), trans.reshape(B, 1)], 1)
+
+    def step_eager(lane=0):
         """One pass over one batch: DeepVCP.forward + deepVCP_loss, issued on the lane's stream."""
         b_src, b_tgt, b_R, b_t = batches[lane]
         starts = plan.starts(model, N)   # this rank's columns of the global batch's draw
@@ -177,8 +184,26 @@ def main():
             kp, vcp = model(b_src, b_tgt, b_R, t_init, starts=starts)
             loss, Rp, tp = dvcp.deepVCP_loss(kp, vcp, b_R, b_t, 0.5)
             rot, trans = dvcp.registration_errors(Rp, tp, b_R, b_t)  # train.py:112-120 harness
-        return Rp, tp, rot, trans
+            return rows(Rp, tp, rot, trans)
 
+    graphs = None
+
+    def step_graph(lane=0):
+        """The same step replayed from the lane's captured graph (dvcp.graphs.CapturedStep): one
+        host call for the whole dependency graph; the rows are copied out on the lane's stream."""
+        starts = plan.starts(model, N)
+        out = graphs[lane].replay(starts)
+        with torch.cuda.stream(lanes[lane]):
+            return rows(*out)
+
+    def step(lane=0):
+        return step_graph(lane) if graphs is not None else step_eager(lane)
+
+    if args.graphs == "on":
+        # one captured graph per lane (after an eager warm-up inside CapturedStep)
+        from dvcp.graphs import CapturedStep
+        graphs = [CapturedStep(model, *batches[ln], alpha=0.5, stream=lanes[ln], starts=plan.starts(model, N))
+                  for ln in range(P)]
     # warmup, and the single-batch latency (strictly serial steps on one stream)
     for _ in range(args.warmup):
         step()
@@ -194,7 +219,7 @@ def main():
     if world > 1:
         dist.barrier()
 
-    _lib.EVENT_LOG = None if args.no_kernel_events else []
+    _lib.EVENT_LOG = None if (args.no_kernel_events or graphs is not None) else []
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     outs = [step(i % P) for i in range(args.steps)]
@@ -202,9 +227,7 @@ def main():
     cur = torch.cuda.current_stream(dev)
     for ln in lanes:
         cur.wait_stream(ln)
-    # per pair: R (9), t (3), rotation error (deg), translation error -> (steps*B, 14)
-    res = torch.cat([torch.cat([o[0].reshape(B, 9), o[1].reshape(B, 3), o[2].reshape(B, 1), o[3].reshape(B, 1)], 1)
-                     for o in outs])
+    res = torch.cat(outs)   # (steps * B, 14)
     if world > 1 and args.dist_backend == "gloo":
         res = res.cpu()   # gloo gathers host tensors (rehearsal only; RCCL gathers in HBM)
     res = D.gather_results(res, world)      # the one collective: RCCL all_gather of the rows
@@ -216,13 +239,22 @@ def main():
     elapsed = D.max_over_ranks(elapsed, dev if args.dist_backend == "nccl" else torch.device("cpu"))
 
     # ---- per-kernel HIP-event timing (events on the stream each kernel is launched on) --------
-    # (1) live over the timed region, 8 batches in flight: per-launch durations under contention
+    # (1) live over the timed region, the batches in flight: per-launch durations under contention
+    #     (graph replays carry no per-kernel events: then an eager pass of the same steps after it)
+    if graphs is not None and not args.no_kernel_events:
+        graphs_keep, graphs = graphs, None
+        _lib.EVENT_LOG = []
+        for i in range(args.steps):
+            step(i % P)
+        torch.cuda.synchronize()
+        log, _lib.EVENT_LOG = _lib.EVENT_LOG, None
+        graphs = graphs_keep
     live = _per_kernel(log)
     # (2) isolated: the same step with one batch in flight (a few steps on lane 0, after the timed
     #     region), for the per-stage roofline; (3) the FPS step floor probe
     _lib.EVENT_LOG = []
     for _ in range(args.iso_steps):
-        step(0)
+        step_eager(0)
         torch.cuda.synchronize()
     iso, _lib.EVENT_LOG = _per_kernel(_lib.EVENT_LOG), None
     floor_us = fps_step_floor_us(dev)
@@ -232,11 +264,11 @@ def main():
     if args.fps_parts_latency and args.config == "c3":
         model.FE1.fps_parts = args.fps_parts_latency
         for _ in range(2):
-            step()
+            step_eager()
         torch.cuda.synchronize()
         t_ls = time.perf_counter()
         for _ in range(2):
-            step()
+            step_eager()
         torch.cuda.synchronize()
         lat_split = {"parts": args.fps_parts_latency, "ms": round((time.perf_counter() - t_ls) / 2 * 1e3, 3)}
         model.FE1.fps_parts = None
@@ -280,7 +312,9 @@ def main():
                           "collapsed, fp16 feature table (dvcp_dfe_tgt_f16)",
                    "sa_layer1": "per-point split: W1f.f + b1 once per point, W1x.(p - c) per grouped row (exact in "
                                 "real arithmetic; held to the fp32 bars)",
-                   "fps": f"select rounds on {model.FE1.fps_parts or _fps_parts_label(N)} workgroup(s) per cloud"},
+                   "fps": f"select rounds on {model.FE1.fps_parts or _fps_parts_label(N)} workgroup(s) per cloud",
+                   "issue": ("each lane's step replayed from a captured HIP graph (dvcp.graphs.CapturedStep)"
+                             if args.graphs == "on" else "eager: one Python + ctypes call per kernel")},
         "latency_ms_single_batch": round(latency_ms, 3),
         "latency_ms_single_batch_split_fps": lat_split,
         "host_issue_ms_per_step": round(t_issue / args.steps * 1e3, 3),

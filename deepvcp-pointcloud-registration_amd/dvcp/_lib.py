@@ -207,9 +207,20 @@ def call(name, *args, work=None):
 # each is copied to pinned host memory behind an event; ``check_device_flags`` raises for any
 # whose event has completed with a nonzero word (block=True waits for all of them).
 _PENDING_FLAGS = []
+# While a step is captured into a graph (dvcp/graphs.py) the error words are collected here
+# instead (a host copy and an event query cannot run inside a capture); the graph's owner checks
+# them after each replay.
+_CAPTURED_FLAGS = None
+
+
+def _capturing():
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
 
 
 def defer_flag_check(what, flag):
+    if _CAPTURED_FLAGS is not None and _capturing():
+        _CAPTURED_FLAGS.append((what, flag))
+        return
     host = torch.empty(flag.shape, dtype=flag.dtype, pin_memory=True)
     host.copy_(flag, non_blocking=True)
     ev = torch.cuda.Event()
@@ -220,6 +231,8 @@ def defer_flag_check(what, flag):
 def check_device_flags(block=False):
     """Raise RuntimeError for a completed launch whose error word is set (see defer_flag_check)."""
     global _PENDING_FLAGS
+    if _capturing():
+        return
     keep, failed = [], None
     for what, ev, host in _PENDING_FLAGS:
         if block:

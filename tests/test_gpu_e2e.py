@@ -286,3 +286,33 @@ def test_dfe_weight_change_between_eval_forwards(cuda):
     # and the change did reach the kernels: the pose moved against the fixture's weights
     _, _, vcp0, _, _, _ = _forward(cuda, _load_model(cuda, z), z)
     assert not torch.equal(vcp0, vcp1)
+
+
+def test_captured_step_equals_eager(cuda):
+    """dvcp.graphs.CapturedStep: the forward + pose solve + registration error captured once as a
+    HIP graph and replayed with new FPS starts equals the eager step with those starts, bit for bit
+    (two replays with different starts; the graph's error words are checked after each)."""
+    import dvcp
+    from dvcp import _lib
+    from dvcp.graphs import CapturedStep
+    z = golden("e2e_c1")
+    model = _load_model(cuda, z)
+    src, tgt = torch.from_numpy(z["src"]).to(cuda), torch.from_numpy(z["tgt"]).to(cuda)
+    R_gt, t_gt = torch.from_numpy(z["R_gt"]).to(cuda), torch.from_numpy(z["t_gt"]).to(cuda)
+    B = src.shape[0]
+    g = CapturedStep(model, src, tgt, R_gt, t_gt, alpha=0.5, starts=torch.from_numpy(z["starts"]))
+    gen = torch.Generator().manual_seed(77)
+    for _ in range(2):
+        sizes = (src.shape[2], model.FE1.sa1.npoint, model.FE1.sa2.npoint, model.K, tgt.shape[2],
+                 model.FE1.sa1.npoint, model.FE1.sa2.npoint)
+        starts = torch.stack([torch.randint(0, n, (B,), generator=gen) for n in sizes])
+        R, t, rot, trans = g.replay(starts)
+        torch.cuda.synchronize()
+        R, t, rot, trans = R.clone(), t.clone(), rot.clone(), trans.clone()
+        with torch.no_grad():
+            kp, vcp = model(src, tgt, R_gt, torch.zeros(1, 3), starts=starts)
+            _, R2, t2 = dvcp.deepVCP_loss(kp, vcp, R_gt, t_gt, 0.5)
+            rot2, trans2 = dvcp.registration_errors(R2, t2, R_gt, t_gt)
+        assert torch.equal(R, R2) and torch.equal(t, t2)
+        assert torch.equal(rot, rot2) and torch.equal(trans, trans2)
+    _lib.check_device_flags(block=True)
