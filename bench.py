@@ -87,15 +87,18 @@ def parse():
     p.add_argument("--inflight", type=int, default=10,
                    help="independent batches in flight (one stream each); 1 = strictly serial steps")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--graphs", choices=["on", "off"], default="on",
-                   help="replay each lane's step as a captured HIP graph (dvcp.graphs.CapturedStep) or issue it "
-                        "eagerly, one Python + ctypes call per kernel")
+    p.add_argument("--graphs", choices=["on", "off"], default="off",
+                   help="replay each lane's step as a captured HIP graph (dvcp.graphs.CapturedStep) instead of "
+                        "issuing it eagerly, one Python + ctypes call per kernel.  Off by default: on this ROCm the "
+                        "replay ran the FPS chain and the side stream's tables one after the other (single-batch "
+                        "latency 13.4 -> 22.3 ms, 2278 -> 2034 pairs/s; profiles/round6/r6k_*)")
     p.add_argument("--lane-priority", choices=["default", "high"], default="default",
                    help="stream priority of the in-flight batches' lanes (FPS chain + head)")
     p.add_argument("--hw-queues", type=int, default=24, help="GPU_MAX_HW_QUEUES for this process (<= 32)")
     p.add_argument("--stage-report", action="store_true", help="print the per-kernel table to stderr")
     p.add_argument("--no-kernel-events", action="store_true",
-                   help="diagnostic: no per-launch HIP events in the timed region")
+                   help="skip the eager pass that times every launch at the run's concurrency (live_launch_ms); "
+                        "the timed region never carries per-launch events")
     p.add_argument("--iso-steps", type=int, default=3,
                    help="steps timed per kernel with one batch in flight (stage roofline)")
     p.add_argument("--cpu-pairs", type=int, default=3,
@@ -219,7 +222,7 @@ def main():
     if world > 1:
         dist.barrier()
 
-    _lib.EVENT_LOG = None if (args.no_kernel_events or graphs is not None) else []
+    _lib.EVENT_LOG = None   # (per-kernel events: a separate eager pass after the timed region)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     outs = [step(i % P) for i in range(args.steps)]
@@ -233,7 +236,7 @@ def main():
     res = D.gather_results(res, world)      # the one collective: RCCL all_gather of the rows
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    log, _lib.EVENT_LOG = _lib.EVENT_LOG or [], None
+    log = []
     if world > 1:
         dist.barrier()
     elapsed = D.max_over_ranks(elapsed, dev if args.dist_backend == "nccl" else torch.device("cpu"))
@@ -241,7 +244,10 @@ def main():
     # ---- per-kernel HIP-event timing (events on the stream each kernel is launched on) --------
     # (1) live over the timed region, the batches in flight: per-launch durations under contention
     #     (graph replays carry no per-kernel events: then an eager pass of the same steps after it)
-    if graphs is not None and not args.no_kernel_events:
+    #     The timed region itself carries no per-kernel events (two HIP events per launch were about
+    #     half of its host issue time); this eager pass of the same steps at the same concurrency
+    #     times every launch.
+    if not args.no_kernel_events:
         graphs_keep, graphs = graphs, None
         _lib.EVENT_LOG = []
         for i in range(args.steps):

@@ -127,6 +127,11 @@ class feat_extraction_layer(nn.Module):
         # reads sa3's rows the same way (dvcp_fe_head_rows).  Training (``saved``) keeps the
         # gathered tables, which its backward consumes.
         fold = saved is None and not train_bn
+        if side is not main:
+            # the side stream reads the input points (and, for a per-point first layer, before any
+            # FPS event): order it after the main stream's work so far (the 2B-cloud cat of
+            # extract_features, a caller's uploads); this also joins it to a graph capture
+            side.wait_stream(main)
         with torch.cuda.stream(side):
             pts_l, f = xyz, feat
             f_rows = None  # (per-point table (B, Nf, C), FPS indices (B, n_l)): f is that gather
