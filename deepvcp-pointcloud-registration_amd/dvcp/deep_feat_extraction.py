@@ -114,6 +114,14 @@ class feat_extraction_layer(nn.Module):
         layers = (self.sa1, self.sa2, self.sa3)
         main = torch.cuda.current_stream()
         side = side_stream if side_stream is not None else main
+        if side is not main:
+            # the side stream reads the input points (for a per-point first layer before any FPS
+            # event): it starts after the main stream's work so far (the 2B-cloud cat of
+            # extract_features, a caller's uploads) -- not after the FPS chain enqueued next.  This
+            # also joins it to a graph capture.
+            ready = torch.cuda.Event()
+            ready.record(main)
+            side.wait_event(ready)
         if fps is not None:  # launched ahead on another stream (launch_fps)
             idxs, centres, events = fps
             for i, c in zip(idxs, centres):  # (the side stream waits for each layer's event)
@@ -127,11 +135,6 @@ class feat_extraction_layer(nn.Module):
         # reads sa3's rows the same way (dvcp_fe_head_rows).  Training (``saved``) keeps the
         # gathered tables, which its backward consumes.
         fold = saved is None and not train_bn
-        if side is not main:
-            # the side stream reads the input points (and, for a per-point first layer, before any
-            # FPS event): order it after the main stream's work so far (the 2B-cloud cat of
-            # extract_features, a caller's uploads); this also joins it to a graph capture
-            side.wait_stream(main)
         with torch.cuda.stream(side):
             pts_l, f = xyz, feat
             f_rows = None  # (per-point table (B, Nf, C), FPS indices (B, n_l)): f is that gather
