@@ -13,6 +13,8 @@
 //     fps_dense_kernel.
 // Every kernel keeps each cloud's coordinates and running minima in VGPRs (Morton-sorted for the
 // first two), so the loop touches no global memory except the output stores.
+#include <type_traits>
+
 #include "common.h"
 
 namespace dvcp {
@@ -534,6 +536,11 @@ __device__ __forceinline__ float fps_update(float m, T px, T py, T pz, T cx, T c
 // on (four waves per SIMD hide the load).  Round 5, tools/fps_lab A/B on one box
 // (profiles/round5/r5bc_fps_acc4.log): 16384 -> 10000 5.20 -> 4.81 ms, 10000 -> 10000 (1024 x 10)
 // 3.25 -> 3.09 ms, 16 clouds, identical indices.
+// DVCP_FPS_RECERT: a round whose first pass stops early ranks the candidates left a second time
+// (step 5b); 0 = one pass per round
+#ifndef DVCP_FPS_RECERT
+#define DVCP_FPS_RECERT 1
+#endif
 #ifndef DVCP_FPS_ACC4
 #define DVCP_FPS_ACC4 1
 #endif
@@ -683,6 +690,9 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
   // (bits 0-15) + count of waves with a toucher (bits 16+); phase 5 reads one word per candidate
   // instead of one per wave (it ran on every wave, 4 per SIMD, with W reads each)
   __shared__ uint32_t srank[kSelMax];
+  __shared__ uint32_t srank2[DVCP_FPS_RECERT ? kSelMax : 1];                   // the second pass's ranks
+  __shared__ __attribute__((aligned(16))) float cvv2[DVCP_FPS_RECERT ? kSelMax : 4];  // its values
+  __shared__ float vpart[DVCP_FPS_RECERT ? THREADS : 1];  // their partial minima (THREADS / 128 centre strides)
   __shared__ float wtf[W];
   // T_f and T (non-negative floats as bits) reduced over the waves by LDS atomicMax: every wave
   // reads one word instead of W
@@ -1350,6 +1360,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
       // (tools/fps_lab/fps_round_sim.py, a CPU model of this round logic; FPS lab: 81 of 382).
       if (na < 4u * static_cast<uint32_t>(seltarget)) f *= 0.9f;
       if (wave * kWave < kSelMax) srank[wave * kWave + lane] = 0u;  // (read last by the previous round)
+      if (DVCP_FPS_RECERT && wave * kWave < kSelMax) srank2[wave * kWave + lane] = 0u;
       if constexpr (MODE == 3) {  // ---- MODE 3, step 2: the other parts' granules of the round ------
         tick(1);
         part_gather();
@@ -1416,14 +1427,20 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
       bool repaired = false;
       int rk[2];
       bool eqp[2] = {false, false};
-      auto rank_decide = [&]() {  // phases 4 and 5's decision (twice in a re-ranked round)
+      int koff = 0, nreal2 = 0;  // the second pass: centres accepted before it, its candidates
+      // phases 4 and 5's decision (twice in a re-ranked round).  P2: the second pass over the
+      // candidates left (values cvv2 > T, ranks in srank2, ranks offset by koff)
+      auto rank_decide = [&](auto p2c) {
+      constexpr bool P2 = decltype(p2c)::value;
+      float* const cv = P2 ? cvv2 : cvv;
+      uint32_t* const sr = P2 ? srank2 : srank;
       {
         const int i_lo = wave * (kSelMax / W);
         int r0 = 0, r1 = 0, t0 = 0, t1 = 0;
         int e0 = 0, e1 = 0;  // MODE 1: c_j has an equal-valued predecessor (bits 24+ of srank)
         if (i_lo < cnt) {  // wave-uniform
           const int j0 = lane, j1 = lane + kWave;
-          const float v0 = cvv[j0], v1 = cvv[j1];
+          const float v0 = cv[j0], v1 = cv[j1];
           const int p0 = cpid[j0], p1 = cpid[j1];
           const T x0 = cxx[j0], y0 = cyy[j0], z0 = czz[j0];
           const T x1 = cxx[j1], y1 = cyy[j1], z1 = czz[j1];
@@ -1433,9 +1450,11 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
           for (int c4 = 0; c4 < kSelMax / W / 4; ++c4) {
             const int i0 = i_lo + 4 * c4;
             if (i0 >= cnt) break;  // wave-uniform
-            const float4 v4 = *reinterpret_cast<const float4*>(&cvv[i0]);
+            const float4 v4 = *reinterpret_cast<const float4*>(&cv[i0]);
             // MODE 3: a part's unused slots (v = -1) follow its candidates; skip all-unused batches
-            if (MODE == 3 && v4.x < 0.0f) continue;  // (wave-uniform)
+            // (P2: batches with no candidate left)
+            if (P2 ? !(fmaxf(fmaxf(v4.x, v4.y), fmaxf(v4.z, v4.w)) > Tb) : (MODE == 3 && v4.x < 0.0f))
+              continue;  // (wave-uniform)
             const int4 p4 = *reinterpret_cast<const int4*>(&cpid[i0]);
             const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
             const int pp[4] = {p4.x, p4.y, p4.z, p4.w};
@@ -1448,7 +1467,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-              const bool in = MODE == 3 ? vv[k] >= 0.0f : i0 + k < cnt;
+              const bool in = P2 ? vv[k] > Tb : MODE == 3 ? vv[k] >= 0.0f : i0 + k < cnt;
               const bool b0 = in & ((vv[k] > v0) | ((vv[k] == v0) & (pp[k] < p0)));
               const bool b1 = in & ((vv[k] > v1) | ((vv[k] == v1) & (pp[k] < p1)));
               const T ax = x0 - xx[k], ay = y0 - yy[k], az = z0 - zz[k];
@@ -1467,41 +1486,44 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
           }
         }
         if (i_lo < cnt) {  // wave-uniform
-          if (MODE == 3) {  // (unused slots take no rank)
-            r0 = cvv[lane] >= 0.0f ? r0 : 0;
-            t0 = cvv[lane] >= 0.0f ? t0 : 0;
-            r1 = cvv[lane + kWave] >= 0.0f ? r1 : 0;
-            t1 = cvv[lane + kWave] >= 0.0f ? t1 : 0;
+          if (MODE == 3 || P2) {  // (unused slots take no rank; P2: nor the candidates not left)
+            const bool in0 = P2 ? cv[lane] > Tb : cv[lane] >= 0.0f;
+            const bool in1 = P2 ? cv[lane + kWave] > Tb : cv[lane + kWave] >= 0.0f;
+            r0 = in0 ? r0 : 0;
+            t0 = in0 ? t0 : 0;
+            r1 = in1 ? r1 : 0;
+            t1 = in1 ? t1 : 0;
           }
-          if (r0 | t0 | e0) atomicAdd(&srank[lane], static_cast<uint32_t>(r0 | (t0 << 16) | (e0 << 24)));
-          if (r1 | t1 | e1) atomicAdd(&srank[lane + kWave], static_cast<uint32_t>(r1 | (t1 << 16) | (e1 << 24)));
+          if (r0 | t0 | e0) atomicAdd(&sr[lane], static_cast<uint32_t>(r0 | (t0 << 16) | (e0 << 24)));
+          if (r1 | t1 | e1) atomicAdd(&sr[lane + kWave], static_cast<uint32_t>(r1 | (t1 << 16) | (e1 << 24)));
         }
       }
       lds_barrier();
       tick(2);
       // ---- 5. k = the smallest rank that fails; accepted = ranks < k (every wave, redundantly) ----
       if (tid == 0) tb_max = 0u;  // every wave read T before the phase-4 barrier
-      const int left = npoint - step;
+      const int left = npoint - step - (P2 ? koff : 0);
       eqp[0] = eqp[1] = false;
       uint32_t failr = 0xFFFFFFFFu;
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const int jj = hh * 64 + lane;
         rk[hh] = 0x7FFFFFFF;
-        if (jj < cnt && (MODE != 3 || cvv[jj] >= 0.0f)) {  // (MODE 3: unused slots are no candidates)
-          const uint32_t e = srank[jj];
+        // (MODE 3: unused slots are no candidates; P2: only those left)
+        if (jj < cnt && (P2 ? cv[jj] > Tb : (MODE != 3 || cv[jj] >= 0.0f))) {
+          const uint32_t e = sr[jj];
           const int r = static_cast<int>(e & 0xFFFFu);
           const bool touched = MODE == 1 ? ((e >> 16) & 0xFFu) != 0u : (e >> 16) != 0u;
           if constexpr (MODE == 1) eqp[hh] = (e >> 24) != 0u;
           rk[hh] = r;
-          const bool fail = r >= left || (r > 0 && (touched || !(cvv[jj] > Tb)));
+          const bool fail = r >= left || (r > 0 && (touched || !(cv[jj] > Tb)));
           failr = fail ? min(failr, static_cast<uint32_t>(r)) : failr;
         }
       }
-      kstar = static_cast<int>(min(min(wave_umin(failr), static_cast<uint32_t>(nreal)),
-                                   static_cast<uint32_t>(kSelAccept)));
+      kstar = static_cast<int>(min(min(wave_umin(failr), static_cast<uint32_t>(P2 ? nreal2 : nreal)),
+                                   static_cast<uint32_t>(kSelAccept - (P2 ? koff : 0))));
       };
-      rank_decide();
+      rank_decide(std::false_type{});
       if constexpr (MODE == 1) {
         // Ties (layer 3).  Values only drop and unlisted ones stay below every listed one, so a
         // step's argmax can only tie with listed candidates of the same round-start value, and
@@ -1550,27 +1572,50 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
           }
           repaired = true;
           ++n_repair;
-          rank_decide();
+          rank_decide(std::false_type{});
 #if DVCP_FPS_PAIR_DIAG == 3
           rep_clk += fps_clock() - t_rep;
 #endif
         }
       }
       // the accepted centres in rank order, for the update: every wave writes the same values
-      // (its own reads below follow its own writes in LDS order)
+      // (its own reads below follow its own writes in LDS order); wave 0 of part 0 writes the
+      // outputs.  base: the ranks' offset (the second pass's follow the first's)
+      auto accept = [&](int base) {
 #pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const int jj = hh * 64 + lane;
-        if (rk[hh] < kstar) {
+        for (int hh = 0; hh < 2; ++hh) {
+          const int jj = hh * 64 + lane;
+          if (rk[hh] < kstar) {
 #if DVCP_FPS_ACC4
-          acc4[rk[hh]] = AccC{cxx[jj], cyy[jj], czz[jj], static_cast<T>(0)};
+            acc4[base + rk[hh]] = AccC{cxx[jj], cyy[jj], czz[jj], static_cast<T>(0)};
 #else
-          acx[rk[hh]] = cxx[jj];
-          acy[rk[hh]] = cyy[jj];
-          acz[rk[hh]] = czz[jj];
+            acx[base + rk[hh]] = cxx[jj];
+            acy[base + rk[hh]] = cyy[jj];
+            acz[base + rk[hh]] = czz[jj];
 #endif
+          }
         }
-      }
+        if (wave == 0 && part == 0) {  // outputs in rank order
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const int jj = hh * 64 + lane;
+            if (rk[hh] < kstar) {
+              const int n = MODE == 1 && repaired ? ckey[jj] : cpid[jj];
+              // MODE 1, layer 3: bit 62 marks a member of a tie group after its first
+              const bool mk = MODE == 1 && consumer && !repaired && eqp[hh];
+              const int o = step + base + rk[hh];
+              oi[o] = static_cast<int64_t>(n) | (mk ? (int64_t(1) << 62) : int64_t(0));
+              publish(o, n);
+              if (ox) {
+                ox[o] = cxx[jj];
+                ox[npoint + o] = cyy[jj];
+                ox[2 * npoint + o] = czz[jj];
+              }
+            }
+          }
+        }
+      };
+      accept(0);
       // upper bound of every running minimum after this round: T, and the listed not accepted
       // (MODE 3: this part's own -- its T_w and its own listed values -- for a tighter histogram)
       float vm = MODE == 3 ? Tw : Tb;
@@ -1580,24 +1625,63 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
         const bool mine = MODE != 3 || (jj >= cbase && jj < cbase + capw);
         vm = (mine && jj < cnt && rk[hh] >= kstar) ? fmaxf(vm, cvv[jj]) : vm;
       }
-      if (wave == 0 && part == 0) {  // outputs in rank order
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          const int jj = hh * 64 + lane;
-          if (rk[hh] < kstar) {
-            const int n = MODE == 1 && repaired ? ckey[jj] : cpid[jj];
-            // MODE 1, layer 3: bit 62 marks a member of a tie group after its first
-            const bool mk = MODE == 1 && consumer && !repaired && eqp[hh];
-            oi[step + rk[hh]] = static_cast<int64_t>(n) | (mk ? (int64_t(1) << 62) : int64_t(0));
-            publish(step + rk[hh], n);
-            if (ox) {
-              ox[step + rk[hh]] = cxx[jj];
-              ox[npoint + step + rk[hh]] = cyy[jj];
-              ox[2 * npoint + step + rk[hh]] = czz[jj];
+#if DVCP_FPS_RECERT
+      // ---- 5b. the second pass: the first pass stops at the first candidate whose order it cannot
+      // certify, usually one its accepted centres moved.  The candidates left, with their values
+      // after those centres (the update's formula: exactly the points' minima after this round's
+      // first pass), are ranked and tested again under the same T -- rank 0 of them is the next
+      // step's argmax (above T, hence above every unlisted point) -- so one round accepts more
+      // centres for one more pair pass.  (Not for layer 3 of the paired launch: its tie handling
+      // ranks by layer 2's pick numbers.)
+      if constexpr (MODE == 0 || MODE == 1 || MODE == 3) {
+        const bool may = MODE != 1 || !consumer;
+        if (may && kstar < nreal && kstar < kSelAccept && kstar < npoint - step) {  // (uniform)
+          koff = kstar;
+          {  // thread t: candidate t % 128 against centres t / 128, + THREADS / 128, ...
+            constexpr int G = THREADS / kSelMax;
+            const int j = tid % kSelMax;
+            float m = cvv[j];
+            const T qx = cxx[j], qy = cyy[j], qz = czz[j];
+            for (int i = tid / kSelMax; i < koff; i += G) {  // (acc4: this wave's own rows)
+#if DVCP_FPS_ACC4
+              const AccC c = acc4[i];
+              m = fps_update<T>(m, qx, qy, qz, c.x, c.y, c.z);
+#else
+              m = fps_update<T>(m, qx, qy, qz, acx[i], acy[i], acz[i]);
+#endif
             }
+            vpart[tid] = m;
+          }
+          lds_barrier();
+          int n2 = 0;
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const int jj = hh * 64 + lane;
+            float v2 = -1.0f;  // (no candidate: unused slots, beyond the list, accepted)
+            if (jj < cnt && rk[hh] != 0x7FFFFFFF && rk[hh] >= koff) {
+              v2 = vpart[jj];
+#pragma unroll
+              for (int g = 1; g < THREADS / kSelMax; ++g) v2 = fminf(v2, vpart[g * kSelMax + jj]);
+            }
+            cvv2[jj] = v2;
+            n2 += __popcll(__ballot(v2 > Tb));
+          }
+          nreal2 = n2;
+          if (n2 > 0) {  // (uniform: every wave computed every value)
+            rank_decide(std::true_type{});
+            accept(koff);
+            vm = MODE == 3 ? Tw : Tb;
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+              const int jj = hh * 64 + lane;
+              const bool mine = MODE != 3 || (jj >= cbase && jj < cbase + capw);
+              vm = (mine && jj < cnt && rk[hh] >= kstar) ? fmaxf(vm, cvv2[jj]) : vm;
+            }
+            kstar += koff;
           }
         }
       }
+#endif
       vmax = wave_fmax_clamp0(vm);
       tick(3);
       break;
