@@ -9,7 +9,9 @@
 //     wave-box pruning);
 //   * 2048 <= N <= 16384 (8192 fp64): fps_select_kernel, which certifies a whole prefix of the
 //     serial chain per round (~27 centres on C3 clouds) from a threshold-selected candidate list;
-//   * larger: fps_split_kernel (S workgroups per cloud exchanging one key per step), then
+//   * larger, fp32 up to 65536: the split select (fps_part_kernel: 8 workgroups per cloud run
+//     the select rounds together, one candidate-list exchange per round; opt-in below 16384);
+//     else fps_split_kernel (S workgroups per cloud exchanging one key per step), then
 //     fps_dense_kernel.
 // Every kernel keeps each cloud's coordinates and running minima in VGPRs (Morton-sorted for the
 // first two), so the loop touches no global memory except the output stores.
@@ -103,10 +105,10 @@ __device__ __forceinline__ uint64_t fps_clock() {
 }
 
 // Setup shared by the FPS kernels: counting sort of the cloud by 12-bit Morton cell (16^3 cells
-// over its bounding box) in LDS.  perm[pos] = original index of sorted position pos.  Only the
+// over its bounding box): put(pos, n) for each point n and its sorted position pos.  Only the
 // point -> wave/group assignment depends on it, never a result.
-template <typename T, int THREADS>
-__device__ void fps_morton_sort(const PointsView<T>& pts, int b, int N, uint32_t* bins, uint16_t* perm,
+template <typename T, int THREADS, typename Put>
+__device__ void fps_morton_sort(const PointsView<T>& pts, int b, int N, uint32_t* bins, Put put,
                                 T (*red)[3][THREADS / kWave], uint32_t* wsum) {
   constexpr int W = THREADS / kWave;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -183,7 +185,7 @@ __device__ void fps_morton_sort(const PointsView<T>& pts, int b, int N, uint32_t
     }
   }
   __syncthreads();
-  for (int n = tid; n < N; n += THREADS) perm[atomicAdd(&bins[cell_of(n)], 1u)] = static_cast<uint16_t>(n);
+  for (int n = tid; n < N; n += THREADS) put(atomicAdd(&bins[cell_of(n)], 1u), n);
   __syncthreads();
 }
 
@@ -206,7 +208,8 @@ __global__ __launch_bounds__(THREADS) void fps_kernel(PointsView<T> pts, int N, 
   __shared__ uint32_t wsum[W];
 
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  fps_morton_sort<T, THREADS>(pts, b, N, bins, perm, red, wsum);
+  fps_morton_sort<T, THREADS>(pts, b, N, bins, [&](uint32_t pos, int n) { perm[pos] = static_cast<uint16_t>(n); },
+                              red, wsum);
   for (int pos = tid; pos < N; pos += THREADS) owner[perm[pos]] = static_cast<uint8_t>(pos / RANGE);
   __syncthreads();
   // ---- setup 3: each wave lists its points in ascending original index (stream compaction) ---
@@ -606,8 +609,8 @@ struct FpsPairArgs {
 constexpr uint32_t kFpsPairSpinCap = 1u << 22;
 
 // Split select (MODE 3, round 6): S workgroups per cloud run the select rounds together.  Every
-// workgroup sorts the whole cloud (the same Morton order), keeps the 64-point groups g with
-// g % S == part (then dealt round robin over its waves, as above) and, per round:
+// workgroup takes the 64-point groups g of the cloud's Morton order with g % S == part (then dealt
+// round robin over its waves, as above) and, per round:
 //   1. scans, decides and lists its OWN points exactly as the one-workgroup kernel does, with a
 //      per-workgroup candidate cap of 128 / S: its candidates and T_w, the largest of its running
 //      minima it did not list;
@@ -624,31 +627,36 @@ constexpr uint32_t kFpsPairSpinCap = 1u << 22;
 // such a round, or one without any candidate, accepts the single global argmax (value desc,
 // index asc) -- the reference's step.  Slots are double-buffered by round parity (a workgroup
 // can publish round r + 2 only after every peer published r + 1, i.e. finished reading r).
-// Roles: block b -> cloud (b / 8 / S) * 8 + b % 8, part (b / 8) % S, so a cloud's workgroups share
-// b % 8 -- one XCD (one L2) under the observed round-robin placement, for speed only -- and,
-// blocks being dispatched in order, a waiting workgroup waits for blocks at most 8 (S - 1)
-// behind it.  The wait is bounded (spin_cap polls) as a guard: a workgroup that gives up raises
-// err and the cloud's remaining outputs repeat the start point (in range, finite).
+// Roles (default, `ticket`): a workgroup takes ticket t when it starts running, cloud t / S, part
+// t % S, so the tickets handed out cover whole clouds plus at most one partly started cloud: a
+// waiting workgroup waits only for peers that already run or take the next free slots on the
+// device.  (Without tickets: block b -> cloud (b / 8 / S) * 8 + b % 8, part (b / 8) % S, a
+// cloud's workgroups on one XCD under round-robin placement; with ten batches in flight a peer
+// 8 (S - 1) blocks behind could wait behind other batches' kernels past the guard.)  The wait is
+// bounded (spin_cap polls) as a guard: a workgroup that gives up raises err and the cloud's
+// remaining outputs repeat the start point (in range, finite).
 // The Morton order is computed once per cloud, by part 0: its within-cell order comes from LDS
 // atomics and differs between workgroups, so independent sorts would deal some points to two parts
-// and others to none.  Part 0 hands its permutation to the other parts through `perm` (write-through
-// stores, then the cloud's flag), once per launch.
+// and others to none.  Part 0 writes the order to `perm` (write-through stores, then the cloud's
+// flag), once per launch, and each part reads the indices of its own groups into LDS: clouds of
+// up to 65536 points (16-bit indices in LDS).
 struct FpsPartArgs {
   uint64_t* slots;   // [B][2][S][kPartHdr + W + 5 * (128 / S)] granules, all ones before the launch
   uint32_t* flag;    // [B], all ones before the launch; 1 once part 0 has published the permutation
-  uint32_t* perm;    // [B][perm_words]: the cloud's Morton permutation, two u16 per word
+  uint32_t* perm;    // [B][perm_words]: the cloud's Morton order (original index per sorted position)
   int32_t* err;
   int S;             // workgroups per cloud: 2, 4 or 8
-  int B;             // clouds (the grid is ceil(B / 8) * 8 * S blocks)
-  int perm_words;    // ceil(N / 2)
+  int B;             // clouds (the grid is ceil(B / 8) * 8 * S blocks; B * S with tickets)
+  int perm_words;    // N
   uint32_t spin_cap;
   int target;        // candidates a part aims to list per round (0: max(kSelMin, kSelTarget / S))
+  uint32_t* ticket;  // all ones before the launch: roles by start order; nullptr: roles by blockIdx
 };
 // a part's slot: kPartHdr header granules (count | flags << 16, best v, best idx, its x, y, z, two
 // spare), then one T granule per wave (the largest running minimum it did not list), then the
 // candidates' v, idx, x, y, z (capw each)
 constexpr int kPartHdr = 8;
-constexpr int kPartMaxN = 16384;       // the whole cloud's Morton order is kept in LDS
+constexpr int kPartMaxN = 65536;       // 16-bit point indices in LDS
 constexpr uint32_t kPartFlagFb = 1u, kPartFlagEmpty = 2u;
 __device__ __forceinline__ void granule_put(uint64_t* g, uint32_t data, uint32_t tag) {
   __hip_atomic_store(g, (static_cast<uint64_t>(tag) << 32) | data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -676,7 +684,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
   constexpr int GP = PPT <= 2 ? 2 : PPT <= 4 ? 4 : PPT <= 8 ? 8 : PPT <= 16 ? 16 : 32;
   constexpr int QC = kWave / GP;
   __shared__ uint32_t bins[kMortonBins];  // setup; then the list's values [0, kSelCap) and positions
-  __shared__ uint16_t perm[MODE == 3 ? kPartMaxN : THREADS * PPT];
+  __shared__ uint16_t perm[THREADS * PPT];  // original index of each of this workgroup's slots
   __shared__ T red[2][3][W];
   __shared__ uint32_t wsum[W];
   __shared__ T lx[kSelCap], ly[kSelCap], lz[kSelCap];
@@ -729,9 +737,18 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
   int slotsz = 0;
   if constexpr (MODE == 3) {
     S = qa.S;
-    const int x = static_cast<int>(blockIdx.x) & 7, q = static_cast<int>(blockIdx.x) >> 3;
-    b = (q / S) * 8 + x;
-    part = q % S;
+    if (qa.ticket) {
+      __shared__ uint32_t s_ticket;
+      if (tid == 0) s_ticket = __hip_atomic_fetch_add(qa.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+      __syncthreads();
+      const int t = __builtin_amdgcn_readfirstlane(static_cast<int>(s_ticket));  // (from all ones: 0, 1, ...)
+      b = t / S;
+      part = t % S;
+    } else {
+      const int x = static_cast<int>(blockIdx.x) & 7, q = static_cast<int>(blockIdx.x) >> 3;
+      b = (q / S) * 8 + x;
+      part = q % S;
+    }
     if (b >= qa.B) return;  // grid padding: no partner waits for it (its whole cloud is padding)
     capw = kSelMax / S;
     seltarget = qa.target > 0 ? min(qa.target, capw) : max(kSelMin, kSelTarget / S);
@@ -740,7 +757,8 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
     if (tid == 0) s_gaveup = 0;
   }
   // sorted position of point slot p of `wv`'s lane `ln` (groups dealt to the parts, then the waves)
-  auto posof = [&](int p, int wv, int ln) { return ((p * W + wv) * S + part) * kWave + ln; };
+  auto posof = [&](int p, int wv, int ln) { return ((p * W + wv) * S + part) * kWave + ln; };  // sorted position
+  auto locof = [&](int p, int wv, int ln) { return (p * W + wv) * kWave + ln; };  // this part's slot (perm)
   bool consumer = false;  // MODE 1: this workgroup runs layer 3
   int s3 = -1;            // MODE 1, layer 2: the pick number whose index layer 3 waits for
   if constexpr (MODE == 1) {
@@ -775,16 +793,20 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
   [[maybe_unused]] int n_repair = 0;
   [[maybe_unused]] uint64_t rep_clk = 0;
   if constexpr (MODE == 3) {
+    // part 0 sorts the whole cloud into the workspace (write-through stores, drained, then the flag);
+    // every part then reads its own groups' original indices into perm, by local slot
     uint32_t* const gperm = qa.perm + static_cast<int64_t>(b) * qa.perm_words;
-    uint32_t* const lperm = reinterpret_cast<uint32_t*>(perm);
-    if (part == 0) {  // sort, publish: write-through stores, drained, then the flag (one lane)
-      fps_morton_sort<T, THREADS>(pts, b, N, bins, perm, red, wsum);
-      for (int w = tid; w < qa.perm_words; w += THREADS)
-        __hip_atomic_store(gperm + w, lperm[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (part == 0) {
+      fps_morton_sort<T, THREADS>(
+          pts, b, N, bins,
+          [&](uint32_t pos, int n) {
+            __hip_atomic_store(gperm + pos, static_cast<uint32_t>(n), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          },
+          red, wsum);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) __hip_atomic_store(qa.flag + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {          // wait for part 0's flag (one lane), then read the permutation write-through
+    } else {  // wait for part 0's flag (one lane)
       if (tid == 0) {
         uint32_t polls = 0;
         while (__hip_atomic_load(qa.flag + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1u) {
@@ -800,12 +822,17 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
         if (tid == 0) __hip_atomic_fetch_or(qa.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
-      for (int w = tid; w < qa.perm_words; w += THREADS)
-        lperm[w] = __hip_atomic_load(gperm + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
     }
+#pragma unroll 1
+    for (int p = 0; p < PPT; ++p) {
+      const int pos = posof(p, wave, lane);
+      perm[locof(p, wave, lane)] = static_cast<uint16_t>(
+          pos < N ? __hip_atomic_load(gperm + pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u);
+    }
+    __syncthreads();
   } else {
-    fps_morton_sort<T, THREADS>(pts, b, N, bins, perm, red, wsum);
+    fps_morton_sort<T, THREADS>(pts, b, N, bins, [&](uint32_t pos, int n) { perm[pos] = static_cast<uint16_t>(n); },
+                                red, wsum);
   }
 
   T px[PPT], py[PPT], pz[PPT];
@@ -821,7 +848,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
   for (int p = 0; p < PPT; ++p) {
     const int pos = posof(p, wave, lane);  // groups interleaved over the (parts and) waves
     const bool real = pos < N;
-    const uint32_t n = perm[real ? pos : 0];
+    const uint32_t n = perm[real ? locof(p, wave, lane) : 0];
     const T x = pts.at(b, 0, n), y = pts.at(b, 1, n), z = pts.at(b, 2, n);
     px[p] = real ? x : static_cast<T>(0);
     py[p] = real ? y : static_cast<T>(0);
@@ -855,7 +882,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
 #pragma unroll 1
     for (int p = 0; p < PPT; ++p) {
       const int pos = posof(p, wave, lane);
-      if (pos < N) mi = min(mi, static_cast<uint32_t>(perm[pos]));
+      if (pos < N) mi = min(mi, static_cast<uint32_t>(perm[locof(p, wave, lane)]));
     }
     mi = wave_umin(mi);
     if (lane == 0 && mi != 0xFFFFFFFFu) atomicMin(&s_minidx, mi);
@@ -1120,7 +1147,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
             atomicAdd(&hist[bin], 1u);
             if (li < kSelCap) {
               lv[li] = v;
-              lpos[li] = static_cast<uint32_t>(posof(p, wave, lane));
+              lpos[li] = static_cast<uint32_t>(locof(p, wave, lane));
               lx[li] = px[p];
               ly[li] = py[p];
               lz[li] = pz[p];
@@ -1248,9 +1275,8 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
         uint32_t mp = 0xFFFFFFFFu;
 #pragma unroll
         for (int p = 0; p < PPT; ++p) {
-          const int pos = posof(p, wave, lane);
           if (__ballot(dmin[p] == gmax)) {
-            if (dmin[p] == gmax) mp = min(mp, static_cast<uint32_t>(perm[pos]));
+            if (dmin[p] == gmax) mp = min(mp, static_cast<uint32_t>(perm[locof(p, wave, lane)]));
           }
         }
         mp = wave_umin(mp);
@@ -1638,11 +1664,14 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
         if (may && kstar < nreal && kstar < kSelAccept && kstar < npoint - step) {  // (uniform)
           koff = kstar;
           {  // thread t: candidate t % 128 against centres t / 128, + THREADS / 128, ...
+            // (the thread index re-materialised: hoisted out of the round loop, the addresses below
+            // stayed live in VGPRs and spilled)
             constexpr int G = THREADS / kSelMax;
-            const int j = tid % kSelMax;
+            const int t = wave * kWave + fresh_lane();
+            const int j = t % kSelMax;
             float m = cvv[j];
             const T qx = cxx[j], qy = cyy[j], qz = czz[j];
-            for (int i = tid / kSelMax; i < koff; i += G) {  // (acc4: this wave's own rows)
+            for (int i = t / kSelMax; i < koff; i += G) {  // (acc4: this wave's own rows)
 #if DVCP_FPS_ACC4
               const AccC c = acc4[i];
               m = fps_update<T>(m, qx, qy, qz, c.x, c.y, c.z);
@@ -1650,13 +1679,14 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
               m = fps_update<T>(m, qx, qy, qz, acx[i], acy[i], acz[i]);
 #endif
             }
-            vpart[tid] = m;
+            vpart[t] = m;
           }
           lds_barrier();
           int n2 = 0;
+          const int ln2 = fresh_lane();
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
-            const int jj = hh * 64 + lane;
+            const int jj = hh * 64 + ln2;
             float v2 = -1.0f;  // (no candidate: unused slots, beyond the list, accepted)
             if (jj < cnt && rk[hh] != 0x7FFFFFFF && rk[hh] >= koff) {
               v2 = vpart[jj];
@@ -2170,10 +2200,11 @@ static int launch_fps_split(PointsView<T> v, int B, int N, int npoint, const int
 }
 
 // Workgroups per cloud of the select rounds when the caller does not choose (dvcp_fps_ws, parts 0):
-// one, unless DVCP_FPS_PARTS asks for the split select (2, 4 or 8).  The split select shortens a
-// lone batch's chain, but its workgroups wait for each other: with many batches in flight (the
-// bench's ten) a waiting full-CU workgroup's peer can starve behind other kernels' smaller
-// workgroups, which take every CU that frees (round 6: the guard fired at four parts).
+// 8 above 16384 points, else one, unless DVCP_FPS_PARTS asks for the split select (2, 4 or 8).
+// The split select shortens a lone batch's chain, but its workgroups wait for each other: with
+// many batches in flight (the bench's ten) a waiting full-CU workgroup's peer can starve behind
+// other kernels' smaller workgroups, which take every CU that frees (round 6: the guard fired at
+// four parts with roles by blockIdx).
 // DVCP_FPS_PART_THREADS sets its workgroup size (256, 512 or 1024; A/B runs).
 static int fps_env_int(const char* name, int dflt) {
   const char* s = getenv(name);
@@ -2181,15 +2212,17 @@ static int fps_env_int(const char* name, int dflt) {
 }
 static int fps_parts(int N) {
   static const int forced = fps_env_int("DVCP_FPS_PARTS", 0);
-  (void)N;
-  return forced == 2 || forced == 4 || forced == 8 ? forced : 1;
+  if (forced == 1 || forced == 2 || forced == 4 || forced == 8) return forced;
+  // above the one-workgroup kernel's 16384 points: 8 workgroups of up to 8192 (C5's layer 1,
+  // 65536 -> 10000: 9.65 ms per launch with the per-step split kernel, 4.4 ms split select)
+  return N > 16 * kFpsSel1024 ? 8 : 1;
 }
 
 // Launch the split select over B fp32 clouds with S workgroups each; returns 1 (nothing launched)
 // when the workspace or the instantiated point slots do not cover this (N, S).
 // Workspace of the split select, carved from the caller's buffer: slots [B][2][S][slot] u64 |
-// flags [B] u32 (padded to 8 bytes) | perm [B][ceil(N / 2)] u32 | err i32.  The slots and flags are
-// set to all ones per launch.
+// flags [B] u32 + the ticket u32 (padded to 8 bytes) | perm [B][N] u32 | err i32.  The slots,
+// flags and ticket are set to all ones per launch.
 struct FpsPartWs {
   int64_t slot_bytes, flag_bytes, total;
 };
@@ -2197,8 +2230,8 @@ static FpsPartWs fps_part_ws(int B, int N, int S) {
   const int64_t slotsz = kPartHdr + 5 * (kSelMax / S);
   FpsPartWs w;
   w.slot_bytes = static_cast<int64_t>(B) * 2 * S * slotsz * 8;
-  w.flag_bytes = (static_cast<int64_t>(B) * 4 + 7) / 8 * 8;
-  w.total = w.slot_bytes + w.flag_bytes + static_cast<int64_t>(B) * ((N + 1) / 2) * 4 + 8;
+  w.flag_bytes = (static_cast<int64_t>(B) * 4 + 4 + 7) / 8 * 8;  // B flags, the ticket
+  w.total = w.slot_bytes + w.flag_bytes + static_cast<int64_t>(B) * N * 4 + 8;
   return w;
 }
 static int64_t fps_workspace_bytes(int B, int N) {  // the split path's B x N fp32, or the split select's
@@ -2222,8 +2255,9 @@ static int launch_fps_part(PointsView<float> v, int B, int N, int npoint, const 
   if (hipMemsetAsync(slots, 0xFF, static_cast<size_t>(w.slot_bytes + w.flag_bytes), st) != hipSuccess)
     return launch_status("dvcp_fps(part memset)");
   static const int target = fps_env_int("DVCP_FPS_PART_TARGET", 0);
-  const FpsPartArgs qa{slots, flags, permw, err, S, B, (N + 1) / 2, kFpsSpinCap, target};
-  const dim3 grid(ceil_div(B, 8) * 8 * S);
+  static const bool tickets = fps_env_int("DVCP_FPS_PART_TICKET", 1) != 0;
+  const FpsPartArgs qa{slots, flags, permw, err, S, B, N, kFpsSpinCap, target, tickets ? flags + B : nullptr};
+  const dim3 grid(tickets ? B * S : ceil_div(B, 8) * 8 * S);
   const int groups = ceil_div(ceil_div(N, kWave), S);  // 64-point groups per part (at most)
 #define DVCP_FPS_PART(P, NT)                                                                                  \
   if (threads == NT && groups <= P * (NT / kWave)) {                                                          \
@@ -2393,8 +2427,9 @@ extern "C" int64_t dvcp_fps_workspace_bytes(int B, int N) {
 }
 
 // dvcp_fps_ws with a sized workspace and the split select's workgroups per cloud: parts 0 = the
-// library's choice (dvcp_fps_ws's), 1 = the one-workgroup select kernel, 2 / 4 / 8 = the split select
-// (fp32, 2048 <= N <= 16384).  ws: ws_bytes >= dvcp_fps_workspace_bytes(B, N) bytes (8-aligned).
+// library's choice (dvcp_fps_ws's), 1 = the one-workgroup select kernel (the per-step split kernel
+// above 16384 points), 2 / 4 / 8 = the split select (fp32, 2048 <= N <= 65536, as far as its
+// instantiated slots reach).  ws: ws_bytes >= dvcp_fps_workspace_bytes(B, N) bytes (8-aligned).
 extern "C" int dvcp_fps_parts(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N,
                               int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz, void* ws,
                               int64_t ws_bytes, int32_t* err, int parts, void* stream) {

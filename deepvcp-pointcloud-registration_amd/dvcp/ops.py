@@ -26,22 +26,26 @@ FPS_REG_LIMIT = {torch.float32: 16384, torch.float64: 8192}
 
 # fp32 clouds the split select takes (several workgroups per cloud, one exchange per round;
 # csrc/fps.hip FpsPartArgs), given a workspace
-FPS_PART_RANGE = (2048, 16384)
+FPS_PART_RANGE = (2048, 65536)
 
 
 def fps_parts(N, dtype=torch.float32):
     """Workgroups per cloud of the select kernel for an N-point cloud when the caller does not say
-    (csrc/fps.hip fps_parts): one, unless DVCP_FPS_PARTS (2, 4 or 8) asks for the split select."""
+    (csrc/fps.hip fps_parts): above the one-workgroup kernel's 16384 points, 8 (C5's 65536-point
+    layer 1); up to it one, unless DVCP_FPS_PARTS (2, 4 or 8) asks for the split select."""
     if dtype != torch.float32 or not FPS_PART_RANGE[0] <= N <= FPS_PART_RANGE[1]:
         return 1
     forced = int(os.environ.get("DVCP_FPS_PARTS", "0") or 0)
-    return forced if forced in (1, 2, 4, 8) else 1
+    if forced in (1, 2, 4, 8):
+        return forced
+    return 8 if N > FPS_REG_LIMIT[dtype] else 1
 
 
 def fps(xyz, npoint, start, pdim=1, parts=None):
     """pointnet2_utils.py:63-84.  Returns (idx (B, npoint) int64, centres (B, 3, npoint)).
     ``parts`` (tests, A/B): workgroups per cloud of the select kernel (1, 2, 4 or 8; fp32 clouds of
-    2048..16384 points), else ``fps_parts``; the indices are the same for every choice."""
+    2048..65536 points), else ``fps_parts``; the indices are the same for every choice.  (Above
+    16384 points, parts=1 takes the per-step split kernel, dvcp_fps_ws's.)"""
     _lib.require_gpu(xyz, start)
     B = xyz.shape[0]
     N, sb, sc, sn = _pts(xyz, pdim)
@@ -52,15 +56,16 @@ def fps(xyz, npoint, start, pdim=1, parts=None):
     _lib.check_device_flags()   # earlier launches' guards (non-blocking)
     split = N > limit
     S = parts if parts is not None else fps_parts(N, xyz.dtype)
-    multi = split or (S > 1 and xyz.dtype == torch.float32 and FPS_PART_RANGE[0] <= N <= FPS_PART_RANGE[1])
+    part = S > 1 and xyz.dtype == torch.float32 and FPS_PART_RANGE[0] <= N <= FPS_PART_RANGE[1]
+    multi = split or part
     nbytes = int(_lib.load().dvcp_fps_workspace_bytes(B, N))
     ws = torch.empty((nbytes + 7) // 8, dtype=torch.int64, device=xyz.device)
     err = torch.zeros(1, dtype=torch.int32, device=xyz.device) if multi else None
     es = xyz.element_size()
-    wgs = B * (-(-N // 16384) if split else S if multi else 1)
+    wgs = B * (S if part else -(-N // 16384) if split else 1)
     work = (9.0 * B * npoint * N, B * (3 * N * es + npoint * (8 + 3 * es)), None, wgs, npoint)
     call("dvcp_fps_parts", dtype_code(xyz), ptr(xyz), sb, sc, sn, B, N, npoint, ptr(start), ptr(idx), ptr(ctr),
-         ptr(ws), ws.numel() * 8, ptr(err), int(parts or 0), stream(), work=work)
+         ptr(ws), ws.numel() * 8, ptr(err), int(parts if parts is not None else S), stream(), work=work)
     if multi:
         _lib.defer_flag_check(f"dvcp_fps: FPS workgroups gave up waiting for their peers (N={N})", err)
     return idx, ctr

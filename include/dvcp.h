@@ -56,8 +56,10 @@ int dvcp_fps(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int
  * With DVCP_FPS_PARTS=2|4|8 in the environment, fp32 clouds of 2048..16384 points whose
  * exchange slots fit in B x N x 4 bytes run their select rounds on that many workgroups per
  * cloud, exchanging one candidate list per round (the split select, csrc/fps.hip FpsPartArgs;
- * dvcp_fps_parts chooses per call).  Same indices either way.  err (optional int32, zeroed by the caller): set to 1 if a workgroup
- * gave up waiting for its peers (a guard; the indices then stay in range but are not FPS). */
+ * dvcp_fps_parts chooses per call, and takes it by default above 16384 points, where its
+ * workspace exceeds B x N x 4).  Same indices either way.  err (optional int32, zeroed by the
+ * caller): set to 1 if a workgroup gave up waiting for its peers (a guard; the indices then stay
+ * in range but are not FPS). */
 int dvcp_fps_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N,
                 int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz, float* ws,
                 int32_t* err, void* stream);
@@ -66,9 +68,11 @@ int dvcp_fps_ws(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, 
 int64_t dvcp_fps_workspace_bytes(int B, int N);
 
 /* dvcp_fps_ws with a sized workspace (ws_bytes >= dvcp_fps_workspace_bytes(B, N), 8-byte aligned)
- * and the split select's workgroups per cloud: parts = 0 (the library's choice, as dvcp_fps_ws),
- * 1 (the one-workgroup select kernel), 2, 4 or 8 (fp32, 2048 <= N <= 16384).  Same contract and
- * results as dvcp_fps; err as for dvcp_fps_ws.  The product path (dvcp/ops.py fps) calls this. */
+ * and the split select's workgroups per cloud: parts = 0 (the library's choice: 8 above 16384
+ * fp32 points, else 1 unless DVCP_FPS_PARTS says), 1 (the one-workgroup select kernel; above 16384
+ * points the per-step split kernel), 2, 4 or 8 (the split select: fp32, 2048 <= N <= 65536; 8
+ * above 32768 points).  Same contract and results as dvcp_fps; err as for dvcp_fps_ws.  The
+ * product path (dvcp/ops.py fps) calls this. */
 int dvcp_fps_parts(int dtype, const void* xyz, int64_t sb, int64_t sc, int64_t sn, int B, int N,
                    int npoint, const int64_t* start, int64_t* out_idx, void* out_xyz, void* ws,
                    int64_t ws_bytes, int32_t* err, int parts, void* stream);

@@ -5,7 +5,7 @@ test_gpu_e2e.py's):
   batch in one forward; pairs 0, 13 and 31 each equal their own single-pair run (pairs are
   independent in eval mode) and match the oracle (key points exact, R, t within
   1e-4).
-* C5 -- synthetic 65536-point clouds, K = 256: the first FPS (65536 -> 10000, the dense kernel
+* C5 -- synthetic 65536-point clouds, K = 256: the first FPS (65536 -> 10000, the split select
   above the register-resident limit) is bit-exact against the oracle, and the full forward +
   pose solve runs with its structural properties intact, with the reference's fp32 features and
   with BASELINE's fp16 feature storage (DeepVCP(feat_dtype=torch.float16): same key points, vcp
@@ -104,7 +104,8 @@ def test_c2_pair_vs_oracle(cuda, c2_batch, b):
 
 
 def test_c5_first_fps_full_size_vs_oracle(cuda):
-    """65536 -> 10000 (sa1 of C5): the dense FPS kernel, bit-exact against the oracle's FPS."""
+    """65536 -> 10000 (sa1 of C5): the default FPS path (round 6: the split select, 8 workgroups
+    per cloud), bit-exact against the oracle's FPS."""
     import oracle as O
     from dvcp import ops
     g = torch.Generator().manual_seed(505)
@@ -302,15 +303,16 @@ def test_c5_head_stage_decoupled_vs_oracle(cuda):
 
 @pytest.mark.parametrize("dtype,N,npoint,B", [(torch.float32, 40000, 3000, 3), (torch.float64, 20000, 2000, 2)])
 def test_split_fps_vs_oracle(cuda, dtype, N, npoint, B):
-    """The split FPS (S workgroups per cloud, ragged last chunk, several clouds per launch) is
-    bit-exact against the oracle's FPS."""
+    """The per-step split FPS (S workgroups per cloud, ragged last chunk, several clouds per
+    launch; parts=1 -- the default above 16384 fp32 points is the split select) is bit-exact
+    against the oracle's FPS."""
     import oracle as O
     from dvcp import ops
     g = torch.Generator().manual_seed(N + B)
     xyz = (torch.rand(B, N, 3, generator=g) * 2 - 1).to(dtype)
     start = torch.randint(0, N, (B,), generator=g)
     want = O.farthest_point_sample(xyz, npoint, start)
-    got, ctr = ops.fps(xyz.to(cuda), npoint, start.to(cuda), pdim=1)
+    got, ctr = ops.fps(xyz.to(cuda), npoint, start.to(cuda), pdim=1, parts=1)
     assert torch.equal(got.cpu(), want)
     assert torch.equal(ctr.cpu(), torch.gather(xyz, 1, want[..., None].expand(B, npoint, 3)).transpose(1, 2))
 

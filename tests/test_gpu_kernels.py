@@ -161,6 +161,32 @@ def test_fps_split_select_c3_equals_one_workgroup(cuda, N):
         assert torch.equal(cg, cw)
 
 
+@pytest.mark.parametrize("N,parts", [(65536, 8), (40000, 8), (32768, 4), (20000, 2)])
+def test_fps_split_select_large_clouds(cuda, N, parts):
+    """Above the one-workgroup kernel's 16384 points (C5's layer 1 is 65536 -> 10000) the split
+    select is the default: part 0 sorts the whole cloud into the workspace and each part reads its
+    own groups' indices.  Against the oracle on a prefix, and against the per-step split kernel
+    (parts=1) on the C5 chain length, bit for bit."""
+    import oracle as O
+    from dvcp import ops
+    g = torch.Generator().manual_seed(540 + N % 97)
+    xyz = torch.rand(2, N, 3, generator=g) * 2 - 1
+    start = torch.randint(0, N, (2,), generator=g)
+    want = O.farthest_point_sample(xyz, 1500, start)
+    got, ctr = ops.fps(xyz.to(cuda), 1500, start.to(cuda), pdim=1, parts=parts)
+    assert torch.equal(got.cpu(), want), int((got.cpu() != want).nonzero()[0, 1])
+    gathered = torch.stack([xyz[b, want[b]] for b in range(2)]).transpose(1, 2)
+    assert torch.equal(ctr.cpu(), gathered)
+    xt = xyz.transpose(1, 2).contiguous().to(cuda)
+    ref, cref = ops.fps(xt, 10000, start.to(cuda), pdim=2, parts=1)
+    got, cgot = ops.fps(xt, 10000, start.to(cuda), pdim=2)  # the default: 8 parts above 16384 points
+    assert torch.equal(got, ref), int((got != ref).nonzero()[0, 1])
+    assert torch.equal(cgot, cref)
+    if parts != 8:
+        got, _ = ops.fps(xt, 10000, start.to(cuda), pdim=2, parts=parts)
+        assert torch.equal(got, ref), int((got != ref).nonzero()[0, 1])
+
+
 def test_fps_split_select_many_launches_in_flight(cuda):
     """Ten split-select launches of 16 clouds on ten streams at once (more workgroups than the
     chip holds beside each other): every cloud's workgroups find their peers, the guard word stays

@@ -131,7 +131,11 @@ int main(int argc, char** argv) {
         PART(4, 1024, 4, false, "part 4 x 1024x4"),      PART(4, 1024, 4, true, "part 4 x 1024x4 +stats"),
         PART(2, 1024, 8, false, "part 8 x 1024x2"),      PART(2, 1024, 8, true, "part 8 x 1024x2 +stats"),
         PART(8, 512, 4, false, "part 4 x 512x8"),        PART(8, 512, 4, true, "part 4 x 512x8 +stats"),
+        PART(8, 1024, 8, false, "part 8 x 1024x8"),      PART(8, 1024, 8, true, "part 8 x 1024x8 +stats"),
+        PART(16, 1024, 4, false, "part 4 x 1024x16"),    PART(16, 1024, 4, true, "part 4 x 1024x16 +stats"),
     };
+    // argv[6]: 1 (default) roles by ticket, 0 by blockIdx
+    const bool tickets = argc > 6 ? atoi(argv[6]) != 0 : true;
 #undef PART
     uint64_t* dws;
     const size_t ws_bytes = static_cast<size_t>(dvcp::fps_workspace_bytes(B, N));
@@ -141,21 +145,23 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dpp, pprof_words * 8));
     for (const auto& c : pcs) {
       const int groups = (N + 63) / 64, gpart = (groups + c.S - 1) / c.S;
-      if (gpart > c.ppt * (c.threads / 64)) continue;
+      if (gpart > c.ppt * (c.threads / 64) || (c.ppt > 2 * gpart / (c.threads / 64) + 2 && c.ppt >= 8)) continue;
       const dvcp::FpsPartWs w = dvcp::fps_part_ws(B, N, c.S);
       const int capw = dvcp::kSelMax / c.S;
       char* base = reinterpret_cast<char*>(dws);
       const dvcp::FpsPartArgs qa{dws, reinterpret_cast<uint32_t*>(base + w.slot_bytes),
                                  reinterpret_cast<uint32_t*>(base + w.slot_bytes + w.flag_bytes),
-                                 reinterpret_cast<int32_t*>(base + w.total - 8), c.S, B, (N + 1) / 2, dvcp::kFpsSpinCap,
-                                 argc > 5 ? atoi(argv[5]) : 0};
+                                 reinterpret_cast<int32_t*>(base + w.total - 8), c.S, B, N, dvcp::kFpsSpinCap,
+                                 argc > 5 ? atoi(argv[5]) : 0,
+                                 tickets ? reinterpret_cast<uint32_t*>(base + w.slot_bytes) + B : nullptr};
       (void)capw;
       CK(hipMemset(dpp, 0, pprof_words * 8));
       float best = 1e30f;
       for (int rep = 0; rep < 3; ++rep) {
         CK(hipMemset(dws, 0xFF, w.slot_bytes + w.flag_bytes));
         CK(hipEventRecord(e0));
-        hipLaunchKernelGGL(c.fn, dim3((B + 7) / 8 * 8 * c.S), dim3(c.threads), 0, 0, view, N, npoint, ds, dout, dox, qa,
+        hipLaunchKernelGGL(c.fn, dim3(tickets ? B * c.S : (B + 7) / 8 * 8 * c.S), dim3(c.threads), 0, 0, view, N, npoint,
+                           ds, dout, dox, qa,
                            dpp);
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
