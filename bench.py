@@ -264,8 +264,8 @@ def main():
         torch.cuda.synchronize()
     iso, _lib.EVENT_LOG = _per_kernel(_lib.EVENT_LOG), None
     floor_us = fps_step_floor_us(dev)
-    # the single-batch latency with the split-select FPS (opt-in: it shortens a lone batch's chain;
-    # with batches in flight its workgroups' waits can starve), same batch and model
+    # the single-batch latency with the split-select FPS (opt-in at C3: it shortens a lone batch's
+    # chain, but with batches in flight its CU time costs pairs/s), same batch and model
     lat_split = None
     if args.fps_parts_latency and args.config == "c3":
         model.FE1.fps_parts = args.fps_parts_latency

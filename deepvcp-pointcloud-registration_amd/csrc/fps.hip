@@ -630,11 +630,13 @@ constexpr uint32_t kFpsPairSpinCap = 1u << 22;
 // Roles (default, `ticket`): a workgroup takes ticket t when it starts running, cloud t / S, part
 // t % S, so the tickets handed out cover whole clouds plus at most one partly started cloud: a
 // waiting workgroup waits only for peers that already run or take the next free slots on the
-// device.  (Without tickets: block b -> cloud (b / 8 / S) * 8 + b % 8, part (b / 8) % S, a
-// cloud's workgroups on one XCD under round-robin placement; with ten batches in flight a peer
-// 8 (S - 1) blocks behind could wait behind other batches' kernels past the guard.)  The wait is
-// bounded (spin_cap polls) as a guard: a workgroup that gives up raises err and the cloud's
-// remaining outputs repeat the start point (in range, finite).
+// device.  (DVCP_FPS_PART_TICKET=0: block b -> cloud (b / 8 / S) * 8 + b % 8, part (b / 8) % S,
+// a cloud's workgroups on one XCD under round-robin placement; same speed in the lab and the
+// bench.)  The wait is bounded (spin_cap polls) as a guard: a workgroup that gives up raises err
+// and the cloud's remaining outputs repeat the start point (in range, finite).  (Early in round 6
+// the guard fired with ten batches in flight; the cause was the workspace, not the wait: its
+// slots lacked the per-wave T granules, so the last clouds' exchange overran into the flags --
+// fps_part_ws, kPartMaxWaves.)
 // The Morton order is computed once per cloud, by part 0: its within-cell order comes from LDS
 // atomics and differs between workgroups, so independent sorts would deal some points to two parts
 // and others to none.  Part 0 writes the order to `perm` (write-through stores, then the cloud's
@@ -656,6 +658,7 @@ struct FpsPartArgs {
 // spare), then one T granule per wave (the largest running minimum it did not list), then the
 // candidates' v, idx, x, y, z (capw each)
 constexpr int kPartHdr = 8;
+constexpr int kPartMaxWaves = 16;  // the workspace's T granules per slot (fps_part_ws): up to 1024 threads
 constexpr int kPartMaxN = 65536;       // 16-bit point indices in LDS
 constexpr uint32_t kPartFlagFb = 1u, kPartFlagEmpty = 2u;
 __device__ __forceinline__ void granule_put(uint64_t* g, uint32_t data, uint32_t tag) {
@@ -679,6 +682,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
   constexpr int W = THREADS / kWave;
   static_assert(PPT <= 32 && kSelMax == 128 && (THREADS == 256 || THREADS == 512 || THREADS == 1024), "layout");
   static_assert(MODE != 3 || (sizeof(T) == 4 && DVCP_FPS_ACC4), "split select: fp32, centres as LDS rows");
+  static_assert(MODE != 3 || THREADS / kWave <= kPartMaxWaves, "split select: slot layout of fps_part_ws");
   // group lanes: lane l holds the box and exact maximum of the wave's group p = l % GP, replicated
   // over the QC = 64 / GP lane blocks, so one update test covers QC (centre, group) pairs per group
   constexpr int GP = PPT <= 2 ? 2 : PPT <= 4 ? 4 : PPT <= 8 ? 8 : PPT <= 16 ? 16 : 32;
@@ -2201,10 +2205,10 @@ static int launch_fps_split(PointsView<T> v, int B, int N, int npoint, const int
 
 // Workgroups per cloud of the select rounds when the caller does not choose (dvcp_fps_ws, parts 0):
 // 8 above 16384 points, else one, unless DVCP_FPS_PARTS asks for the split select (2, 4 or 8).
-// The split select shortens a lone batch's chain, but its workgroups wait for each other: with
-// many batches in flight (the bench's ten) a waiting full-CU workgroup's peer can starve behind
-// other kernels' smaller workgroups, which take every CU that frees (round 6: the guard fired at
-// four parts with roles by blockIdx).
+// The split select shortens a lone batch's chain but costs CU time: S full-CU workgroups per
+// cloud for 1 / 1.3 / 1.6 the time at S = 2 / 4 / 8 (C3), so with the bench's ten batches in
+// flight the one-workgroup kernel gives the most pairs/s (round 6: 2300 against 1630 at S = 4 and
+// 1310 at S = 8).  Above 16384 points the alternative is the per-step split kernel, slower still.
 // DVCP_FPS_PART_THREADS sets its workgroup size (256, 512 or 1024; A/B runs).
 static int fps_env_int(const char* name, int dflt) {
   const char* s = getenv(name);
@@ -2227,7 +2231,8 @@ struct FpsPartWs {
   int64_t slot_bytes, flag_bytes, total;
 };
 static FpsPartWs fps_part_ws(int B, int N, int S) {
-  const int64_t slotsz = kPartHdr + 5 * (kSelMax / S);
+  // a part's slot as fps_select_body lays it out (slotsz there): header, per-wave T, candidates
+  const int64_t slotsz = kPartHdr + kPartMaxWaves + 5 * (kSelMax / S);
   FpsPartWs w;
   w.slot_bytes = static_cast<int64_t>(B) * 2 * S * slotsz * 8;
   w.flag_bytes = (static_cast<int64_t>(B) * 4 + 4 + 7) / 8 * 8;  // B flags, the ticket
@@ -2248,6 +2253,7 @@ static int launch_fps_part(PointsView<float> v, int B, int N, int npoint, const 
   static const int threads = fps_env_int("DVCP_FPS_PART_THREADS", 1024);
   const FpsPartWs w = fps_part_ws(B, N, S);
   if (w.total > ws_bytes || N > kPartMaxN) return 1;
+  if (threads / kWave > kPartMaxWaves) return 1;
   uint64_t* slots = reinterpret_cast<uint64_t*>(ws);
   uint32_t* flags = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + w.slot_bytes);
   uint32_t* permw = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + w.slot_bytes + w.flag_bytes);

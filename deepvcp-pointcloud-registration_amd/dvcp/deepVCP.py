@@ -53,10 +53,10 @@ class DeepVCP(nn.Module):
         SURVEY App. A.3 Q14) instead of the collapsed 32x35 map (dvcp_dfe_tgt, the default: fc3.fc2.fc1
         formed in fp64 and rounded once; the same within 1e-7 on the tests).
         ``fps_parts``: workgroups per cloud of the feature extractor's FPS select rounds (1, 2, 4 or 8;
-        None: one, or DVCP_FPS_PARTS).  More workgroups shorten a lone batch's FPS chain (the split
-        select, csrc/fps.hip FpsPartArgs: the same indices); with many batches in flight they cost
-        CU time and their waits for each other's workgroups can starve, so one is the default
-        (DESIGN.md section 4.1, round 6)."""
+        None: ops.fps_parts -- one up to 16384 points, eight above, or DVCP_FPS_PARTS).  More workgroups shorten a lone batch's FPS chain (the split
+        select, csrc/fps.hip FpsPartArgs: the same indices); with many batches in flight the CU time
+        they take costs more pairs/s than the shorter chain gains, so one is the default below
+        16384 points."""
         super().__init__()
         self.dfe_literal = bool(dfe_literal)
         if feat_dtype not in (torch.float32, torch.float16):

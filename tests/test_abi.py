@@ -117,3 +117,26 @@ def test_fps_pair_gating(monkeypatch):
     assert not ops.fps_pair_ok(torch.zeros(2, 3, 1000), 1000, 1000, pdim=2)
     assert not ops.fps_pair_ok(torch.zeros(2, 3, 20000), 20000, 20000, pdim=2)
     assert _lib.load().dvcp_fps_pair_workspace_bytes(16, 10000) == 4 * (1 + 32 + 160000)
+
+
+def test_fps_parts_choice_and_workspace(monkeypatch):
+    """The split select's defaults (8 workgroups per cloud above 16384 fp32 points, else one unless
+    DVCP_FPS_PARTS asks) and its workspace: every part's exchange slot as the kernel lays it out
+    (8 header granules, one T granule per wave of a 1024-thread workgroup, 5 x 128 / S candidate
+    granules, 8 bytes each), double-buffered, plus B flags and the ticket, the B x N permutation
+    and the error word.  (Round 6: slots sized without the T granules overran into the flags and
+    the permutation; a part starting late read another cloud's candidates as point indices.)"""
+    from dvcp import _lib, ops
+    monkeypatch.delenv("DVCP_FPS_PARTS", raising=False)
+    assert ops.fps_parts(16384) == 1 and ops.fps_parts(10000) == 1
+    assert ops.fps_parts(16385) == 8 and ops.fps_parts(65536) == 8
+    assert ops.fps_parts(65537) == 1 and ops.fps_parts(40000, torch.float64) == 1
+    monkeypatch.setenv("DVCP_FPS_PARTS", "4")
+    assert ops.fps_parts(10000) == 4 and ops.fps_parts(1000) == 1
+    for B, N in ((16, 10000), (16, 16384), (4, 65536), (3, 2048)):
+        need = 0
+        for S in (2, 4, 8):
+            slots = B * 2 * S * (8 + 16 + 5 * (128 // S)) * 8
+            flags = (B * 4 + 4 + 7) // 8 * 8
+            need = max(need, slots + flags + B * N * 4 + 8)
+        assert _lib.load().dvcp_fps_workspace_bytes(B, N) >= need, (B, N)
