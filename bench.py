@@ -318,7 +318,7 @@ def main():
                           "collapsed, fp16 feature table (dvcp_dfe_tgt_f16)",
                    "sa_layer1": "per-point split: W1f.f + b1 once per point, W1x.(p - c) per grouped row (exact in "
                                 "real arithmetic; held to the fp32 bars)",
-                   "fps": f"select rounds on {model.FE1.fps_parts or _fps_parts_label(N)} workgroup(s) per cloud",
+                   "fps": _fps_parts_label(N, model.FE1.fps_parts),
                    "issue": ("each lane's step replayed from a captured HIP graph (dvcp.graphs.CapturedStep)"
                              if args.graphs == "on" else "eager: one Python + ctypes call per kernel")},
         "latency_ms_single_batch": round(latency_ms, 3),
@@ -360,9 +360,13 @@ HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per
                  "latency_ms_single_batch_split_fps", "roofline", "cpu_baseline", "parity", "registration_error_vs_gt")
 
 
-def _fps_parts_label(N):
+def _fps_parts_label(N, forced=None):
+    """The FE chain's FPS layers (N -> 10000, then 10000 -> 10000 twice): workgroups per cloud."""
     from dvcp import ops
-    return ops.fps_parts(N)
+    p1, p2 = (forced, forced) if forced else (ops.fps_parts(N), ops.fps_parts(10000))
+    if p1 == p2:
+        return f"select rounds on {p1} workgroup(s) per cloud"
+    return f"select rounds on {p1} workgroups per cloud (layer 1, {N} points), {p2} (layers 2, 3)"
 
 
 def headline(out):
@@ -387,17 +391,21 @@ def headline(out):
 
 
 def _per_kernel(log):
-    """EVENT_LOG -> {entry point: {n, ms, flops, bytes, exec_flops, mfma_flops, wgs, steps}} (sums).
-    Executed work given as a callable (the SA tables' real ball-query hit counts) is evaluated
-    here, after the timed region."""
+    """EVENT_LOG -> {entry point: {n, ms, cu_ms, flops, bytes, exec_flops, mfma_flops, wgs, steps}}
+    (sums; cu_ms: each launch's duration x the CU share of its grid, so an entry point whose launches
+    differ in grid size -- C5's 65536-point FPS layer on 8 workgroups per cloud, its 10000-point
+    layers on one -- gets a time-weighted share).  Executed work given as a callable (the SA tables'
+    real ball-query hit counts) is evaluated here, after the timed region."""
     out = {}
     for name, e0, e1, w in log:
         d = out.setdefault(name, {"n": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0, "exec_flops": 0.0,
                                   "mfma_flops": 0.0, "bf16_alg": 0.0, "bf16_hw": 0.0, "exec_known": True,
-                                  "wgs": None, "steps": 0})
+                                  "wgs": None, "steps": 0, "cu_ms": 0.0})
         d["n"] += 1
-        d["ms"] += e0.elapsed_time(e1)
+        ms = e0.elapsed_time(e1)
+        d["ms"] += ms
         w = tuple(w or ()) + (None,) * 5
+        d["cu_ms"] += ms * (min(1.0, w[3] / N_CU) if w[3] else 1.0)
         d["flops"] += w[0] or 0.0
         d["bytes"] += w[1] or 0.0
         ex = w[2]
@@ -447,7 +455,7 @@ def stage_roofline(iso, iso_steps, ms_step):
     stages, ideal_dev, meas_dev = {}, 0.0, 0.0
     for k, v in sorted(iso.items(), key=lambda kv: -kv[1]["ms"]):
         ms = v["ms"] / iso_steps
-        share = min(1.0, v["wgs"] / N_CU) if v["wgs"] else 1.0
+        share = v["cu_ms"] / v["ms"] if v["ms"] > 0 else 1.0
         dev_ms = ms * share
         t_byte = v["bytes"] / iso_steps / (PEAK_HBM_GBS * 1e9) * 1e3
         t_ref = v["flops"] / iso_steps / (PEAK_FP32_TFLOPS * 1e12) * 1e3
@@ -568,7 +576,7 @@ def fps_roofline(live, iso, floor_us, pmc):
     us_iso = v["ms"] * 1e3 / v["steps"]
     us_live = w["ms"] * 1e3 / w["steps"] if w and w["steps"] else None
     tf = v["flops"] / (v["ms"] * 1e-3) / 1e12
-    share = min(1.0, v["wgs"] / N_CU)
+    share = v["cu_ms"] / v["ms"]
     return {"kernel": name, "us_per_centre": round(us_iso, 4), "step_floor_us": round(floor_us, 4),
             "frac_of_step_floor": round(floor_us / us_iso, 4),
             "tflops_ref_graph": round(tf, 3), "frac_of_fp32_peak_chip": round(tf / PEAK_FP32_TFLOPS, 4),
