@@ -129,7 +129,9 @@ __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >
 // The accumulation is a k-ordered fp32 chain (the MFMA adds its two k-products per step).
 // (Round 4 had a row-per-thread VALU form of this pass, float4 FMA chains that hipcc packed into
 // v_pk_fma_f32.  With a second process on the GPU, single fp32 lanes of its accumulators came out
-// different -- the round-4 two-rank test failure, DESIGN.md section 5 -- so it was removed.)
+// different -- the round-4 two-rank test failure -- so it was removed.  The cause is not proven:
+// DESIGN.md section 5 names the one distinctive sequence, a v_mov-written register broadcast into
+// a packed FMA one instruction later, which no shipped kernel contains.)
 template <int D, int C1>
 __global__ __launch_bounds__(256) void sa_pre_mfma_kernel(const float* __restrict__ feat, int64_t fb, int64_t fn, int N,
                                                           int B, const float* __restrict__ params,
