@@ -549,7 +549,10 @@ __device__ __forceinline__ float fps_update(float m, T px, T py, T pz, T cx, T c
 #endif
 constexpr int kSelCap = 1024;    // list capacity
 constexpr int kSelBins = 256;
-constexpr int kSelTarget = 64;
+#ifndef DVCP_FPS_SEL_TARGET
+#define DVCP_FPS_SEL_TARGET 64
+#endif
+constexpr int kSelTarget = DVCP_FPS_SEL_TARGET;
 constexpr int kSelMax = 128;
 constexpr int kSelMin = 16;
 constexpr int kSelMaxScans = 8;  // rescans per round before the fallback (a guard)
@@ -651,7 +654,7 @@ struct FpsPartArgs {
   int B;             // clouds (the grid is ceil(B / 8) * 8 * S blocks; B * S with tickets)
   int perm_words;    // N
   uint32_t spin_cap;
-  int target;        // candidates a part aims to list per round (0: max(kSelMin, kSelTarget / S))
+  int target;        // candidates a part aims to list per round (0: min(128 / S, max(kSelMin, 96 / S)))
   uint32_t* ticket;  // all ones before the launch: roles by start order; nullptr: roles by blockIdx
 };
 // a part's slot: kPartHdr header granules (count | flags << 16, best v, best idx, its x, y, z, two
@@ -755,7 +758,10 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
     }
     if (b >= qa.B) return;  // grid padding: no partner waits for it (its whole cloud is padding)
     capw = kSelMax / S;
-    seltarget = qa.target > 0 ? min(qa.target, capw) : max(kSelMin, kSelTarget / S);
+    // (1.5 x the one-workgroup target over the parts: with the second pass, S = 4 ran 10000 ->
+    // 10000 in 2.58 instead of 2.89 ms at 24 per part; S = 2 and 8 the same within 1 %,
+    // profiles/round6/r6y_fps_target_sweep.log; the one-workgroup kernel is fastest at 64)
+    seltarget = qa.target > 0 ? min(qa.target, capw) : min(capw, max(kSelMin, (3 * kSelTarget / 2) / S));
     slotsz = kPartHdr + W + 5 * capw;
     qslot = qa.slots + static_cast<int64_t>(b) * 2 * S * slotsz;
     if (tid == 0) s_gaveup = 0;
