@@ -187,6 +187,58 @@ def test_fps_split_select_large_clouds(cuda, N, parts):
         assert torch.equal(got, ref), int((got != ref).nonzero()[0, 1])
 
 
+@pytest.mark.parametrize("case", ["duplicates", "clustered", "dyadic"])
+def test_fps_split_select_large_cloud_edge_cases(cuda, case):
+    """The large-cloud split select (8 parts, 32768 points) on the inputs that stress the select's
+    exactness argument: repeated points (minima reaching 0, parts running empty), a dense blob in a
+    sparse halo, and a dyadic grid of equal minima (ties to the lowest index), against the oracle."""
+    import oracle as O
+    from dvcp import ops
+    g = torch.Generator().manual_seed(560 + ["duplicates", "clustered", "dyadic"].index(case))
+    B, N = 2, 32768
+    if case == "duplicates":
+        xyz = (torch.rand(B, N // 8, 3, generator=g) * 2 - 1).repeat_interleave(8, dim=1)
+        npoint = 5000   # beyond the 4096 distinct points: the chain continues at minimum 0
+    elif case == "clustered":
+        xyz = torch.cat([torch.randn(B, N // 2, 3, generator=g) * 0.02,
+                         torch.rand(B, N - N // 2, 3, generator=g) * 2 - 1], 1)
+        xyz = xyz[:, torch.randperm(N, generator=g)]
+        npoint = 2000
+    else:
+        xyz = torch.randint(-16, 17, (B, N, 3), generator=g).float() / 16
+        npoint = 2000
+    start = torch.randint(0, N, (B,), generator=g)
+    want = O.farthest_point_sample(xyz, npoint, start)
+    got, _ = ops.fps(xyz.to(cuda), npoint, start.to(cuda), pdim=1)
+    got = got.cpu()
+    assert torch.equal(got, want), (case, int((got != want).nonzero()[0, 1]) if (got != want).any() else -1)
+
+
+def test_fps_split_select_large_clouds_many_launches_in_flight(cuda):
+    """Ten launches of the large-cloud split select (4 clouds x 8 parts each: 320 full-CU
+    workgroups, more than the chip holds at once) on ten streams: roles by start ticket, so every
+    waiting workgroup's peers run or come next; the guard word stays clear and every launch equals
+    the per-step split kernel's indices."""
+    from dvcp import _lib, ops
+    g = torch.Generator().manual_seed(570)
+    N = 40000
+    xyz = (torch.rand(4, 3, N, generator=g) * 2 - 1).to(cuda)
+    starts = [torch.randint(0, N, (4,), generator=g).to(cuda) for _ in range(10)]
+    streams = [torch.cuda.Stream() for _ in starts]
+    outs = []
+    for st, s in zip(streams, starts):
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            outs.append(ops.fps(xyz, 3000, s, pdim=2)[0])
+    for st in streams:
+        torch.cuda.current_stream().wait_stream(st)
+    torch.cuda.synchronize()
+    _lib.check_device_flags(block=True)
+    for s, got in zip(starts, outs):
+        want, _ = ops.fps(xyz, 3000, s, pdim=2, parts=1)
+        assert torch.equal(got, want)
+
+
 def test_fps_split_select_many_launches_in_flight(cuda):
     """Ten split-select launches of 16 clouds on ten streams at once (more workgroups than the
     chip holds beside each other): every cloud's workgroups find their peers, the guard word stays
