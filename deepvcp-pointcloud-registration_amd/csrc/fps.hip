@@ -541,6 +541,10 @@ __device__ __forceinline__ float fps_update(float m, T px, T py, T pz, T cx, T c
 // 3.25 -> 3.09 ms, 16 clouds, identical indices.
 // DVCP_FPS_RECERT: a round whose first pass stops early ranks the candidates left a second time
 // (step 5b); 0 = one pass per round
+// DVCP_FPS_PRIO: the select kernel's waves raise their issue priority (s_setprio) by this much
+#ifndef DVCP_FPS_PRIO
+#define DVCP_FPS_PRIO 0
+#endif
 #ifndef DVCP_FPS_RECERT
 #define DVCP_FPS_RECERT 1
 #endif
@@ -1822,6 +1826,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(fps_sel
 void fps_select_kernel(PointsView<T> pts, int N, int npoint, const int64_t* __restrict__ start,
                        int64_t* __restrict__ out_idx, T* __restrict__ out_xyz,
                        unsigned long long* __restrict__ prof) {
+#if DVCP_FPS_PRIO
+  __builtin_amdgcn_s_setprio(DVCP_FPS_PRIO);  // (A/B: issue priority over co-resident waves)
+#endif
   fps_select_body<T, PPT, TIMING, THREADS, 0>(pts, N, npoint, start, out_idx, out_xyz, prof, FpsPairArgs<T>{});
 }
 
@@ -2310,7 +2317,9 @@ static int launch_fps(const T* xyz, int64_t sb, int64_t sc, int64_t sn, int B, i
   // up to 16 points per lane): per-wave scan and update halve while the per-round decisions stay
   // (tools/fps_lab: 16384 -> 10000 5.52 -> 5.07 ms, 10000 -> 10000 4.13 -> 3.30 ms on 16 clouds)
   if constexpr (sizeof(T) == 4) {
-    if (N >= kFpsBatchedMinN && N <= 16 * kFpsSel1024) {
+    // DVCP_FPS_THREADS=512 (A/B runs): the 512-thread select below instead
+    static const bool sel1024 = fps_env_int("DVCP_FPS_THREADS", 1024) != 512;
+    if (sel1024 && N >= kFpsBatchedMinN && N <= 16 * kFpsSel1024) {
       const int p16 = ceil_div(N, kFpsSel1024);
       const dim3 blk(kFpsSel1024);
 #define DVCP_FPS_SEL1024(P)                                                                                   \
