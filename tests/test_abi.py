@@ -140,3 +140,15 @@ def test_fps_parts_choice_and_workspace(monkeypatch):
             flags = (B * 4 + 4 + 7) // 8 * 8
             need = max(need, slots + flags + B * N * 4 + 8)
         assert _lib.load().dvcp_fps_workspace_bytes(B, N) >= need, (B, N)
+
+
+def test_graft_entry_build():
+    """__graft_entry__.build(): make (nothing to do once built) and the library's ABI version
+    against dvcp/_lib.py's (round 6 left a stale literal there for a while)."""
+    import importlib
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    ge = importlib.import_module("__graft_entry__")
+    ge.build()
