@@ -15,10 +15,10 @@ from tests_helpers import golden, golden_state_dict, topk_parity
 pytestmark = pytest.mark.gpu
 
 
-def _load_model(cuda, z):
+def _load_model(cuda, z, dfe_literal=False):
     import dvcp
     model = dvcp.DeepVCP(use_normal=bool(z["normals"]), K=int(z["K"]), r=float(z["r"]), s=float(z["s"]),
-                         fe_npoint=int(z["fe_npoint"])).eval()
+                         fe_npoint=int(z["fe_npoint"]), dfe_literal=dfe_literal).eval()
     model.load_state_dict(golden_state_dict(z))
     return model.to(cuda)
 
@@ -63,12 +63,16 @@ def test_e2e_fixture_front(cuda, name):
     # half is checked from the oracle's top-k in test_e2e_fixture_back
 
 
+@pytest.mark.parametrize("dfe", ["collapsed", "literal"])
 @pytest.mark.parametrize("name", ["e2e_c3small", "e2e_c1"])
-def test_e2e_fixture_back(cuda, name):
+def test_e2e_fixture_back(cuda, name, dfe):
     """Stage-decoupled back half: the oracle's top-k indices are fed in, then key points,
-    candidates and kNN indices must be exact and vcp / R / t / loss within tolerance."""
+    candidates and kNN indices must be exact and vcp / R / t / loss within tolerance -- with the
+    product's collapsed DFE map and with the literal fc1 -> fc2 -> fc3 chain (SURVEY App. A.3 Q14's
+    parity path, DeepVCP(dfe_literal=True))."""
     z = golden(name)
-    tr, kp, vcp, loss, R, t = _forward(cuda, _load_model(cuda, z), z, keypoint_idx=torch.from_numpy(z["topk"]))
+    tr, kp, vcp, loss, R, t = _forward(cuda, _load_model(cuda, z, dfe_literal=dfe == "literal"), z,
+                                       keypoint_idx=torch.from_numpy(z["topk"]))
     B = kp.shape[0]
     assert torch.equal(kp.cpu(), torch.from_numpy(z["keypts_out"]))
     torch.testing.assert_close(tr["src_cat"].cpu(), torch.from_numpy(z["src_cat"]).float(), rtol=1e-4, atol=1e-5)
