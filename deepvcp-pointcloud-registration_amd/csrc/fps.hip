@@ -712,6 +712,14 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
   __shared__ uint32_t srank2[DVCP_FPS_RECERT ? kSelMax : 1];                   // the second pass's ranks
   __shared__ __attribute__((aligned(16))) float cvv2[DVCP_FPS_RECERT ? kSelMax : 4];  // its values
   __shared__ float vpart[DVCP_FPS_RECERT ? THREADS : 1];  // their partial minima (THREADS / 128 centre strides)
+  // MODE 3: the second pass's candidates compacted into a dense list (index, coordinates, merged-
+  // list slot; values in cvv2): the merged list's unused slots and dropped candidates leave it
+  constexpr int kC2 = DVCP_FPS_RECERT && MODE == 3 ? kSelMax : 4;
+  __shared__ __attribute__((aligned(16))) int c2pid[kC2];
+  __shared__ __attribute__((aligned(16))) T c2x[kC2];
+  __shared__ __attribute__((aligned(16))) T c2y[kC2];
+  __shared__ __attribute__((aligned(16))) T c2z[kC2];
+  __shared__ int c2slot[kC2];
   __shared__ float wtf[W];
   // T_f and T (non-negative floats as bits) reduced over the waves by LDS atomicMax: every wave
   // reads one word instead of W
@@ -1472,42 +1480,48 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
       // candidates left (values cvv2 > T, ranks in srank2, ranks offset by koff)
       auto rank_decide = [&](auto p2c) {
       constexpr bool P2 = decltype(p2c)::value;
+      constexpr bool D2 = P2 && MODE == 3;  // MODE 3's second pass: the compacted (dense) list
       float* const cv = P2 ? cvv2 : cvv;
+      const int* const cp = D2 ? c2pid : cpid;
+      const T* const cX = D2 ? c2x : cxx;
+      const T* const cY = D2 ? c2y : cyy;
+      const T* const cZ = D2 ? c2z : czz;
+      const int cn = D2 ? nreal2 : cnt;
       uint32_t* const sr = P2 ? srank2 : srank;
       {
         const int i_lo = wave * (kSelMax / W);
         int r0 = 0, r1 = 0, t0 = 0, t1 = 0;
         int e0 = 0, e1 = 0;  // MODE 1: c_j has an equal-valued predecessor (bits 24+ of srank)
-        if (i_lo < cnt) {  // wave-uniform
+        if (i_lo < cn) {  // wave-uniform
           const int j0 = lane, j1 = lane + kWave;
           const float v0 = cv[j0], v1 = cv[j1];
-          const int p0 = cpid[j0], p1 = cpid[j1];
-          const T x0 = cxx[j0], y0 = cyy[j0], z0 = czz[j0];
-          const T x1 = cxx[j1], y1 = cyy[j1], z1 = czz[j1];
+          const int p0 = cp[j0], p1 = cp[j1];
+          const T x0 = cX[j0], y0 = cY[j0], z0 = cZ[j0];
+          const T x1 = cX[j1], y1 = cY[j1], z1 = cZ[j1];
           // rolled at PPT 16 x 1024 threads (128 VGPRs): one batch of four candidates live at a time
           constexpr int kPairUnroll = PPT >= 16 && THREADS == 1024 ? 1 : kSelMax / W / 4;
 #pragma unroll kPairUnroll
           for (int c4 = 0; c4 < kSelMax / W / 4; ++c4) {
             const int i0 = i_lo + 4 * c4;
-            if (i0 >= cnt) break;  // wave-uniform
+            if (i0 >= cn) break;  // wave-uniform
             const float4 v4 = *reinterpret_cast<const float4*>(&cv[i0]);
             // MODE 3: a part's unused slots (v = -1) follow its candidates; skip all-unused batches
             // (P2: batches with no candidate left)
-            if (P2 ? !(fmaxf(fmaxf(v4.x, v4.y), fmaxf(v4.z, v4.w)) > Tb) : (MODE == 3 && v4.x < 0.0f))
+            if (!D2 && (P2 ? !(fmaxf(fmaxf(v4.x, v4.y), fmaxf(v4.z, v4.w)) > Tb) : (MODE == 3 && v4.x < 0.0f)))
               continue;  // (wave-uniform)
-            const int4 p4 = *reinterpret_cast<const int4*>(&cpid[i0]);
+            const int4 p4 = *reinterpret_cast<const int4*>(&cp[i0]);
             const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
             const int pp[4] = {p4.x, p4.y, p4.z, p4.w};
             T xx[4], yy[4], zz[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-              xx[k] = cxx[i0 + k];
-              yy[k] = cyy[i0 + k];
-              zz[k] = czz[i0 + k];
+              xx[k] = cX[i0 + k];
+              yy[k] = cY[i0 + k];
+              zz[k] = cZ[i0 + k];
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-              const bool in = P2 ? vv[k] > Tb : MODE == 3 ? vv[k] >= 0.0f : i0 + k < cnt;
+              const bool in = D2 ? i0 + k < cn : P2 ? vv[k] > Tb : MODE == 3 ? vv[k] >= 0.0f : i0 + k < cnt;
               const bool b0 = in & ((vv[k] > v0) | ((vv[k] == v0) & (pp[k] < p0)));
               const bool b1 = in & ((vv[k] > v1) | ((vv[k] == v1) & (pp[k] < p1)));
               const T ax = x0 - xx[k], ay = y0 - yy[k], az = z0 - zz[k];
@@ -1525,10 +1539,10 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
             }
           }
         }
-        if (i_lo < cnt) {  // wave-uniform
+        if (i_lo < cn) {  // wave-uniform
           if (MODE == 3 || P2) {  // (unused slots take no rank; P2: nor the candidates not left)
-            const bool in0 = P2 ? cv[lane] > Tb : cv[lane] >= 0.0f;
-            const bool in1 = P2 ? cv[lane + kWave] > Tb : cv[lane + kWave] >= 0.0f;
+            const bool in0 = D2 ? lane < cn : P2 ? cv[lane] > Tb : cv[lane] >= 0.0f;
+            const bool in1 = D2 ? lane + kWave < cn : P2 ? cv[lane + kWave] > Tb : cv[lane + kWave] >= 0.0f;
             r0 = in0 ? r0 : 0;
             t0 = in0 ? t0 : 0;
             r1 = in1 ? r1 : 0;
@@ -1550,7 +1564,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
         const int jj = hh * 64 + lane;
         rk[hh] = 0x7FFFFFFF;
         // (MODE 3: unused slots are no candidates; P2: only those left)
-        if (jj < cnt && (P2 ? cv[jj] > Tb : (MODE != 3 || cv[jj] >= 0.0f))) {
+        if (jj < cn && (D2 || (P2 ? cv[jj] > Tb : (MODE != 3 || cv[jj] >= 0.0f)))) {
           const uint32_t e = sr[jj];
           const int r = static_cast<int>(e & 0xFFFFu);
           const bool touched = MODE == 1 ? ((e >> 16) & 0xFFu) != 0u : (e >> 16) != 0u;
@@ -1621,17 +1635,23 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
       // the accepted centres in rank order, for the update: every wave writes the same values
       // (its own reads below follow its own writes in LDS order); wave 0 of part 0 writes the
       // outputs.  base: the ranks' offset (the second pass's follow the first's)
-      auto accept = [&](int base) {
+      // (d2c: MODE 3's second pass, whose candidates are the compacted c2 rows)
+      auto accept = [&](int base, auto d2c) {
+        constexpr bool D2 = decltype(d2c)::value;
+        const int* const cp = D2 ? c2pid : cpid;
+        const T* const cX = D2 ? c2x : cxx;
+        const T* const cY = D2 ? c2y : cyy;
+        const T* const cZ = D2 ? c2z : czz;
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
           const int jj = hh * 64 + lane;
           if (rk[hh] < kstar) {
 #if DVCP_FPS_ACC4
-            acc4[base + rk[hh]] = AccC{cxx[jj], cyy[jj], czz[jj], static_cast<T>(0)};
+            acc4[base + rk[hh]] = AccC{cX[jj], cY[jj], cZ[jj], static_cast<T>(0)};
 #else
-            acx[base + rk[hh]] = cxx[jj];
-            acy[base + rk[hh]] = cyy[jj];
-            acz[base + rk[hh]] = czz[jj];
+            acx[base + rk[hh]] = cX[jj];
+            acy[base + rk[hh]] = cY[jj];
+            acz[base + rk[hh]] = cZ[jj];
 #endif
           }
         }
@@ -1640,22 +1660,22 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
           for (int hh = 0; hh < 2; ++hh) {
             const int jj = hh * 64 + lane;
             if (rk[hh] < kstar) {
-              const int n = MODE == 1 && repaired ? ckey[jj] : cpid[jj];
+              const int n = MODE == 1 && repaired ? ckey[jj] : cp[jj];
               // MODE 1, layer 3: bit 62 marks a member of a tie group after its first
               const bool mk = MODE == 1 && consumer && !repaired && eqp[hh];
               const int o = step + base + rk[hh];
               oi[o] = static_cast<int64_t>(n) | (mk ? (int64_t(1) << 62) : int64_t(0));
               publish(o, n);
               if (ox) {
-                ox[o] = cxx[jj];
-                ox[npoint + o] = cyy[jj];
-                ox[2 * npoint + o] = czz[jj];
+                ox[o] = cX[jj];
+                ox[npoint + o] = cY[jj];
+                ox[2 * npoint + o] = cZ[jj];
               }
             }
           }
         }
       };
-      accept(0);
+      accept(0, std::false_type{});
       // upper bound of every running minimum after this round: T, and the listed not accepted
       // (MODE 3: this part's own -- its T_w and its own listed values -- for a tighter histogram)
       float vm = MODE == 3 ? Tw : Tb;
@@ -1698,6 +1718,7 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
           lds_barrier();
           int n2 = 0;
           const int ln2 = fresh_lane();
+          [[maybe_unused]] float vmd = 0.0f;  // MODE 3: this part's candidates dropped at or below T
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
             const int jj = hh * 64 + ln2;
@@ -1707,19 +1728,51 @@ __device__ __forceinline__ void fps_select_body(PointsView<T> pts, int N, int np
 #pragma unroll
               for (int g = 1; g < THREADS / kSelMax; ++g) v2 = fminf(v2, vpart[g * kSelMax + jj]);
             }
-            cvv2[jj] = v2;
-            n2 += __popcll(__ballot(v2 > Tb));
+            const uint64_t m = __ballot(v2 > Tb);
+            if constexpr (MODE == 3) {
+              // compacted in list order (every wave writes the same rows of the c2 arrays, which
+              // no wave reads before its own writes): the merged list's unused slots and the
+              // dropped candidates leave the pair pass
+              if (v2 > Tb) {
+                const int o = n2 + static_cast<int>(__builtin_amdgcn_mbcnt_hi(
+                                       static_cast<uint32_t>(m >> 32),
+                                       __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0)));
+                cvv2[o] = v2;
+                c2pid[o] = cpid[jj];
+                c2x[o] = cxx[jj];
+                c2y[o] = cyy[jj];
+                c2z[o] = czz[jj];
+                c2slot[o] = jj;
+              }
+              const bool mine = jj >= cbase && jj < cbase + capw;
+              vmd = mine && !(v2 > Tb) ? fmaxf(vmd, v2) : vmd;
+            } else {
+              cvv2[jj] = v2;
+            }
+            n2 += __popcll(m);
           }
           nreal2 = n2;
           if (n2 > 0) {  // (uniform: every wave computed every value)
             rank_decide(std::true_type{});
-            accept(koff);
-            vm = MODE == 3 ? Tw : Tb;
+            if constexpr (MODE == 3) {
+              accept(koff, std::true_type{});
+              vm = fmaxf(Tw, vmd);
 #pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-              const int jj = hh * 64 + lane;
-              const bool mine = MODE != 3 || (jj >= cbase && jj < cbase + capw);
-              vm = (mine && jj < cnt && rk[hh] >= kstar) ? fmaxf(vm, cvv2[jj]) : vm;
+              for (int hh = 0; hh < 2; ++hh) {
+                const int o = hh * 64 + lane;
+                if (o < n2 && rk[hh] >= kstar) {
+                  const int jj = c2slot[o];
+                  vm = jj >= cbase && jj < cbase + capw ? fmaxf(vm, cvv2[o]) : vm;
+                }
+              }
+            } else {
+              accept(koff, std::false_type{});
+              vm = Tb;
+#pragma unroll
+              for (int hh = 0; hh < 2; ++hh) {
+                const int jj = hh * 64 + lane;
+                vm = (jj < cnt && rk[hh] >= kstar) ? fmaxf(vm, cvv2[jj]) : vm;
+              }
             }
             kstar += koff;
           }
