@@ -42,6 +42,12 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef DVCP_DFE_WAHEAD
 #define DVCP_DFE_WAHEAD 1
 #endif
+// DVCP_DFE_W2 (with WAHEAD): the w rows of two candidates per pass, one per lane half (the fp64
+// sum, division and DPP moves run once for two candidates instead of once per candidate on
+// mirrored halves); formed at every other step
+#ifndef DVCP_DFE_W2
+#define DVCP_DFE_W2 1
+#endif
 // DVCP_DFE_SCAND: the candidate's coordinates as scalar loads (its index is wave-uniform; measured
 // equal to vector loads, 0.694 / 0.696 ms, profiles/round5/r5r_dfe_ab.log)
 #ifndef DVCP_DFE_SCAND
@@ -232,11 +238,13 @@ constexpr int kDfe1Waves = 4;
 // 0.674 / 0.670 / 0.666 ms and 0.682 / 0.687 / 0.665 / 0.663 (profiles/round5/r5s_dfe_grid_ab.log)
 constexpr int kDfeGrid = DVCP_DFE_GRID;
 
-// v + (v moved by the DPP pattern CTRL), fp64 (the two halves moved separately)
+// v + (v moved by the DPP pattern CTRL), fp64 (the two halves moved separately).  Every pattern
+// used (quad permutes, row rotations) reads a lane of the same row for every lane, so the moves
+// need no old value (mov_dpp: no zeroed destination register per move)
 template <int CTRL>
 __device__ __forceinline__ double dpp_add_f64(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
   return v + __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ double readlane_f64(double v, int l) {
@@ -264,7 +272,9 @@ struct Dfe1Lds {
 // (B, 3, M) layout.  Round 5 ablation at C3: the three scattered coordinate loads alone cost
 // 0.664 -> 0.513 ms, the 128-byte feature rows 0.664 -> 0.62 (profiles/round5/r5ac_dfe_abl.log);
 // with packed rows the call (pack included) runs 0.54 ms (r5ad_p4.log).
-template <typename T, typename FT = float>
+// P4: the target points are (x, y, z, pad) rows (PointsView::rows4, known at launch): one
+// 16-byte gather per neighbour with no per-candidate layout branch.
+template <typename T, typename FT = float, bool P4 = false>
 __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per_eu(DVCP_DFE_WPE))) void dfe_tgt_mfma1_kernel(
     PointsView<T> ref, const FT* __restrict__ feat, int M, const float* __restrict__ cand,
     const float* __restrict__ dist, const int32_t* __restrict__ idx, int Q, int B, const float* __restrict__ params,
@@ -420,7 +430,16 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
     G.py = ref.at(bb, 1, r32);
     G.pz = ref.at(bb, 2, r32);
 #else
-    ref.load3(bb, n, G.px, G.py, G.pz);
+    if constexpr (P4) {
+      const float4 q = *reinterpret_cast<const float4*>(ref.p + bb * ref.sb + 4 * static_cast<int64_t>(n));
+      G.px = q.x;
+      G.py = q.y;
+      G.pz = q.z;
+    } else {
+      G.px = ref.at(bb, 0, n);
+      G.py = ref.at(bb, 1, n);
+      G.pz = ref.at(bb, 2, n);
+    }
 #endif
 #if DVCP_DFE_SCAND
     const float* cq = cand + static_cast<int64_t>(__builtin_amdgcn_readfirstlane(gc)) * 3;
@@ -452,6 +471,24 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
     v = dpp_add_f64<0x128>(v);  // row_ror:8
     const double dsum = readlane_f64(v, 15) + readlane_f64(v, 31);
     L.w[wave][buf][r32] = static_cast<float>(static_cast<double>(dj) / dsum);  // both halves write the same value
+  };
+  // the same for two candidates at once: lane half 0 forms candidate A's row (dja) into slot bufa,
+  // half 1 candidate B's (djb) into bufb (the DPP patterns stay inside 16-lane rows, so the halves'
+  // sums do not mix: rows 0-1 are A's 32 distances, rows 2-3 B's)
+  auto weights2 = [&](float dja, float djb, int bufa, int bufb) {
+#if DVCP_DFE_ABL == 3  // (ablation builds only: no distance sum / division)
+    L.w[wave][h ? bufb : bufa][r32] = h ? djb : dja;
+    return;
+#endif
+    const float dj = h ? djb : dja;
+    double v = static_cast<double>(dj);
+    v = dpp_add_f64<0xB1>(v);
+    v = dpp_add_f64<0x4E>(v);
+    v = dpp_add_f64<0x124>(v);
+    v = dpp_add_f64<0x128>(v);
+    const double sa = readlane_f64(v, 15) + readlane_f64(v, 31);
+    const double sb = readlane_f64(v, 47) + readlane_f64(v, 63);
+    L.w[wave][h ? bufb : bufa][r32] = static_cast<float>(static_cast<double>(dj) / (h ? sb : sa));
   };
   // A operands of a candidate: the xyz k-steps ((dx|dy), (dz|0)) and the 32 weighted features as
   // split-3 bf16 pieces (lane half h: features 16h .. 16h + 15, k-step t: 16h + 8t ..)
@@ -556,8 +593,12 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
     advance(c1);
     gather(t0, nn[0], G[0]);
     gather(c1, nn[1], G[1]);
-    weights(dj[0], 0);
-    if (WA) weights(dj[1], 1);
+    if (WA && DVCP_DFE_W2) {
+      weights2(dj[0], dj[1], 0, 1);
+    } else {
+      weights(dj[0], 0);
+      if (WA) weights(dj[1], 1);
+    }
     prep(G[0], 0, X[0]);
   }
 #define DVCP_DFE_STEP(U)                                              \
@@ -565,7 +606,10 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
     const f32x16 acc = mfma(X[(U)&1]);                                \
     if (!WA) weights(dj[((U) + 1) & 7], ((U) + 1) & 3);               \
     prep(G[((U) + 1) & 1], ((U) + 1) & 3, X[((U) + 1) & 1]);          \
-    if (WA) weights(dj[((U) + 2) & 7], ((U) + 2) & 3);                \
+    if (WA && DVCP_DFE_W2 && ((U)&1) == 0)                            \
+      weights2(dj[((U) + 2) & 7], dj[((U) + 3) & 7], ((U) + 2) & 3,   \
+               ((U) + 3) & 3);                                        \
+    if (WA && !DVCP_DFE_W2) weights(dj[((U) + 2) & 7], ((U) + 2) & 3); \
     load_row(t6, dj[((U) + 6) & 7], nn[((U) + 6) & 7]);               \
     gather(t2, nn[((U) + 2) & 7], G[(U)&1]);                          \
     pin(X[((U) + 1) & 1]);                                            \
@@ -615,8 +659,12 @@ int launch_dfe_tgt_mfma(PointsView<T> ref, const float* feat, int M, const float
     // a few resident workgroups per CU amortise the fp64 prologue over many candidates
     const int xcd = B % 8 == 0 && need >= kDfeGrid ? 1 : 0;  // equal pairs per XCD
     const int grid = static_cast<int>(need < kDfeGrid ? need : kDfeGrid);
-    hipLaunchKernelGGL((dfe_tgt_mfma1_kernel<T>), dim3(grid), dim3(kDfe1Waves * kWave), 0, st, ref, feat, M, cand,
-                       dist, idx, Q, B, params, out, xcd);
+    if (sizeof(T) == 4 && ref.rows4())
+      hipLaunchKernelGGL((dfe_tgt_mfma1_kernel<T, float, sizeof(T) == 4>), dim3(grid), dim3(kDfe1Waves * kWave), 0, st,
+                         ref, feat, M, cand, dist, idx, Q, B, params, out, xcd);
+    else
+      hipLaunchKernelGGL((dfe_tgt_mfma1_kernel<T>), dim3(grid), dim3(kDfe1Waves * kWave), 0, st, ref, feat, M, cand,
+                         dist, idx, Q, B, params, out, xcd);
   }
   return launch_status("dvcp_dfe_tgt(mfma)");
 }
@@ -633,8 +681,12 @@ int launch_dfe_tgt_mfma_f16(PointsView<T> ref, const _Float16* feat, int M, cons
   const int64_t need = (total + kDfeMfmaWaves - 1) / kDfeMfmaWaves;
   const int xcd = B % 8 == 0 && need >= kDfeGrid ? 1 : 0;
   const int grid = static_cast<int>(need < kDfeGrid ? need : kDfeGrid);
-  hipLaunchKernelGGL((dfe_tgt_mfma1_kernel<T, _Float16>), dim3(grid), dim3(kDfe1Waves * kWave), 0, st, ref, feat, M,
-                     cand, dist, idx, Q, B, params, out, xcd);
+  if (sizeof(T) == 4 && ref.rows4())
+    hipLaunchKernelGGL((dfe_tgt_mfma1_kernel<T, _Float16, sizeof(T) == 4>), dim3(grid), dim3(kDfe1Waves * kWave), 0,
+                       st, ref, feat, M, cand, dist, idx, Q, B, params, out, xcd);
+  else
+    hipLaunchKernelGGL((dfe_tgt_mfma1_kernel<T, _Float16>), dim3(grid), dim3(kDfe1Waves * kWave), 0, st, ref, feat, M,
+                       cand, dist, idx, Q, B, params, out, xcd);
   return launch_status("dvcp_dfe_tgt_f16");
 }
 
