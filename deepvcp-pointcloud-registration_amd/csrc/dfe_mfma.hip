@@ -231,11 +231,16 @@ __global__ __launch_bounds__(kDfeMfmaWaves * kWave) void dfe_tgt_mfma_kernel(
 // ordered sum; w_j = dist_j / dist_sum in fp64 is then bit-identical.
 constexpr int kDfe1Waves = 4;
 #ifndef DVCP_DFE_GRID
-#define DVCP_DFE_GRID 768
+#define DVCP_DFE_GRID 512
 #endif
-// workgroups (a multiple of 8): 768 = three per CU, every wave resident from the start (one fp64
-// prologue per workgroup, no tail of late workgroups); 2048 / 1536 / 1024 / 768 measured 0.703 /
-// 0.674 / 0.670 / 0.666 ms and 0.682 / 0.687 / 0.665 / 0.663 (profiles/round5/r5s_dfe_grid_ab.log)
+// workgroups (a multiple of 8), every wave resident from the start (one fp64 prologue per
+// workgroup, no tail of late workgroups).  Round 5: 2048 / 1536 / 1024 / 768 measured 0.703 /
+// 0.674 / 0.670 / 0.666 ms and 0.682 / 0.687 / 0.665 / 0.663 (profiles/round5/r5s_dfe_grid_ab.log).
+// Round 6, after the packed-row gather and the paired w rows cut the per-candidate instructions:
+// 1024 / 768 / 512 / 256 workgroups 0.565 / 0.545 / 0.535 / 0.639 ms (tools/knn_bench.py --fast,
+// two runs each, profiles/round6/r6aj_dfe_*.log): two workgroups per CU (two waves per SIMD) now
+// keep the gathers and the matrix cores as busy as three, and leave the CU room to other kernels'
+// waves
 constexpr int kDfeGrid = DVCP_DFE_GRID;
 
 // v + (v moved by the DPP pattern CTRL), fp64 (the two halves moved separately).  Every pattern
@@ -567,7 +572,10 @@ __global__ __launch_bounds__(kDfe1Waves * kWave) __attribute__((amdgpu_waves_per
     float m = a[0];
 #pragma unroll
     for (int r = 1; r < 16; ++r) m = fmaxf(m, a[r]);
-    m = fmaxf(m, __shfl_xor(m, 32, kWave));
+    // the other lane half's rows: v_permlane32_swap (lanes 0..31 receive lanes 32..63; only they
+    // store) instead of an LDS-crossbar shuffle
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+    m = fmaxf(m, __uint_as_float(sw[1]));
     m += eb;
     if (h == 0) out[static_cast<int64_t>(glob_of(cg)) * 32 + r32] = m;
   };
