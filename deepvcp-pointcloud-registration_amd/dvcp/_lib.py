@@ -5,6 +5,7 @@ The library is built in-tree (``make`` in deepvcp-pointcloud-registration_amd/, 
 HIP runtime (SONAME libamdhip64.so.7) that owns torch's device memory and streams.  There is
 no fallback: if the library is missing or no GPU is present, every op raises.
 """
+import contextlib
 import ctypes
 import os
 
@@ -217,15 +218,51 @@ def _capturing():
     return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
 
 
+# Inside a step (``deferred_flags``, DeepVCP.forward) the words wait for the step's end: they are
+# gathered per stream and copied once (one cat, one host copy) when the step closes, instead of
+# one copy behind each flagged launch on the step's serial chain (the split-select FPS launches).
+_STEP_FLAGS = None  # {stream handle: (stream, [(what, flag)])} while a step is open
+
+
+def _queue_host_copy(items):
+    """One pinned host copy of the error words ``items`` [(what, flag)] on the current stream."""
+    words = items[0][1].reshape(-1) if len(items) == 1 else torch.cat([f.reshape(-1) for _, f in items])
+    host = torch.empty(words.shape, dtype=words.dtype, pin_memory=True)
+    host.copy_(words, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    off = 0
+    for what, f in items:
+        _PENDING_FLAGS.append((what, ev, host[off:off + f.numel()]))
+        off += f.numel()
+
+
+@contextlib.contextmanager
+def deferred_flags():
+    """Defer the error-word copies of the launches issued inside to the end of the block."""
+    global _STEP_FLAGS
+    if _STEP_FLAGS is not None or _capturing():  # nested, or captured (the graph collects them)
+        yield
+        return
+    _STEP_FLAGS = {}
+    try:
+        yield
+    finally:
+        pending, _STEP_FLAGS = _STEP_FLAGS, None
+        for s, items in pending.values():
+            with torch.cuda.stream(s):  # the stream the flagged launches ran on
+                _queue_host_copy(items)
+
+
 def defer_flag_check(what, flag):
     if _CAPTURED_FLAGS is not None and _capturing():
         _CAPTURED_FLAGS.append((what, flag))
         return
-    host = torch.empty(flag.shape, dtype=flag.dtype, pin_memory=True)
-    host.copy_(flag, non_blocking=True)
-    ev = torch.cuda.Event()
-    ev.record()
-    _PENDING_FLAGS.append((what, ev, host))
+    if _STEP_FLAGS is not None:
+        s = torch.cuda.current_stream(flag.device)
+        _STEP_FLAGS.setdefault(s.cuda_stream, (s, []))[1].append((what, flag))
+        return
+    _queue_host_copy([(what, flag)])
 
 
 def check_device_flags(block=False):

@@ -175,8 +175,9 @@ class DeepVCP(nn.Module):
         weights of the paper's weighted pose solve (dvcp.paper)."""
         train_head, train_fe = self._training_mode()
         tr = {} if (return_weights and trace is None) else trace
-        feats = self.extract_features(src_pts, tgt_pts, starts, train_fe=train_fe, trace=trace)
-        keypts, vcp = self._head(feats, R_init, train_head, tr, keypoint_idx)
+        with _lib.deferred_flags():  # the guards' host copies once, after the step's launches
+            feats = self.extract_features(src_pts, tgt_pts, starts, train_fe=train_fe, trace=trace)
+            keypts, vcp = self._head(feats, R_init, train_head, tr, keypoint_idx)
         if not return_weights:
             return keypts, vcp
         return keypts, vcp, torch.gather(feats["score"].detach(), 1, tr["topk"])

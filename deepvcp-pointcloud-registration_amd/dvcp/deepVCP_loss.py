@@ -25,8 +25,10 @@ def svd_optimization(x, y_pred, R_true, t_true):
 
 def deepVCP_loss(x, y_pred, R_true, t_true, alpha):
     """x, y_pred (B, K, 3); R_true (B, 3, 3); t_true (B, 3, 1) -> (loss, R (B,3,3), t (B,3,1))."""
-    x = x.permute(0, 2, 1).double()
-    y_pred = y_pred.permute(0, 2, 1).double()
+    # (B, 3, K) fp64 in one copy each (a permuted .double() left a strided tensor that the pose
+    # kernels' operand preparation copied once more)
+    x = x.transpose(1, 2).to(torch.float64, memory_format=torch.contiguous_format)
+    y_pred = y_pred.transpose(1, 2).to(torch.float64, memory_format=torch.contiguous_format)
     if torch.is_grad_enabled() and y_pred.requires_grad:
         # train.py:121 loss.backward(): both Kabsch solves differentiated on the GPU
         loss, R, t = autograd.pose_loss(x, y_pred, R_true, t_true, alpha)

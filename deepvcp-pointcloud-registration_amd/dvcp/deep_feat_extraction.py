@@ -61,6 +61,7 @@ class feat_extraction_layer(nn.Module):
         idxs, centres, events = [], [], []
         prev = xyz
         li = 0
+        errs = None
         while li < 3:
             sa, st = layers[li], starts[li]
             if li == 1 and ops.fps_pair_ok(prev, sa.npoint, layers[2].npoint, pdim=2):
@@ -71,7 +72,12 @@ class feat_extraction_layer(nn.Module):
                 centres += [c2, c3]
                 events += [ev, ev]
                 break
-            i, c = ops.fps(prev, sa.npoint, st.to(prev.device), pdim=2, parts=self.fps_parts)
+            if errs is None and ops.fps_uses_guard(prev, pdim=2, parts=self.fps_parts):
+                # the guards' error words of the chain's split launches: one zeroed buffer
+                errs = torch.zeros(3, dtype=torch.int32, device=prev.device)
+            i, c = ops.fps(prev, sa.npoint, st.to(prev.device), pdim=2, parts=self.fps_parts,
+                           err=errs[li:li + 1] if errs is not None and ops.fps_uses_guard(prev, 2, self.fps_parts)
+                           else None)
             idxs.append(i)
             centres.append(c)
             ev = torch.cuda.Event()

@@ -41,11 +41,13 @@ def fps_parts(N, dtype=torch.float32):
     return 8 if N > FPS_REG_LIMIT[dtype] else 1
 
 
-def fps(xyz, npoint, start, pdim=1, parts=None):
+def fps(xyz, npoint, start, pdim=1, parts=None, err=None):
     """pointnet2_utils.py:63-84.  Returns (idx (B, npoint) int64, centres (B, 3, npoint)).
     ``parts`` (tests, A/B): workgroups per cloud of the select kernel (1, 2, 4 or 8; fp32 clouds of
     2048..65536 points), else ``fps_parts``; the indices are the same for every choice.  (Above
-    16384 points, parts=1 takes the per-step split kernel, dvcp_fps_ws's.)"""
+    16384 points, parts=1 takes the per-step split kernel, dvcp_fps_ws's.)  ``err``: the guard's
+    error word (a zeroed int32 tensor of one element) when the launch takes several workgroups
+    per cloud (``fps_uses_guard``); allocated here when None."""
     _lib.require_gpu(xyz, start)
     B = xyz.shape[0]
     N, sb, sc, sn = _pts(xyz, pdim)
@@ -60,7 +62,8 @@ def fps(xyz, npoint, start, pdim=1, parts=None):
     multi = split or part
     nbytes = int(_lib.load().dvcp_fps_workspace_bytes(B, N))
     ws = torch.empty((nbytes + 7) // 8, dtype=torch.int64, device=xyz.device)
-    err = torch.zeros(1, dtype=torch.int32, device=xyz.device) if multi else None
+    # (``err``: a caller's zeroed int32 word, e.g. one of a chain's; else a fresh one)
+    err = (err if err is not None else torch.zeros(1, dtype=torch.int32, device=xyz.device)) if multi else None
     es = xyz.element_size()
     wgs = B * (S if part else -(-N // 16384) if split else 1)
     work = (9.0 * B * npoint * N, B * (3 * N * es + npoint * (8 + 3 * es)), None, wgs, npoint)
@@ -69,6 +72,14 @@ def fps(xyz, npoint, start, pdim=1, parts=None):
     if multi:
         _lib.defer_flag_check(f"dvcp_fps: FPS workgroups gave up waiting for their peers (N={N})", err)
     return idx, ctr
+
+
+def fps_uses_guard(xyz, pdim=1, parts=None):
+    """Whether ``fps`` on this cloud takes several workgroups per cloud (and an error word)."""
+    N = xyz.shape[pdim]
+    S = parts if parts is not None else fps_parts(N, xyz.dtype)
+    part = S > 1 and xyz.dtype == torch.float32 and FPS_PART_RANGE[0] <= N <= FPS_PART_RANGE[1]
+    return N > FPS_REG_LIMIT[xyz.dtype] or part
 
 
 FPS_PAIR_RANGE = (2048, 16384)

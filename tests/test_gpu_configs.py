@@ -380,3 +380,24 @@ def test_device_flag_check_raises(cuda):
     with pytest.raises(RuntimeError, match="probe flag"):
         dvcp.check_device_flags(block=True)
     dvcp.check_device_flags(block=True)   # reported once
+
+
+def test_device_flags_deferred_to_step_end(cuda):
+    """Inside ``deferred_flags`` (DeepVCP.forward's scope) the words are copied once when the block
+    closes, on the stream each was flagged on: a set word still raises (after the block), and the
+    clear words of the same block do not."""
+    import dvcp
+    from dvcp import _lib
+    dvcp.check_device_flags(block=True)
+    side = torch.cuda.Stream(device=cuda)
+    with _lib.deferred_flags():
+        _lib.defer_flag_check("clear word", torch.zeros(1, dtype=torch.int32, device=cuda))
+        with torch.cuda.stream(side):
+            w = torch.zeros(1, dtype=torch.int32, device=cuda)
+            w.fill_(3)
+            _lib.defer_flag_check("deferred probe", w)
+        assert not _lib._PENDING_FLAGS        # nothing copied yet
+    assert len(_lib._PENDING_FLAGS) == 2      # one copy per stream, one entry per word
+    with pytest.raises(RuntimeError, match="deferred probe"):
+        dvcp.check_device_flags(block=True)
+    dvcp.check_device_flags(block=True)
