@@ -127,7 +127,17 @@ class DeepVCP(nn.Module):
         dev = src_pts.device
         if starts is None:
             starts = self.draw_starts(B, src_pts.shape[2], tgt_pts.shape[2])
-        starts = starts.to(dev, non_blocking=True)
+        one_pass = src_pts.shape == tgt_pts.shape and src_pts.dtype == tgt_pts.dtype and not self.FE1.training
+        fe_starts = None
+        if one_pass and starts.device.type == "cpu":
+            # the 2B-cloud pass's start rows (src then tgt per layer) formed on the host and
+            # uploaded with the seven draws in one copy (no per-layer concatenation on the GPU)
+            fe = torch.stack([torch.cat([starts[i], starts[4 + i]]) for i in range(3)])
+            both_rows = torch.cat([starts.reshape(-1), fe.reshape(-1)]).to(dev, non_blocking=True)
+            starts = both_rows[:7 * B].view(7, B)
+            fe_starts = list(both_rows[7 * B:].view(3, 2 * B))
+        else:
+            starts = starts.to(dev, non_blocking=True)
         side = self._side_stream(dev)
         if train_fe:  # differentiable in FE1's parameters (autograd.feat_extraction)
             def run(pts, st, wl=None, fps=None):
@@ -137,12 +147,13 @@ class DeepVCP(nn.Module):
 
             def run(pts, st, wl=None, side_stream=None):
                 return self.FE1.run(pts, st, wl=wl, side_stream=side_stream, layer_trace=lt)
-        if src_pts.shape == tgt_pts.shape and src_pts.dtype == tgt_pts.dtype and not self.FE1.training:
+        if one_pass:
             # src and tgt share FE1's weights and eval-mode FE is per cloud: one 2B-cloud pass
             # (in training mode each call normalises with its own batch statistics: two passes)
             # (the serial FPS chain then runs once for both clouds, on 2B workgroups)
             both = torch.cat([src_pts, tgt_pts], 0)
-            fe_starts = [torch.cat([starts[i], starts[4 + i]]) for i in range(3)]
+            if fe_starts is None:
+                fe_starts = [torch.cat([starts[i], starts[4 + i]]) for i in range(3)]
             xyz2, feat2, score2 = (run(both, fe_starts, wl=self.WL) if train_fe
                                    else run(both, fe_starts, wl=self.WL, side_stream=side))
             src_xyz, tgt_xyz = xyz2[:B], xyz2[B:]
